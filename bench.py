@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Benchmark of the shard-groupby hot path (BASELINE.json metric) on MI355X.
+
+A "step" is one bqueryd per-shard calc (``bqueryd/worker.py:313``: where-terms + groupby +
+emit back to host memory) over one synthetic taxi-shaped shard already resident in HBM.
+Default workload = BASELINE.json configs[1] (C2): 100 M rows, groupby ``payment_type``,
+sum/mean/count of ``fare_amount`` where ``passenger_count >= 2``.
+
+Multi-GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``): one
+process per GPU, each owns its own 100 M-row shard (weak scaling: shards are independent in
+bqueryd, there is no data-path collective without ``aggregate=True``); barrier + max over
+ranks around the timed region, gloo used only for that bookkeeping.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def _dist_env():
+    ws = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', str(rank)))
+    return ws, rank, local
+
+
+class _Comm:
+    """Barrier / max-reduce across ranks (gloo, CPU only).  Single process: no-ops."""
+
+    def __init__(self, ws):
+        self.ws = ws
+        self.dist = None
+        if ws > 1:
+            import torch.distributed as dist  # imported before libbqgpu: one HIP runtime
+            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+            dist.init_process_group('gloo')
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def _cpu_baseline(cols, cfg, reps=2):
+    """The C port of bquery's per-shard algorithm (oracle/cbquery.c), one thread."""
+    from oracle import cbquery
+    cbquery.build()
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        cbquery.handle_work(cols, cfg['groupby'], cfg['aggs'], cfg['where'])
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    n = len(next(iter(cols.values())))
+    return n / best, best
+
+
+def _load_traffic(config, rows):
+    """HBM bytes per scan launch from the committed rocprofv3 PMC summaries, if present."""
+    path = os.path.join(HERE, 'profiles', 'pmc_%s.json' % config)
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get('rows') == rows:
+            return d.get('hbm_bytes_per_launch')
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4'])
+    ap.add_argument('--rows', type=int, default=None, help='override rows per shard')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--variant', default='exact', choices=['exact', 'raw'])
+    args = ap.parse_args(argv)
+
+    ws, rank, local = _dist_env()
+    comm = _Comm(ws)
+
+    from bqueryd_amd import synth
+    from bqueryd_amd.engine import Device, ShardTable
+
+    cfg = synth.CONFIGS[args.config]
+    rows = args.rows or cfg['rows']
+    cols = synth.taxi_shard(rows, config_id=synth.CONFIG_ID[args.config], n_shards=max(ws, 1),
+                            shard=rank, variant=args.variant, columns=synth.query_columns(cfg))
+    dev = Device(local)
+    table = ShardTable(cols, device=dev)
+    npass_expected = None
+    if cfg['where']:
+        npass_expected = int(np.count_nonzero(cols['passenger_count'] >= 2))
+
+    def step():
+        out, _ = table.groupby(cfg['groupby'], cfg['aggs'], where_terms=cfg['where'])
+        return out
+
+    for _ in range(args.warmup):
+        out = step()
+    cnt_col = [a[2] for a in cfg['aggs'] if a[1] == 'count']
+    if npass_expected is not None and cnt_col:
+        got = int(out[cnt_col[0]].sum())
+        if got != npass_expected:
+            raise SystemExit('sanity check failed: %d != %d passing rows' % (got, npass_expected))
+
+    # device timing of the dominant (scan) kernel: HIP events on the library's stream
+    dev.enable_timing(True)
+    scan_ms = []
+    bytes_per_launch = 0
+    mode = None
+    comm.barrier()
+    dev.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        tm = dev.last_timing()
+        scan_ms.append(tm['scan_ms'])
+        bytes_per_launch = tm['bytes']
+        mode = tm['mode']
+    dev.synchronize()
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = comm.max(t1 - t0)
+    total_rows = comm.sum(rows * args.steps)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_rows / elapsed
+
+    scan_avg = float(np.mean(scan_ms)) if scan_ms else float('nan')
+    achieved = bytes_per_launch / (scan_avg * 1e-3) / 1e9 if scan_avg > 0 else 0.0
+
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        rate, secs = _cpu_baseline(cols, cfg)
+        cpu = {'value': rate, 'unit': 'rows/s', 'cores': 1, 'kind': 'port',
+               'sample': 'full %s shard (%d rows), oracle/cbquery.c single-threaded C port of '
+                         'bquery\'s multi-pass per-shard groupby (where mask, khash factorize, '
+                         'filter re-factorize, one pass per aggregation), best of 2 (%.2f s), '
+                         'host %s' % (args.config.upper(), rows, secs, platform.processor() or
+                                      platform.machine())}
+    traffic = _load_traffic(args.config, rows)
+    comm.close()
+    if rank != 0:
+        return
+    line = {
+        'metric': 'groupby rows/sec (whole node) + achieved HBM GB/s vs peak, 1/2/4/8 GPUs',
+        'value': value,
+        'unit': 'rows/s',
+        'n_gpus': ws,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': ms_per_step,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f64',
+        'data': 'synthetic taxi-shaped shards (SURVEY.md §8d generator, %s variant), resident in HBM' % args.variant,
+        'config': {
+            'workload': '%s: %d rows/shard, 1 shard per GPU, groupby %s, aggs %s, where %s' % (
+                args.config.upper(), rows, cfg['groupby'], [a[1] for a in cfg['aggs']], cfg['where']),
+            'rows_per_gpu': rows,
+            'parallelism': 'shard-per-rank x%d' % ws,
+            'engine_mode': ['private-lds', 'shared-lds', 'global-dense', 'global-hash'][mode or 0],
+        },
+        'roofline': {
+            'bound': 'hbm',
+            'achieved': achieved,
+            'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s',
+            'frac': achieved / HBM_PEAK_GBS,
+            'traffic': traffic,
+            'kernel': 'k_scan_private' if (mode or 0) == 0 else 'k_scan_*',
+            'kernel_avg_ms': scan_avg,
+            'algorithmic_bytes_per_launch': bytes_per_launch,
+        },
+        'cpu_baseline': cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,1257 @@
+// api.hip -- host runtime of libbqgpu: contexts, device-resident shard tables, the query
+// planner and the C ABI declared in include/bqgpu.h.
+//
+// The planner maps one bquery ctable.groupby call (bqueryd/worker.py:313) onto:
+//   1. key coding: every key column is coded as (v - min) from the column statistics, and
+//      the codes are combined mixed-radix into one dense slot id; sparse key spaces fall back
+//      to an open-addressing hash of the packed code (float keys: canonical bits);
+//   2. one fused scan over the columns (where-terms + slot + sums/counts/first row), in the
+//      private-LDS, shared-LDS or global-atomic flavour by slot-space size;
+//   3. extra ordered passes only for std (centered second moments), count_distinct and
+//      sorted_count_distinct;
+//   4. emit in first-appearance order of the passing rows (bquery's group order).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+using namespace bqg;
+
+namespace {
+
+struct HipError {
+  hipError_t e;
+  const char* what;
+  int line;
+};
+struct ApiError {
+  int code;
+  std::string msg;
+};
+
+#define HIPCHECK(x)                                 \
+  do {                                              \
+    hipError_t _e = (x);                            \
+    if (_e != hipSuccess) throw HipError{_e, #x, __LINE__}; \
+  } while (0)
+
+[[noreturn]] void fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  throw ApiError{code, buf};
+}
+
+thread_local std::string g_err;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  void* ensure(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (bytes > cap) {
+      if (p) HIPCHECK(hipFree(p));
+      p = nullptr;
+      size_t c = std::max<size_t>(bytes, cap + cap / 2);
+      c = (c + 255) & ~size_t(255);
+      if (hipMalloc(&p, c) != hipSuccess) {
+        p = nullptr;
+        cap = 0;
+        fail(BQG_E_OOM, "device allocation of %zu bytes failed", c);
+      }
+      cap = c;
+    }
+    return p;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  void* ensure(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (bytes > cap) {
+      if (p) HIPCHECK(hipHostFree(p));
+      p = nullptr;
+      size_t c = std::max<size_t>(bytes, cap + cap / 2);
+      if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) {
+        p = nullptr;
+        cap = 0;
+        fail(BQG_E_OOM, "pinned allocation of %zu bytes failed", c);
+      }
+      cap = c;
+    }
+    return p;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+size_t dtype_size(int dt) { return size_t(1) << dtype_lg(dt); }
+
+}  // namespace
+
+struct ColStats {
+  bool valid = false;
+  bool empty = true;
+  int64_t imin = 0, imax = 0;
+  double fmin = 0, fmax = 0;
+  bool has_nan = false;
+};
+
+struct Column {
+  int dtype = 0;
+  unsigned char* dev = nullptr;
+  size_t bytes = 0;
+  ColStats stats;
+};
+
+struct bqg_table {
+  bqg_ctx* ctx = nullptr;
+  int64_t nrows = 0;
+  std::vector<Column> cols;
+};
+
+struct bqg_result {
+  int64_t n_rows = 0;
+  int32_t filtered = 0;
+  std::vector<int32_t> dtypes;
+  std::vector<std::vector<unsigned char>> data;
+  std::vector<const void*> ptrs;
+};
+
+struct bqg_ctx {
+  int device = 0;
+  int cu = 256;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // staging for pushes
+  static constexpr size_t kStage = 8u << 20;
+  void* stage[2] = {nullptr, nullptr};
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  int stage_i = 0;
+  // scratch
+  DevBuf partials, counter, hdr, slots, terms, outcols, lists, bitmap, prefix, cdbuf, scdbuf, mask, misc;
+  HostBuf hhdr, hout;
+  // timing
+  bool timing = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bqg_timing last{};
+};
+
+namespace {
+
+void set_stream_device(bqg_ctx* c) { HIPCHECK(hipSetDevice(c->device)); }
+
+template <typename F>
+int guard(bqg_ctx* ctx, F&& f) {
+  try {
+    if (ctx) set_stream_device(ctx);
+    f();
+    return BQG_OK;
+  } catch (const ApiError& e) {
+    if (ctx) ctx->err = e.msg;
+    g_err = e.msg;
+    return e.code;
+  } catch (const HipError& e) {
+    char buf[512];
+    snprintf(buf, sizeof(buf), "HIP error %d (%s) in %s (api.hip:%d)", (int)e.e, hipGetErrorString(e.e), e.what,
+             e.line);
+    if (ctx) ctx->err = buf;
+    g_err = buf;
+    return BQG_E_HIP;
+  } catch (const std::bad_alloc&) {
+    if (ctx) ctx->err = "host out of memory";
+    g_err = "host out of memory";
+    return BQG_E_OOM;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// statistics
+// ------------------------------------------------------------------------------------
+void compute_stats(bqg_table* t, int col) {
+  bqg_ctx* c = t->ctx;
+  Column& k = t->cols[col];
+  if (k.stats.valid) return;
+  unsigned long long* d = (unsigned long long*)c->misc.ensure(4 * sizeof(unsigned long long));
+  unsigned long long init[4] = {~0ull, 0ull, 0ull, 0ull};
+  unsigned long long* h = (unsigned long long*)c->hhdr.ensure(64);
+  memcpy(h, init, sizeof(init));
+  HIPCHECK(hipMemcpyAsync(d, h, sizeof(init), hipMemcpyHostToDevice, c->stream));
+  DevCol dc{k.dev, k.dtype, dtype_lg(k.dtype)};
+  if (t->nrows > 0) launch_stats(dc, t->nrows, d, c->stream);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemcpyAsync(h + 4, d, sizeof(init), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  const unsigned long long mn = h[4], mx = h[5];
+  k.stats.has_nan = h[6] != 0;
+  k.stats.empty = mn > mx;
+  if (!k.stats.empty) {
+    if (dtype_is_float(k.dtype)) {
+      auto dec = [](unsigned long long u) {
+        u = (u & 0x8000000000000000ull) ? (u & ~0x8000000000000000ull) : ~u;
+        double d;
+        memcpy(&d, &u, 8);
+        return d;
+      };
+      k.stats.fmin = dec(mn);
+      k.stats.fmax = dec(mx);
+    } else if (k.dtype == BQG_U64) {
+      k.stats.imin = (int64_t)mn;
+      k.stats.imax = (int64_t)mx;
+    } else {
+      k.stats.imin = (int64_t)(mn ^ 0x8000000000000000ull);
+      k.stats.imax = (int64_t)(mx ^ 0x8000000000000000ull);
+    }
+  }
+  k.stats.valid = true;
+}
+
+// ------------------------------------------------------------------------------------
+// query planning
+// ------------------------------------------------------------------------------------
+enum Mode { kPrivate = 0, kShared = 1, kGlobalDense = 2, kGlobalHash = 3 };
+
+struct Plan {
+  ScanParams p{};
+  std::vector<int> tcol;       // table column of each scan column
+  int mode = kGlobalDense;
+  uint64_t nslots = 1;
+  int nsum = 0;                // sum states (SUM / MEAN)
+  std::vector<int> std_cols;   // scan columns needing a centered pass (subset of sum states)
+  int32_t agg_state[kMaxAggs];
+  bool has_filter = false;
+  int64_t alg_bytes = 0;
+};
+
+int scan_col(Plan& pl, int tc) {
+  for (size_t i = 0; i < pl.tcol.size(); ++i)
+    if (pl.tcol[i] == tc) return (int)i;
+  if ((int)pl.tcol.size() >= kMaxCols)
+    fail(BQG_E_UNSUPPORTED, "query touches more than %d distinct columns", kMaxCols);
+  pl.tcol.push_back(tc);
+  return (int)pl.tcol.size() - 1;
+}
+
+bool is_float_op_input(int dt) { return dtype_is_float(dt); }
+
+uint64_t bits_for(uint64_t range) {  // bits needed to code values 0..range-1
+  uint64_t b = 0;
+  while (b < 64 && (range - 1) >> b) ++b;
+  return b;
+}
+
+void build_terms(bqg_ctx* c, bqg_table* t, Plan& pl, int n_terms, const bqg_term* terms) {
+  if (n_terms > kMaxTerms) fail(BQG_E_UNSUPPORTED, "more than %d where terms", kMaxTerms);
+  size_t need = 0;
+  for (int i = 0; i < n_terms; ++i)
+    if (terms[i].op == BQG_T_IN || terms[i].op == BQG_T_NIN) need += (size_t)terms[i].nvals * 8;
+  unsigned char* dv = (unsigned char*)c->terms.ensure(need + 64);
+  std::vector<unsigned char> host(need + 64);
+  size_t off = 0;
+  pl.p.nterms = n_terms;
+  for (int i = 0; i < n_terms; ++i) {
+    const bqg_term& tm = terms[i];
+    if (tm.col < 0 || tm.col >= (int)t->cols.size()) fail(BQG_E_INVALID, "where term column %d out of range", tm.col);
+    if (tm.op < BQG_T_FALSE || tm.op > BQG_T_LE) fail(BQG_E_INVALID, "unknown where operator code %d", tm.op);
+    DevTerm& d = pl.p.terms[i];
+    d.col = scan_col(pl, tm.col);
+    d.op = tm.op;
+    d.is_float = dtype_is_float(t->cols[tm.col].dtype);
+    d.nvals = (int32_t)tm.nvals;
+    d.ivals = nullptr;
+    d.fvals = nullptr;
+    d.iv0 = 0;
+    d.fv0 = 0;
+    if (tm.op == BQG_T_TRUE || tm.op == BQG_T_FALSE) continue;
+    if (tm.nvals < 1) fail(BQG_E_INVALID, "where term without values");
+    if (d.is_float) {
+      if (!tm.fvals) fail(BQG_E_INVALID, "float where term without fvals");
+      d.fv0 = tm.fvals[0];
+    } else {
+      if (!tm.ivals) fail(BQG_E_INVALID, "integer where term without ivals");
+      d.iv0 = tm.ivals[0];
+    }
+    if (tm.op == BQG_T_IN || tm.op == BQG_T_NIN) {
+      const void* src = d.is_float ? (const void*)tm.fvals : (const void*)tm.ivals;
+      memcpy(host.data() + off, src, (size_t)tm.nvals * 8);
+      if (d.is_float) d.fvals = (const double*)(dv + off);
+      else d.ivals = (const int64_t*)(dv + off);
+      off += (size_t)tm.nvals * 8;
+    }
+  }
+  if (off) HIPCHECK(hipMemcpyAsync(dv, host.data(), off, hipMemcpyHostToDevice, c->stream));
+  // the staging vector must outlive the async copy: synchronise (tiny, once per query)
+  if (off) HIPCHECK(hipStreamSynchronize(c->stream));
+}
+
+void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
+  const int ncols_t = (int)t->cols.size();
+  if (q->n_keys < 0 || q->n_keys > kMaxKeys) fail(BQG_E_UNSUPPORTED, "at most %d groupby columns", kMaxKeys);
+  if (q->n_aggs < 0 || q->n_aggs > kMaxAggs) fail(BQG_E_UNSUPPORTED, "at most %d aggregations", kMaxAggs);
+  for (int i = 0; i < q->n_keys; ++i)
+    if (q->key_cols[i] < 0 || q->key_cols[i] >= ncols_t) fail(BQG_E_INVALID, "groupby column %d out of range", q->key_cols[i]);
+  // 1. sum states (value columns first), deduplicated by column
+  for (int a = 0; a < q->n_aggs; ++a) {
+    const bqg_agg& g = q->aggs[a];
+    if (g.col < 0 || g.col >= ncols_t) fail(BQG_E_INVALID, "aggregation column %d out of range", g.col);
+    if (g.op < BQG_SUM || g.op > BQG_STD) fail(BQG_E_INVALID, "unknown aggregation op %d", g.op);
+    pl.agg_state[a] = -1;
+    if (g.op == BQG_SUM || g.op == BQG_MEAN || g.op == BQG_STD) {
+      const int dt = t->cols[g.col].dtype;
+      if (dt == BQG_BOOL) fail(BQG_E_UNSUPPORTED, "sum/mean/std of a bool column");
+      int st = -1;
+      for (int s = 0; s < (int)pl.tcol.size(); ++s)
+        if (pl.tcol[s] == g.col) st = s;
+      if (st < 0) {
+        if ((int)pl.tcol.size() >= kMaxSums) fail(BQG_E_UNSUPPORTED, "more than %d summed columns", kMaxSums);
+        pl.tcol.push_back(g.col);
+        st = (int)pl.tcol.size() - 1;
+        pl.p.sum_is_float[st] = dtype_is_float(dt);
+        pl.p.sum_centered[st] = 0;
+        pl.p.centers[st] = nullptr;
+      }
+      pl.agg_state[a] = st;
+      if (g.op == BQG_STD && std::find(pl.std_cols.begin(), pl.std_cols.end(), st) == pl.std_cols.end())
+        pl.std_cols.push_back(st);
+    }
+  }
+  pl.nsum = (int)pl.tcol.size();
+  pl.p.nsum = pl.nsum;
+  // 2. where terms and mask
+  build_terms(c, t, pl, q->n_terms, q->terms);
+  pl.p.mask_col = -1;
+  if (q->mask_col >= 0) {
+    if (q->mask_col >= ncols_t || t->cols[q->mask_col].dtype != BQG_BOOL)
+      fail(BQG_E_INVALID, "mask column must be a BOOL column");
+    pl.p.mask_col = scan_col(pl, q->mask_col);
+  }
+  pl.has_filter = q->n_terms > 0 || q->mask_col >= 0;
+  // 3. keys
+  pl.p.nkeys = q->n_keys;
+  bool any_float = false;
+  unsigned __int128 space = 1;
+  uint64_t bits = 0;
+  for (int k = 0; k < q->n_keys; ++k) {
+    const int tc = q->key_cols[k];
+    Column& col = t->cols[tc];
+    compute_stats(t, tc);
+    DevKey& dk = pl.p.keys[k];
+    dk.col = scan_col(pl, tc);
+    dk.is_float = dtype_is_float(col.dtype);
+    if (dk.is_float) {
+      any_float = true;
+      dk.min = 0;
+      dk.range = 0;
+      continue;
+    }
+    if (col.stats.empty) {
+      dk.min = 0;
+      dk.range = 1;
+    } else {
+      dk.min = col.stats.imin;
+      const uint64_t r = (uint64_t)col.stats.imax - (uint64_t)col.stats.imin;  // may wrap to 2^64-1
+      dk.range = r + 1;                                                       // 0 means 2^64
+    }
+    const unsigned __int128 rr = dk.range ? (unsigned __int128)dk.range : ((unsigned __int128)1 << 64);
+    space *= rr;
+    if (space > ((unsigned __int128)1 << 100)) space = ((unsigned __int128)1 << 100);
+    bits += dk.range ? bits_for(dk.range) : 64;
+  }
+  pl.p.ncols = (int)pl.tcol.size();
+  for (int i = 0; i < pl.p.ncols; ++i) {
+    const Column& col = t->cols[pl.tcol[i]];
+    pl.p.cols[i] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
+    pl.alg_bytes += (int64_t)dtype_size(col.dtype) * t->nrows;
+  }
+  pl.p.nrows = t->nrows;
+  // 4. mode
+  const uint64_t kDenseMax = std::max<uint64_t>(1ull << 24, std::min<uint64_t>(2ull * (uint64_t)t->nrows, 1ull << 27));
+  bool hash = any_float || space > kDenseMax;
+  if (hash) {
+    if (any_float && q->n_keys > 1)
+      fail(BQG_E_UNSUPPORTED, "float groupby columns are supported only as the single key");
+    if (!any_float && bits > 63) fail(BQG_E_UNSUPPORTED, "groupby key space wider than 63 bits");
+    // packed power-of-two strides: last key in the low bits
+    uint64_t shift = 0;
+    for (int k = q->n_keys - 1; k >= 0; --k) {
+      DevKey& dk = pl.p.keys[k];
+      if (dk.is_float) {
+        dk.stride = 1;
+        dk.range = 0;
+        continue;
+      }
+      dk.stride = 1ull << shift;
+      shift += bits_for(dk.range);
+    }
+    uint64_t est = std::min<uint64_t>((uint64_t)std::max<int64_t>(t->nrows, 1), 1ull << 26);
+    uint64_t cap = 1024;
+    while (cap < 2 * est) cap <<= 1;
+    pl.nslots = cap;
+    pl.mode = kGlobalHash;
+    pl.p.hash = 1;
+  } else {
+    uint64_t stride = 1;
+    for (int k = q->n_keys - 1; k >= 0; --k) {
+      DevKey& dk = pl.p.keys[k];
+      dk.stride = stride;
+      stride *= dk.range;
+    }
+    pl.nslots = (uint64_t)space;
+    pl.p.hash = 0;
+    const size_t per_slot_private = 8 + 8 * (size_t)pl.nsum;  // bytes per lane per slot
+    const size_t per_slot_shared = 8 + 8 * (size_t)pl.nsum;
+    if (pl.nslots * per_slot_private * kBlock <= 80 * 1024) pl.mode = kPrivate;
+    else if (pl.nslots * per_slot_shared <= 64 * 1024) pl.mode = kShared;
+    else pl.mode = kGlobalDense;
+  }
+  pl.p.nslots = pl.nslots;
+}
+
+// ------------------------------------------------------------------------------------
+// emit description
+// ------------------------------------------------------------------------------------
+int agg_out_dtype(int op, int in_dt) {
+  if (op == BQG_COUNT || op == BQG_COUNT_DISTINCT || op == BQG_SORTED_COUNT_DISTINCT) return BQG_I64;
+  if (op == BQG_MEAN || op == BQG_STD) return BQG_F64;
+  return in_dt;
+}
+
+void build_emit(bqg_table* t, const bqg_query* q, const Plan& pl, EmitParams& e, std::vector<int>& out_dt) {
+  memset(&e, 0, sizeof(e));
+  e.nkeys = q->n_keys;
+  e.hash = pl.p.hash;
+  e.ncols = q->n_keys + q->n_aggs;
+  for (int k = 0; k < q->n_keys; ++k) {
+    e.keys[k] = pl.p.keys[k];
+    e.key_dtype[k] = t->cols[q->key_cols[k]].dtype;
+    EmitCol& ec = e.cols[k];
+    ec.kind = 0;
+    ec.key = k;
+    ec.out_dtype = e.key_dtype[k];
+    out_dt.push_back(ec.out_dtype);
+  }
+  int ncd = 0, nscd = 0;
+  for (int a = 0; a < q->n_aggs; ++a) {
+    const bqg_agg& g = q->aggs[a];
+    EmitCol& ec = e.cols[q->n_keys + a];
+    const int in_dt = t->cols[g.col].dtype;
+    ec.kind = 1;
+    ec.op = g.op;
+    ec.in_dtype = in_dt;
+    ec.in_float = dtype_is_float(in_dt);
+    ec.out_dtype = agg_out_dtype(g.op, in_dt);
+    if (g.op == BQG_SUM || g.op == BQG_MEAN) ec.state = pl.agg_state[a];
+    else if (g.op == BQG_STD) {
+      int idx = 0;
+      for (size_t i = 0; i < pl.std_cols.size(); ++i)
+        if (pl.std_cols[i] == pl.agg_state[a]) idx = (int)i;
+      ec.state = idx;
+    } else if (g.op == BQG_COUNT_DISTINCT) ec.state = ncd++;
+    else if (g.op == BQG_SORTED_COUNT_DISTINCT) ec.state = nscd++;
+    out_dt.push_back(ec.out_dtype);
+  }
+  e.nsum2 = (int)pl.std_cols.size();
+}
+
+int scan_blocks(bqg_ctx* c, int64_t nrows, int per_cu) {
+  const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
+  int64_t b = (int64_t)c->cu * per_cu;
+  if (b > tiles) b = tiles;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+bqg_result* empty_result(const std::vector<int>& dts, int filtered) {
+  bqg_result* r = new bqg_result();
+  r->n_rows = 0;
+  r->filtered = filtered;
+  for (int dt : dts) {
+    r->dtypes.push_back(dt);
+    r->data.emplace_back(8);
+  }
+  for (auto& d : r->data) r->ptrs.push_back(d.data());
+  return r;
+}
+
+// Runs the passes of one groupby; returns the device output columns through `res`.
+void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out) {
+  Plan pl;
+  plan_query(c, t, q, pl);
+  EmitParams e;
+  std::vector<int> out_dt;
+  build_emit(t, q, pl, e, out_dt);
+  const int64_t N = t->nrows;
+  c->last = bqg_timing{};
+  c->last.rows = N;
+  c->last.mode = pl.mode;
+
+  // bquery's zero-key, unfiltered, empty-table case yields one 'Total' row of zeros
+  if (N == 0) {
+    if (q->n_keys == 0 && !pl.has_filter) {
+      bqg_result* r = new bqg_result();
+      r->n_rows = 1;
+      for (size_t j = 0; j < out_dt.size(); ++j) {
+        r->dtypes.push_back(out_dt[j]);
+        r->data.emplace_back(8, 0);
+        const bqg_agg& g = q->aggs[j];
+        if (g.op == BQG_STD) {
+          const double nan = NAN;
+          memcpy(r->data.back().data(), &nan, 8);
+        }
+      }
+      for (auto& d : r->data) r->ptrs.push_back(d.data());
+      *out = r;
+    } else {
+      *out = empty_result(out_dt, 0);
+    }
+    return;
+  }
+
+  bool distinct_ops = false;
+  for (int a = 0; a < q->n_aggs; ++a)
+    if (q->aggs[a].op == BQG_COUNT_DISTINCT || q->aggs[a].op == BQG_SORTED_COUNT_DISTINCT) distinct_ops = true;
+  const bool need_generic = distinct_ops || !pl.std_cols.empty() || pl.mode != kPrivate;
+
+  const uint64_t S = pl.nslots;
+  const int nsum = pl.nsum;
+  const int nsum2 = (int)pl.std_cols.size();
+  // slot arrays: cnt | fst | acc | acc2 | keys | hash counters
+  size_t off = 0;
+  auto carve = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  const size_t o_cnt = carve(S * 8), o_fst = carve(S * 4), o_acc = carve(S * 8 * std::max(nsum, 1)),
+               o_acc2 = carve(S * 8 * std::max(nsum2, 1)), o_keys = carve(pl.p.hash ? S * 8 : 8),
+               o_hc = carve(16);
+  unsigned char* sbase = (unsigned char*)c->slots.ensure(off);
+  SlotArrays sa{};
+  sa.cnt = (unsigned long long*)(sbase + o_cnt);
+  sa.fst = (uint32_t*)(sbase + o_fst);
+  sa.acc = (unsigned long long*)(sbase + o_acc);
+  sa.acc2 = nsum2 ? (unsigned long long*)(sbase + o_acc2) : nullptr;
+  sa.keys = pl.p.hash ? (unsigned long long*)(sbase + o_keys) : nullptr;
+  sa.hash_fill = (unsigned int*)(sbase + o_hc);
+  sa.overflow = sa.hash_fill + 1;
+
+  // output columns (device), capacity S rows (private) or G rows (generic, sized later)
+  hipStream_t st = c->stream;
+  if (c->timing) HIPCHECK(hipEventRecord(c->ev[0], st));
+
+  if (pl.mode == kPrivate) {
+    const size_t lds = (size_t)S * kBlock * (8 + 8 * (size_t)nsum);
+    int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
+    if (per_cu < 1) per_cu = 1;
+    PrivateLaunch L{};
+    L.blocks = scan_blocks(c, N, per_cu);
+    L.lds_bytes = lds;
+    L.partials = (unsigned long long*)c->partials.ensure((size_t)(2 + nsum) * L.blocks * S * 8);
+    if (!c->counter.p) {
+      c->counter.ensure(256);
+      HIPCHECK(hipMemsetAsync(c->counter.p, 0, 256, st));
+    }
+    L.done_counter = (unsigned int*)c->counter.p;
+    L.out_hdr = (unsigned long long*)c->hdr.ensure(64);
+    L.emit_inline = need_generic ? 0 : 1;
+    if (L.emit_inline) {
+      unsigned char* ob = (unsigned char*)c->outcols.ensure((size_t)e.ncols * S * 8 + 256);
+      for (int j = 0; j < e.ncols; ++j) e.cols[j].out = ob + (size_t)j * S * 8;
+    }
+    if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
+    launch_scan_private(pl.p, sa, L, e, st);
+    HIPCHECK(hipGetLastError());
+    if (c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));
+    if (!need_generic) {
+      // one D2H of header + columns
+      const size_t colbytes = (size_t)e.ncols * S * 8;
+      unsigned char* h = (unsigned char*)c->hout.ensure(colbytes + 64);
+      HIPCHECK(hipMemcpyAsync(h, L.out_hdr, 16, hipMemcpyDeviceToHost, st));
+      if (colbytes) HIPCHECK(hipMemcpyAsync(h + 64, c->outcols.p, colbytes, hipMemcpyDeviceToHost, st));
+      if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
+      HIPCHECK(hipStreamSynchronize(st));
+      const unsigned long long G = ((unsigned long long*)h)[0], total = ((unsigned long long*)h)[1];
+      bqg_result* r = new bqg_result();
+      r->n_rows = (int64_t)G;
+      r->filtered = pl.has_filter && (int64_t)total < N;
+      for (int j = 0; j < e.ncols; ++j) {
+        const size_t isz = dtype_size(out_dt[j]);
+        r->dtypes.push_back(out_dt[j]);
+        r->data.emplace_back(std::max<size_t>(G * isz, 8));
+        memcpy(r->data.back().data(), h + 64 + (size_t)j * S * 8, G * isz);
+      }
+      for (auto& d : r->data) r->ptrs.push_back(d.data());
+      if (c->timing) {
+        float ms = 0;
+        HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+        c->last.scan_ms = ms;
+        c->last.scan_launches = 1;
+        HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+        c->last.total_ms = ms;
+      }
+      c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
+      *out = r;
+      return;
+    }
+  } else {
+    launch_init_slots(sa, nsum, S, st);
+    HIPCHECK(hipMemsetAsync(sa.hash_fill, 0, 8, st));
+    if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
+    if (pl.mode == kShared) {
+      const size_t lds = (size_t)S * (8 + 8 * (size_t)nsum);
+      int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
+      launch_scan_shared(pl.p, sa, scan_blocks(c, N, std::max(per_cu, 1)), lds, st);
+    } else {
+      launch_scan_global(pl.p, sa, scan_blocks(c, N, 8), st);
+    }
+    HIPCHECK(hipGetLastError());
+    if (c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));
+    if (pl.p.hash) {
+      unsigned int hc[2];
+      HIPCHECK(hipMemcpyAsync(hc, sa.hash_fill, 8, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (hc[1]) fail(BQG_E_STATE, "hash table overflow");  // caller retries with a bigger table
+    }
+  }
+
+  // ---- std: centered second moments
+  if (nsum2) {
+    // means per slot into scratch: centers[v][s] = acc[v][s] / cnt[s]  (computed on host side of
+    // a tiny kernel would be nicer; use a D2H/H2D round trip only for small S, else device)
+    DevBuf& mb = c->misc;
+    double* centers = (double*)mb.ensure((size_t)nsum2 * S * 8 + 64);
+    std::vector<double> hc((size_t)nsum2 * S);
+    std::vector<unsigned long long> hcnt(S), hacc((size_t)nsum * S);
+    HIPCHECK(hipMemcpyAsync(hcnt.data(), sa.cnt, S * 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(hacc.data(), sa.acc, (size_t)nsum * S * 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    for (int i = 0; i < nsum2; ++i) {
+      const int v = pl.std_cols[i];
+      const int dt = t->cols[pl.tcol[v]].dtype;
+      for (uint64_t s = 0; s < S; ++s) {
+        double sum;
+        if (dtype_is_float(dt)) memcpy(&sum, &hacc[(size_t)v * S + s], 8);
+        else if (dt == BQG_U64) sum = (double)(uint64_t)hacc[(size_t)v * S + s];
+        else sum = (double)(int64_t)hacc[(size_t)v * S + s];
+        hc[(size_t)i * S + s] = hcnt[s] ? sum / (double)hcnt[s] : 0.0;
+      }
+    }
+    HIPCHECK(hipMemcpyAsync(centers, hc.data(), hc.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    Plan p2 = pl;
+    // sum states of pass 2: the std columns, centered, in std order (they are the first
+    // nsum2 scan columns after re-ordering)
+    std::vector<int> order;
+    for (int v : pl.std_cols) order.push_back(v);
+    for (int i = 0; i < pl.p.ncols; ++i)
+      if (std::find(order.begin(), order.end(), i) == order.end()) order.push_back(i);
+    ScanParams& q2 = p2.p;
+    for (int i = 0; i < pl.p.ncols; ++i) q2.cols[i] = pl.p.cols[order[i]];
+    auto remap = [&](int oldc) { return (int)(std::find(order.begin(), order.end(), oldc) - order.begin()); };
+    for (int i = 0; i < q2.nterms; ++i) q2.terms[i].col = remap(pl.p.terms[i].col);
+    for (int k = 0; k < q2.nkeys; ++k) q2.keys[k].col = remap(pl.p.keys[k].col);
+    if (q2.mask_col >= 0) q2.mask_col = remap(pl.p.mask_col);
+    q2.nsum = nsum2;
+    for (int i = 0; i < nsum2; ++i) {
+      q2.sum_is_float[i] = 1;
+      q2.sum_centered[i] = 1;
+      q2.centers[i] = centers + (size_t)i * S;
+    }
+    SlotArrays sa2 = sa;
+    sa2.acc = sa.acc2;
+    // pass 2 recomputes cnt/fst identically into scratch copies
+    unsigned char* b2 = (unsigned char*)c->cdbuf.ensure(S * 12 + 512);
+    sa2.cnt = (unsigned long long*)b2;
+    sa2.fst = (uint32_t*)(b2 + ((S * 8 + 255) & ~size_t(255)));
+    if (pl.mode == kPrivate) {
+      const size_t lds = (size_t)S * kBlock * (8 + 8 * (size_t)nsum2);
+      int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
+      PrivateLaunch L{};
+      L.blocks = scan_blocks(c, N, std::max(per_cu, 1));
+      L.lds_bytes = lds;
+      L.partials = (unsigned long long*)c->partials.ensure((size_t)(2 + nsum2) * L.blocks * S * 8);
+      L.done_counter = (unsigned int*)c->counter.p;
+      L.out_hdr = (unsigned long long*)c->hdr.ensure(64);
+      L.emit_inline = 0;
+      launch_scan_private(q2, sa2, L, e, st);
+    } else {
+      sa2.keys = nullptr;  // keep the hash table built by pass 1: init only the accumulators
+      launch_init_slots(sa2, nsum2, S, st);
+      sa2.keys = sa.keys;
+      if (pl.mode == kShared) {
+        const size_t lds = (size_t)S * (8 + 8 * (size_t)nsum2);
+        int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
+        launch_scan_shared(q2, sa2, scan_blocks(c, N, std::max(per_cu, 1)), lds, st);
+      } else {
+        launch_scan_global(q2, sa2, scan_blocks(c, N, 8), st);
+      }
+    }
+    HIPCHECK(hipGetLastError());
+  }
+
+  // ---- count_distinct
+  int ncd = 0, nscd = 0;
+  for (int a = 0; a < q->n_aggs; ++a) ncd += q->aggs[a].op == BQG_COUNT_DISTINCT, nscd += q->aggs[a].op == BQG_SORTED_COUNT_DISTINCT;
+  std::vector<DevBuf> tmp_bufs;  // per-op scratch
+  unsigned long long* cd_out = nullptr;
+  if (ncd) cd_out = (unsigned long long*)c->cdbuf.ensure((size_t)ncd * S * 8 + (nsum2 ? 0 : 0));
+  // note: cdbuf is reused by std pass 2 above only before this point
+  if (ncd) {
+    HIPCHECK(hipMemsetAsync(cd_out, 0, (size_t)ncd * S * 8, st));
+    int i = 0;
+    for (int a = 0; a < q->n_aggs; ++a) {
+      if (q->aggs[a].op != BQG_COUNT_DISTINCT) continue;
+      const int tc = q->aggs[a].col;
+      Column& col = t->cols[tc];
+      compute_stats(t, tc);
+      Plan pc = pl;
+      DistinctLaunch d{};
+      d.vcol = scan_col(pc, tc);
+      pc.p.ncols = (int)pc.tcol.size();
+      pc.p.cols[d.vcol] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
+      d.out = cd_out + (size_t)i * S;
+      if (dtype_is_float(col.dtype)) {
+        if (S != 1) fail(BQG_E_UNSUPPORTED, "count_distinct of a float column with groupby keys");
+        d.vmin = 0;
+        d.vrange = 1;  // key = value bits (S == 1)
+      } else {
+        d.vmin = col.stats.empty ? 0 : col.stats.imin;
+        d.vrange = col.stats.empty ? 1 : (uint64_t)col.stats.imax - (uint64_t)col.stats.imin + 1;
+        if (d.vrange == 0) fail(BQG_E_UNSUPPORTED, "count_distinct value range too wide");
+      }
+      const unsigned __int128 pairs = (unsigned __int128)S * (dtype_is_float(col.dtype) ? 1 : d.vrange);
+      if (!dtype_is_float(col.dtype) && pairs <= ((unsigned __int128)1 << 30)) {
+        const size_t words = (size_t)((pairs + 31) / 32);
+        d.bitmap = (unsigned int*)c->bitmap.ensure(words * 4);
+        HIPCHECK(hipMemsetAsync(d.bitmap, 0, words * 4, st));
+        d.lds_bitmap_words = words * 4 <= 32 * 1024 ? (int)words : 0;
+      } else {
+        if (!dtype_is_float(col.dtype) && pairs >= ((unsigned __int128)1 << 63))
+          fail(BQG_E_UNSUPPORTED, "count_distinct pair space wider than 63 bits");
+        uint64_t cap = 1024;
+        const uint64_t est = std::min<uint64_t>((uint64_t)N, 1ull << 27);
+        while (cap < 2 * est) cap <<= 1;
+        unsigned char* sb = (unsigned char*)c->bitmap.ensure(cap * 8 + 256);
+        d.set = (unsigned long long*)sb;
+        d.set_mask = cap - 1;
+        d.set_fill = (unsigned int*)(sb + cap * 8);
+        d.overflow = d.set_fill + 1;
+        HIPCHECK(hipMemsetAsync(d.set, 0xFF, cap * 8, st));
+        HIPCHECK(hipMemsetAsync(d.set_fill, 0, 8, st));
+      }
+      launch_count_distinct(pc.p, sa, d, scan_blocks(c, N, 8), st);
+      HIPCHECK(hipGetLastError());
+      if (d.set) {
+        unsigned int hc[2];
+        HIPCHECK(hipMemcpyAsync(hc, d.set_fill, 8, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        if (hc[1]) fail(BQG_E_STATE, "count_distinct set overflow");
+      }
+      e.cd[i] = d.out;
+      ++i;
+    }
+  }
+
+  // ---- sorted_count_distinct
+  if (nscd) {
+    unsigned long long* so = (unsigned long long*)c->scdbuf.ensure((size_t)nscd * S * 16 + 256);
+    int i = 0;
+    for (int a = 0; a < q->n_aggs; ++a) {
+      if (q->aggs[a].op != BQG_SORTED_COUNT_DISTINCT) continue;
+      const int tc = q->aggs[a].col;
+      Column& col = t->cols[tc];
+      Plan pc = pl;
+      ScdLaunch d{};
+      d.vcol = scan_col(pc, tc);
+      pc.p.ncols = (int)pc.tcol.size();
+      pc.p.cols[d.vcol] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
+      const uint64_t budget = 1ull << 30;
+      uint64_t waves = (uint64_t)c->cu * 16;
+      const uint64_t need64 = ((uint64_t)N + 63) / 64;
+      if (waves > need64) waves = need64;
+      while (waves > 64 && waves * S * 24 > budget) waves /= 2;
+      if (waves < 1) waves = 1;
+      d.waves = (int)waves;
+      d.chunk_rows = (((int64_t)((N + waves - 1) / waves)) + 63) / 64 * 64;
+      d.lds_state = (S * 24 * (kBlock / 64) <= 64 * 1024) ? 1 : 0;
+      unsigned char* b = (unsigned char*)c->prefix.ensure(waves * S * 24 + 1024);
+      d.st_first = (unsigned long long*)b;
+      d.st_last = d.st_first + waves * S;
+      d.st_first_row = (uint32_t*)(d.st_last + waves * S);
+      d.st_changes = d.st_first_row + waves * S;
+      if (!d.lds_state) {
+        HIPCHECK(hipMemsetAsync(d.st_first_row, 0xFF, waves * S * 4, st));
+        HIPCHECK(hipMemsetAsync(d.st_changes, 0, waves * S * 4, st));
+      }
+      d.out_changes = so + (size_t)i * S * 2;
+      d.out_first = d.out_changes + S;
+      launch_scd(pc.p, sa, d, st);
+      HIPCHECK(hipGetLastError());
+      e.scd_changes[i] = d.out_changes;
+      e.scd_first[i] = d.out_first;
+      ++i;
+    }
+  }
+
+  // ---- generic emit
+  unsigned char* lb = (unsigned char*)c->lists.ensure(S * 8 + 256);
+  uint32_t* list_fst = (uint32_t*)lb;
+  uint32_t* list_slot = list_fst + S;
+  unsigned char* hb = (unsigned char*)c->hdr.ensure(64);
+  unsigned int* gcount = (unsigned int*)hb;
+  unsigned long long* gtotal = (unsigned long long*)(hb + 8);
+  HIPCHECK(hipMemsetAsync(hb, 0, 16, st));
+  launch_compact(sa, S, list_fst, list_slot, gcount, gtotal, st);
+  HIPCHECK(hipGetLastError());
+  unsigned char* hh = (unsigned char*)c->hhdr.ensure(64);
+  HIPCHECK(hipMemcpyAsync(hh, hb, 16, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  const unsigned int G = *(unsigned int*)hh;
+  const unsigned long long total = *(unsigned long long*)(hh + 8);
+  if (G == 0) {
+    *out = empty_result(out_dt, pl.has_filter && (int64_t)total < N);
+    return;
+  }
+  uint32_t* order = (uint32_t*)c->misc.ensure((size_t)G * 4 + 256);
+  if (G <= 8192) {
+    launch_sort_small(list_fst, list_slot, G, order, st);
+  } else {
+    const uint64_t nwords = ((uint64_t)N + 31) / 32;
+    const uint64_t nblocks = (nwords + 1023) / 1024;
+    unsigned char* pb = (unsigned char*)c->prefix.ensure(nwords * 8 + nblocks * 4 + 1024);
+    unsigned int* bitmap = (unsigned int*)pb;
+    unsigned int* wprefix = bitmap + nwords;
+    unsigned int* bprefix = wprefix + nwords;
+    launch_rank_bitmap(list_fst, list_slot, G, N, bitmap, wprefix, bprefix, order, st);
+  }
+  HIPCHECK(hipGetLastError());
+  size_t obytes = 0;
+  for (int j = 0; j < e.ncols; ++j) obytes += ((size_t)G * dtype_size(out_dt[j]) + 255) & ~size_t(255);
+  unsigned char* ob = (unsigned char*)c->outcols.ensure(obytes + 256);
+  {
+    size_t o = 0;
+    for (int j = 0; j < e.ncols; ++j) {
+      e.cols[j].out = ob + o;
+      o += ((size_t)G * dtype_size(out_dt[j]) + 255) & ~size_t(255);
+    }
+  }
+  launch_emit(e, sa, order, G, nsum, S, st);
+  HIPCHECK(hipGetLastError());
+  unsigned char* h = (unsigned char*)c->hout.ensure(obytes + 64);
+  HIPCHECK(hipMemcpyAsync(h, ob, obytes, hipMemcpyDeviceToHost, st));
+  if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
+  HIPCHECK(hipStreamSynchronize(st));
+  bqg_result* r = new bqg_result();
+  r->n_rows = G;
+  r->filtered = pl.has_filter && (int64_t)total < N;
+  {
+    size_t o = 0;
+    for (int j = 0; j < e.ncols; ++j) {
+      const size_t nb = (size_t)G * dtype_size(out_dt[j]);
+      r->dtypes.push_back(out_dt[j]);
+      r->data.emplace_back(std::max<size_t>(nb, 8));
+      memcpy(r->data.back().data(), h + o, nb);
+      o += (nb + 255) & ~size_t(255);
+    }
+  }
+  for (auto& d : r->data) r->ptrs.push_back(d.data());
+  if (c->timing) {
+    float ms = 0;
+    HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+    c->last.scan_ms = ms;
+    c->last.scan_launches = 1;
+    HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+    c->last.total_ms = ms;
+  }
+  c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
+  *out = r;
+}
+
+}  // namespace
+
+// ======================================================================================
+// C ABI
+// ======================================================================================
+extern "C" {
+
+int bqg_abi_version(void) { return BQG_ABI_VERSION; }
+
+int bqg_device_count(int* n) {
+  return guard(nullptr, [&] {
+    int k = 0;
+    HIPCHECK(hipGetDeviceCount(&k));
+    *n = k;
+  });
+}
+
+int bqg_create(int device_ordinal, bqg_ctx** out) {
+  bqg_ctx* c = nullptr;
+  int rc = guard(nullptr, [&] {
+    if (!out) fail(BQG_E_INVALID, "null output pointer");
+    int n = 0;
+    HIPCHECK(hipGetDeviceCount(&n));
+    if (device_ordinal < 0 || device_ordinal >= n) fail(BQG_E_INVALID, "device %d not present (%d devices)", device_ordinal, n);
+    HIPCHECK(hipSetDevice(device_ordinal));
+    c = new bqg_ctx();
+    c->device = device_ordinal;
+    HIPCHECK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+    c->stream = c->own;
+    c->cu = device_cu_count();
+    for (int i = 0; i < 2; ++i) {
+      HIPCHECK(hipHostMalloc(&c->stage[i], bqg_ctx::kStage, hipHostMallocDefault));
+      HIPCHECK(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
+    }
+    for (int i = 0; i < 4; ++i) HIPCHECK(hipEventCreate(&c->ev[i]));
+    *out = c;
+  });
+  if (rc != BQG_OK && c) {
+    delete c;
+    *out = nullptr;
+  }
+  return rc;
+}
+
+int bqg_destroy(bqg_ctx* c) {
+  if (!c) return BQG_OK;
+  int rc = guard(c, [&] {
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    for (DevBuf* b : {&c->partials, &c->counter, &c->hdr, &c->slots, &c->terms, &c->outcols, &c->lists,
+                      &c->bitmap, &c->prefix, &c->cdbuf, &c->scdbuf, &c->mask, &c->misc})
+      b->release();
+    c->hhdr.release();
+    c->hout.release();
+    for (int i = 0; i < 2; ++i) {
+      if (c->stage[i]) (void)hipHostFree(c->stage[i]);
+      if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
+    }
+    for (int i = 0; i < 4; ++i)
+      if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->own) (void)hipStreamDestroy(c->own);
+  });
+  delete c;
+  return rc;
+}
+
+const char* bqg_last_error(bqg_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
+
+int bqg_set_stream(bqg_ctx* c, void* s) {
+  return guard(c, [&] { c->stream = s ? (hipStream_t)s : c->own; });
+}
+
+int bqg_synchronize(bqg_ctx* c) {
+  return guard(c, [&] { HIPCHECK(hipStreamSynchronize(c->stream)); });
+}
+
+int bqg_enable_timing(bqg_ctx* c, int on) {
+  return guard(c, [&] { c->timing = on != 0; });
+}
+
+int bqg_last_timing(bqg_ctx* c, bqg_timing* out) {
+  return guard(c, [&] { *out = c->last; });
+}
+
+int bqg_alloc_pinned(bqg_ctx* c, size_t bytes, void** out) {
+  return guard(c, [&] {
+    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) fail(BQG_E_OOM, "pinned allocation failed");
+  });
+}
+
+int bqg_free_pinned(bqg_ctx* c, void* p) {
+  return guard(c, [&] { HIPCHECK(hipHostFree(p)); });
+}
+
+int bqg_table_create(bqg_ctx* c, int64_t nrows, int32_t ncols, const int32_t* dtypes, bqg_table** out) {
+  bqg_table* t = nullptr;
+  int rc = guard(c, [&] {
+    if (nrows < 0 || nrows >= (int64_t)0xFFFFFFFF) fail(BQG_E_INVALID, "table rows must be in [0, 2^32-1)");
+    if (ncols < 0) fail(BQG_E_INVALID, "negative column count");
+    t = new bqg_table();
+    t->ctx = c;
+    t->nrows = nrows;
+    for (int i = 0; i < ncols; ++i) {
+      int32_t slot;
+      if (dtypes[i] < BQG_BOOL || dtypes[i] > BQG_F64) fail(BQG_E_INVALID, "unknown dtype %d", dtypes[i]);
+      Column col;
+      col.dtype = dtypes[i];
+      t->cols.push_back(col);
+      (void)slot;
+    }
+    for (Column& col : t->cols) {
+      col.bytes = (((size_t)nrows << dtype_lg(col.dtype)) + 255) / 256 * 256 + 256;  // padded for 4-row loads
+      if (hipMalloc(&col.dev, col.bytes) != hipSuccess) fail(BQG_E_OOM, "device allocation of a column failed");
+      HIPCHECK(hipMemsetAsync(col.dev, 0, col.bytes, c->stream));
+    }
+    *out = t;
+  });
+  if (rc != BQG_OK && t) {
+    for (Column& col : t->cols)
+      if (col.dev) (void)hipFree(col.dev);
+    delete t;
+  }
+  return rc;
+}
+
+int bqg_table_destroy(bqg_table* t) {
+  if (!t) return BQG_OK;
+  int rc = guard(t->ctx, [&] {
+    HIPCHECK(hipStreamSynchronize(t->ctx->stream));
+    for (Column& col : t->cols)
+      if (col.dev) HIPCHECK(hipFree(col.dev));
+  });
+  delete t;
+  return rc;
+}
+
+int bqg_table_add_column(bqg_table* t, int32_t dtype, int32_t* slot_out) {
+  return guard(t->ctx, [&] {
+    if (dtype < BQG_BOOL || dtype > BQG_F64) fail(BQG_E_INVALID, "unknown dtype %d", dtype);
+    Column col;
+    col.dtype = dtype;
+    col.bytes = (((size_t)t->nrows << dtype_lg(dtype)) + 255) / 256 * 256 + 256;
+    if (hipMalloc(&col.dev, col.bytes) != hipSuccess) fail(BQG_E_OOM, "device allocation of a column failed");
+    HIPCHECK(hipMemsetAsync(col.dev, 0, col.bytes, t->ctx->stream));
+    t->cols.push_back(col);
+    *slot_out = (int32_t)t->cols.size() - 1;
+  });
+}
+
+int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows, int64_t row_offset) {
+  bqg_ctx* c = t->ctx;
+  return guard(c, [&] {
+    if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
+    if (row_offset < 0 || nrows < 0 || row_offset + nrows > t->nrows) fail(BQG_E_INVALID, "rows out of range");
+    Column& k = t->cols[col];
+    k.stats.valid = false;
+    const size_t isz = dtype_size(k.dtype);
+    const unsigned char* src = (const unsigned char*)host;
+    size_t left = (size_t)nrows * isz;
+    unsigned char* dst = k.dev + (size_t)row_offset * isz;
+    while (left) {
+      const size_t n = std::min(left, bqg_ctx::kStage);
+      const int i = c->stage_i;
+      c->stage_i ^= 1;
+      HIPCHECK(hipEventSynchronize(c->stage_ev[i]));
+      memcpy(c->stage[i], src, n);
+      HIPCHECK(hipMemcpyAsync(dst, c->stage[i], n, hipMemcpyHostToDevice, c->stream));
+      HIPCHECK(hipEventRecord(c->stage_ev[i], c->stream));
+      src += n;
+      dst += n;
+      left -= n;
+    }
+  });
+}
+
+int bqg_table_sync(bqg_table* t) {
+  return guard(t->ctx, [&] {
+    HIPCHECK(hipStreamSynchronize(t->ctx->stream));
+    for (int i = 0; i < (int)t->cols.size(); ++i) compute_stats(t, i);
+  });
+}
+
+int bqg_table_column_ptr(bqg_table* t, int32_t col, void** dev_ptr) {
+  return guard(t->ctx, [&] {
+    if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
+    *dev_ptr = t->cols[col].dev;
+  });
+}
+
+int bqg_table_stats(bqg_table* t, int32_t col, int64_t* imin, int64_t* imax, double* fmin, double* fmax,
+                    int32_t* has_nan) {
+  return guard(t->ctx, [&] {
+    if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
+    compute_stats(t, col);
+    const ColStats& s = t->cols[col].stats;
+    if (imin) *imin = s.imin;
+    if (imax) *imax = s.imax;
+    if (fmin) *fmin = s.fmin;
+    if (fmax) *fmax = s.fmax;
+    if (has_nan) *has_nan = s.has_nan ? 1 : (s.empty ? -1 : 0);
+  });
+}
+
+int bqg_table_read(bqg_table* t, int32_t col, void* host, int64_t nrows, int64_t row_offset) {
+  return guard(t->ctx, [&] {
+    if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
+    if (row_offset < 0 || nrows < 0 || row_offset + nrows > t->nrows) fail(BQG_E_INVALID, "rows out of range");
+    const size_t isz = dtype_size(t->cols[col].dtype);
+    HIPCHECK(hipMemcpyAsync(host, t->cols[col].dev + (size_t)row_offset * isz, (size_t)nrows * isz,
+                            hipMemcpyDeviceToHost, t->ctx->stream));
+    HIPCHECK(hipStreamSynchronize(t->ctx->stream));
+  });
+}
+
+int bqg_where(bqg_ctx* c, bqg_table* t, int32_t n_terms, const bqg_term* terms, int32_t out_mask_col,
+              int64_t* n_pass) {
+  return guard(c, [&] {
+    if (out_mask_col < 0 || out_mask_col >= (int)t->cols.size() || t->cols[out_mask_col].dtype != BQG_BOOL)
+      fail(BQG_E_INVALID, "where output must be a BOOL column");
+    Plan pl;
+    build_terms(c, t, pl, n_terms, terms);
+    if (pl.tcol.empty()) scan_col(pl, out_mask_col);  // no terms: every row passes
+    pl.p.ncols = (int)pl.tcol.size();
+    for (int i = 0; i < pl.p.ncols; ++i) {
+      const Column& col = t->cols[pl.tcol[i]];
+      pl.p.cols[i] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
+    }
+    pl.p.nrows = t->nrows;
+    pl.p.mask_col = -1;
+    unsigned long long* d = (unsigned long long*)c->hdr.ensure(64);
+    HIPCHECK(hipMemsetAsync(d, 0, 8, c->stream));
+    if (t->nrows > 0) launch_where(pl.p, t->cols[out_mask_col].dev, d, scan_blocks(c, t->nrows, 8), c->stream);
+    HIPCHECK(hipGetLastError());
+    unsigned long long* h = (unsigned long long*)c->hhdr.ensure(64);
+    HIPCHECK(hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    t->cols[out_mask_col].stats.valid = false;
+    if (n_pass) *n_pass = (int64_t)h[0];
+  });
+}
+
+int bqg_expand_subgroups(bqg_ctx* c, bqg_table* t, int32_t basket_col, int32_t mask_col, int32_t out_mask_col) {
+  return guard(c, [&] {
+    const int nc = (int)t->cols.size();
+    if (basket_col < 0 || basket_col >= nc) fail(BQG_E_INVALID, "basket column out of range");
+    if (mask_col < 0 || mask_col >= nc || t->cols[mask_col].dtype != BQG_BOOL) fail(BQG_E_INVALID, "mask must be BOOL");
+    if (out_mask_col < 0 || out_mask_col >= nc || t->cols[out_mask_col].dtype != BQG_BOOL)
+      fail(BQG_E_INVALID, "output mask must be BOOL");
+    if (out_mask_col == mask_col) fail(BQG_E_INVALID, "output mask must differ from the input mask");
+    const int64_t N = t->nrows;
+    if (N == 0) return;
+    const int64_t tiles = (N + kTileRows - 1) / kTileRows;
+    unsigned int* scratch = (unsigned int*)c->misc.ensure((size_t)(tiles + 1) * 4 + (size_t)N + 256);
+    const Column& b = t->cols[basket_col];
+    DevCol bc{b.dev, b.dtype, dtype_lg(b.dtype)};
+    launch_expand_subgroups(bc, t->cols[mask_col].dev, t->cols[out_mask_col].dev, N, 0, scratch, c->stream);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    t->cols[out_mask_col].stats.valid = false;
+  });
+}
+
+int bqg_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out) {
+  return guard(c, [&] {
+    if (!q || !out) fail(BQG_E_INVALID, "null query/output");
+    *out = nullptr;
+    run_groupby(c, t, q, out);
+  });
+}
+
+int bqg_select_rows(bqg_ctx* c, bqg_table* t, const bqg_query* q, int32_t n_cols, const int32_t* cols,
+                    bqg_result** out) {
+  return guard(c, [&] {
+    if (n_cols < 0 || n_cols > kMaxKeys + kMaxAggs) fail(BQG_E_UNSUPPORTED, "too many selected columns");
+    for (int i = 0; i < n_cols; ++i)
+      if (cols[i] < 0 || cols[i] >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", cols[i]);
+    const int64_t N = t->nrows;
+    const int64_t tiles = (N + kTileRows - 1) / kTileRows;
+    // mask: precomputed column, fused terms, or all rows
+    unsigned char* mask = nullptr;
+    if (q && q->n_terms > 0) {
+      Plan pl;
+      build_terms(c, t, pl, q->n_terms, q->terms);
+      pl.p.ncols = (int)pl.tcol.size();
+      for (int i = 0; i < pl.p.ncols; ++i) {
+        const Column& col = t->cols[pl.tcol[i]];
+        pl.p.cols[i] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
+      }
+      pl.p.nrows = N;
+      pl.p.mask_col = -1;
+      if (q->mask_col >= 0) {
+        pl.p.mask_col = scan_col(pl, q->mask_col);
+        pl.p.ncols = (int)pl.tcol.size();
+        const Column& col = t->cols[q->mask_col];
+        pl.p.cols[pl.p.mask_col] = DevCol{col.dev, col.dtype, 0};
+      }
+      mask = (unsigned char*)c->mask.ensure((size_t)N + 256);
+      unsigned long long* d = (unsigned long long*)c->hdr.ensure(64);
+      HIPCHECK(hipMemsetAsync(d, 0, 8, c->stream));
+      if (N > 0) launch_where(pl.p, mask, d, scan_blocks(c, N, 8), c->stream);
+    } else if (q && q->mask_col >= 0) {
+      if (t->cols[q->mask_col].dtype != BQG_BOOL) fail(BQG_E_INVALID, "mask must be BOOL");
+      mask = t->cols[q->mask_col].dev;
+    } else {
+      mask = (unsigned char*)c->mask.ensure((size_t)N + 256);
+      HIPCHECK(hipMemsetAsync(mask, 1, (size_t)N + 4, c->stream));
+    }
+    bqg_result* r = new bqg_result();
+    std::unique_ptr<bqg_result> guard_r(r);
+    unsigned int* tc = (unsigned int*)c->lists.ensure((size_t)(tiles + 1) * 4 + 256);
+    int64_t total = 0;
+    if (N > 0) {
+      launch_select_count(mask, N, tc, c->stream);
+      launch_select_scan(tc, tiles, c->stream);
+      // total = offset of the last tile + its count: recount on host from the mask tail
+      unsigned int* hc = (unsigned int*)c->hhdr.ensure(64);
+      HIPCHECK(hipMemcpyAsync(hc, tc + tiles - 1, 4, hipMemcpyDeviceToHost, c->stream));
+      std::vector<unsigned char> tail((size_t)(N - (tiles - 1) * kTileRows));
+      HIPCHECK(hipMemcpyAsync(tail.data(), mask + (tiles - 1) * kTileRows, tail.size(), hipMemcpyDeviceToHost, c->stream));
+      HIPCHECK(hipStreamSynchronize(c->stream));
+      total = hc[0];
+      for (unsigned char v : tail) total += v ? 1 : 0;
+    }
+    r->n_rows = total;
+    r->filtered = total < N;
+    std::vector<DevCol> dcs;
+    std::vector<void*> outs;
+    size_t obytes = 0;
+    std::vector<size_t> offs;
+    for (int i = 0; i < n_cols; ++i) {
+      const Column& col = t->cols[cols[i]];
+      dcs.push_back(DevCol{col.dev, col.dtype, dtype_lg(col.dtype)});
+      offs.push_back(obytes);
+      obytes += ((size_t)total * dtype_size(col.dtype) + 255) & ~size_t(255);
+    }
+    unsigned char* ob = (unsigned char*)c->outcols.ensure(obytes + 256);
+    for (int i = 0; i < n_cols; ++i) outs.push_back(ob + offs[i]);
+    if (total > 0) launch_select_gather(mask, N, tc, dcs.data(), n_cols, outs.data(), c->stream);
+    HIPCHECK(hipGetLastError());
+    for (int i = 0; i < n_cols; ++i) {
+      const int dt = t->cols[cols[i]].dtype;
+      const size_t nb = (size_t)total * dtype_size(dt);
+      r->dtypes.push_back(dt);
+      r->data.emplace_back(std::max<size_t>(nb, 8));
+      if (nb) HIPCHECK(hipMemcpyAsync(r->data.back().data(), outs[i], nb, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    for (auto& d : r->data) r->ptrs.push_back(d.data());
+    *out = guard_r.release();
+  });
+}
+
+int bqg_result_view_get(bqg_result* r, bqg_result_view* out) {
+  if (!r || !out) return BQG_E_INVALID;
+  out->n_rows = r->n_rows;
+  out->n_cols = (int32_t)r->dtypes.size();
+  out->dtypes = r->dtypes.data();
+  out->cols = r->ptrs.data();
+  out->filtered = r->filtered;
+  return BQG_OK;
+}
+
+int bqg_result_free(bqg_result* r) {
+  delete r;
+  return BQG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,249 @@
+// common.h -- shared host/device definitions for libbqgpu (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bqgpu.h"
+
+namespace bqg {
+
+constexpr int kMaxCols = 6;    // distinct input columns one scan kernel streams
+constexpr int kMaxTerms = 8;   // where terms fused into one scan
+constexpr int kMaxKeys = 4;    // groupby columns
+constexpr int kMaxSums = 4;    // summed value columns per scan
+constexpr int kMaxAggs = 16;   // aggregations per query
+constexpr int kBlock = 256;    // threads per workgroup of the scan kernels (4 wave64)
+constexpr int kRowsPerThread = 4;
+constexpr int kTileRows = kBlock * kRowsPerThread;  // rows per workgroup iteration
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
+constexpr uint64_t kEmpty = ~0ull;  // empty hash slot
+
+__host__ __device__ inline int dtype_lg(int dt) {
+  switch (dt) {
+    case BQG_BOOL: case BQG_I8: case BQG_U8: return 0;
+    case BQG_I16: case BQG_U16: return 1;
+    case BQG_I32: case BQG_U32: case BQG_F32: return 2;
+    default: return 3;
+  }
+}
+__host__ __device__ inline bool dtype_is_float(int dt) { return dt == BQG_F32 || dt == BQG_F64; }
+__host__ __device__ inline bool dtype_is_unsigned(int dt) {
+  return dt == BQG_BOOL || dt == BQG_U8 || dt == BQG_U16 || dt == BQG_U32 || dt == BQG_U64;
+}
+
+// ------------------------------------------------------------------------------------
+// Kernel parameter block (passed by value; < 4 KiB).
+// ------------------------------------------------------------------------------------
+struct DevCol {
+  const unsigned char* ptr;
+  int32_t dtype;
+  int32_t lg;
+};
+
+struct DevTerm {
+  int32_t col;       // index into ScanParams::cols
+  int32_t op;        // bqg_term_op
+  int32_t is_float;
+  int32_t nvals;
+  int64_t iv0;       // first value (scalar ops)
+  double fv0;
+  const int64_t* ivals;  // sorted list for IN / NIN (device)
+  const double* fvals;
+};
+
+struct DevKey {
+  int32_t col;       // index into ScanParams::cols
+  int32_t is_float;  // float key: code = canonical bits (single-key hash mode)
+  int64_t min;       // code = (v - min) * stride
+  uint64_t stride;
+  uint64_t range;
+};
+
+struct ScanParams {
+  int64_t nrows;
+  int32_t ncols;
+  int32_t nterms;
+  int32_t nkeys;
+  int32_t nsum;      // sum states = cols[0 .. nsum-1]
+  int32_t mask_col;  // index into cols of a BOOL mask column, or -1
+  int32_t hash;      // 1: slot = hash-table position of the packed key code
+  uint64_t nslots;   // dense slot space (or hash capacity)
+  DevCol cols[kMaxCols];
+  DevTerm terms[kMaxTerms];
+  DevKey keys[kMaxKeys];
+  int32_t sum_is_float[kMaxSums];
+  int32_t sum_centered[kMaxSums];      // accumulate (v - center[slot])^2 (std pass 2)
+  const double* centers[kMaxSums];
+};
+
+// Per-slot aggregation state in device memory (global modes, and the target of the
+// private/shared modes' block flush).
+struct SlotArrays {
+  unsigned long long* cnt;   // [nslots]
+  uint32_t* fst;             // [nslots]  first passing row (kNoRow = none)
+  unsigned long long* acc;   // [nsum][nslots]  f64 or i64 bit patterns
+  unsigned long long* acc2;  // [nsum2][nslots] centered second moments (std), or null
+  unsigned long long* keys;  // hash mode: [nslots] packed key code or kEmpty
+  unsigned int* hash_fill;   // hash mode: number of occupied positions
+  unsigned int* overflow;    // hash mode: set when the table is over-full
+};
+
+// ------------------------------------------------------------------------------------
+// Device helpers: 4-row column chunks.
+// ------------------------------------------------------------------------------------
+struct Chunk {
+  uint4 a, b;  // up to 32 bytes = 4 rows x 8 bytes
+};
+
+__device__ __forceinline__ void load_chunk(Chunk& c, const DevCol& col, int64_t row0) {
+  const unsigned char* p = col.ptr + (row0 << col.lg);
+  switch (col.lg) {
+    case 0: c.a.x = *reinterpret_cast<const uint32_t*>(p); break;
+    case 1: {
+      const uint2 t = *reinterpret_cast<const uint2*>(p);
+      c.a.x = t.x; c.a.y = t.y;
+    } break;
+    case 2: c.a = *reinterpret_cast<const uint4*>(p); break;
+    default:
+      c.a = *reinterpret_cast<const uint4*>(p);
+      c.b = *reinterpret_cast<const uint4*>(p + 16);
+      break;
+  }
+}
+
+__device__ __forceinline__ uint32_t chunk_u32(const Chunk& c, int i) {
+  // i in [0, 8): 32-bit word i of the 32-byte chunk (i is a compile-time constant after unroll)
+  switch (i) {
+    case 0: return c.a.x; case 1: return c.a.y; case 2: return c.a.z; case 3: return c.a.w;
+    case 4: return c.b.x; case 5: return c.b.y; case 6: return c.b.z; default: return c.b.w;
+  }
+}
+
+// element r (0..3) of the chunk as raw 64-bit pattern, sign/zero-extended as int64
+__device__ __forceinline__ int64_t chunk_i64(const Chunk& c, int dt, int r) {
+  switch (dt) {
+    case BQG_BOOL: case BQG_U8: return (int64_t)((chunk_u32(c, 0) >> (8 * r)) & 0xFF);
+    case BQG_I8: return (int64_t)(int8_t)((chunk_u32(c, 0) >> (8 * r)) & 0xFF);
+    case BQG_U16: return (int64_t)((chunk_u32(c, r >> 1) >> (16 * (r & 1))) & 0xFFFF);
+    case BQG_I16: return (int64_t)(int16_t)((chunk_u32(c, r >> 1) >> (16 * (r & 1))) & 0xFFFF);
+    case BQG_I32: return (int64_t)(int32_t)chunk_u32(c, r);
+    case BQG_U32: return (int64_t)chunk_u32(c, r);
+    case BQG_F32: return (int64_t)__uint_as_float(chunk_u32(c, r));
+    case BQG_F64: {
+      const uint64_t u = ((uint64_t)chunk_u32(c, 2 * r + 1) << 32) | chunk_u32(c, 2 * r);
+      return (int64_t)__longlong_as_double((long long)u);
+    }
+    default:  // I64, U64
+      return (int64_t)(((uint64_t)chunk_u32(c, 2 * r + 1) << 32) | chunk_u32(c, 2 * r));
+  }
+}
+
+__device__ __forceinline__ double chunk_f64(const Chunk& c, int dt, int r) {
+  switch (dt) {
+    case BQG_F32: return (double)__uint_as_float(chunk_u32(c, r));
+    case BQG_F64: {
+      const uint64_t u = ((uint64_t)chunk_u32(c, 2 * r + 1) << 32) | chunk_u32(c, 2 * r);
+      return __longlong_as_double((long long)u);
+    }
+    case BQG_U64: return (double)(uint64_t)chunk_i64(c, dt, r);
+    default: return (double)chunk_i64(c, dt, r);
+  }
+}
+
+// canonical 64-bit identity (khash equality: NaN == NaN, -0.0 == +0.0)
+__device__ __forceinline__ uint64_t chunk_bits(const Chunk& c, int dt, int r) {
+  if (dtype_is_float(dt)) {
+    double d = chunk_f64(c, dt, r);
+    if (d != d) return 0x7ff8000000000000ull;
+    d += 0.0;
+    return (uint64_t)__double_as_longlong(d);
+  }
+  return (uint64_t)chunk_i64(c, dt, r);
+}
+
+// where-term on one 4-row chunk -> 4-bit pass mask
+__device__ __forceinline__ bool term_cmp_i(int op, int64_t x, int64_t v, bool uns) {
+  if (uns) {
+    const uint64_t a = (uint64_t)x, b = (uint64_t)v;
+    switch (op) {
+      case BQG_T_EQ: return a == b; case BQG_T_NE: return a != b;
+      case BQG_T_GT: return a > b; case BQG_T_GE: return a >= b;
+      case BQG_T_LT: return a < b; default: return a <= b;
+    }
+  }
+  switch (op) {
+    case BQG_T_EQ: return x == v; case BQG_T_NE: return x != v;
+    case BQG_T_GT: return x > v; case BQG_T_GE: return x >= v;
+    case BQG_T_LT: return x < v; default: return x <= v;
+  }
+}
+__device__ __forceinline__ bool term_cmp_f(int op, double x, double v) {
+  switch (op) {
+    case BQG_T_EQ: return x == v; case BQG_T_NE: return x != v;
+    case BQG_T_GT: return x > v; case BQG_T_GE: return x >= v;
+    case BQG_T_LT: return x < v; default: return x <= v;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ bool sorted_contains(const T* vals, int n, T x) {
+  if (n <= 8) {
+    bool hit = false;
+    for (int i = 0; i < n; ++i) hit |= (vals[i] == x);
+    return hit;
+  }
+  int lo = 0, hi = n - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    const T m = vals[mid];
+    if (m == x) return true;
+    if (m < x) lo = mid + 1; else hi = mid - 1;
+  }
+  return false;
+}
+
+__device__ __forceinline__ uint32_t eval_term(const DevTerm& t, const Chunk& c, int dt) {
+  if (t.op == BQG_T_TRUE) return 0xF;
+  if (t.op == BQG_T_FALSE) return 0;
+  uint32_t m = 0;
+  if (t.is_float) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double x = chunk_f64(c, dt, r);
+      bool hit;
+      if (t.op == BQG_T_IN || t.op == BQG_T_NIN) {
+        hit = sorted_contains<double>(t.fvals, t.nvals, x);
+        if (t.op == BQG_T_NIN) hit = !hit;
+      } else {
+        hit = term_cmp_f(t.op, x, t.fv0);
+      }
+      m |= (uint32_t)hit << r;
+    }
+  } else {
+    const bool uns = (dt == BQG_U64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t x = chunk_i64(c, dt, r);
+      bool hit;
+      if (t.op == BQG_T_IN || t.op == BQG_T_NIN) {
+        hit = uns ? sorted_contains<uint64_t>(reinterpret_cast<const uint64_t*>(t.ivals), t.nvals,
+                                              (uint64_t)x)
+                  : sorted_contains<int64_t>(t.ivals, t.nvals, x);
+        if (t.op == BQG_T_NIN) hit = !hit;
+      } else {
+        hit = term_cmp_i(t.op, x, t.iv0, uns);
+      }
+      m |= (uint32_t)hit << r;
+    }
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+}  // namespace bqg

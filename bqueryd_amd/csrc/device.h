@@ -1,0 +1,210 @@
+// device.h -- device-side building blocks shared by the libbqgpu kernel translation units.
+#pragma once
+
+#include "kernels.h"
+
+namespace bqg {
+
+// ------------------------------------------------------------------------------------
+// wave64 reductions (fixed butterfly order: bitwise deterministic)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ double as_f64(unsigned long long u) { return __longlong_as_double((long long)u); }
+__device__ __forceinline__ unsigned long long as_u64(double d) { return (unsigned long long)__double_as_longlong(d); }
+
+// ------------------------------------------------------------------------------------
+// Row prologue: loads, where-terms, group code
+// ------------------------------------------------------------------------------------
+template <int NC>
+__device__ __forceinline__ void load_rows4(const ScanParams& p, int64_t row0, Chunk (&raw)[NC]) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) load_chunk(raw[c], p.cols[c], row0);
+}
+
+__device__ __forceinline__ void load_one(Chunk& c, const DevCol& col, int64_t row) {
+  switch (col.lg) {
+    case 0: c.a.x = col.ptr[row]; break;
+    case 1: c.a.x = reinterpret_cast<const uint16_t*>(col.ptr)[row]; break;
+    case 2: c.a.x = reinterpret_cast<const uint32_t*>(col.ptr)[row]; break;
+    default: {
+      const uint2 t = reinterpret_cast<const uint2*>(col.ptr)[row];
+      c.a.x = t.x; c.a.y = t.y;
+    }
+  }
+}
+
+template <int NC>
+__device__ __forceinline__ void load_rows1(const ScanParams& p, int64_t row, Chunk (&raw)[NC]) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) load_one(raw[c], p.cols[c], row);
+}
+
+// 4-bit (R = 4) or 1-bit (R = 1) pass mask of the rows starting at row0
+template <int NC, int R>
+__device__ __forceinline__ uint32_t rows_pass(const ScanParams& p, int64_t row0, const Chunk (&raw)[NC]) {
+  const int64_t rem = p.nrows - row0;
+  uint32_t pass = rem >= R ? ((1u << R) - 1u) : (rem > 0 ? ((1u << rem) - 1u) : 0u);
+  for (int t = 0; t < p.nterms; ++t) {
+    const DevTerm& tm = p.terms[t];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (tm.col == c) pass &= eval_term(tm, raw[c], p.cols[c].dtype);
+  }
+  if (p.mask_col >= 0) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (p.mask_col == c) {
+        const uint32_t w = raw[c].a.x;
+        uint32_t m = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) m |= (((w >> (8 * r)) & 0xFFu) != 0u) ? (1u << r) : 0u;
+        pass &= m;
+      }
+  }
+  return pass;
+}
+
+template <int NC, int R>
+__device__ __forceinline__ void rows_code(const ScanParams& p, const Chunk (&raw)[NC], uint64_t (&code)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) code[r] = 0;
+  for (int k = 0; k < p.nkeys; ++k) {
+    const DevKey& key = p.keys[k];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (key.col == c) {
+        const int dt = p.cols[c].dtype;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint64_t v = key.is_float ? chunk_bits(raw[c], dt, r)
+                                          : (uint64_t)chunk_i64(raw[c], dt, r) - (uint64_t)key.min;
+          code[r] += v * key.stride;
+        }
+      }
+  }
+}
+
+// open-addressing hash of packed key codes -> table position (the slot)
+__device__ __forceinline__ uint64_t hash_slot(const SlotArrays& sa, uint64_t mask, uint64_t code,
+                                              bool insert) {
+  uint64_t pos = mix64(code) & mask;
+  for (uint64_t i = 0; i <= mask; ++i) {
+    const unsigned long long k = sa.keys[pos];
+    if (k == code) return pos;
+    if (k == kEmpty) {
+      if (!insert) return kEmpty;
+      const unsigned long long prev = atomicCAS(&sa.keys[pos], kEmpty, (unsigned long long)code);
+      if (prev == kEmpty) {
+        const unsigned int f = atomicAdd(sa.hash_fill, 1u);
+        if ((uint64_t)(f + 1) * 2 > mask + 1) atomicOr(sa.overflow, 1u);
+        return pos;
+      }
+      if (prev == code) return pos;
+    }
+    pos = (pos + 1) & mask;
+  }
+  atomicOr(sa.overflow, 1u);
+  return kEmpty;
+}
+
+// ------------------------------------------------------------------------------------
+// Emit helpers (shared by the inline private emit and the generic emit kernel)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void store_elem(void* base, int dt, uint64_t idx, uint64_t bits) {
+  switch (dtype_lg(dt)) {
+    case 0: reinterpret_cast<uint8_t*>(base)[idx] = (uint8_t)bits; break;
+    case 1: reinterpret_cast<uint16_t*>(base)[idx] = (uint16_t)bits; break;
+    case 2: reinterpret_cast<uint32_t*>(base)[idx] = (uint32_t)bits; break;
+    default: reinterpret_cast<unsigned long long*>(base)[idx] = bits; break;
+  }
+}
+
+struct SlotTotals {
+  unsigned long long cnt;
+  uint32_t fst;
+  unsigned long long acc[kMaxSums];
+  unsigned long long acc2[kMaxSums];  // centered second moments (std pass 2)
+};
+
+__device__ inline void emit_slot(const EmitParams& e, uint64_t slot, uint64_t code, unsigned int rank,
+                          const SlotTotals& t) {
+  for (int j = 0; j < e.ncols; ++j) {
+    const EmitCol& c = e.cols[j];
+    uint64_t bits = 0;
+    if (c.kind == 0) {
+      const DevKey& k = e.keys[c.key];
+      if (k.is_float) {
+        bits = code;
+        if (c.out_dtype == BQG_F32) bits = __float_as_uint((float)as_f64(code));
+      } else {
+        const uint64_t off = (code / k.stride) % k.range;
+        bits = (uint64_t)k.min + off;
+      }
+    } else {
+      switch (c.op) {
+        case BQG_SUM: {
+          const unsigned long long a = t.acc[c.state];
+          if (c.in_float) {
+            bits = (c.out_dtype == BQG_F32) ? (uint64_t)__float_as_uint((float)as_f64(a)) : a;
+          } else {
+            bits = a;  // wrap-around to the output width happens in store_elem
+          }
+        } break;
+        case BQG_COUNT: bits = t.cnt; break;
+        case BQG_MEAN: {
+          const unsigned long long a = t.acc[c.state];
+          const double s = c.in_float ? as_f64(a)
+                                      : (c.in_dtype == BQG_U64 ? (double)(uint64_t)a : (double)(long long)a);
+          bits = as_u64(s / (double)t.cnt);
+        } break;
+        case BQG_STD: {
+          const double m2 = as_f64(t.acc2[c.state]);
+          bits = as_u64(t.cnt ? sqrt(m2 / (double)t.cnt) : __builtin_nan(""));
+        } break;
+        case BQG_COUNT_DISTINCT: bits = e.cd[c.state][slot]; break;
+        case BQG_SORTED_COUNT_DISTINCT: {
+          // literal bquery rule: the first processed row initialises slot 0 (counts 1 only when
+          // that row has label 0, i.e. row 0 passes); every other group's first value is
+          // compared with the zero-initialised last value.
+          unsigned long long ch = e.scd_changes[c.state][slot];
+          const unsigned long long fv = e.scd_first[c.state][slot];
+          bool first_differs;
+          if (c.in_float) first_differs = !(as_f64(fv) == 0.0);
+          else first_differs = (fv != 0ull);
+          if (rank == 0) ch += (t.fst == 0u) ? 1ull : 0ull;
+          else ch += first_differs ? 1ull : 0ull;
+          bits = ch;
+        } break;
+      }
+    }
+    store_elem(c.out, c.out_dtype, rank, bits);
+  }
+}
+
+
+#define BQG_DISPATCH_NC(NCV, ...)                                         \
+  switch (NCV) {                                                          \
+    case 1: { constexpr int NC = 1; __VA_ARGS__; } break;                \
+    case 2: { constexpr int NC = 2; __VA_ARGS__; } break;                \
+    case 3: { constexpr int NC = 3; __VA_ARGS__; } break;                \
+    case 4: { constexpr int NC = 4; __VA_ARGS__; } break;                \
+    case 5: { constexpr int NC = 5; __VA_ARGS__; } break;                \
+    default: { constexpr int NC = 6; __VA_ARGS__; } break;               \
+  }
+
+}  // namespace bqg

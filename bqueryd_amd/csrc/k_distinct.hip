@@ -1,0 +1,254 @@
+// k_distinct.hip -- count_distinct and sorted_count_distinct
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device.h"
+
+namespace bqg {
+
+// ------------------------------------------------------------------------------------
+// count_distinct: set of (slot, value code) pairs; a bit per pair when the pair space is
+// small (LDS pre-filter + HBM bitmap), else an open-addressing set of packed pairs.
+// ------------------------------------------------------------------------------------
+template <int NC, bool HASH>
+__global__ __launch_bounds__(kBlock) void k_count_distinct(ScanParams p, SlotArrays sa, DistinctLaunch d) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  unsigned int* lbits = reinterpret_cast<unsigned int*>(smem);
+  const int tid = threadIdx.x;
+  for (int i = tid; i < d.lds_bitmap_words; i += kBlock) lbits[i] = 0;
+  __syncthreads();
+  const uint64_t hmask = p.nslots - 1;
+  const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
+    Chunk raw[NC];
+    load_rows4<NC>(p, row0, raw);
+    const uint32_t pass = rows_pass<NC, 4>(p, row0, raw);
+    uint64_t code[4];
+    rows_code<NC, 4>(p, raw, code);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (!(pass & (1u << r))) continue;
+      uint64_t s = code[r];
+      if (HASH) {
+        s = hash_slot(sa, hmask, code[r], false);
+        if (s == kEmpty) continue;
+      }
+      uint64_t vcode = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (d.vcol == c) {
+          const int dt = p.cols[c].dtype;
+          vcode = dtype_is_float(dt) ? chunk_bits(raw[c], dt, r)
+                                     : (uint64_t)chunk_i64(raw[c], dt, r) - (uint64_t)d.vmin;
+        }
+      if (d.bitmap) {
+        const uint64_t bit = s * d.vrange + vcode;
+        const unsigned int m = 1u << (bit & 31);
+        if (d.lds_bitmap_words > 0) {
+          if (atomicOr(&lbits[bit >> 5], m) & m) continue;
+        }
+        if (d.bitmap[bit >> 5] & m) continue;
+        if (!(atomicOr(&d.bitmap[bit >> 5], m) & m)) atomicAdd(&d.out[s], 1ull);
+      } else {
+        const uint64_t key = s * d.vrange + vcode;
+        uint64_t pos = mix64(key) & d.set_mask;
+        for (uint64_t i = 0; i <= d.set_mask; ++i) {
+          const unsigned long long k = d.set[pos];
+          if (k == key) break;
+          if (k == kEmpty) {
+            const unsigned long long prev = atomicCAS(&d.set[pos], kEmpty, (unsigned long long)key);
+            if (prev == kEmpty) {
+              atomicAdd(&d.out[s], 1ull);
+              const unsigned int f = atomicAdd(d.set_fill, 1u);
+              if ((uint64_t)(f + 1) * 2 > d.set_mask + 1) atomicOr(d.overflow, 1u);
+              break;
+            }
+            if (prev == key) break;
+          }
+          pos = (pos + 1) & d.set_mask;
+          if (i == d.set_mask) atomicOr(d.overflow, 1u);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// sorted_count_distinct: each wave walks a contiguous chunk of rows 64 at a time and keeps
+// per-slot (first row, first value, last value, changes) for its chunk; runs of one slot
+// inside a 64-row step are resolved with ballots, so the whole chunk is processed in row
+// order.  Chunk states are then combined in chunk order (k_scd_combine).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ bool scd_equal(uint64_t a, uint64_t b, bool isf) {
+  return isf ? (as_f64(a) == as_f64(b)) : (a == b);
+}
+
+template <int NC, bool HASH>
+__global__ __launch_bounds__(kBlock) void k_scd(ScanParams p, SlotArrays sa, ScdLaunch d) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int S = (int)p.nslots;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = blockIdx.x * (kBlock / 64) + wave;
+  uint32_t* fr;
+  unsigned long long *fv, *lv;
+  uint32_t* ch;
+  if (d.lds_state) {
+    unsigned char* base = smem + (size_t)wave * S * 24;
+    fv = reinterpret_cast<unsigned long long*>(base);
+    lv = fv + S;
+    fr = reinterpret_cast<uint32_t*>(lv + S);
+    ch = fr + S;
+    for (int i = lane; i < S; i += 64) {
+      fr[i] = kNoRow;
+      ch[i] = 0;
+    }
+  } else {
+    fr = d.st_first_row + (size_t)w * S;
+    fv = d.st_first + (size_t)w * S;
+    lv = d.st_last + (size_t)w * S;
+    ch = d.st_changes + (size_t)w * S;
+  }
+  if (w >= d.waves) return;
+  const int64_t start = (int64_t)w * d.chunk_rows;
+  int64_t end = start + d.chunk_rows;
+  if (end > p.nrows) end = p.nrows;
+  int vc = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (d.vcol == c) vc = c;
+  const bool isf = dtype_is_float(p.cols[vc].dtype);
+  const uint64_t hmask = p.nslots - 1;
+  for (int64_t base = start; base < end; base += 64) {
+    const int64_t row = base + lane;
+    Chunk raw[NC];
+    bool act = false;
+    uint64_t slot = 0, vb = 0;
+    if (row < end) {
+      load_rows1<NC>(p, row, raw);
+      act = rows_pass<NC, 1>(p, row, raw) & 1u;
+      uint64_t code[1];
+      rows_code<NC, 1>(p, raw, code);
+      slot = code[0];
+      if (HASH && act) {
+        slot = hash_slot(sa, hmask, code[0], false);
+        if (slot == kEmpty) act = false;
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (vc == c) {
+          const int dt = p.cols[c].dtype;
+          vb = isf ? as_u64(chunk_f64(raw[c], dt, 0)) : (uint64_t)chunk_i64(raw[c], dt, 0);
+        }
+    }
+    uint64_t active = __ballot(act);
+    while (active) {
+      const int leader = __ffsll((unsigned long long)active) - 1;
+      const uint64_t ls = __shfl(slot, leader, 64);
+      const uint64_t m = __ballot(act && slot == ls) & active;
+      active &= ~m;
+      const bool mine = (m >> lane) & 1ull;
+      const uint64_t below = m & ((1ull << lane) - 1ull);
+      const int pl = below ? 63 - __clzll((long long)below) : lane;
+      const uint64_t pv = __shfl(vb, pl, 64);
+      const bool diff = mine && below != 0 && !scd_equal(vb, pv, isf);
+      unsigned int nchg = (unsigned int)__popcll(__ballot(diff));
+      const int hl = 63 - __clzll((long long)m);
+      const uint64_t lastv = __shfl(vb, hl, 64);
+      const uint64_t firstv = __shfl(vb, leader, 64);
+      const uint32_t firstrow = (uint32_t)__shfl((int)(uint32_t)row, leader, 64);
+      if (lane == 0) {
+        if (fr[ls] == kNoRow) {
+          fr[ls] = firstrow;
+          fv[ls] = firstv;
+        } else if (!scd_equal(lv[ls], firstv, isf)) {
+          ++nchg;
+        }
+        lv[ls] = lastv;
+        ch[ls] += nchg;
+      }
+    }
+  }
+  if (d.lds_state) {
+    for (int i = lane; i < S; i += 64) {
+      d.st_first_row[(size_t)w * S + i] = fr[i];
+      d.st_first[(size_t)w * S + i] = fv[i];
+      d.st_last[(size_t)w * S + i] = lv[i];
+      d.st_changes[(size_t)w * S + i] = ch[i];
+    }
+  }
+}
+
+struct ScdState {
+  uint32_t present;
+  unsigned long long first, last, changes;
+};
+
+__device__ __forceinline__ ScdState scd_combine(const ScdState& a, const ScdState& b, bool isf) {
+  if (!a.present) return b;
+  if (!b.present) return a;
+  ScdState r;
+  r.present = 1;
+  r.first = a.first;
+  r.last = b.last;
+  r.changes = a.changes + b.changes + (scd_equal(a.last, b.first, isf) ? 0ull : 1ull);
+  return r;
+}
+
+// one wave per slot; lanes take contiguous ranges of chunks, then an ordered tree
+__global__ __launch_bounds__(kBlock) void k_scd_combine(ScdLaunch d, uint64_t nslots, int isf) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t s = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
+  if (s >= nslots) return;
+  const int per = (d.waves + 63) / 64;
+  ScdState st = {0, 0, 0, 0};
+  for (int i = 0; i < per; ++i) {
+    const int w = lane * per + i;
+    if (w >= d.waves) break;
+    const size_t idx = (size_t)w * nslots + s;
+    ScdState x;
+    x.present = d.st_first_row[idx] != kNoRow;
+    x.first = d.st_first[idx];
+    x.last = d.st_last[idx];
+    x.changes = d.st_changes[idx];
+    st = scd_combine(st, x, isf);
+  }
+  for (int o = 1; o < 64; o <<= 1) {
+    ScdState other;
+    other.present = __shfl_down(st.present, o, 64);
+    other.first = __shfl_down(st.first, o, 64);
+    other.last = __shfl_down(st.last, o, 64);
+    other.changes = __shfl_down(st.changes, o, 64);
+    if ((lane % (2 * o)) == 0 && lane + o < 64) st = scd_combine(st, other, isf);
+  }
+  if (lane == 0) {
+    d.out_changes[s] = st.changes;
+    d.out_first[s] = st.first;
+  }
+}
+
+void launch_count_distinct(const ScanParams& p, const SlotArrays& s, const DistinctLaunch& d, int blocks,
+                           hipStream_t st) {
+  const size_t lds = (size_t)d.lds_bitmap_words * 4;
+  if (p.hash) {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_count_distinct<NC, true>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
+  } else {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_count_distinct<NC, false>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
+  }
+}
+void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st) {
+  const int blocks = (d.waves + (kBlock / 64) - 1) / (kBlock / 64);
+  const size_t lds = d.lds_state ? (size_t)(kBlock / 64) * p.nslots * 24 : 0;
+  if (p.hash) {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd<NC, true>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
+  } else {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd<NC, false>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
+  }
+  int isf = 0;
+  for (int c = 0; c < p.ncols; ++c)
+    if (c == d.vcol) isf = dtype_is_float(p.cols[c].dtype);
+  const uint64_t cblocks = (p.nslots + (kBlock / 64) - 1) / (kBlock / 64);
+  hipLaunchKernelGGL(k_scd_combine, dim3((unsigned)cblocks), dim3(kBlock), 0, st, d, p.nslots, isf);
+}
+}  // namespace bqg

@@ -1,0 +1,448 @@
+// k_misc.hip -- emit, stats, where_terms mask, row selection, basket expansion
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device.h"
+
+namespace bqg {
+
+// ------------------------------------------------------------------------------------
+// Emit: occupied slots -> first-appearance order -> output columns
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_compact(SlotArrays sa, uint64_t nslots, uint32_t* list_fst,
+                                                    uint32_t* list_slot, unsigned int* count,
+                                                    unsigned long long* total) {
+  __shared__ unsigned int s_base;
+  __shared__ unsigned int s_wave[kBlock / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < nslots; base += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t s = base + tid;
+    const unsigned long long cs = s < nslots ? sa.cnt[s] : 0ull;
+    const bool occ = cs > 0;
+    const unsigned long long csum = wave_sum_u64(cs);
+    if (lane == 0 && csum) atomicAdd(total, csum);
+    const uint64_t bal = __ballot(occ);
+    const unsigned int before = (unsigned int)__popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wave[wave] = (unsigned int)__popcll(bal);
+    __syncthreads();
+    if (tid == 0) {
+      unsigned int tot = 0;
+      for (int q = 0; q < kBlock / 64; ++q) {
+        const unsigned int t = s_wave[q];
+        s_wave[q] = tot;
+        tot += t;
+      }
+      s_base = tot ? atomicAdd(count, tot) : 0u;
+    }
+    __syncthreads();
+    if (occ) {
+      const unsigned int i = s_base + s_wave[wave] + before;
+      list_fst[i] = sa.fst[s];
+      list_slot[i] = (uint32_t)s;
+    }
+    __syncthreads();
+  }
+}
+
+// single-workgroup bitonic sort of up to 8192 (first_row, slot) pairs by first_row
+__global__ __launch_bounds__(1024) void k_sort_small(const uint32_t* list_fst, const uint32_t* list_slot,
+                                                     unsigned int n, uint32_t* order) {
+  __shared__ uint32_t kf[8192];
+  __shared__ uint32_t ks[8192];
+  unsigned int m = 1;
+  while (m < n) m <<= 1;
+  for (unsigned int i = threadIdx.x; i < m; i += blockDim.x) {
+    kf[i] = i < n ? list_fst[i] : kNoRow;
+    ks[i] = i < n ? list_slot[i] : 0u;
+  }
+  __syncthreads();
+  for (unsigned int k = 2; k <= m; k <<= 1) {
+    for (unsigned int j = k >> 1; j > 0; j >>= 1) {
+      for (unsigned int i = threadIdx.x; i < m; i += blockDim.x) {
+        const unsigned int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const uint32_t a = kf[i], b = kf[ixj];
+          if ((a > b) == up) {
+            kf[i] = b; kf[ixj] = a;
+            const uint32_t t = ks[i]; ks[i] = ks[ixj]; ks[ixj] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (unsigned int i = threadIdx.x; i < n; i += blockDim.x) order[i] = ks[i];
+}
+
+// rank of each group = number of groups whose first row precedes its first row, read off a
+// bitmap of first rows (N bits) with a two-level popcount prefix.
+__global__ void k_setbits(const uint32_t* list_fst, unsigned int n, unsigned int* bitmap) {
+  for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t f = list_fst[i];
+    atomicOr(&bitmap[f >> 5], 1u << (f & 31));
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_word_scan(const unsigned int* bitmap, uint64_t nwords,
+                                                    unsigned int* word_prefix, unsigned int* block_sum) {
+  __shared__ unsigned int sh[1024];
+  const uint64_t w = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  const unsigned int c = w < nwords ? (unsigned int)__popc(bitmap[w]) : 0u;
+  sh[threadIdx.x] = c;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const unsigned int t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
+    __syncthreads();
+    sh[threadIdx.x] += t;
+    __syncthreads();
+  }
+  if (w < nwords) word_prefix[w] = sh[threadIdx.x] - c;
+  if (threadIdx.x == 1023) block_sum[blockIdx.x] = sh[1023];
+}
+
+__global__ __launch_bounds__(1024) void k_block_scan(unsigned int* block_sum, uint64_t nblocks) {
+  __shared__ unsigned int sh[1024];
+  __shared__ unsigned int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint64_t base = 0; base < nblocks; base += 1024) {
+    const uint64_t i = base + threadIdx.x;
+    const unsigned int c = i < nblocks ? block_sum[i] : 0u;
+    sh[threadIdx.x] = c;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const unsigned int t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
+      __syncthreads();
+      sh[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < nblocks) block_sum[i] = carry + sh[threadIdx.x] - c;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += sh[1023];
+    __syncthreads();
+  }
+}
+
+__global__ void k_rank(const uint32_t* list_fst, const uint32_t* list_slot, unsigned int n,
+                       const unsigned int* bitmap, const unsigned int* word_prefix,
+                       const unsigned int* block_prefix, uint32_t* order) {
+  for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t f = list_fst[i];
+    const uint32_t w = f >> 5;
+    const unsigned int r = block_prefix[w >> 10] + word_prefix[w] +
+                           (unsigned int)__popc(bitmap[w] & ((1u << (f & 31)) - 1u));
+    order[r] = list_slot[i];
+  }
+}
+
+__global__ void k_emit(EmitParams e, SlotArrays sa, const uint32_t* order, unsigned int n, int nsum,
+                       uint64_t nslots) {
+  const int nsum2 = e.nsum2;
+  for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t s = order[i];
+    SlotTotals t;
+    t.cnt = sa.cnt[s];
+    t.fst = sa.fst[s];
+#pragma unroll
+    for (int v = 0; v < kMaxSums; ++v) {
+      t.acc[v] = v < nsum ? sa.acc[(size_t)v * nslots + s] : 0ull;
+      t.acc2[v] = (sa.acc2 && v < nsum2) ? sa.acc2[(size_t)v * nslots + s] : 0ull;
+    }
+    const uint64_t code = e.hash ? (uint64_t)sa.keys[s] : (uint64_t)s;
+    emit_slot(e, s, code, i, t);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Column statistics: order-preserving 64-bit keys, min/max by atomics
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long ord_key_i(int64_t x) { return (unsigned long long)x ^ 0x8000000000000000ull; }
+__device__ __forceinline__ unsigned long long ord_key_f(double d) {
+  const unsigned long long u = as_u64(d);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsigned long long* out) {
+  unsigned long long mn = ~0ull, mx = 0ull, nan = 0ull;
+  const bool isf = dtype_is_float(c.dtype);
+  const bool u64 = c.dtype == BQG_U64;
+  for (int64_t row0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4; row0 < nrows;
+       row0 += (int64_t)gridDim.x * kBlock * 4) {
+    Chunk ch;
+    load_chunk(ch, c, row0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (row0 + r >= nrows) break;
+      unsigned long long k;
+      if (isf) {
+        const double d = chunk_f64(ch, c.dtype, r);
+        if (d != d) { nan = 1; continue; }
+        k = ord_key_f(d + 0.0);
+      } else if (u64) {
+        k = (unsigned long long)chunk_i64(ch, c.dtype, r);
+      } else {
+        k = ord_key_i(chunk_i64(ch, c.dtype, r));
+      }
+      mn = min(mn, k);
+      mx = max(mx, k);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    mn = min(mn, (unsigned long long)__shfl_xor(mn, o, 64));
+    mx = max(mx, (unsigned long long)__shfl_xor(mx, o, 64));
+    nan |= (unsigned long long)__shfl_xor(nan, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&out[0], mn);
+    atomicMax(&out[1], mx);
+    if (nan) atomicOr(&out[2], 1ull);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// where_terms -> uint8 mask (worker.py:303), counting passing rows
+// ------------------------------------------------------------------------------------
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_where(ScanParams p, unsigned char* out, unsigned long long* npass) {
+  unsigned long long cnt = 0;
+  const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row0 = tile * kTileRows + (int64_t)threadIdx.x * kRowsPerThread;
+    if (row0 >= p.nrows) continue;
+    Chunk raw[NC];
+    load_rows4<NC>(p, row0, raw);
+    const uint32_t pass = rows_pass<NC, 4>(p, row0, raw);
+    const uint32_t bytes = (pass & 1u) | ((pass & 2u) << 7) | ((pass & 4u) << 14) | ((pass & 8u) << 21);
+    *reinterpret_cast<uint32_t*>(out + row0) = bytes;  // mask buffer is padded
+    cnt += (unsigned long long)__popc(pass);
+  }
+  cnt = wave_sum_u64(cnt);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(npass, cnt);
+}
+
+// ------------------------------------------------------------------------------------
+// Tile scans for selection and basket expansion (tiles of 1024 rows, 4 per lane)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned int block_excl_scan(unsigned int v, unsigned int* total) {
+  __shared__ unsigned int sh[kBlock];
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 1; o < kBlock; o <<= 1) {
+    const unsigned int t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
+    __syncthreads();
+    sh[threadIdx.x] += t;
+    __syncthreads();
+  }
+  const unsigned int incl = sh[threadIdx.x];
+  if (total) *total = sh[kBlock - 1];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_select_count(const unsigned char* mask, int64_t nrows,
+                                                         unsigned int* tile_counts) {
+  const int64_t row0 = (int64_t)blockIdx.x * kTileRows + threadIdx.x * 4;
+  unsigned int c = 0;
+  if (row0 < nrows) {
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(mask + row0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c += (row0 + r < nrows && ((w >> (8 * r)) & 0xFF)) ? 1u : 0u;
+  }
+  c = (unsigned int)wave_sum_u64(c);
+  __shared__ unsigned int sw[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_counts[blockIdx.x] = sw[0] + sw[1] + sw[2] + sw[3];
+}
+
+__global__ __launch_bounds__(1024) void k_excl_scan_u32(unsigned int* v, int64_t n) {
+  __shared__ unsigned int sh[1024];
+  __shared__ unsigned int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const unsigned int c = i < n ? v[i] : 0u;
+    sh[threadIdx.x] = c;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const unsigned int t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
+      __syncthreads();
+      sh[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < n) v[i] = carry + sh[threadIdx.x] - c;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += sh[1023];
+    __syncthreads();
+  }
+}
+
+struct GatherCols {
+  DevCol cols[kMaxKeys + kMaxAggs];
+  void* outs[kMaxKeys + kMaxAggs];
+  int ncols;
+};
+
+__global__ __launch_bounds__(kBlock) void k_select_gather(const unsigned char* mask, int64_t nrows,
+                                                          const unsigned int* tile_offsets, GatherCols g) {
+  const int64_t row0 = (int64_t)blockIdx.x * kTileRows + threadIdx.x * 4;
+  uint32_t pass = 0;
+  if (row0 < nrows) {
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(mask + row0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pass |= (row0 + r < nrows && ((w >> (8 * r)) & 0xFF)) ? (1u << r) : 0u;
+  }
+  const unsigned int off = tile_offsets[blockIdx.x] + block_excl_scan((unsigned int)__popc(pass), nullptr);
+  unsigned int k = 0;
+  for (int r = 0; r < 4; ++r) {
+    if (!(pass & (1u << r))) continue;
+    const int64_t row = row0 + r;
+    for (int c = 0; c < g.ncols; ++c) {
+      const DevCol& col = g.cols[c];
+      switch (col.lg) {
+        case 0: reinterpret_cast<uint8_t*>(g.outs[c])[off + k] = col.ptr[row]; break;
+        case 1: reinterpret_cast<uint16_t*>(g.outs[c])[off + k] = reinterpret_cast<const uint16_t*>(col.ptr)[row]; break;
+        case 2: reinterpret_cast<uint32_t*>(g.outs[c])[off + k] = reinterpret_cast<const uint32_t*>(col.ptr)[row]; break;
+        default: reinterpret_cast<unsigned long long*>(g.outs[c])[off + k] = reinterpret_cast<const unsigned long long*>(col.ptr)[row]; break;
+      }
+    }
+    ++k;
+  }
+}
+
+// basket runs: boundary where basket[i] != basket[i-1]; run id = inclusive boundary count - 1
+__device__ __forceinline__ bool basket_differs(const Chunk& a, int ra, const Chunk& b, int rb, int dt) {
+  if (dtype_is_float(dt)) return chunk_f64(a, dt, ra) != chunk_f64(b, dt, rb);
+  return chunk_i64(a, dt, ra) != chunk_i64(b, dt, rb);
+}
+
+__device__ __forceinline__ uint32_t run_starts(const DevCol& b, int64_t row0, int64_t nrows) {
+  Chunk cur, pc;
+  load_chunk(cur, b, row0);
+  if (row0 > 0) load_one(pc, b, row0 - 1);
+  uint32_t st = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (row0 + r >= nrows) break;
+    bool start;
+    if (r == 0) start = (row0 == 0) || basket_differs(cur, 0, pc, 0, b.dtype);
+    else start = basket_differs(cur, r, cur, r - 1, b.dtype);
+    if (start) st |= 1u << r;
+  }
+  return st;
+}
+
+__global__ __launch_bounds__(kBlock) void k_runs_count(DevCol b, int64_t nrows, unsigned int* tile_counts) {
+  const int64_t row0 = (int64_t)blockIdx.x * kTileRows + threadIdx.x * 4;
+  const unsigned int c = row0 < nrows ? (unsigned int)__popc(run_starts(b, row0, nrows)) : 0u;
+  unsigned int total;
+  block_excl_scan(c, &total);
+  if (threadIdx.x == 0) tile_counts[blockIdx.x] = total;
+}
+
+template <bool APPLY>
+__global__ __launch_bounds__(kBlock) void k_runs_mark(DevCol b, int64_t nrows, const unsigned int* tile_offsets,
+                                                      const unsigned char* mask, unsigned char* out,
+                                                      unsigned char* run_any) {
+  const int64_t row0 = (int64_t)blockIdx.x * kTileRows + threadIdx.x * 4;
+  const uint32_t st = row0 < nrows ? run_starts(b, row0, nrows) : 0u;
+  const unsigned int before = tile_offsets[blockIdx.x] + block_excl_scan((unsigned int)__popc(st), nullptr);
+  if (row0 >= nrows) return;
+  unsigned int id = before;  // inclusive count of starts up to row r, minus one
+  for (int r = 0; r < 4; ++r) {
+    const int64_t row = row0 + r;
+    if (row >= nrows) break;
+    if (st & (1u << r)) ++id;
+    const unsigned int run = id - 1;
+    if (!APPLY) {
+      if (mask[row]) run_any[run] = 1;
+    } else {
+      out[row] = run_any[run];
+    }
+  }
+}
+
+void launch_compact(const SlotArrays& s, uint64_t nslots, uint32_t* list_fst, uint32_t* list_slot,
+                    unsigned int* count, unsigned long long* total, hipStream_t st) {
+  uint64_t blocks = (nslots + kBlock - 1) / kBlock;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_compact, dim3((unsigned)blocks), dim3(kBlock), 0, st, s, nslots, list_fst, list_slot, count, total);
+}
+void launch_sort_small(uint32_t* list_fst, uint32_t* list_slot, unsigned int n, uint32_t* order, hipStream_t st) {
+  hipLaunchKernelGGL(k_sort_small, dim3(1), dim3(1024), 0, st, list_fst, list_slot, n, order);
+}
+void launch_rank_bitmap(const uint32_t* list_fst, const uint32_t* list_slot, unsigned int n, int64_t nrows,
+                        unsigned int* bitmap, unsigned int* word_prefix, unsigned int* block_prefix,
+                        uint32_t* order, hipStream_t st) {
+  const uint64_t nwords = ((uint64_t)nrows + 31) / 32;
+  const uint64_t nblocks = (nwords + 1023) / 1024;
+  (void)hipMemsetAsync(bitmap, 0, nwords * 4, st);
+  const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_setbits, dim3(g ? g : 1), dim3(256), 0, st, list_fst, n, bitmap);
+  hipLaunchKernelGGL(k_word_scan, dim3((unsigned)nblocks), dim3(1024), 0, st, bitmap, nwords, word_prefix, block_prefix);
+  hipLaunchKernelGGL(k_block_scan, dim3(1), dim3(1024), 0, st, block_prefix, nblocks);
+  hipLaunchKernelGGL(k_rank, dim3(g ? g : 1), dim3(256), 0, st, list_fst, list_slot, n, bitmap, word_prefix,
+                     block_prefix, order);
+}
+void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order, unsigned int n, int nsum,
+                 uint64_t nslots, hipStream_t st) {
+  const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_emit, dim3(g ? g : 1), dim3(256), 0, st, e, s, order, n, nsum, nslots);
+}
+void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, hipStream_t st) {
+  int64_t blocks = (nrows + kTileRows - 1) / kTileRows;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_stats, dim3((unsigned)blocks), dim3(kBlock), 0, st, c, nrows, out4);
+}
+void launch_where(const ScanParams& p, unsigned char* out_mask, unsigned long long* npass, int blocks, hipStream_t st) {
+  BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_where<NC>), dim3(blocks), dim3(kBlock), 0, st, p, out_mask, npass));
+}
+void launch_select_count(const unsigned char* mask, int64_t nrows, unsigned int* tile_counts, hipStream_t st) {
+  const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
+  if (tiles > 0) hipLaunchKernelGGL(k_select_count, dim3((unsigned)tiles), dim3(kBlock), 0, st, mask, nrows, tile_counts);
+}
+void launch_select_scan(unsigned int* tile_counts, int64_t ntiles, hipStream_t st) {
+  if (ntiles > 0) hipLaunchKernelGGL(k_excl_scan_u32, dim3(1), dim3(1024), 0, st, tile_counts, ntiles);
+}
+void launch_select_gather(const unsigned char* mask, int64_t nrows, const unsigned int* tile_offsets,
+                          const DevCol* cols, int ncols, void* const* outs, hipStream_t st) {
+  GatherCols g;
+  g.ncols = ncols;
+  for (int c = 0; c < ncols; ++c) {
+    g.cols[c] = cols[c];
+    g.outs[c] = outs[c];
+  }
+  const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
+  if (tiles > 0) hipLaunchKernelGGL(k_select_gather, dim3((unsigned)tiles), dim3(kBlock), 0, st, mask, nrows, tile_offsets, g);
+}
+void launch_expand_subgroups(const DevCol& basket, const unsigned char* mask, unsigned char* out, int64_t nrows,
+                             int blocks, unsigned int* scratch, hipStream_t st) {
+  (void)blocks;
+  const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
+  if (tiles <= 0) return;
+  unsigned int* tile_counts = scratch;
+  unsigned char* run_any = reinterpret_cast<unsigned char*>(scratch + tiles + 1);
+  hipLaunchKernelGGL(k_runs_count, dim3((unsigned)tiles), dim3(kBlock), 0, st, basket, nrows, tile_counts);
+  hipLaunchKernelGGL(k_excl_scan_u32, dim3(1), dim3(1024), 0, st, tile_counts, tiles);
+  (void)hipMemsetAsync(run_any, 0, (size_t)nrows, st);
+  hipLaunchKernelGGL((k_runs_mark<false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, basket, nrows, tile_counts,
+                     mask, out, run_any);
+  hipLaunchKernelGGL((k_runs_mark<true>), dim3((unsigned)tiles), dim3(kBlock), 0, st, basket, nrows, tile_counts,
+                     mask, out, run_any);
+}
+
+int device_cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
+  return n;
+}
+
+
+}  // namespace bqg

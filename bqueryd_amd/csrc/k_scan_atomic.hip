@@ -1,0 +1,150 @@
+// k_scan_atomic.hip -- shared-LDS and global (dense / hashed) fused scans
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device.h"
+
+namespace bqg {
+
+// ------------------------------------------------------------------------------------
+// SHARED mode: one LDS table per workgroup with LDS atomics, flushed with global atomics.
+// ------------------------------------------------------------------------------------
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_scan_shared(ScanParams p, SlotArrays sa) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int S = (int)p.nslots;
+  const int tid = threadIdx.x;
+  const int nsum = p.nsum;
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][S]
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)nsum * S);    // [S]
+  uint32_t* fst = cnt + S;                                                 // [S]
+  for (int i = tid; i < S; i += kBlock) {
+    cnt[i] = 0;
+    fst[i] = kNoRow;
+  }
+  for (int i = tid; i < nsum * S; i += kBlock) acc[i] = 0;
+  __syncthreads();
+
+  const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
+    Chunk raw[NC];
+    load_rows4<NC>(p, row0, raw);
+    const uint32_t pass = rows_pass<NC, 4>(p, row0, raw);
+    uint64_t code[4];
+    rows_code<NC, 4>(p, raw, code);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (pass & (1u << r)) {
+        const int s = (int)code[r];
+        const uint32_t row = (uint32_t)(row0 + r);
+        atomicAdd(&cnt[s], 1u);
+        if (fst[s] > row) atomicMin(&fst[s], row);
+#pragma unroll
+        for (int v = 0; v < (NC < kMaxSums ? NC : kMaxSums); ++v) {
+          if (v < nsum) {
+            if (p.sum_is_float[v]) {
+              double x = chunk_f64(raw[v], p.cols[v].dtype, r);
+              if (p.sum_centered[v]) {
+                const double d = x - p.centers[v][s];
+                x = d * d;
+              }
+              unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)v * S + s]), x);
+            } else {
+              atomicAdd(&acc[(size_t)v * S + s], (unsigned long long)chunk_i64(raw[v], p.cols[v].dtype, r));
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int s = tid; s < S; s += kBlock) {
+    const uint32_t c = cnt[s];
+    if (c == 0) continue;
+    atomicAdd(&sa.cnt[s], (unsigned long long)c);
+    atomicMin(&sa.fst[s], fst[s]);
+    for (int v = 0; v < nsum; ++v) {
+      const unsigned long long a = acc[(size_t)v * S + s];
+      if (p.sum_is_float[v]) unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)v * p.nslots + s]), as_f64(a));
+      else atomicAdd(&sa.acc[(size_t)v * p.nslots + s], a);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// GLOBAL mode: per-slot arrays in HBM updated with device-scope atomics (large dense slot
+// spaces, and the hashed key mode).
+// ------------------------------------------------------------------------------------
+template <int NC, bool HASH>
+__global__ __launch_bounds__(kBlock) void k_scan_global(ScanParams p, SlotArrays sa) {
+  const int tid = threadIdx.x;
+  const int nsum = p.nsum;
+  const uint64_t hmask = p.nslots - 1;
+  const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
+    Chunk raw[NC];
+    load_rows4<NC>(p, row0, raw);
+    const uint32_t pass = rows_pass<NC, 4>(p, row0, raw);
+    uint64_t code[4];
+    rows_code<NC, 4>(p, raw, code);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (pass & (1u << r)) {
+        uint64_t s = code[r];
+        if (HASH) {
+          s = hash_slot(sa, hmask, code[r], true);
+          if (s == kEmpty) continue;
+        }
+        const uint32_t row = (uint32_t)(row0 + r);
+        atomicAdd(&sa.cnt[s], 1ull);
+        if (sa.fst[s] > row) atomicMin(&sa.fst[s], row);
+#pragma unroll
+        for (int v = 0; v < (NC < kMaxSums ? NC : kMaxSums); ++v) {
+          if (v < nsum) {
+            if (p.sum_is_float[v]) {
+              double x = chunk_f64(raw[v], p.cols[v].dtype, r);
+              if (p.sum_centered[v]) {
+                const double d = x - p.centers[v][s];
+                x = d * d;
+              }
+              unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)v * p.nslots + s]), x);
+            } else {
+              atomicAdd(&sa.acc[(size_t)v * p.nslots + s], (unsigned long long)chunk_i64(raw[v], p.cols[v].dtype, r));
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ void k_init_slots(SlotArrays sa, int nsum, uint64_t nslots) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    sa.cnt[i] = 0;
+    sa.fst[i] = kNoRow;
+    for (int v = 0; v < nsum; ++v) sa.acc[(size_t)v * nslots + i] = 0;
+    if (sa.keys) sa.keys[i] = kEmpty;
+  }
+}
+
+void launch_scan_shared(const ScanParams& p, const SlotArrays& s, int blocks, size_t lds, hipStream_t st) {
+  BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scan_shared<NC>), dim3(blocks), dim3(kBlock), lds, st, p, s));
+}
+void launch_scan_global(const ScanParams& p, const SlotArrays& s, int blocks, hipStream_t st) {
+  if (p.hash) {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scan_global<NC, true>), dim3(blocks), dim3(kBlock), 0, st, p, s));
+  } else {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scan_global<NC, false>), dim3(blocks), dim3(kBlock), 0, st, p, s));
+  }
+}
+void launch_init_slots(const SlotArrays& s, int nsum, uint64_t nslots, hipStream_t st) {
+  uint64_t blocks = (nslots + kBlock - 1) / kBlock;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_init_slots, dim3((unsigned)blocks), dim3(kBlock), 0, st, s, nsum, nslots);
+}
+}  // namespace bqg

@@ -1,0 +1,116 @@
+// kernels.h -- launch interface between the host planner (api.hip) and the gfx950 kernels.
+#pragma once
+
+#include "common.h"
+
+namespace bqg {
+
+// Output column of the emit step (keys first, then aggregations).
+struct EmitCol {
+  int32_t kind;       // 0 = key, 1 = aggregation
+  int32_t out_dtype;  // bqg_dtype of the output column
+  int32_t op;         // bqg_agg_op (aggregations)
+  int32_t state;      // sum-state index (SUM / MEAN / STD) or distinct-state index (CD / SCD)
+  int32_t key;        // key index (keys)
+  int32_t in_float;   // aggregation input column is float
+  int32_t in_dtype;   // aggregation input dtype
+  int32_t pad;
+  void* out;          // device output array (capacity >= groups)
+};
+
+struct EmitParams {
+  int32_t ncols;
+  int32_t nkeys;
+  int32_t hash;
+  int32_t nsum2;  // std second-moment states in SlotArrays::acc2
+  DevKey keys[kMaxKeys];
+  int32_t key_dtype[kMaxKeys];
+  EmitCol cols[kMaxKeys + kMaxAggs];
+  const unsigned long long* cd[kMaxAggs];        // count_distinct per slot
+  const unsigned long long* scd_changes[kMaxAggs];
+  const unsigned long long* scd_first[kMaxAggs]; // first value bits per slot
+};
+
+// Private-LDS mode launch (small dense slot spaces).  When `emit` is non-null the last
+// workgroup finalises and emits the groups itself; otherwise it writes the per-slot totals
+// into `slots`.
+struct PrivateLaunch {
+  int blocks;
+  size_t lds_bytes;
+  unsigned long long* partials;   // [(2 + nsum)][blocks][nslots]
+  unsigned int* done_counter;     // zero before launch; reset by the last workgroup
+  unsigned long long* out_hdr;    // [0] = groups, [1] = passing rows
+  int emit_inline;                // 1: last workgroup emits (EmitParams passed alongside)
+};
+
+void launch_scan_private(const ScanParams& p, const SlotArrays& s, const PrivateLaunch& l,
+                         const EmitParams& e, hipStream_t st);
+void launch_scan_shared(const ScanParams& p, const SlotArrays& s, int blocks, size_t lds_bytes,
+                        hipStream_t st);
+void launch_scan_global(const ScanParams& p, const SlotArrays& s, int blocks, hipStream_t st);
+void launch_init_slots(const SlotArrays& s, int nsum, uint64_t nslots, hipStream_t st);
+
+// count_distinct: pair (slot, value-code) set; bitmap when bitmap != nullptr, else hash set
+struct DistinctLaunch {
+  int vcol;                 // index into ScanParams::cols of the value column
+  int64_t vmin;             // value code = v - vmin (ints) or canonical bits (floats)
+  uint64_t vrange;          // value code space (bitmap mode)
+  unsigned int* bitmap;     // [ceil(nslots * vrange / 32)]
+  unsigned long long* set;  // hash set of packed (slot, vcode) keys (bitmap == nullptr)
+  uint64_t set_mask;
+  unsigned int* set_fill;
+  unsigned int* overflow;
+  unsigned long long* out;  // [nslots] distinct counts
+  int lds_bitmap_words;     // > 0: per-workgroup LDS pre-filter of this many words
+};
+void launch_count_distinct(const ScanParams& p, const SlotArrays& s, const DistinctLaunch& d,
+                           int blocks, hipStream_t st);
+
+// sorted_count_distinct: per-wave contiguous chunks, ordered monoid per slot
+struct ScdLaunch {
+  int vcol;
+  int waves;                         // number of row chunks (one wave each)
+  int64_t chunk_rows;                // rows per chunk (multiple of 64)
+  int lds_state;                     // 1: per-wave state staged in LDS
+  uint32_t* st_first_row;            // [waves][nslots]   (kNoRow = absent)
+  unsigned long long* st_first;      // [waves][nslots]   first value bits
+  unsigned long long* st_last;       // [waves][nslots]
+  uint32_t* st_changes;              // [waves][nslots]
+  unsigned long long* out_changes;   // [nslots]
+  unsigned long long* out_first;     // [nslots]
+};
+void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st);
+
+// emit: occupied slots -> first-appearance order -> finalised output columns
+void launch_compact(const SlotArrays& s, uint64_t nslots, uint32_t* list_fst,
+                    uint32_t* list_slot, unsigned int* count, unsigned long long* total,
+                    hipStream_t st);
+void launch_sort_small(uint32_t* list_fst, uint32_t* list_slot, unsigned int n,
+                       uint32_t* order, hipStream_t st);
+void launch_rank_bitmap(const uint32_t* list_fst, const uint32_t* list_slot, unsigned int n,
+                        int64_t nrows, unsigned int* bitmap, unsigned int* word_prefix,
+                        unsigned int* block_prefix, uint32_t* order, hipStream_t st);
+void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order,
+                 unsigned int n, int nsum, uint64_t nslots, hipStream_t st);
+
+// column statistics (min / max / nan) of one column
+void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, hipStream_t st);
+
+// where_terms -> uint8 mask column, passing-row count
+void launch_where(const ScanParams& p, unsigned char* out_mask, unsigned long long* npass,
+                  int blocks, hipStream_t st);
+// is_in_ordered_subgroups
+void launch_expand_subgroups(const DevCol& basket, const unsigned char* mask,
+                             unsigned char* out, int64_t nrows, int blocks,
+                             unsigned int* run_any_scratch, hipStream_t st);
+// aggregate=False row selection: per-tile pass counts, then ordered compaction
+void launch_select_count(const unsigned char* mask, int64_t nrows, unsigned int* tile_counts,
+                         hipStream_t st);
+void launch_select_scan(unsigned int* tile_counts, int64_t ntiles, hipStream_t st);
+void launch_select_gather(const unsigned char* mask, int64_t nrows,
+                          const unsigned int* tile_offsets, const DevCol* cols, int ncols,
+                          void* const* outs, hipStream_t st);
+
+int device_cu_count();
+
+}  // namespace bqg

@@ -1,0 +1,277 @@
+"""Device contexts and device-resident shard tables over libbqgpu.
+
+``ShardTable`` is the GPU analogue of the ``bquery.ctable`` a bqueryd worker opens per shard
+(``bqueryd/worker.py:291``): its columns live in HBM, and ``groupby`` / ``where`` /
+``select_rows`` / ``expand_subgroups`` run the gfx950 kernels of libbqgpu.  All results come
+back as numpy arrays in bquery's group order (first appearance among the passing rows).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from collections import OrderedDict
+
+import numpy as np
+
+from . import _lib as L
+from .terms import normalize, parse_agg_list, parse_terms
+
+
+class Device:
+    """One libbqgpu context (one per GPU per host thread)."""
+
+    def __init__(self, ordinal=0):
+        self._lib = L.lib()
+        h = ctypes.c_void_p()
+        L.check(self._lib.bqg_create(int(ordinal), ctypes.byref(h)), None)
+        self.handle = h
+        self.ordinal = int(ordinal)
+
+    def close(self):
+        if self.handle:
+            self._lib.bqg_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc):
+        L.check(rc, self.handle)
+
+    def set_stream(self, stream_ptr):
+        self.check(self._lib.bqg_set_stream(self.handle, ctypes.c_void_p(stream_ptr or 0)))
+
+    def synchronize(self):
+        self.check(self._lib.bqg_synchronize(self.handle))
+
+    def enable_timing(self, on=True):
+        self.check(self._lib.bqg_enable_timing(self.handle, 1 if on else 0))
+
+    def last_timing(self):
+        t = L.Timing()
+        self.check(self._lib.bqg_last_timing(self.handle, ctypes.byref(t)))
+        return {'scan_ms': t.scan_ms, 'scan_launches': t.scan_launches, 'total_ms': t.total_ms,
+                'rows': t.rows, 'bytes': t.bytes, 'mode': t.mode}
+
+
+_devices = {}
+
+
+def device_count():
+    n = ctypes.c_int()
+    L.check(L.lib().bqg_device_count(ctypes.byref(n)), None)
+    return n.value
+
+
+def get_device(ordinal=None):
+    """Process-wide cached context; ``BQGPU_DEVICE`` selects the default GPU."""
+    if ordinal is None:
+        ordinal = int(os.environ.get('BQGPU_DEVICE', '0'))
+    dev = _devices.get(ordinal)
+    if dev is None:
+        dev = _devices[ordinal] = Device(ordinal)
+    return dev
+
+
+def _result_to_columns(dev, res_handle, names):
+    view = L.ResultView()
+    dev.check(L.lib().bqg_result_view_get(res_handle, ctypes.byref(view)))
+    try:
+        n = view.n_rows
+        out = OrderedDict()
+        for j, name in enumerate(names):
+            dt = L.DTYPES[view.dtypes[j]]
+            nbytes = n * dt.itemsize
+            buf = ctypes.string_at(view.cols[j], nbytes) if nbytes else b''
+            out[name] = np.frombuffer(buf, dtype=dt).copy()
+        return out, bool(view.filtered)
+    finally:
+        L.lib().bqg_result_free(res_handle)
+
+
+class ShardTable:
+    """Device-resident columns of one shard."""
+
+    def __init__(self, columns, device=None):
+        """``columns``: mapping name -> 1-D numpy array (all the same length)."""
+        self.dev = device or get_device()
+        self._lib = L.lib()
+        names = list(columns.keys())
+        arrays = [np.ascontiguousarray(columns[n]) for n in names]
+        n = len(arrays[0]) if arrays else 0
+        for a in arrays:
+            if a.ndim != 1 or len(a) != n:
+                raise ValueError('all columns must be 1-D arrays of the same length')
+            if a.dtype not in L.DTYPE_CODE:
+                raise NotImplementedError('column dtype %s is not supported on the GPU' % a.dtype)
+        codes = (ctypes.c_int32 * max(1, len(arrays)))(*[L.DTYPE_CODE[a.dtype] for a in arrays])
+        h = ctypes.c_void_p()
+        self.dev.check(self._lib.bqg_table_create(self.dev.handle, n, len(arrays), codes,
+                                                  ctypes.byref(h)))
+        self.handle = h
+        self.nrows = n
+        self.names = names
+        self.dtypes = OrderedDict((nm, a.dtype) for nm, a in zip(names, arrays))
+        self._slot = {nm: i for i, nm in enumerate(names)}
+        self._scratch = []
+        for i, a in enumerate(arrays):
+            self.push(i, a)
+        self.sync()
+
+    # ---- lifecycle
+    def close(self):
+        if getattr(self, 'handle', None):
+            self._lib.bqg_table_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return self.nrows
+
+    # ---- data movement
+    def slot(self, name):
+        if isinstance(name, int):
+            return name
+        if name not in self._slot:
+            raise KeyError(str(name))
+        return self._slot[name]
+
+    def push(self, col, array, row_offset=0):
+        a = np.ascontiguousarray(array)
+        self.dev.check(self._lib.bqg_push_chunk(self.handle, self.slot(col), a.ctypes.data,
+                                                len(a), int(row_offset)))
+
+    def sync(self):
+        self.dev.check(self._lib.bqg_table_sync(self.handle))
+
+    def add_column(self, name, dtype):
+        s = ctypes.c_int32()
+        self.dev.check(self._lib.bqg_table_add_column(self.handle, L.DTYPE_CODE[np.dtype(dtype)],
+                                                      ctypes.byref(s)))
+        self._slot[name] = s.value
+        self.dtypes[name] = np.dtype(dtype)
+        return s.value
+
+    def scratch_mask(self):
+        """A fresh device BOOL column for masks (reused across calls)."""
+        name = '__mask_%d__' % len(self._scratch)
+        s = self.add_column(name, np.bool_)
+        self._scratch.append(name)
+        return name
+
+    def read(self, col):
+        s = self.slot(col)
+        dt = self.dtypes[self.names[s]] if s < len(self.names) else None
+        if dt is None:
+            for k, v in self._slot.items():
+                if v == s:
+                    dt = self.dtypes[k]
+        out = np.empty(self.nrows, dtype=dt)
+        self.dev.check(self._lib.bqg_table_read(self.handle, s, out.ctypes.data, self.nrows, 0))
+        return out
+
+    def stats(self, col):
+        imin, imax = ctypes.c_int64(), ctypes.c_int64()
+        fmin, fmax = ctypes.c_double(), ctypes.c_double()
+        nan = ctypes.c_int32()
+        self.dev.check(self._lib.bqg_table_stats(self.handle, self.slot(col), ctypes.byref(imin),
+                                                 ctypes.byref(imax), ctypes.byref(fmin),
+                                                 ctypes.byref(fmax), ctypes.byref(nan)))
+        dt = self.dtypes[col] if not isinstance(col, int) else None
+        empty = nan.value < 0
+        if dt is not None and dt.kind == 'f':
+            return {'min': fmin.value, 'max': fmax.value, 'has_nan': nan.value > 0, 'empty': empty}
+        if dt is not None and dt == np.uint64:
+            return {'min': imin.value & 0xFFFFFFFFFFFFFFFF, 'max': imax.value & 0xFFFFFFFFFFFFFFFF,
+                    'has_nan': False, 'empty': empty}
+        return {'min': imin.value, 'max': imax.value, 'has_nan': False, 'empty': empty}
+
+    # ---- query construction
+    def _terms(self, term_list, keep):
+        parsed = parse_terms(self.dtypes, term_list)
+        arr = (L.Term * max(1, len(parsed)))()
+        for i, (col, code, value) in enumerate(parsed):
+            dt = self.dtypes[col]
+            op, ivals, fvals = normalize(dt, code, value)
+            if dt == np.uint64:
+                iv = np.array([v & 0xFFFFFFFFFFFFFFFF for v in ivals] or [0], np.uint64).view(np.int64)
+            else:
+                iv = np.array(ivals or [0], np.int64)
+            fv = np.array(fvals or [0.0], np.float64)
+            keep += [iv, fv]
+            arr[i] = L.Term(self.slot(col), op, max(len(ivals), len(fvals)), iv.ctypes.data,
+                            fv.ctypes.data)
+        return arr, len(parsed)
+
+    def _query(self, groupby_cols, aggs, term_list, mask, keep):
+        keys = np.array([self.slot(c) for c in groupby_cols] or [0], np.int32)
+        keep.append(keys)
+        terms, nt = self._terms(term_list or [], keep)
+        keep.append(terms)
+        agg_arr = (L.Agg * max(1, len(aggs)))(*[L.Agg(self.slot(c), L.AGG_CODE[op])
+                                                for c, op in aggs])
+        keep.append(agg_arr)
+        q = L.Query(len(groupby_cols), keys.ctypes.data, nt, ctypes.addressof(terms),
+                    -1 if mask is None else self.slot(mask), len(aggs), ctypes.addressof(agg_arr))
+        return q
+
+    # ---- calc path
+    def where(self, term_list, out_mask=None):
+        """Evaluate where-terms into a device BOOL column; returns (mask name, passing rows)."""
+        keep = []
+        terms, nt = self._terms(term_list, keep)
+        if out_mask is None:
+            out_mask = self.scratch_mask()
+        npass = ctypes.c_int64()
+        self.dev.check(self._lib.bqg_where(self.dev.handle, self.handle, nt,
+                                           ctypes.addressof(terms), self.slot(out_mask),
+                                           ctypes.byref(npass)))
+        return out_mask, npass.value
+
+    def expand_subgroups(self, basket_col, mask, out_mask=None):
+        if out_mask is None:
+            out_mask = self.scratch_mask()
+        self.dev.check(self._lib.bqg_expand_subgroups(self.dev.handle, self.handle,
+                                                      self.slot(basket_col), self.slot(mask),
+                                                      self.slot(out_mask)))
+        return out_mask
+
+    def groupby(self, groupby_cols, agg_list, where_terms=None, mask=None):
+        """bquery ``ctable.groupby`` semantics; returns (OrderedDict of columns, filtered)."""
+        groupby_cols = list(groupby_cols)
+        for c in groupby_cols:
+            self.slot(c)
+        ops = parse_agg_list(self.dtypes, agg_list)
+        names = groupby_cols + [o[1] for o in ops]
+        if len(set(names)) != len(names):
+            raise ValueError('duplicate output column names: %s' % names)
+        keep = []
+        q = self._query(groupby_cols, [(o[0], o[2]) for o in ops], where_terms, mask, keep)
+        res = ctypes.c_void_p()
+        self.dev.check(self._lib.bqg_groupby(self.dev.handle, self.handle, ctypes.byref(q),
+                                             ctypes.byref(res)))
+        out, filtered = _result_to_columns(self.dev, res, names)
+        for (in_col, out_col, op, dt) in ops:
+            if out[out_col].dtype != dt:
+                out[out_col] = out[out_col].astype(dt)
+        return out, filtered
+
+    def select_rows(self, cols, where_terms=None, mask=None):
+        """aggregate=False: the passing rows of ``cols`` in row order."""
+        cols = list(cols)
+        keep = []
+        q = self._query([], [], where_terms, mask, keep)
+        sel = np.array([self.slot(c) for c in cols] or [0], np.int32)
+        res = ctypes.c_void_p()
+        self.dev.check(self._lib.bqg_select_rows(self.dev.handle, self.handle, ctypes.byref(q),
+                                                 len(cols), sel.ctypes.data, ctypes.byref(res)))
+        out, _ = _result_to_columns(self.dev, res, cols)
+        return out

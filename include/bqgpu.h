@@ -1,0 +1,177 @@
+/*
+ * bqgpu.h -- C ABI of libbqgpu, the MI355X (gfx950) shard-groupby engine.
+ *
+ * This is the drop-in boundary for bqueryd's per-shard calc path.  It replaces the block
+ * of WorkerNode.handle_work that calls bquery (bqueryd/worker.py:291-323):
+ *
+ *   worker.py:291  ct = bquery.ctable(rootdir, mode='r', auto_cache=True)
+ *                    -> bqg_table_create + bqg_push_chunk (+ bqg_table_sync)
+ *   worker.py:298  ct.where_terms_factorization_check(terms)
+ *                    -> host layer (bqueryd_amd/ctable.py) over the <col>.values caches
+ *   worker.py:303  bool_arr = ct.where_terms(terms, cache=True)
+ *                    -> bqg_where (device mask column) -- or fused into bqg_groupby
+ *   worker.py:307  ct.is_in_ordered_subgroups(basket_col, bool_arr)
+ *                    -> bqg_expand_subgroups
+ *   worker.py:313  ct.groupby(groupby_cols, agg_list, bool_arr=bool_arr, rootdir=tmp_dir)
+ *                    -> bqg_groupby
+ *   worker.py:319  bcolz.fromiter(ct[cols].where(bool_arr), ...)   (aggregate=False)
+ *                    -> bqg_select_rows
+ * and the co-located cross-shard merge that the client does at bqueryd/rpc.py:164-173
+ * ("we can only sum now") -> bqg_partition_result / bqg_merge_partials.
+ *
+ * Conventions
+ *  - Every function returns 0 on success and a negative BQG_E_* code on failure; the
+ *    message is available from bqg_last_error(ctx) (per-context; ctx may be NULL for
+ *    errors raised before a context exists).  The Python layer turns it into
+ *    RuntimeError / KeyError / NotImplementedError so that the worker's ErrorMessage path
+ *    (worker.py:171-176) is unchanged.
+ *  - One context per device per host thread; a context is not re-entrant.
+ *  - Host buffers passed to bqg_push_chunk are owned by the caller and may be reused as
+ *    soon as the call returns (the library stages them through its own pinned buffers).
+ *  - Result memory (bqg_result) is owned by the library until bqg_result_free.
+ *  - Row counts of one table must be < 2^32 (row indices are carried as uint32 on device).
+ */
+#ifndef BQGPU_H
+#define BQGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BQG_ABI_VERSION 1
+
+/* error codes */
+#define BQG_OK 0
+#define BQG_E_INVALID (-1)      /* bad argument / unknown column (KeyError/ValueError) */
+#define BQG_E_UNSUPPORTED (-2)  /* query shape not supported (NotImplementedError) */
+#define BQG_E_HIP (-3)          /* HIP runtime error */
+#define BQG_E_OOM (-4)          /* device or pinned allocation failed */
+#define BQG_E_STATE (-5)        /* call out of sequence */
+
+/* column dtypes (numpy kinds: ?, i1, i2, i4, i8, u1, u2, u4, u8, f4, f8) */
+enum bqg_dtype {
+  BQG_BOOL = 0, BQG_I8, BQG_I16, BQG_I32, BQG_I64,
+  BQG_U8, BQG_U16, BQG_U32, BQG_U64, BQG_F32, BQG_F64
+};
+
+/* aggregation ops, as accepted by bquery's create_agg_ctable */
+enum bqg_agg_op {
+  BQG_SUM = 0, BQG_COUNT, BQG_COUNT_DISTINCT, BQG_SORTED_COUNT_DISTINCT, BQG_MEAN, BQG_STD
+};
+
+/* where-term ops: bquery's codes 1..8 (==, !=, in, nin, >, >=, <, <=) plus two folded
+ * constants produced by the host normaliser (e.g. int_col == 2.5 -> BQG_T_FALSE) */
+enum bqg_term_op {
+  BQG_T_FALSE = -1, BQG_T_TRUE = 0,
+  BQG_T_EQ = 1, BQG_T_NE, BQG_T_IN, BQG_T_NIN, BQG_T_GT, BQG_T_GE, BQG_T_LT, BQG_T_LE
+};
+
+typedef struct bqg_ctx bqg_ctx;
+typedef struct bqg_table bqg_table;
+typedef struct bqg_result bqg_result;
+
+/* One normalised where-term.  Integer/bool columns compare against ivals (uint64 columns:
+ * the bit pattern), float columns against fvals (after promotion to float64).  For
+ * IN/NIN the value list must be sorted ascending and duplicate-free. */
+typedef struct {
+  int32_t col;
+  int32_t op;
+  int64_t nvals;
+  const int64_t* ivals;
+  const double* fvals;
+} bqg_term;
+
+typedef struct {
+  int32_t col;  /* input column */
+  int32_t op;   /* enum bqg_agg_op */
+} bqg_agg;
+
+typedef struct {
+  int32_t n_keys;
+  const int32_t* key_cols;  /* groupby_col_list, in order */
+  int32_t n_terms;
+  const bqg_term* terms;    /* where_terms_list, AND-ed */
+  int32_t mask_col;         /* -1, or a BOOL column holding a precomputed bool_arr */
+  int32_t n_aggs;
+  const bqg_agg* aggs;      /* aggregation_list, in order */
+} bqg_query;
+
+/* Read-only view of a result.  Columns: groupby keys (input dtypes) then one column per
+ * aggregation (dtype per create_agg_ctable: sum keeps the input dtype, count /
+ * count_distinct / sorted_count_distinct are int64, mean / std are float64).  Groups are
+ * in first-appearance order of the passing rows, exactly as bquery emits them. */
+typedef struct {
+  int64_t n_rows;
+  int32_t n_cols;
+  const int32_t* dtypes;
+  const void* const* cols;  /* host pointers, n_rows elements each */
+  int32_t filtered;         /* 1 when the filter removed at least one row */
+} bqg_result_view;
+
+/* Per-query device timing of the dominant scan kernel (HIP events on the library stream). */
+typedef struct {
+  double scan_ms;        /* summed duration of the row-scan kernel launches of the last call */
+  int32_t scan_launches;
+  double total_ms;       /* all device work of the last call */
+  int64_t rows;          /* input rows scanned */
+  int64_t bytes;         /* algorithmic bytes: distinct input columns x itemsize x rows + output */
+  int32_t mode;          /* 0 private-LDS, 1 shared-LDS, 2 global dense, 3 global hash */
+} bqg_timing;
+
+/* ---------------- lifecycle ---------------- */
+int bqg_abi_version(void);
+int bqg_device_count(int* n);
+int bqg_create(int device_ordinal, bqg_ctx** out);
+int bqg_destroy(bqg_ctx* ctx);
+const char* bqg_last_error(bqg_ctx* ctx);
+/* Run library work on an external HIP stream (e.g. torch's current stream); NULL restores
+ * the library's own stream. */
+int bqg_set_stream(bqg_ctx* ctx, void* hip_stream);
+int bqg_synchronize(bqg_ctx* ctx);
+int bqg_enable_timing(bqg_ctx* ctx, int on);
+int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
+
+/* ---------------- pinned host memory ---------------- */
+int bqg_alloc_pinned(bqg_ctx* ctx, size_t bytes, void** out);
+int bqg_free_pinned(bqg_ctx* ctx, void* p);
+
+/* ---------------- device-resident shard tables ---------------- */
+int bqg_table_create(bqg_ctx* ctx, int64_t nrows, int32_t ncols, const int32_t* dtypes,
+                     bqg_table** out);
+int bqg_table_destroy(bqg_table* t);
+int bqg_table_add_column(bqg_table* t, int32_t dtype, int32_t* slot_out);
+/* Copy rows [row_offset, row_offset + nrows) of column `col` from host memory. */
+int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows,
+                   int64_t row_offset);
+/* Wait for pushes and compute per-column statistics (min / max / has_nan). */
+int bqg_table_sync(bqg_table* t);
+int bqg_table_column_ptr(bqg_table* t, int32_t col, void** dev_ptr);
+int bqg_table_stats(bqg_table* t, int32_t col, int64_t* imin, int64_t* imax, double* fmin,
+                    double* fmax, int32_t* has_nan);
+/* Copy rows of a device column back to host memory. */
+int bqg_table_read(bqg_table* t, int32_t col, void* host, int64_t nrows, int64_t row_offset);
+
+/* ---------------- calc path ---------------- */
+/* where_terms: AND of the terms -> BOOL column `out_mask_col` (device); *n_pass receives the
+ * number of passing rows.  (worker.py:303) */
+int bqg_where(bqg_ctx* ctx, bqg_table* t, int32_t n_terms, const bqg_term* terms,
+              int32_t out_mask_col, int64_t* n_pass);
+/* is_in_ordered_subgroups: widen mask to whole runs of equal basket values that contain a
+ * passing row.  (worker.py:306-307) */
+int bqg_expand_subgroups(bqg_ctx* ctx, bqg_table* t, int32_t basket_col, int32_t mask_col,
+                         int32_t out_mask_col);
+/* groupby with the predicate fused into the scan.  (worker.py:313-314) */
+int bqg_groupby(bqg_ctx* ctx, bqg_table* t, const bqg_query* q, bqg_result** out);
+/* aggregate=False: the passing rows of `cols`, in row order.  (worker.py:316-323) */
+int bqg_select_rows(bqg_ctx* ctx, bqg_table* t, const bqg_query* q, int32_t n_cols,
+                    const int32_t* cols, bqg_result** out);
+int bqg_result_view_get(bqg_result* r, bqg_result_view* out);
+int bqg_result_free(bqg_result* r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BQGPU_H */

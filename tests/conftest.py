@@ -1,0 +1,26 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (runs libbqgpu kernels)')
+    config.addinivalue_line('markers', 'slow: full-size (BASELINE) parity runs')
+
+
+@pytest.fixture(scope='session')
+def oracle_c():
+    from oracle import cbquery
+    cbquery.build()
+    return cbquery
+
+
+@pytest.fixture(scope='session')
+def gpu_device():
+    from bqueryd_amd.engine import get_device
+    return get_device()
