@@ -421,7 +421,8 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     pl.p.hash = 0;
     const size_t per_slot_private = 8 + 8 * (size_t)pl.nsum;  // bytes per lane per slot
     const size_t per_slot_shared = 8 + 8 * (size_t)pl.nsum;
-    if (pl.nslots * per_slot_private * kBlock <= 80 * 1024) pl.mode = kPrivate;
+    if (pl.nslots <= (uint64_t)kMaxPrivateSlots && pl.nslots * per_slot_private * kBlock <= 80 * 1024)
+      pl.mode = kPrivate;
     else if (pl.nslots * per_slot_shared <= 64 * 1024) pl.mode = kShared;
     else pl.mode = kGlobalDense;
   }
@@ -568,26 +569,29 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     L.blocks = scan_blocks(c, N, per_cu);
     L.lds_bytes = lds;
     L.partials = (unsigned long long*)c->partials.ensure((size_t)(2 + nsum) * L.blocks * S * 8);
-    if (!c->counter.p) {
-      c->counter.ensure(256);
-      HIPCHECK(hipMemsetAsync(c->counter.p, 0, 256, st));
-    }
-    L.done_counter = (unsigned int*)c->counter.p;
-    L.out_hdr = (unsigned long long*)c->hdr.ensure(64);
-    L.emit_inline = need_generic ? 0 : 1;
-    if (L.emit_inline) {
+    FinishParams F{};
+    F.nslots = (int)S;
+    F.blocks = L.blocks;
+    F.nsum = nsum;
+    for (int i = 0; i < kMaxSums; ++i) F.sum_is_float[i] = pl.p.sum_is_float[i];
+    F.partials = L.partials;
+    F.out_hdr = (unsigned long long*)c->hdr.ensure(64);
+    F.emit_inline = need_generic ? 0 : 1;
+    if (F.emit_inline) {
       unsigned char* ob = (unsigned char*)c->outcols.ensure((size_t)e.ncols * S * 8 + 256);
       for (int j = 0; j < e.ncols; ++j) e.cols[j].out = ob + (size_t)j * S * 8;
     }
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
-    launch_scan_private(pl.p, sa, L, e, st);
+    launch_scan_private(pl.p, L, st);
     HIPCHECK(hipGetLastError());
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));
+    launch_private_finish(F, sa, e, st);
+    HIPCHECK(hipGetLastError());
     if (!need_generic) {
       // one D2H of header + columns
       const size_t colbytes = (size_t)e.ncols * S * 8;
       unsigned char* h = (unsigned char*)c->hout.ensure(colbytes + 64);
-      HIPCHECK(hipMemcpyAsync(h, L.out_hdr, 16, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipMemcpyAsync(h, F.out_hdr, 16, hipMemcpyDeviceToHost, st));
       if (colbytes) HIPCHECK(hipMemcpyAsync(h + 64, c->outcols.p, colbytes, hipMemcpyDeviceToHost, st));
       if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
       HIPCHECK(hipStreamSynchronize(st));
@@ -691,10 +695,16 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.blocks = scan_blocks(c, N, std::max(per_cu, 1));
       L.lds_bytes = lds;
       L.partials = (unsigned long long*)c->partials.ensure((size_t)(2 + nsum2) * L.blocks * S * 8);
-      L.done_counter = (unsigned int*)c->counter.p;
-      L.out_hdr = (unsigned long long*)c->hdr.ensure(64);
-      L.emit_inline = 0;
-      launch_scan_private(q2, sa2, L, e, st);
+      FinishParams F{};
+      F.nslots = (int)S;
+      F.blocks = L.blocks;
+      F.nsum = nsum2;
+      for (int i = 0; i < kMaxSums; ++i) F.sum_is_float[i] = q2.sum_is_float[i];
+      F.partials = L.partials;
+      F.out_hdr = (unsigned long long*)c->hdr.ensure(64);
+      F.emit_inline = 0;
+      launch_scan_private(q2, L, st);
+      launch_private_finish(F, sa2, e, st);
     } else {
       sa2.keys = nullptr;  // keep the hash table built by pass 1: init only the accumulators
       launch_init_slots(sa2, nsum2, S, st);

@@ -162,84 +162,6 @@ __device__ __forceinline__ uint64_t chunk_bits(const Chunk& c, int dt, int r) {
   return (uint64_t)chunk_i64(c, dt, r);
 }
 
-// where-term on one 4-row chunk -> 4-bit pass mask
-__device__ __forceinline__ bool term_cmp_i(int op, int64_t x, int64_t v, bool uns) {
-  if (uns) {
-    const uint64_t a = (uint64_t)x, b = (uint64_t)v;
-    switch (op) {
-      case BQG_T_EQ: return a == b; case BQG_T_NE: return a != b;
-      case BQG_T_GT: return a > b; case BQG_T_GE: return a >= b;
-      case BQG_T_LT: return a < b; default: return a <= b;
-    }
-  }
-  switch (op) {
-    case BQG_T_EQ: return x == v; case BQG_T_NE: return x != v;
-    case BQG_T_GT: return x > v; case BQG_T_GE: return x >= v;
-    case BQG_T_LT: return x < v; default: return x <= v;
-  }
-}
-__device__ __forceinline__ bool term_cmp_f(int op, double x, double v) {
-  switch (op) {
-    case BQG_T_EQ: return x == v; case BQG_T_NE: return x != v;
-    case BQG_T_GT: return x > v; case BQG_T_GE: return x >= v;
-    case BQG_T_LT: return x < v; default: return x <= v;
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ bool sorted_contains(const T* vals, int n, T x) {
-  if (n <= 8) {
-    bool hit = false;
-    for (int i = 0; i < n; ++i) hit |= (vals[i] == x);
-    return hit;
-  }
-  int lo = 0, hi = n - 1;
-  while (lo <= hi) {
-    const int mid = (lo + hi) >> 1;
-    const T m = vals[mid];
-    if (m == x) return true;
-    if (m < x) lo = mid + 1; else hi = mid - 1;
-  }
-  return false;
-}
-
-__device__ __forceinline__ uint32_t eval_term(const DevTerm& t, const Chunk& c, int dt) {
-  if (t.op == BQG_T_TRUE) return 0xF;
-  if (t.op == BQG_T_FALSE) return 0;
-  uint32_t m = 0;
-  if (t.is_float) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const double x = chunk_f64(c, dt, r);
-      bool hit;
-      if (t.op == BQG_T_IN || t.op == BQG_T_NIN) {
-        hit = sorted_contains<double>(t.fvals, t.nvals, x);
-        if (t.op == BQG_T_NIN) hit = !hit;
-      } else {
-        hit = term_cmp_f(t.op, x, t.fv0);
-      }
-      m |= (uint32_t)hit << r;
-    }
-  } else {
-    const bool uns = (dt == BQG_U64);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t x = chunk_i64(c, dt, r);
-      bool hit;
-      if (t.op == BQG_T_IN || t.op == BQG_T_NIN) {
-        hit = uns ? sorted_contains<uint64_t>(reinterpret_cast<const uint64_t*>(t.ivals), t.nvals,
-                                              (uint64_t)x)
-                  : sorted_contains<int64_t>(t.ivals, t.nvals, x);
-        if (t.op == BQG_T_NIN) hit = !hit;
-      } else {
-        hit = term_cmp_i(t.op, x, t.iv0, uns);
-      }
-      m |= (uint32_t)hit << r;
-    }
-  }
-  return m;
-}
-
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
   x ^= x >> 33;

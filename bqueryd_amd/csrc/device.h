@@ -1,4 +1,9 @@
 // device.h -- device-side building blocks shared by the libbqgpu kernel translation units.
+//
+// Row prologue ("decode once"): every column of a 4-row chunk is loaded with one vector
+// load, then decoded ONCE into canonical 64-bit values -- two's-complement int64 for integer
+// and bool columns, the raw bits for uint64, IEEE double bits for float32/float64.  Terms,
+// key coding and aggregation then work on those values without further dtype dispatch.
 #pragma once
 
 #include "kernels.h"
@@ -27,8 +32,15 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 __device__ __forceinline__ double as_f64(unsigned long long u) { return __longlong_as_double((long long)u); }
 __device__ __forceinline__ unsigned long long as_u64(double d) { return (unsigned long long)__double_as_longlong(d); }
 
+// canonical identity of a double (khash equality: NaN == NaN, -0.0 == +0.0)
+__device__ __forceinline__ uint64_t canon_f64_bits(uint64_t bits) {
+  const double d = as_f64(bits);
+  if (d != d) return 0x7ff8000000000000ull;
+  return as_u64(d + 0.0);
+}
+
 // ------------------------------------------------------------------------------------
-// Row prologue: loads, where-terms, group code
+// loads and decode
 // ------------------------------------------------------------------------------------
 template <int NC>
 __device__ __forceinline__ void load_rows4(const ScanParams& p, int64_t row0, Chunk (&raw)[NC]) {
@@ -43,7 +55,8 @@ __device__ __forceinline__ void load_one(Chunk& c, const DevCol& col, int64_t ro
     case 2: c.a.x = reinterpret_cast<const uint32_t*>(col.ptr)[row]; break;
     default: {
       const uint2 t = reinterpret_cast<const uint2*>(col.ptr)[row];
-      c.a.x = t.x; c.a.y = t.y;
+      c.a.x = t.x;
+      c.a.y = t.y;
     }
   }
 }
@@ -54,33 +67,145 @@ __device__ __forceinline__ void load_rows1(const ScanParams& p, int64_t row, Chu
   for (int c = 0; c < NC; ++c) load_one(raw[c], p.cols[c], row);
 }
 
-// 4-bit (R = 4) or 1-bit (R = 1) pass mask of the rows starting at row0
+template <int R>
+__device__ __forceinline__ void decode(const Chunk& c, int dt, uint64_t (&v)[R]) {
+  switch (dt) {
+    case BQG_BOOL:
+    case BQG_U8:
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = (c.a.x >> (8 * r)) & 0xFFu;
+      break;
+    case BQG_I8:
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = (uint64_t)(int64_t)(int8_t)((c.a.x >> (8 * r)) & 0xFFu);
+      break;
+    case BQG_U16:
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = (chunk_u32(c, r >> 1) >> (16 * (r & 1))) & 0xFFFFu;
+      break;
+    case BQG_I16:
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        v[r] = (uint64_t)(int64_t)(int16_t)((chunk_u32(c, r >> 1) >> (16 * (r & 1))) & 0xFFFFu);
+      break;
+    case BQG_I32:
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = (uint64_t)(int64_t)(int32_t)chunk_u32(c, r);
+      break;
+    case BQG_U32:
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = chunk_u32(c, r);
+      break;
+    case BQG_F32:
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = as_u64((double)__uint_as_float(chunk_u32(c, r)));
+      break;
+    default:  // I64, U64, F64: raw 64-bit pattern
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = ((uint64_t)chunk_u32(c, 2 * r + 1) << 32) | chunk_u32(c, 2 * r);
+      break;
+  }
+}
+
 template <int NC, int R>
-__device__ __forceinline__ uint32_t rows_pass(const ScanParams& p, int64_t row0, const Chunk (&raw)[NC]) {
+__device__ __forceinline__ void decode_all(const ScanParams& p, const Chunk (&raw)[NC], uint64_t (&v)[NC][R]) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) decode<R>(raw[c], p.cols[c].dtype, v[c]);
+}
+
+// ------------------------------------------------------------------------------------
+// where-terms on canonical values
+// ------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ bool sorted_contains(const T* vals, int n, T x) {
+  if (n <= 8) {
+    bool hit = false;
+    for (int i = 0; i < n; ++i) hit |= (vals[i] == x);
+    return hit;
+  }
+  int lo = 0, hi = n - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    const T m = vals[mid];
+    if (m == x) return true;
+    if (m < x) lo = mid + 1;
+    else hi = mid - 1;
+  }
+  return false;
+}
+
+template <typename T>
+__device__ __forceinline__ bool cmp_op(int op, T x, T v) {
+  switch (op) {
+    case BQG_T_EQ: return x == v;
+    case BQG_T_NE: return x != v;
+    case BQG_T_GT: return x > v;
+    case BQG_T_GE: return x >= v;
+    case BQG_T_LT: return x < v;
+    default: return x <= v;
+  }
+}
+
+template <int R>
+__device__ __forceinline__ uint32_t eval_term(const DevTerm& t, const uint64_t (&v)[R], bool uns) {
+  const int op = t.op;
+  if (op == BQG_T_TRUE) return (1u << R) - 1u;
+  if (op == BQG_T_FALSE) return 0u;
+  uint32_t m = 0;
+  const bool list = (op == BQG_T_IN || op == BQG_T_NIN);
+  if (t.is_float) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double x = as_f64(v[r]);
+      bool hit = list ? (sorted_contains<double>(t.fvals, t.nvals, x) == (op == BQG_T_IN)) : cmp_op<double>(op, x, t.fv0);
+      m |= (uint32_t)hit << r;
+    }
+  } else if (uns) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      bool hit = list ? (sorted_contains<uint64_t>(reinterpret_cast<const uint64_t*>(t.ivals), t.nvals, v[r]) ==
+                         (op == BQG_T_IN))
+                      : cmp_op<uint64_t>(op, v[r], (uint64_t)t.iv0);
+      m |= (uint32_t)hit << r;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t x = (int64_t)v[r];
+      bool hit = list ? (sorted_contains<int64_t>(t.ivals, t.nvals, x) == (op == BQG_T_IN)) : cmp_op<int64_t>(op, x, t.iv0);
+      m |= (uint32_t)hit << r;
+    }
+  }
+  return m;
+}
+
+// R-bit pass mask of the rows starting at row0
+template <int NC, int R>
+__device__ __forceinline__ uint32_t vals_pass(const ScanParams& p, int64_t row0, const uint64_t (&v)[NC][R]) {
   const int64_t rem = p.nrows - row0;
   uint32_t pass = rem >= R ? ((1u << R) - 1u) : (rem > 0 ? ((1u << rem) - 1u) : 0u);
   for (int t = 0; t < p.nterms; ++t) {
     const DevTerm& tm = p.terms[t];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
-      if (tm.col == c) pass &= eval_term(tm, raw[c], p.cols[c].dtype);
+      if (tm.col == c) pass &= eval_term<R>(tm, v[c], p.cols[c].dtype == BQG_U64);
   }
   if (p.mask_col >= 0) {
 #pragma unroll
     for (int c = 0; c < NC; ++c)
       if (p.mask_col == c) {
-        const uint32_t w = raw[c].a.x;
         uint32_t m = 0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) m |= (((w >> (8 * r)) & 0xFFu) != 0u) ? (1u << r) : 0u;
+        for (int r = 0; r < R; ++r) m |= (v[c][r] != 0) ? (1u << r) : 0u;
         pass &= m;
       }
   }
   return pass;
 }
 
+// dense mixed-radix (or packed, hash mode) group code of each row
 template <int NC, int R>
-__device__ __forceinline__ void rows_code(const ScanParams& p, const Chunk (&raw)[NC], uint64_t (&code)[R]) {
+__device__ __forceinline__ void vals_code(const ScanParams& p, const uint64_t (&v)[NC][R], uint64_t (&code)[R]) {
 #pragma unroll
   for (int r = 0; r < R; ++r) code[r] = 0;
   for (int k = 0; k < p.nkeys; ++k) {
@@ -88,20 +213,19 @@ __device__ __forceinline__ void rows_code(const ScanParams& p, const Chunk (&raw
 #pragma unroll
     for (int c = 0; c < NC; ++c)
       if (key.col == c) {
-        const int dt = p.cols[c].dtype;
+        if (key.is_float) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const uint64_t v = key.is_float ? chunk_bits(raw[c], dt, r)
-                                          : (uint64_t)chunk_i64(raw[c], dt, r) - (uint64_t)key.min;
-          code[r] += v * key.stride;
+          for (int r = 0; r < R; ++r) code[r] += canon_f64_bits(v[c][r]) * key.stride;
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) code[r] += (v[c][r] - (uint64_t)key.min) * key.stride;
         }
       }
   }
 }
 
 // open-addressing hash of packed key codes -> table position (the slot)
-__device__ __forceinline__ uint64_t hash_slot(const SlotArrays& sa, uint64_t mask, uint64_t code,
-                                              bool insert) {
+__device__ __forceinline__ uint64_t hash_slot(const SlotArrays& sa, uint64_t mask, uint64_t code, bool insert) {
   uint64_t pos = mix64(code) & mask;
   for (uint64_t i = 0; i <= mask; ++i) {
     const unsigned long long k = sa.keys[pos];
@@ -123,7 +247,7 @@ __device__ __forceinline__ uint64_t hash_slot(const SlotArrays& sa, uint64_t mas
 }
 
 // ------------------------------------------------------------------------------------
-// Emit helpers (shared by the inline private emit and the generic emit kernel)
+// Emit helpers (shared by the private finish kernel and the generic emit kernel)
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ void store_elem(void* base, int dt, uint64_t idx, uint64_t bits) {
   switch (dtype_lg(dt)) {
@@ -141,8 +265,8 @@ struct SlotTotals {
   unsigned long long acc2[kMaxSums];  // centered second moments (std pass 2)
 };
 
-__device__ inline void emit_slot(const EmitParams& e, uint64_t slot, uint64_t code, unsigned int rank,
-                          const SlotTotals& t) {
+__device__ __forceinline__ void emit_slot(const EmitParams& e, uint64_t slot, uint64_t code, unsigned int rank,
+                                       const SlotTotals& t) {
   for (int j = 0; j < e.ncols; ++j) {
     const EmitCol& c = e.cols[j];
     uint64_t bits = 0;
@@ -159,17 +283,13 @@ __device__ inline void emit_slot(const EmitParams& e, uint64_t slot, uint64_t co
       switch (c.op) {
         case BQG_SUM: {
           const unsigned long long a = t.acc[c.state];
-          if (c.in_float) {
-            bits = (c.out_dtype == BQG_F32) ? (uint64_t)__float_as_uint((float)as_f64(a)) : a;
-          } else {
-            bits = a;  // wrap-around to the output width happens in store_elem
-          }
+          if (c.in_float) bits = (c.out_dtype == BQG_F32) ? (uint64_t)__float_as_uint((float)as_f64(a)) : a;
+          else bits = a;  // wrap-around to the output width happens in store_elem
         } break;
         case BQG_COUNT: bits = t.cnt; break;
         case BQG_MEAN: {
           const unsigned long long a = t.acc[c.state];
-          const double s = c.in_float ? as_f64(a)
-                                      : (c.in_dtype == BQG_U64 ? (double)(uint64_t)a : (double)(long long)a);
+          const double s = c.in_float ? as_f64(a) : (c.in_dtype == BQG_U64 ? (double)(uint64_t)a : (double)(long long)a);
           bits = as_u64(s / (double)t.cnt);
         } break;
         case BQG_STD: {
@@ -178,14 +298,12 @@ __device__ inline void emit_slot(const EmitParams& e, uint64_t slot, uint64_t co
         } break;
         case BQG_COUNT_DISTINCT: bits = e.cd[c.state][slot]; break;
         case BQG_SORTED_COUNT_DISTINCT: {
-          // literal bquery rule: the first processed row initialises slot 0 (counts 1 only when
-          // that row has label 0, i.e. row 0 passes); every other group's first value is
-          // compared with the zero-initialised last value.
+          // bquery rule: the first processed row initialises slot 0 (counts 1 only when that
+          // row has label 0, i.e. row 0 passes); every other group's first value is compared
+          // with the zero-initialised last value.
           unsigned long long ch = e.scd_changes[c.state][slot];
           const unsigned long long fv = e.scd_first[c.state][slot];
-          bool first_differs;
-          if (c.in_float) first_differs = !(as_f64(fv) == 0.0);
-          else first_differs = (fv != 0ull);
+          const bool first_differs = c.in_float ? !(as_f64(fv) == 0.0) : (fv != 0ull);
           if (rank == 0) ch += (t.fst == 0u) ? 1ull : 0ull;
           else ch += first_differs ? 1ull : 0ull;
           bits = ch;
@@ -196,15 +314,14 @@ __device__ inline void emit_slot(const EmitParams& e, uint64_t slot, uint64_t co
   }
 }
 
-
-#define BQG_DISPATCH_NC(NCV, ...)                                         \
-  switch (NCV) {                                                          \
-    case 1: { constexpr int NC = 1; __VA_ARGS__; } break;                \
-    case 2: { constexpr int NC = 2; __VA_ARGS__; } break;                \
-    case 3: { constexpr int NC = 3; __VA_ARGS__; } break;                \
-    case 4: { constexpr int NC = 4; __VA_ARGS__; } break;                \
-    case 5: { constexpr int NC = 5; __VA_ARGS__; } break;                \
-    default: { constexpr int NC = 6; __VA_ARGS__; } break;               \
+#define BQG_DISPATCH_NC(NCV, ...)                       \
+  switch (NCV) {                                        \
+    case 1: { constexpr int NC = 1; __VA_ARGS__; } break; \
+    case 2: { constexpr int NC = 2; __VA_ARGS__; } break; \
+    case 3: { constexpr int NC = 3; __VA_ARGS__; } break; \
+    case 4: { constexpr int NC = 4; __VA_ARGS__; } break; \
+    case 5: { constexpr int NC = 5; __VA_ARGS__; } break; \
+    default: { constexpr int NC = 6; __VA_ARGS__; } break; \
   }
 
 }  // namespace bqg

@@ -12,7 +12,7 @@ namespace bqg {
 // small (LDS pre-filter + HBM bitmap), else an open-addressing set of packed pairs.
 // ------------------------------------------------------------------------------------
 template <int NC, bool HASH>
-__global__ __launch_bounds__(kBlock) void k_count_distinct(ScanParams p, SlotArrays sa, DistinctLaunch d) {
+__global__ __launch_bounds__(kBlock, 4) void k_count_distinct(ScanParams p, SlotArrays sa, DistinctLaunch d) {
   extern __shared__ __align__(16) unsigned char smem[];
   unsigned int* lbits = reinterpret_cast<unsigned int*>(smem);
   const int tid = threadIdx.x;
@@ -24,9 +24,11 @@ __global__ __launch_bounds__(kBlock) void k_count_distinct(ScanParams p, SlotArr
     const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
     Chunk raw[NC];
     load_rows4<NC>(p, row0, raw);
-    const uint32_t pass = rows_pass<NC, 4>(p, row0, raw);
+    uint64_t v[NC][4];
+    decode_all<NC, 4>(p, raw, v);
+    const uint32_t pass = vals_pass<NC, 4>(p, row0, v);
     uint64_t code[4];
-    rows_code<NC, 4>(p, raw, code);
+    vals_code<NC, 4>(p, v, code);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (!(pass & (1u << r))) continue;
@@ -40,8 +42,7 @@ __global__ __launch_bounds__(kBlock) void k_count_distinct(ScanParams p, SlotArr
       for (int c = 0; c < NC; ++c)
         if (d.vcol == c) {
           const int dt = p.cols[c].dtype;
-          vcode = dtype_is_float(dt) ? chunk_bits(raw[c], dt, r)
-                                     : (uint64_t)chunk_i64(raw[c], dt, r) - (uint64_t)d.vmin;
+          vcode = dtype_is_float(dt) ? canon_f64_bits(v[c][r]) : v[c][r] - (uint64_t)d.vmin;
         }
       if (d.bitmap) {
         const uint64_t bit = s * d.vrange + vcode;
@@ -86,7 +87,7 @@ __device__ __forceinline__ bool scd_equal(uint64_t a, uint64_t b, bool isf) {
 }
 
 template <int NC, bool HASH>
-__global__ __launch_bounds__(kBlock) void k_scd(ScanParams p, SlotArrays sa, ScdLaunch d) {
+__global__ __launch_bounds__(kBlock, 4) void k_scd(ScanParams p, SlotArrays sa, ScdLaunch d) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = (int)p.nslots;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -127,9 +128,11 @@ __global__ __launch_bounds__(kBlock) void k_scd(ScanParams p, SlotArrays sa, Scd
     uint64_t slot = 0, vb = 0;
     if (row < end) {
       load_rows1<NC>(p, row, raw);
-      act = rows_pass<NC, 1>(p, row, raw) & 1u;
+      uint64_t v[NC][1];
+      decode_all<NC, 1>(p, raw, v);
+      act = vals_pass<NC, 1>(p, row, v) & 1u;
       uint64_t code[1];
-      rows_code<NC, 1>(p, raw, code);
+      vals_code<NC, 1>(p, v, code);
       slot = code[0];
       if (HASH && act) {
         slot = hash_slot(sa, hmask, code[0], false);
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void k_scd(ScanParams p, SlotArrays sa, Scd
       for (int c = 0; c < NC; ++c)
         if (vc == c) {
           const int dt = p.cols[c].dtype;
-          vb = isf ? as_u64(chunk_f64(raw[c], dt, 0)) : (uint64_t)chunk_i64(raw[c], dt, 0);
+          vb = v[c][0];
         }
     }
     uint64_t active = __ballot(act);

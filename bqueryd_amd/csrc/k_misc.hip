@@ -214,7 +214,9 @@ __global__ __launch_bounds__(kBlock) void k_where(ScanParams p, unsigned char* o
     if (row0 >= p.nrows) continue;
     Chunk raw[NC];
     load_rows4<NC>(p, row0, raw);
-    const uint32_t pass = rows_pass<NC, 4>(p, row0, raw);
+    uint64_t v[NC][4];
+    decode_all<NC, 4>(p, raw, v);
+    const uint32_t pass = vals_pass<NC, 4>(p, row0, v);
     const uint32_t bytes = (pass & 1u) | ((pass & 2u) << 7) | ((pass & 4u) << 14) | ((pass & 8u) << 21);
     *reinterpret_cast<uint32_t*>(out + row0) = bytes;  // mask buffer is padded
     cnt += (unsigned long long)__popc(pass);

@@ -1,4 +1,4 @@
-// k_scan_atomic.hip -- shared-LDS and global (dense / hashed) fused scans
+// k_scan_atomic.hip -- shared-LDS and global (dense / hashed) fused scans.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -7,11 +7,11 @@
 
 namespace bqg {
 
-// ------------------------------------------------------------------------------------
-// SHARED mode: one LDS table per workgroup with LDS atomics, flushed with global atomics.
-// ------------------------------------------------------------------------------------
+// SHARED mode: one LDS table per workgroup updated with LDS atomics (ds_add_u32/ds_min_u32/
+// ds_add_f64/ds_add_u64), flushed to the per-slot HBM arrays with device-scope atomics.
+// Used for mid-size dense slot spaces (e.g. config C4's 265 pickup locations).
 template <int NC>
-__global__ __launch_bounds__(kBlock) void k_scan_shared(ScanParams p, SlotArrays sa) {
+__global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArrays sa) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = (int)p.nslots;
   const int tid = threadIdx.x;
@@ -27,13 +27,18 @@ __global__ __launch_bounds__(kBlock) void k_scan_shared(ScanParams p, SlotArrays
   __syncthreads();
 
   const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  int64_t tile = blockIdx.x;
+  Chunk raw[NC];
+  if (tile < ntiles) load_rows4<NC>(p, tile * kTileRows + (int64_t)tid * kRowsPerThread, raw);
+  for (; tile < ntiles; tile += gridDim.x) {
     const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
-    Chunk raw[NC];
-    load_rows4<NC>(p, row0, raw);
-    const uint32_t pass = rows_pass<NC, 4>(p, row0, raw);
+    uint64_t v[NC][4];
+    decode_all<NC, 4>(p, raw, v);
+    const int64_t next = tile + gridDim.x;
+    if (next < ntiles) load_rows4<NC>(p, next * kTileRows + (int64_t)tid * kRowsPerThread, raw);
+    const uint32_t pass = vals_pass<NC, 4>(p, row0, v);
     uint64_t code[4];
-    rows_code<NC, 4>(p, raw, code);
+    vals_code<NC, 4>(p, v, code);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (pass & (1u << r)) {
@@ -42,17 +47,17 @@ __global__ __launch_bounds__(kBlock) void k_scan_shared(ScanParams p, SlotArrays
         atomicAdd(&cnt[s], 1u);
         if (fst[s] > row) atomicMin(&fst[s], row);
 #pragma unroll
-        for (int v = 0; v < (NC < kMaxSums ? NC : kMaxSums); ++v) {
-          if (v < nsum) {
-            if (p.sum_is_float[v]) {
-              double x = chunk_f64(raw[v], p.cols[v].dtype, r);
-              if (p.sum_centered[v]) {
-                const double d = x - p.centers[v][s];
+        for (int q = 0; q < (NC < kMaxSums ? NC : kMaxSums); ++q) {
+          if (q < nsum) {
+            if (p.sum_is_float[q]) {
+              double x = as_f64(v[q][r]);
+              if (p.sum_centered[q]) {
+                const double d = x - p.centers[q][s];
                 x = d * d;
               }
-              unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)v * S + s]), x);
+              unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * S + s]), x);
             } else {
-              atomicAdd(&acc[(size_t)v * S + s], (unsigned long long)chunk_i64(raw[v], p.cols[v].dtype, r));
+              atomicAdd(&acc[(size_t)q * S + s], (unsigned long long)v[q][r]);
             }
           }
         }
@@ -65,31 +70,34 @@ __global__ __launch_bounds__(kBlock) void k_scan_shared(ScanParams p, SlotArrays
     if (c == 0) continue;
     atomicAdd(&sa.cnt[s], (unsigned long long)c);
     atomicMin(&sa.fst[s], fst[s]);
-    for (int v = 0; v < nsum; ++v) {
-      const unsigned long long a = acc[(size_t)v * S + s];
-      if (p.sum_is_float[v]) unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)v * p.nslots + s]), as_f64(a));
-      else atomicAdd(&sa.acc[(size_t)v * p.nslots + s], a);
+    for (int q = 0; q < nsum; ++q) {
+      const unsigned long long a = acc[(size_t)q * S + s];
+      if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)q * p.nslots + s]), as_f64(a));
+      else atomicAdd(&sa.acc[(size_t)q * p.nslots + s], a);
     }
   }
 }
 
-// ------------------------------------------------------------------------------------
 // GLOBAL mode: per-slot arrays in HBM updated with device-scope atomics (large dense slot
-// spaces, and the hashed key mode).
-// ------------------------------------------------------------------------------------
+// spaces, and the hashed key mode where the slot is the hash-table position).
 template <int NC, bool HASH>
-__global__ __launch_bounds__(kBlock) void k_scan_global(ScanParams p, SlotArrays sa) {
+__global__ __launch_bounds__(kBlock, 4) void k_scan_global(ScanParams p, SlotArrays sa) {
   const int tid = threadIdx.x;
   const int nsum = p.nsum;
   const uint64_t hmask = p.nslots - 1;
   const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  int64_t tile = blockIdx.x;
+  Chunk raw[NC];
+  if (tile < ntiles) load_rows4<NC>(p, tile * kTileRows + (int64_t)tid * kRowsPerThread, raw);
+  for (; tile < ntiles; tile += gridDim.x) {
     const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
-    Chunk raw[NC];
-    load_rows4<NC>(p, row0, raw);
-    const uint32_t pass = rows_pass<NC, 4>(p, row0, raw);
+    uint64_t v[NC][4];
+    decode_all<NC, 4>(p, raw, v);
+    const int64_t next = tile + gridDim.x;
+    if (next < ntiles) load_rows4<NC>(p, next * kTileRows + (int64_t)tid * kRowsPerThread, raw);
+    const uint32_t pass = vals_pass<NC, 4>(p, row0, v);
     uint64_t code[4];
-    rows_code<NC, 4>(p, raw, code);
+    vals_code<NC, 4>(p, v, code);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (pass & (1u << r)) {
@@ -102,17 +110,17 @@ __global__ __launch_bounds__(kBlock) void k_scan_global(ScanParams p, SlotArrays
         atomicAdd(&sa.cnt[s], 1ull);
         if (sa.fst[s] > row) atomicMin(&sa.fst[s], row);
 #pragma unroll
-        for (int v = 0; v < (NC < kMaxSums ? NC : kMaxSums); ++v) {
-          if (v < nsum) {
-            if (p.sum_is_float[v]) {
-              double x = chunk_f64(raw[v], p.cols[v].dtype, r);
-              if (p.sum_centered[v]) {
-                const double d = x - p.centers[v][s];
+        for (int q = 0; q < (NC < kMaxSums ? NC : kMaxSums); ++q) {
+          if (q < nsum) {
+            if (p.sum_is_float[q]) {
+              double x = as_f64(v[q][r]);
+              if (p.sum_centered[q]) {
+                const double d = x - p.centers[q][s];
                 x = d * d;
               }
-              unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)v * p.nslots + s]), x);
+              unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)q * p.nslots + s]), x);
             } else {
-              atomicAdd(&sa.acc[(size_t)v * p.nslots + s], (unsigned long long)chunk_i64(raw[v], p.cols[v].dtype, r));
+              atomicAdd(&sa.acc[(size_t)q * p.nslots + s], (unsigned long long)v[q][r]);
             }
           }
         }
@@ -122,8 +130,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_global(ScanParams p, SlotArrays
 }
 
 __global__ void k_init_slots(SlotArrays sa, int nsum, uint64_t nslots) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots;
-       i += (uint64_t)gridDim.x * blockDim.x) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * blockDim.x) {
     sa.cnt[i] = 0;
     sa.fst[i] = kNoRow;
     for (int v = 0; v < nsum; ++v) sa.acc[(size_t)v * nslots + i] = 0;
@@ -134,6 +141,7 @@ __global__ void k_init_slots(SlotArrays sa, int nsum, uint64_t nslots) {
 void launch_scan_shared(const ScanParams& p, const SlotArrays& s, int blocks, size_t lds, hipStream_t st) {
   BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scan_shared<NC>), dim3(blocks), dim3(kBlock), lds, st, p, s));
 }
+
 void launch_scan_global(const ScanParams& p, const SlotArrays& s, int blocks, hipStream_t st) {
   if (p.hash) {
     BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scan_global<NC, true>), dim3(blocks), dim3(kBlock), 0, st, p, s));
@@ -141,10 +149,12 @@ void launch_scan_global(const ScanParams& p, const SlotArrays& s, int blocks, hi
     BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scan_global<NC, false>), dim3(blocks), dim3(kBlock), 0, st, p, s));
   }
 }
+
 void launch_init_slots(const SlotArrays& s, int nsum, uint64_t nslots, hipStream_t st) {
   uint64_t blocks = (nslots + kBlock - 1) / kBlock;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_init_slots, dim3((unsigned)blocks), dim3(kBlock), 0, st, s, nsum, nslots);
 }
+
 }  // namespace bqg

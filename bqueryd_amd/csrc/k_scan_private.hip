@@ -1,4 +1,5 @@
-// k_scan_private.hip -- private-LDS fused scan (hot path of the low-cardinality groupby)
+// k_scan_private.hip -- private-LDS fused scan: the hot path of the filtered
+// low-cardinality groupby (config C2: bqueryd/worker.py:303 + :313 in one pass).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -7,13 +8,13 @@
 
 namespace bqg {
 
-// ------------------------------------------------------------------------------------
-// PRIVATE mode: every lane owns a private accumulator row per slot in LDS ([slot][lane]
-// layout: conflict-free ds_read/ds_write, no atomics).  Used for small dense slot spaces
-// (the filtered low-cardinality groupby of config C2).
-// ------------------------------------------------------------------------------------
+// Every lane owns a private accumulator row per slot in LDS, laid out [slot][lane] so that
+// the per-row read-modify-writes are conflict-free ds_read/ds_write with no atomics.  Rows
+// of a lane are processed in increasing order, so its first write to a slot is that slot's
+// first row for the lane.  A workgroup streams tiles of 1024 rows (4 per lane, one 16-byte
+// load per 4-byte column) and prefetches the next tile while it aggregates the current one.
 template <int NC>
-__global__ __launch_bounds__(kBlock) void k_scan_private(ScanParams p, SlotArrays sa, PrivateLaunch L, EmitParams e) {
+__global__ __launch_bounds__(kBlock, 4) void k_scan_private(ScanParams p, PrivateLaunch L) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = (int)p.nslots;
   const int tid = threadIdx.x;
@@ -28,13 +29,18 @@ __global__ __launch_bounds__(kBlock) void k_scan_private(ScanParams p, SlotArray
   for (int i = 0; i < nsum * S; ++i) acc[i * kBlock + tid] = 0;
 
   const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  int64_t tile = blockIdx.x;
+  Chunk raw[NC];
+  if (tile < ntiles) load_rows4<NC>(p, tile * kTileRows + (int64_t)tid * kRowsPerThread, raw);
+  for (; tile < ntiles; tile += gridDim.x) {
     const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
-    Chunk raw[NC];
-    load_rows4<NC>(p, row0, raw);
-    const uint32_t pass = rows_pass<NC, 4>(p, row0, raw);
+    uint64_t v[NC][4];
+    decode_all<NC, 4>(p, raw, v);
+    const int64_t next = tile + gridDim.x;
+    if (next < ntiles) load_rows4<NC>(p, next * kTileRows + (int64_t)tid * kRowsPerThread, raw);
+    const uint32_t pass = vals_pass<NC, 4>(p, row0, v);
     uint64_t code[4];
-    rows_code<NC, 4>(p, raw, code);
+    vals_code<NC, 4>(p, v, code);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (pass & (1u << r)) {
@@ -43,18 +49,18 @@ __global__ __launch_bounds__(kBlock) void k_scan_private(ScanParams p, SlotArray
         if (c0 == 0) fst[idx] = (uint32_t)(row0 + r);
         cnt[idx] = c0 + 1;
 #pragma unroll
-        for (int v = 0; v < (NC < kMaxSums ? NC : kMaxSums); ++v) {
-          if (v < nsum) {
-            unsigned long long* a = &acc[(size_t)v * S * kBlock + idx];
-            if (p.sum_is_float[v]) {
-              double x = chunk_f64(raw[v], p.cols[v].dtype, r);
-              if (p.sum_centered[v]) {
-                const double d = x - p.centers[v][code[r]];
+        for (int s = 0; s < (NC < kMaxSums ? NC : kMaxSums); ++s) {
+          if (s < nsum) {
+            unsigned long long* a = &acc[(size_t)s * S * kBlock + idx];
+            if (p.sum_is_float[s]) {
+              double x = as_f64(v[s][r]);
+              if (p.sum_centered[s]) {
+                const double d = x - p.centers[s][code[r]];
                 x = d * d;
               }
               *a = as_u64(as_f64(*a) + x);
             } else {
-              *a += (unsigned long long)chunk_i64(raw[v], p.cols[v].dtype, r);
+              *a += v[s][r];
             }
           }
         }
@@ -63,7 +69,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_private(ScanParams p, SlotArray
   }
   __syncthreads();
 
-  // ---- workgroup reduction of the lane-private tables -> partials[comp][block][slot]
+  // workgroup reduction of the lane-private tables -> partials[comp][block][slot]
   const int wave = tid >> 6, lane = tid & 63;
   const int nb = gridDim.x, b = blockIdx.x;
   for (int s = wave; s < S; s += kBlock / 64) {
@@ -80,10 +86,10 @@ __global__ __launch_bounds__(kBlock) void k_scan_private(ScanParams p, SlotArray
       L.partials[((size_t)0 * nb + b) * S + s] = c;
       L.partials[((size_t)1 * nb + b) * S + s] = f;
     }
-    for (int v = 0; v < nsum; ++v) {
-      const unsigned long long* a = &acc[(size_t)v * S * kBlock + s * kBlock];
+    for (int q = 0; q < nsum; ++q) {
+      const unsigned long long* a = &acc[(size_t)q * S * kBlock + s * kBlock];
       unsigned long long out;
-      if (p.sum_is_float[v]) {
+      if (p.sum_is_float[q]) {
         double x = 0.0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) x += as_f64(a[lane + 64 * j]);
@@ -94,56 +100,48 @@ __global__ __launch_bounds__(kBlock) void k_scan_private(ScanParams p, SlotArray
         for (int j = 0; j < 4; ++j) x += a[lane + 64 * j];
         out = wave_sum_u64(x);
       }
-      if (lane == 0) L.partials[((size_t)(2 + v) * nb + b) * S + s] = out;
+      if (lane == 0) L.partials[((size_t)(2 + q) * nb + b) * S + s] = out;
     }
   }
+}
 
-  // ---- last-arriving workgroup combines the partials (Guideline 16 release/acquire)
-  __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned int ticket = atomicAdd(L.done_counter, 1u);
-    s_last = (ticket == (unsigned int)nb - 1u);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
+// Combines the per-workgroup partials in a fixed order (bitwise deterministic), then either
+// emits the groups in first-appearance order (S is small: rank by counting) or stores the
+// per-slot totals for the generic emit path.
+__global__ __launch_bounds__(kBlock) void k_private_finish(FinishParams f, SlotArrays sa, EmitParams e) {
+  __shared__ unsigned long long red[kBlock];
+  __shared__ unsigned long long tot[kMaxPrivateSlots * (2 + kMaxSums)];
+  const int tid = threadIdx.x;
+  const int S = f.nslots, nb = f.blocks, nsum = f.nsum;
   const int P = (2 + nsum) * S;
   int tpp = 1;
   while (tpp * 2 * P <= kBlock) tpp *= 2;
-  const int ppr = kBlock / tpp;  // pairs per round
-  unsigned long long* red = reinterpret_cast<unsigned long long*>(smem);  // [256]
-  unsigned long long* tot = red + kBlock;                                  // [P]
+  const int ppr = kBlock / tpp;
   for (int base = 0; base < P; base += ppr) {
     const int pair = base + tid / tpp, j = tid % tpp;
     const int comp = pair / S, s = pair % S;
-    const bool isf = comp >= 2 && pair < P && p.sum_is_float[comp - 2];
+    const bool valid = pair < P;
+    const bool isf = valid && comp >= 2 && f.sum_is_float[comp - 2];
     unsigned long long v = (comp == 1) ? (unsigned long long)kNoRow : 0ull;
-    if (pair < P) {
+    if (valid) {
       if (comp == 1) {
-        uint32_t f = kNoRow;
-        for (int bb = j; bb < nb; bb += tpp) f = min(f, (uint32_t)L.partials[((size_t)comp * nb + bb) * S + s]);
-        v = f;
+        uint32_t m = kNoRow;
+        for (int bb = j; bb < nb; bb += tpp) m = min(m, (uint32_t)f.partials[((size_t)comp * nb + bb) * S + s]);
+        v = m;
       } else if (isf) {
         double x = 0.0;
-        for (int bb = j; bb < nb; bb += tpp) x += as_f64(L.partials[((size_t)comp * nb + bb) * S + s]);
+        for (int bb = j; bb < nb; bb += tpp) x += as_f64(f.partials[((size_t)comp * nb + bb) * S + s]);
         v = as_u64(x);
       } else {
         unsigned long long x = 0;
-        for (int bb = j; bb < nb; bb += tpp) x += L.partials[((size_t)comp * nb + bb) * S + s];
+        for (int bb = j; bb < nb; bb += tpp) x += f.partials[((size_t)comp * nb + bb) * S + s];
         v = x;
       }
     }
     red[tid] = v;
     __syncthreads();
     for (int w = tpp / 2; w >= 1; w >>= 1) {
-      if (j < w && pair < P) {
+      if (j < w && valid) {
         const unsigned long long o = red[tid + w];
         if (comp == 1) red[tid] = min(red[tid], o);
         else if (isf) red[tid] = as_u64(as_f64(red[tid]) + as_f64(o));
@@ -151,35 +149,33 @@ __global__ __launch_bounds__(kBlock) void k_scan_private(ScanParams p, SlotArray
       }
       __syncthreads();
     }
-    if (j == 0 && pair < P) tot[pair] = red[tid];
+    if (j == 0 && valid) tot[pair] = red[tid];
     __syncthreads();
   }
 
-  if (!L.emit_inline) {
+  if (!f.emit_inline) {
     for (int i = tid; i < P; i += kBlock) {
       const int comp = i / S, s = i % S;
       if (comp == 0) sa.cnt[s] = tot[i];
       else if (comp == 1) sa.fst[s] = (uint32_t)tot[i];
-      else sa.acc[(size_t)(comp - 2) * p.nslots + s] = tot[i];
+      else sa.acc[(size_t)(comp - 2) * S + s] = tot[i];
     }
-    if (tid == 0) *L.done_counter = 0u;
     return;
   }
-  // inline emit: rank occupied slots by first row (S is small)
   if (tid < S) {
     const int s = tid;
     if (tot[s] > 0) {
-      const uint32_t f = (uint32_t)tot[S + s];
+      const uint32_t first = (uint32_t)tot[S + s];
       unsigned int rank = 0;
       for (int q = 0; q < S; ++q)
-        if (tot[q] > 0 && (uint32_t)tot[S + q] < f) ++rank;
+        if (tot[q] > 0 && (uint32_t)tot[S + q] < first) ++rank;
       SlotTotals t;
       t.cnt = tot[s];
-      t.fst = f;
+      t.fst = first;
 #pragma unroll
-      for (int v = 0; v < kMaxSums; ++v) {
-        t.acc[v] = (v < nsum) ? tot[(2 + v) * S + s] : 0ull;
-        t.acc2[v] = 0ull;
+      for (int q = 0; q < kMaxSums; ++q) {
+        t.acc[q] = (q < nsum) ? tot[(2 + q) * S + s] : 0ull;
+        t.acc2[q] = 0ull;
       }
       emit_slot(e, (uint64_t)s, (uint64_t)s, rank, t);
     }
@@ -190,14 +186,17 @@ __global__ __launch_bounds__(kBlock) void k_scan_private(ScanParams p, SlotArray
       g += tot[q] > 0 ? 1 : 0;
       total += tot[q];
     }
-    L.out_hdr[0] = g;
-    L.out_hdr[1] = total;
-    *L.done_counter = 0u;
+    f.out_hdr[0] = g;
+    f.out_hdr[1] = total;
   }
 }
 
-void launch_scan_private(const ScanParams& p, const SlotArrays& s, const PrivateLaunch& l, const EmitParams& e,
-                         hipStream_t st) {
-  BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scan_private<NC>), dim3(l.blocks), dim3(kBlock), l.lds_bytes, st, p, s, l, e));
+void launch_scan_private(const ScanParams& p, const PrivateLaunch& l, hipStream_t st) {
+  BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scan_private<NC>), dim3(l.blocks), dim3(kBlock), l.lds_bytes, st, p, l));
 }
+
+void launch_private_finish(const FinishParams& f, const SlotArrays& s, const EmitParams& e, hipStream_t st) {
+  hipLaunchKernelGGL(k_private_finish, dim3(1), dim3(kBlock), 0, st, f, s, e);
+}
+
 }  // namespace bqg

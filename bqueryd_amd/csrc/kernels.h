@@ -31,20 +31,30 @@ struct EmitParams {
   const unsigned long long* scd_first[kMaxAggs]; // first value bits per slot
 };
 
-// Private-LDS mode launch (small dense slot spaces).  When `emit` is non-null the last
-// workgroup finalises and emits the groups itself; otherwise it writes the per-slot totals
-// into `slots`.
+// Private-LDS mode (small dense slot spaces): the scan writes per-workgroup partials, the
+// single-workgroup finish kernel combines them and either emits the groups itself
+// (emit_inline) or stores per-slot totals into SlotArrays for the generic emit path.
+constexpr int kMaxPrivateSlots = 40;
+
 struct PrivateLaunch {
   int blocks;
   size_t lds_bytes;
   unsigned long long* partials;   // [(2 + nsum)][blocks][nslots]
-  unsigned int* done_counter;     // zero before launch; reset by the last workgroup
-  unsigned long long* out_hdr;    // [0] = groups, [1] = passing rows
-  int emit_inline;                // 1: last workgroup emits (EmitParams passed alongside)
 };
 
-void launch_scan_private(const ScanParams& p, const SlotArrays& s, const PrivateLaunch& l,
-                         const EmitParams& e, hipStream_t st);
+struct FinishParams {
+  int nslots;
+  int blocks;
+  int nsum;
+  int emit_inline;
+  int32_t sum_is_float[kMaxSums];
+  const unsigned long long* partials;
+  unsigned long long* out_hdr;    // [0] = groups, [1] = passing rows
+};
+
+void launch_scan_private(const ScanParams& p, const PrivateLaunch& l, hipStream_t st);
+void launch_private_finish(const FinishParams& f, const SlotArrays& s, const EmitParams& e,
+                           hipStream_t st);
 void launch_scan_shared(const ScanParams& p, const SlotArrays& s, int blocks, size_t lds_bytes,
                         hipStream_t st);
 void launch_scan_global(const ScanParams& p, const SlotArrays& s, int blocks, hipStream_t st);
