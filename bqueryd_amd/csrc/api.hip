@@ -328,6 +328,7 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
         pl.tcol.push_back(g.col);
         st = (int)pl.tcol.size() - 1;
         pl.p.sum_is_float[st] = dtype_is_float(dt);
+        pl.p.sum_conv[st] = dtype_is_float(dt) ? 0 : (dt == BQG_U64 ? 2 : 1);
         pl.p.sum_centered[st] = 0;
         pl.p.centers[st] = nullptr;
       }
@@ -576,6 +577,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     for (int i = 0; i < kMaxSums; ++i) F.sum_is_float[i] = pl.p.sum_is_float[i];
     F.partials = L.partials;
     F.out_hdr = (unsigned long long*)c->hdr.ensure(64);
+    F.totals = (unsigned long long*)c->counter.ensure((size_t)(2 + kMaxSums) * kMaxPrivateSlots * 8);
     F.emit_inline = need_generic ? 0 : 1;
     if (F.emit_inline) {
       unsigned char* ob = (unsigned char*)c->outcols.ensure((size_t)e.ncols * S * 8 + 256);
@@ -679,6 +681,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     q2.nsum = nsum2;
     for (int i = 0; i < nsum2; ++i) {
       q2.sum_is_float[i] = 1;
+      q2.sum_conv[i] = pl.p.sum_conv[pl.std_cols[i]];
       q2.sum_centered[i] = 1;
       q2.centers[i] = centers + (size_t)i * S;
     }
@@ -702,6 +705,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       for (int i = 0; i < kMaxSums; ++i) F.sum_is_float[i] = q2.sum_is_float[i];
       F.partials = L.partials;
       F.out_hdr = (unsigned long long*)c->hdr.ensure(64);
+      F.totals = (unsigned long long*)c->counter.ensure((size_t)(2 + kMaxSums) * kMaxPrivateSlots * 8);
       F.emit_inline = 0;
       launch_scan_private(q2, L, st);
       launch_private_finish(F, sa2, e, st);

@@ -72,7 +72,8 @@ struct ScanParams {
   DevCol cols[kMaxCols];
   DevTerm terms[kMaxTerms];
   DevKey keys[kMaxKeys];
-  int32_t sum_is_float[kMaxSums];
+  int32_t sum_is_float[kMaxSums];      // accumulate in float64 (else int64)
+  int32_t sum_conv[kMaxSums];          // input: 0 float bits, 1 signed int, 2 uint64
   int32_t sum_centered[kMaxSums];      // accumulate (v - center[slot])^2 (std pass 2)
   const double* centers[kMaxSums];
 };
@@ -93,23 +94,20 @@ struct SlotArrays {
 // Device helpers: 4-row column chunks.
 // ------------------------------------------------------------------------------------
 struct Chunk {
-  uint4 a, b;  // up to 32 bytes = 4 rows x 8 bytes
+  uint4 a, b;    // up to 32 bytes = 4 rows x 8 bytes
+  uint32_t sh;   // word offset of row0 inside `a` (1- and 2-byte columns)
 };
 
+// Branch-free chunk load: 1- to 4-byte columns read the aligned 16-byte block that holds the
+// lane's 4 rows (one global_load_dwordx4; neighbouring lanes share the block, so HBM traffic
+// is unchanged), 8-byte columns read 32 bytes.  A runtime switch on the width here made the
+// compiler split the loads and drain vmcnt at every join.
 __device__ __forceinline__ void load_chunk(Chunk& c, const DevCol& col, int64_t row0) {
-  const unsigned char* p = col.ptr + (row0 << col.lg);
-  switch (col.lg) {
-    case 0: c.a.x = *reinterpret_cast<const uint32_t*>(p); break;
-    case 1: {
-      const uint2 t = *reinterpret_cast<const uint2*>(p);
-      c.a.x = t.x; c.a.y = t.y;
-    } break;
-    case 2: c.a = *reinterpret_cast<const uint4*>(p); break;
-    default:
-      c.a = *reinterpret_cast<const uint4*>(p);
-      c.b = *reinterpret_cast<const uint4*>(p + 16);
-      break;
-  }
+  const int64_t off = row0 << col.lg;
+  const unsigned char* p = col.ptr + (off & ~int64_t(15));
+  c.a = *reinterpret_cast<const uint4*>(p);
+  if (col.lg == 3) c.b = *reinterpret_cast<const uint4*>(p + 16);
+  c.sh = (uint32_t)(off & 15) >> 2;
 }
 
 __device__ __forceinline__ uint32_t chunk_u32(const Chunk& c, int i) {
@@ -120,13 +118,21 @@ __device__ __forceinline__ uint32_t chunk_u32(const Chunk& c, int i) {
   }
 }
 
+// word (sh + i) of `a`, sh a per-lane runtime offset (narrow columns)
+__device__ __forceinline__ uint32_t chunk_word_dyn(const Chunk& c, uint32_t i) {
+  const uint32_t w = c.sh + i;
+  const uint32_t lo = (w & 1u) ? c.a.y : c.a.x;
+  const uint32_t hi = (w & 1u) ? c.a.w : c.a.z;
+  return (w & 2u) ? hi : lo;
+}
+
 // element r (0..3) of the chunk as raw 64-bit pattern, sign/zero-extended as int64
 __device__ __forceinline__ int64_t chunk_i64(const Chunk& c, int dt, int r) {
   switch (dt) {
-    case BQG_BOOL: case BQG_U8: return (int64_t)((chunk_u32(c, 0) >> (8 * r)) & 0xFF);
-    case BQG_I8: return (int64_t)(int8_t)((chunk_u32(c, 0) >> (8 * r)) & 0xFF);
-    case BQG_U16: return (int64_t)((chunk_u32(c, r >> 1) >> (16 * (r & 1))) & 0xFFFF);
-    case BQG_I16: return (int64_t)(int16_t)((chunk_u32(c, r >> 1) >> (16 * (r & 1))) & 0xFFFF);
+    case BQG_BOOL: case BQG_U8: return (int64_t)((chunk_word_dyn(c, 0) >> (8 * r)) & 0xFF);
+    case BQG_I8: return (int64_t)(int8_t)((chunk_word_dyn(c, 0) >> (8 * r)) & 0xFF);
+    case BQG_U16: return (int64_t)((chunk_word_dyn(c, r >> 1) >> (16 * (r & 1))) & 0xFFFF);
+    case BQG_I16: return (int64_t)(int16_t)((chunk_word_dyn(c, r >> 1) >> (16 * (r & 1))) & 0xFFFF);
     case BQG_I32: return (int64_t)(int32_t)chunk_u32(c, r);
     case BQG_U32: return (int64_t)chunk_u32(c, r);
     case BQG_F32: return (int64_t)__uint_as_float(chunk_u32(c, r));

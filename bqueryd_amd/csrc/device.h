@@ -49,6 +49,7 @@ __device__ __forceinline__ void load_rows4(const ScanParams& p, int64_t row0, Ch
 }
 
 __device__ __forceinline__ void load_one(Chunk& c, const DevCol& col, int64_t row) {
+  c.sh = 0;
   switch (col.lg) {
     case 0: c.a.x = col.ptr[row]; break;
     case 1: c.a.x = reinterpret_cast<const uint16_t*>(col.ptr)[row]; break;
@@ -71,22 +72,24 @@ template <int R>
 __device__ __forceinline__ void decode(const Chunk& c, int dt, uint64_t (&v)[R]) {
   switch (dt) {
     case BQG_BOOL:
-    case BQG_U8:
+    case BQG_U8: {
+      const uint32_t w = chunk_word_dyn(c, 0);
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[r] = (c.a.x >> (8 * r)) & 0xFFu;
-      break;
-    case BQG_I8:
+      for (int r = 0; r < R; ++r) v[r] = (w >> (8 * r)) & 0xFFu;
+    } break;
+    case BQG_I8: {
+      const uint32_t w = chunk_word_dyn(c, 0);
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[r] = (uint64_t)(int64_t)(int8_t)((c.a.x >> (8 * r)) & 0xFFu);
-      break;
+      for (int r = 0; r < R; ++r) v[r] = (uint64_t)(int64_t)(int8_t)((w >> (8 * r)) & 0xFFu);
+    } break;
     case BQG_U16:
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[r] = (chunk_u32(c, r >> 1) >> (16 * (r & 1))) & 0xFFFFu;
+      for (int r = 0; r < R; ++r) v[r] = (chunk_word_dyn(c, r >> 1) >> (16 * (r & 1))) & 0xFFFFu;
       break;
     case BQG_I16:
 #pragma unroll
       for (int r = 0; r < R; ++r)
-        v[r] = (uint64_t)(int64_t)(int16_t)((chunk_u32(c, r >> 1) >> (16 * (r & 1))) & 0xFFFFu);
+        v[r] = (uint64_t)(int64_t)(int16_t)((chunk_word_dyn(c, r >> 1) >> (16 * (r & 1))) & 0xFFFFu);
       break;
     case BQG_I32:
 #pragma unroll
@@ -105,6 +108,11 @@ __device__ __forceinline__ void decode(const Chunk& c, int dt, uint64_t (&v)[R])
       for (int r = 0; r < R; ++r) v[r] = ((uint64_t)chunk_u32(c, 2 * r + 1) << 32) | chunk_u32(c, 2 * r);
       break;
   }
+}
+
+// float64 value of an aggregation input held as a canonical value
+__device__ __forceinline__ double value_f64(uint64_t v, int conv) {
+  return conv == 0 ? as_f64(v) : (conv == 1 ? (double)(int64_t)v : (double)v);
 }
 
 template <int NC, int R>

@@ -50,7 +50,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
         for (int q = 0; q < (NC < kMaxSums ? NC : kMaxSums); ++q) {
           if (q < nsum) {
             if (p.sum_is_float[q]) {
-              double x = as_f64(v[q][r]);
+              double x = value_f64(v[q][r], p.sum_conv[q]);
               if (p.sum_centered[q]) {
                 const double d = x - p.centers[q][s];
                 x = d * d;
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_global(ScanParams p, SlotArr
         for (int q = 0; q < (NC < kMaxSums ? NC : kMaxSums); ++q) {
           if (q < nsum) {
             if (p.sum_is_float[q]) {
-              double x = as_f64(v[q][r]);
+              double x = value_f64(v[q][r], p.sum_conv[q]);
               if (p.sum_centered[q]) {
                 const double d = x - p.centers[q][s];
                 x = d * d;

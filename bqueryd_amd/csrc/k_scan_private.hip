@@ -53,7 +53,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_private(ScanParams p, Privat
           if (s < nsum) {
             unsigned long long* a = &acc[(size_t)s * S * kBlock + idx];
             if (p.sum_is_float[s]) {
-              double x = as_f64(v[s][r]);
+              double x = value_f64(v[s][r], p.sum_conv[s]);
               if (p.sum_centered[s]) {
                 const double d = x - p.centers[s][code[r]];
                 x = d * d;
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_private(ScanParams p, Privat
   }
   __syncthreads();
 
-  // workgroup reduction of the lane-private tables -> partials[comp][block][slot]
+  // workgroup reduction of the lane-private tables -> partials[comp][slot][block]
   const int wave = tid >> 6, lane = tid & 63;
   const int nb = gridDim.x, b = blockIdx.x;
   for (int s = wave; s < S; s += kBlock / 64) {
@@ -83,8 +83,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_private(ScanParams p, Privat
     c = wave_sum_u64(c);
     f = wave_min_u32(f);
     if (lane == 0) {
-      L.partials[((size_t)0 * nb + b) * S + s] = c;
-      L.partials[((size_t)1 * nb + b) * S + s] = f;
+      L.partials[((size_t)0 * S + s) * nb + b] = c;
+      L.partials[((size_t)1 * S + s) * nb + b] = f;
     }
     for (int q = 0; q < nsum; ++q) {
       const unsigned long long* a = &acc[(size_t)q * S * kBlock + s * kBlock];
@@ -100,61 +100,57 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_private(ScanParams p, Privat
         for (int j = 0; j < 4; ++j) x += a[lane + 64 * j];
         out = wave_sum_u64(x);
       }
-      if (lane == 0) L.partials[((size_t)(2 + q) * nb + b) * S + s] = out;
+      if (lane == 0) L.partials[((size_t)(2 + q) * S + s) * nb + b] = out;
     }
   }
 }
 
-// Combines the per-workgroup partials in a fixed order (bitwise deterministic), then either
-// emits the groups in first-appearance order (S is small: rank by counting) or stores the
-// per-slot totals for the generic emit path.
-__global__ __launch_bounds__(kBlock) void k_private_finish(FinishParams f, SlotArrays sa, EmitParams e) {
+// One workgroup per (component, slot): sums / mins that slot's per-workgroup partials in a
+// fixed order (coalesced reads, fixed LDS tree: bitwise deterministic).
+__global__ __launch_bounds__(kBlock) void k_private_reduce(FinishParams f) {
   __shared__ unsigned long long red[kBlock];
-  __shared__ unsigned long long tot[kMaxPrivateSlots * (2 + kMaxSums)];
-  const int tid = threadIdx.x;
-  const int S = f.nslots, nb = f.blocks, nsum = f.nsum;
-  const int P = (2 + nsum) * S;
-  int tpp = 1;
-  while (tpp * 2 * P <= kBlock) tpp *= 2;
-  const int ppr = kBlock / tpp;
-  for (int base = 0; base < P; base += ppr) {
-    const int pair = base + tid / tpp, j = tid % tpp;
-    const int comp = pair / S, s = pair % S;
-    const bool valid = pair < P;
-    const bool isf = valid && comp >= 2 && f.sum_is_float[comp - 2];
-    unsigned long long v = (comp == 1) ? (unsigned long long)kNoRow : 0ull;
-    if (valid) {
-      if (comp == 1) {
-        uint32_t m = kNoRow;
-        for (int bb = j; bb < nb; bb += tpp) m = min(m, (uint32_t)f.partials[((size_t)comp * nb + bb) * S + s]);
-        v = m;
-      } else if (isf) {
-        double x = 0.0;
-        for (int bb = j; bb < nb; bb += tpp) x += as_f64(f.partials[((size_t)comp * nb + bb) * S + s]);
-        v = as_u64(x);
-      } else {
-        unsigned long long x = 0;
-        for (int bb = j; bb < nb; bb += tpp) x += f.partials[((size_t)comp * nb + bb) * S + s];
-        v = x;
-      }
+  const int pair = blockIdx.x, tid = threadIdx.x;
+  const int S = f.nslots, nb = f.blocks;
+  const int comp = pair / S;
+  const bool isf = comp >= 2 && f.sum_is_float[comp - 2];
+  const unsigned long long* src = f.partials + (size_t)pair * nb;
+  unsigned long long v;
+  if (comp == 1) {
+    uint32_t m = kNoRow;
+    for (int b = tid; b < nb; b += kBlock) m = min(m, (uint32_t)src[b]);
+    v = m;
+  } else if (isf) {
+    double x = 0.0;
+    for (int b = tid; b < nb; b += kBlock) x += as_f64(src[b]);
+    v = as_u64(x);
+  } else {
+    unsigned long long x = 0;
+    for (int b = tid; b < nb; b += kBlock) x += src[b];
+    v = x;
+  }
+  red[tid] = v;
+  __syncthreads();
+  for (int w = kBlock / 2; w >= 1; w >>= 1) {
+    if (tid < w) {
+      const unsigned long long o = red[tid + w];
+      if (comp == 1) red[tid] = min(red[tid], o);
+      else if (isf) red[tid] = as_u64(as_f64(red[tid]) + as_f64(o));
+      else red[tid] = red[tid] + o;
     }
-    red[tid] = v;
-    __syncthreads();
-    for (int w = tpp / 2; w >= 1; w >>= 1) {
-      if (j < w && valid) {
-        const unsigned long long o = red[tid + w];
-        if (comp == 1) red[tid] = min(red[tid], o);
-        else if (isf) red[tid] = as_u64(as_f64(red[tid]) + as_f64(o));
-        else red[tid] = red[tid] + o;
-      }
-      __syncthreads();
-    }
-    if (j == 0 && valid) tot[pair] = red[tid];
     __syncthreads();
   }
+  if (tid == 0) f.totals[pair] = red[0];
+}
 
+// Emits the groups in first-appearance order (S is small: rank by counting), or stores the
+// per-slot totals for the generic emit path.
+__global__ __launch_bounds__(64) void k_private_finish(FinishParams f, SlotArrays sa, EmitParams e) {
+  const int tid = threadIdx.x;
+  const int S = f.nslots, nsum = f.nsum;
+  const int P = (2 + nsum) * S;
+  const unsigned long long* tot = f.totals;
   if (!f.emit_inline) {
-    for (int i = tid; i < P; i += kBlock) {
+    for (int i = tid; i < P; i += 64) {
       const int comp = i / S, s = i % S;
       if (comp == 0) sa.cnt[s] = tot[i];
       else if (comp == 1) sa.fst[s] = (uint32_t)tot[i];
@@ -196,7 +192,8 @@ void launch_scan_private(const ScanParams& p, const PrivateLaunch& l, hipStream_
 }
 
 void launch_private_finish(const FinishParams& f, const SlotArrays& s, const EmitParams& e, hipStream_t st) {
-  hipLaunchKernelGGL(k_private_finish, dim3(1), dim3(kBlock), 0, st, f, s, e);
+  hipLaunchKernelGGL(k_private_reduce, dim3((2 + f.nsum) * f.nslots), dim3(kBlock), 0, st, f);
+  hipLaunchKernelGGL(k_private_finish, dim3(1), dim3(64), 0, st, f, s, e);
 }
 
 }  // namespace bqg

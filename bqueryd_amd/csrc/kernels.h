@@ -39,7 +39,7 @@ constexpr int kMaxPrivateSlots = 40;
 struct PrivateLaunch {
   int blocks;
   size_t lds_bytes;
-  unsigned long long* partials;   // [(2 + nsum)][blocks][nslots]
+  unsigned long long* partials;   // [(2 + nsum)][nslots][blocks]
 };
 
 struct FinishParams {
@@ -49,6 +49,7 @@ struct FinishParams {
   int emit_inline;
   int32_t sum_is_float[kMaxSums];
   const unsigned long long* partials;
+  unsigned long long* totals;     // [(2 + nsum) * nslots] scratch
   unsigned long long* out_hdr;    // [0] = groups, [1] = passing rows
 };
 
