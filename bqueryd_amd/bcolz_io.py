@@ -1,0 +1,245 @@
+"""bcolz on-disk layout: reader and writer (host side; blosc via libblosc).
+
+bqueryd's shards (``*.bcolz`` / ``*.bcolzs``, ``bqueryd/worker.py:32-33``) and its per-shard
+results (``worker.py:335-346``: ``result_ctable.flush()`` then a tar of the rootdir) are bcolz
+ctable directories.  bcolz is not vendored in the reference, so the layout below
+is restated from the public bcolz 1.x design [ext-bcolz, unverified]:
+
+  <ctable>/__rootdirs__    JSON {"names": [...], "dirs": {name: name}}
+  <ctable>/__attrs__       JSON {}
+  <ctable>/<col>/__attrs__ JSON {}
+  <ctable>/<col>/meta/sizes    JSON {"shape": [n], "nbytes": n*itemsize, "cbytes": c}
+  <ctable>/<col>/meta/storage  JSON {"dtype", "cparams": {clevel, shuffle, cname, quantize},
+                                     "chunklen", "expectedlen", "dflt"}
+  <ctable>/<col>/data/__<i>.blp  16-byte bloscpack header ('blpk', version, 3 reserved bytes,
+                                  int64 nchunks=1) + one blosc1 frame; chunks hold `chunklen`
+                                  items, the last ("leftover") chunk holds the remainder.
+
+The blosc frames are produced/decoded by the system c-blosc 1.x (``libblosc.so.1``), so any
+codec bcolz wrote (blosclz/lz4/zstd/zlib/snappy) decodes.
+"""
+from __future__ import annotations
+
+import ctypes
+import ctypes.util
+import json
+import os
+import struct
+from collections import OrderedDict
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+BLOSCPACK_MAGIC = b'blpk'
+BLOSCPACK_HEADER = 16
+BLOSC_HEADER = 16
+BLOSC_MAX_OVERHEAD = 16
+ROOTDIRS = '__rootdirs__'
+ATTRS = '__attrs__'
+
+_BLOSC_CANDIDATES = ('/opt/conda/lib/libblosc.so.1', '/opt/conda/lib/libblosc.so', 'libblosc.so.1',
+                     'libblosc.so')
+_blosc = None
+
+
+def blosc():
+    global _blosc
+    if _blosc is None:
+        err = None
+        for cand in _BLOSC_CANDIDATES + tuple(filter(None, [ctypes.util.find_library('blosc')])):
+            try:
+                lib = ctypes.CDLL(cand)
+                break
+            except OSError as e:
+                err = e
+        else:
+            raise OSError('libblosc (c-blosc 1.x) not found: %s' % err)
+        lib.blosc_init()
+        lib.blosc_compress.restype = ctypes.c_int
+        lib.blosc_compress.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        lib.blosc_decompress.restype = ctypes.c_int
+        lib.blosc_decompress.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        lib.blosc_decompress_ctx.restype = ctypes.c_int
+        lib.blosc_decompress_ctx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.c_int]
+        lib.blosc_compress_ctx.restype = ctypes.c_int
+        lib.blosc_compress_ctx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+        lib.blosc_cbuffer_sizes.restype = None
+        lib.blosc_cbuffer_sizes.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
+                                            ctypes.POINTER(ctypes.c_size_t),
+                                            ctypes.POINTER(ctypes.c_size_t)]
+        _blosc = lib
+    return _blosc
+
+
+def _dump_json(path, obj):
+    with open(path, 'wb') as f:
+        f.write(json.dumps(obj, ensure_ascii=True).encode('ascii'))
+        f.write(b'\n')
+
+
+def _chunklen_for(itemsize, expectedlen):
+    """Rows per chunk: ~1 MiB chunks for shards, at least 1 row."""
+    target = 1 << 20
+    return max(1, min(target // max(itemsize, 1), max(int(expectedlen), 1)))
+
+
+# ------------------------------------------------------------------------------------------
+# blosc frames
+# ------------------------------------------------------------------------------------------
+def compress_chunk(arr, clevel=5, shuffle=1, cname='lz4', nthreads=1):
+    arr = np.ascontiguousarray(arr)
+    nbytes = arr.nbytes
+    dest = ctypes.create_string_buffer(nbytes + BLOSC_MAX_OVERHEAD)
+    n = blosc().blosc_compress_ctx(clevel, shuffle, arr.dtype.itemsize, nbytes, arr.ctypes.data, dest,
+                                   nbytes + BLOSC_MAX_OVERHEAD, cname.encode('ascii'), 0, nthreads)
+    if n <= 0:
+        raise RuntimeError('blosc compression failed (%d)' % n)
+    return dest.raw[:n]
+
+
+def decompress_into(frame, out_view):
+    """Decode one blosc frame into the writable numpy array ``out_view``; returns bytes."""
+    buf = ctypes.c_char_p(frame)
+    nb, cb, bs = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    blosc().blosc_cbuffer_sizes(buf, ctypes.byref(nb), ctypes.byref(cb), ctypes.byref(bs))
+    if nb.value > out_view.nbytes:
+        raise ValueError('blosc frame larger than destination (%d > %d)' % (nb.value, out_view.nbytes))
+    n = blosc().blosc_decompress_ctx(buf, out_view.ctypes.data, out_view.nbytes, 1)
+    if n < 0:
+        raise RuntimeError('blosc decompression failed (%d)' % n)
+    return n
+
+
+def read_blp(path):
+    with open(path, 'rb') as f:
+        data = f.read()
+    if data[:4] != BLOSCPACK_MAGIC:
+        raise ValueError('%s: not a bloscpack chunk' % path)
+    return data[BLOSCPACK_HEADER:]
+
+
+def bloscpack_header(nchunks=1, version=1):
+    return BLOSCPACK_MAGIC + struct.pack('<B', version) + b'\x00\x00\x00' + struct.pack('<q', nchunks)
+
+
+# ------------------------------------------------------------------------------------------
+# carray
+# ------------------------------------------------------------------------------------------
+class CArrayMeta:
+    def __init__(self, rootdir):
+        self.rootdir = rootdir
+        with open(os.path.join(rootdir, 'meta', 'sizes'), 'rb') as f:
+            sizes = json.loads(f.read().decode('ascii'))
+        with open(os.path.join(rootdir, 'meta', 'storage'), 'rb') as f:
+            storage = json.loads(f.read().decode('ascii'))
+        self.length = int(sizes['shape'][0])
+        self.dtype = np.dtype(storage['dtype'])
+        self.chunklen = int(storage['chunklen'])
+        self.cparams = storage.get('cparams', {})
+        nchunks = -(-self.length // self.chunklen) if self.length else 0
+        self.chunk_files = [os.path.join(rootdir, 'data', '__%d.blp' % i) for i in range(nchunks)]
+
+
+def read_carray(rootdir, out=None, pool=None):
+    """Decode a carray into ``out`` (or a new array); chunks decode in parallel on ``pool``."""
+    meta = CArrayMeta(rootdir)
+    if out is None:
+        out = np.empty(meta.length, dtype=meta.dtype)
+    if meta.length == 0:
+        return out
+
+    def one(i):
+        lo = i * meta.chunklen
+        hi = min(meta.length, lo + meta.chunklen)
+        frame = read_blp(meta.chunk_files[i])
+        tmp = out[lo:hi]
+        n = decompress_into(frame, tmp)
+        if n != tmp.nbytes:
+            raise ValueError('%s: chunk %d decoded %d bytes, expected %d' % (rootdir, i, n, tmp.nbytes))
+
+    if pool is None or len(meta.chunk_files) < 2:
+        for i in range(len(meta.chunk_files)):
+            one(i)
+    else:
+        list(pool.map(one, range(len(meta.chunk_files))))
+    return out
+
+
+def write_carray(rootdir, arr, chunklen=None, clevel=5, shuffle=1, cname='lz4'):
+    arr = np.ascontiguousarray(arr)
+    if arr.dtype.kind not in 'biuf':
+        raise NotImplementedError('bcolz writer: dtype %s' % arr.dtype)
+    os.makedirs(os.path.join(rootdir, 'meta'), exist_ok=True)
+    os.makedirs(os.path.join(rootdir, 'data'), exist_ok=True)
+    n = len(arr)
+    chunklen = chunklen or _chunklen_for(arr.dtype.itemsize, n)
+    cbytes = 0
+    for i, lo in enumerate(range(0, n, chunklen)):
+        frame = compress_chunk(arr[lo:lo + chunklen], clevel, shuffle, cname)
+        with open(os.path.join(rootdir, 'data', '__%d.blp' % i), 'wb') as f:
+            f.write(bloscpack_header(1))
+            f.write(frame)
+        cbytes += len(frame) + BLOSCPACK_HEADER
+    dflt = False if arr.dtype.kind == 'b' else (0.0 if arr.dtype.kind == 'f' else 0)
+    _dump_json(os.path.join(rootdir, 'meta', 'storage'), {
+        'dtype': str(arr.dtype),
+        'cparams': {'clevel': clevel, 'shuffle': shuffle, 'cname': cname, 'quantize': 0},
+        'chunklen': int(chunklen), 'expectedlen': int(max(n, 1)), 'dflt': dflt})
+    _dump_json(os.path.join(rootdir, 'meta', 'sizes'),
+               {'shape': [int(n)], 'nbytes': int(arr.nbytes), 'cbytes': int(cbytes)})
+    _dump_json(os.path.join(rootdir, ATTRS), {})
+
+
+# ------------------------------------------------------------------------------------------
+# ctable
+# ------------------------------------------------------------------------------------------
+def ctable_names(rootdir):
+    with open(os.path.join(rootdir, ROOTDIRS), 'rb') as f:
+        data = json.loads(f.read().decode('ascii'))
+    return [str(n) for n in data['names']]
+
+
+def ctable_column_dir(rootdir, name):
+    return os.path.join(rootdir, name)
+
+
+def read_ctable(rootdir, columns=None, nthreads=None):
+    """-> OrderedDict name -> numpy array (all columns, or the listed ones)."""
+    names = ctable_names(rootdir)
+    if columns is None:
+        columns = names
+    for c in columns:
+        if c not in names:
+            raise KeyError(str(c))
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    out = OrderedDict()
+    with ThreadPoolExecutor(max_workers=nthreads) as pool:
+        for c in columns:
+            out[c] = read_carray(ctable_column_dir(rootdir, c), pool=pool)
+    return out
+
+
+def ctable_len(rootdir):
+    names = ctable_names(rootdir)
+    if not names:
+        return 0
+    return CArrayMeta(ctable_column_dir(rootdir, names[0])).length
+
+
+def ctable_dtypes(rootdir):
+    return OrderedDict((n, CArrayMeta(ctable_column_dir(rootdir, n)).dtype) for n in ctable_names(rootdir))
+
+
+def write_ctable(rootdir, columns, chunklen=None, cname='lz4'):
+    """Write an OrderedDict of equal-length arrays as a bcolz ctable rootdir."""
+    os.makedirs(rootdir, exist_ok=True)
+    names = list(columns.keys())
+    for n in names:
+        write_carray(ctable_column_dir(rootdir, n), columns[n], chunklen=chunklen, cname=cname)
+    _dump_json(os.path.join(rootdir, ROOTDIRS), {'names': names, 'dirs': {n: n for n in names}})
+    _dump_json(os.path.join(rootdir, ATTRS), {})
+    return rootdir

@@ -95,13 +95,14 @@ def _result_to_columns(dev, res_handle, names):
 class ShardTable:
     """Device-resident columns of one shard."""
 
-    def __init__(self, columns, device=None):
-        """``columns``: mapping name -> 1-D numpy array (all the same length)."""
+    def __init__(self, columns, device=None, nrows=None):
+        """``columns``: mapping name -> 1-D numpy array (all the same length); ``nrows`` is
+        required only when ``columns`` is empty (columns added later)."""
         self.dev = device or get_device()
         self._lib = L.lib()
         names = list(columns.keys())
         arrays = [np.ascontiguousarray(columns[n]) for n in names]
-        n = len(arrays[0]) if arrays else 0
+        n = len(arrays[0]) if arrays else int(nrows or 0)
         for a in arrays:
             if a.ndim != 1 or len(a) != n:
                 raise ValueError('all columns must be 1-D arrays of the same length')

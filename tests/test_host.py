@@ -1,0 +1,155 @@
+"""Host-side logic that runs without a GPU: term normalisation, agg-spec parsing, wire
+messages, bcolz layout, tar-of-tars gather, and the libbqgpu C ABI exports."""
+import io
+import os
+import re
+import tarfile
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+
+from bqueryd_amd import _lib, bcolz_io, messages, rpc, terms, worker
+from oracle import bquery_oracle as bo
+from oracle import cbquery
+
+
+# ---------------------------------------------------------------------------- where terms
+@pytest.mark.parametrize('dtype', [np.bool_, np.int8, np.int16, np.int32, np.int64, np.uint8, np.uint16,
+                                   np.uint32, np.uint64, np.float32, np.float64])
+def test_term_normalisation_matches_oracle(dtype):
+    values = [0, 1, -1, 2.5, -2.5, 3.0, 255, 256, -129, 2**31, 2**63, -2**63, 1e300, float('inf'),
+              float('-inf'), float('nan'), True, False]
+    for code in (1, 2, 5, 6, 7, 8):
+        for v in values:
+            got = terms.normalize(dtype, code, v)
+            ref = cbquery.normalize_term(np.dtype(dtype), code, v)
+            assert got[0] == ref[0], (dtype, code, v, got, ref)
+            if got[0] not in (-1, 0):
+                assert list(got[1]) == list(ref[1]) and list(got[2]) == list(ref[2]), (dtype, code, v)
+    for members in ([1, 2, 3], [2.5, 3], [1000, 2, 2.0], [float('nan'), 1]):
+        for code in (3, 4):
+            got = terms.normalize(dtype, code, set(members))
+            ref = cbquery.normalize_term(np.dtype(dtype), code, set(members))
+            assert got[0] == ref[0], (dtype, code, members)
+
+
+def test_term_parsing_errors():
+    names = {'a': np.dtype(np.int32)}
+    with pytest.raises(KeyError):
+        terms.parse_terms(names, [('b', '==', 1)])
+    with pytest.raises(KeyError):
+        terms.parse_terms(names, [('a', 'like', 1)])
+    with pytest.raises(ValueError):
+        terms.parse_terms(names, [('a', 'in', 1)])
+    with pytest.raises(ValueError):
+        terms.parse_terms(names, [('a', 'nin', [])])
+    assert terms.parse_terms(names, [('a', ' IN ', [4])]) == [('a', 1, 4)]
+    assert terms.parse_terms(names, [('a', 'not in', (4,))]) == [('a', 2, 4)]
+
+
+def test_agg_parsing_matches_oracle():
+    dts = OrderedDict(a=np.dtype(np.int16), b=np.dtype(np.float32))
+    cols = OrderedDict(a=np.zeros(1, np.int16), b=np.zeros(1, np.float32))
+    spec = ['a', ['b', 'mean'], ['a', 'count', 'n'], ['b', 'sum', 's'], ['a', 'std', 'sd'],
+            ['a', 'count_distinct', 'cd'], ['b', 'sorted_count_distinct', 'scd']]
+    assert terms.parse_agg_list(dts, spec) == bo.parse_agg_list(cols, spec)
+    with pytest.raises(NotImplementedError):
+        terms.parse_agg_list(dts, [['a', 'median', 'm']])
+    with pytest.raises(KeyError):
+        terms.parse_agg_list(dts, [['z', 'sum', 'z']])
+
+
+# ---------------------------------------------------------------------------- wire format
+# A Python-2 cPickle (protocol 0) of the params the reference RPC sends for
+# rpc.groupby(['f.bcolzs'], ['payment_type'], [['fare_amount', 'sum', 'fare_amount']], [],
+# aggregate=True) (rpc.py:88-96), base64-encoded as str.encode('base64') does.
+PY2_PARAMS = (b"(dp1\nS'args'\np2\n((lp3\nS'f.bcolzs'\np4\na(lp5\nS'payment_type'\np6\na(lp7\n(lp8\n"
+              b"S'fare_amount'\np9\naS'sum'\np10\nag9\naa(lp11\ntp12\nsS'kwargs'\np13\n(dp14\n"
+              b"S'aggregate'\np15\nI01\nss.")
+
+
+def test_py2_params_decode():
+    import base64
+    msg = messages.msg_factory({'msg_type': 'calc', 'payload': 'groupby',
+                                'params': base64.encodebytes(PY2_PARAMS).decode('ascii')})
+    assert isinstance(msg, messages.CalcMessage)
+    args, kwargs = msg.get_args_kwargs()
+    assert args == (['f.bcolzs'], ['payment_type'], [['fare_amount', 'sum', 'fare_amount']], [])
+    assert kwargs == {'aggregate': True}
+
+
+def test_message_roundtrip():
+    m = messages.RPCMessage({'payload': 'groupby'})
+    m.set_args_kwargs(['a.bcolz', ['k'], [['v', 'sum', 'v']], [('k', '>', 1)]], {'aggregate': True})
+    js = m.to_json()
+    m2 = messages.msg_factory(js)
+    assert isinstance(m2, messages.RPCMessage) and m2.isa('groupby') and m2.isa(messages.RPCMessage())
+    args, kwargs = m2.get_args_kwargs()
+    assert args[0] == 'a.bcolz' and kwargs == {'aggregate': True}
+    assert '\n' in m['params']  # MIME base64 like str.encode('base64')
+    assert isinstance(messages.msg_factory('not json'), messages.Message)
+
+
+# ---------------------------------------------------------------------------- bcolz / tar
+def test_bcolz_roundtrip(tmp_path):
+    rng = np.random.default_rng(0)
+    cols = OrderedDict(a=rng.integers(-9, 9, 300_001).astype(np.int8), b=rng.normal(size=300_001),
+                       c=np.arange(300_001, dtype=np.uint64), d=rng.random(300_001) < 0.5,
+                       e=np.zeros(300_001, np.float32))
+    root = str(tmp_path / 's.bcolz')
+    bcolz_io.write_ctable(root, cols, chunklen=65536)
+    assert bcolz_io.ctable_names(root) == list(cols)
+    assert bcolz_io.ctable_len(root) == 300_001
+    back = bcolz_io.read_ctable(root)
+    for k in cols:
+        assert back[k].dtype == cols[k].dtype
+        np.testing.assert_array_equal(back[k], cols[k])
+    # chunk files carry the 16-byte bloscpack header + one blosc frame
+    with open(os.path.join(root, 'b', 'data', '__0.blp'), 'rb') as f:
+        head = f.read(16)
+    assert head[:4] == b'blpk' and int.from_bytes(head[8:16], 'little', signed=True) == 1
+    assert len(os.listdir(os.path.join(root, 'b', 'data'))) == 5  # 4 full chunks + leftover
+
+
+def test_tar_of_tars_and_concat_merge(tmp_path):
+    tables = []
+    results = OrderedDict()
+    for i in range(3):
+        t = OrderedDict(k=np.array([i, i + 1], np.int32), s=np.array([1.5, 2.5]) * i)
+        d = str(tmp_path / ('result_%d' % i))
+        bcolz_io.write_ctable(d, t)
+        results['shard_%d.bcolzs' % i] = worker.tar_directory(d)
+        tables.append(t)
+    results['empty.bcolzs'] = ''
+    blob = rpc.tar_of_tars(results)
+    with tarfile.open(fileobj=io.BytesIO(blob)) as tf:
+        assert sorted(m.name for m in tf.getmembers()) == ['shard_%d.bcolzs' % i for i in range(3)]
+        inner = tarfile.open(fileobj=io.BytesIO(tf.extractfile('shard_0.bcolzs').read()))
+        assert inner.getnames()[0] == 'result_0'
+    back = rpc.read_shard_results(blob)
+    merged = rpc.merge_tables(back, ['k'], [['s', 'sum', 's']], aggregate=False)
+    ref = bo.client_merge(tables, ['k'], [['s', 'sum', 's']], aggregate=False)
+    for c in ref:
+        np.testing.assert_array_equal(merged[c], ref[c])
+    assert rpc.merge_tables([], ['k'], [], aggregate=True) is None
+
+
+# ---------------------------------------------------------------------------- C ABI
+def test_library_exports_every_declared_symbol():
+    header = open(os.path.join(os.path.dirname(__file__), '..', 'include', 'bqgpu.h')).read()
+    declared = sorted(set(re.findall(r'^\s*(?:const\s+)?\w[\w\s\*]*?\b(bqg_\w+)\s*\(', header, re.M)))
+    assert len(declared) >= 25, declared
+    lib = _lib.lib()
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(declared) == set(_lib._PROTOS), set(declared) ^ set(_lib._PROTOS)
+    assert lib.bqg_abi_version() == 1
+
+
+def test_library_fails_loudly_without_gpu():
+    if os.path.exists('/dev/kfd'):
+        pytest.skip('a GPU is present')
+    from bqueryd_amd.engine import Device
+    with pytest.raises(_lib.BqgError):
+        Device(0)
