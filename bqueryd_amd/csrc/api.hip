@@ -107,6 +107,13 @@ struct HostBuf {
 
 size_t dtype_size(int dt) { return size_t(1) << dtype_lg(dt); }
 
+// Column allocations cover whole 1024-row tiles plus 256 bytes: every lane of the last
+// (partial) tile issues its full-width load in bounds, so the scans need no tail branch.
+size_t column_bytes(int64_t nrows, int dtype) {
+  const size_t rows = ((size_t)nrows + kTileRows - 1) / kTileRows * kTileRows;
+  return (rows << dtype_lg(dtype)) + 256;
+}
+
 }  // namespace
 
 struct ColStats {
@@ -230,7 +237,7 @@ void compute_stats(bqg_table* t, int col) {
 // ------------------------------------------------------------------------------------
 // query planning
 // ------------------------------------------------------------------------------------
-enum Mode { kPrivate = 0, kShared = 1, kGlobalDense = 2, kGlobalHash = 3 };
+enum Mode { kPrivate = 0, kShared = 1, kGlobalDense = 2, kGlobalHash = 3, kPartitioned = 4 };
 
 struct Plan {
   ScanParams p{};
@@ -240,6 +247,7 @@ struct Plan {
   int nsum = 0;                // sum states (SUM / MEAN)
   std::vector<int> std_cols;   // scan columns needing a centered pass (subset of sum states)
   int32_t agg_state[kMaxAggs];
+  int wbits = 12;
   bool has_filter = false;
   int64_t alg_bytes = 0;
 };
@@ -425,7 +433,14 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     if (pl.nslots <= (uint64_t)kMaxPrivateSlots && pl.nslots * per_slot_private * kBlock <= 80 * 1024)
       pl.mode = kPrivate;
     else if (pl.nslots * per_slot_shared <= 64 * 1024) pl.mode = kShared;
-    else pl.mode = kGlobalDense;
+    else {
+      // partitioned aggregation: 2^wbits slots of LDS state per partition, <= 8192 partitions
+      int wbits = 12;
+      while (wbits > 6 && ((size_t)1 << wbits) * (8 + 8 * (size_t)pl.nsum) > 64 * 1024) --wbits;
+      pl.wbits = wbits;
+      const uint64_t parts = (pl.nslots + (1ull << wbits) - 1) >> wbits;
+      pl.mode = (parts <= 8192 && getenv("BQGPU_NO_PARTITION") == nullptr) ? kPartitioned : kGlobalDense;
+    }
   }
   pl.p.nslots = pl.nslots;
 }
@@ -507,6 +522,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   c->last = bqg_timing{};
   c->last.rows = N;
   c->last.mode = pl.mode;
+  c->last.scan_launches = pl.mode == kPartitioned ? 6 : 1;
 
   // bquery's zero-key, unfiltered, empty-table case yields one 'Total' row of zeros
   if (N == 0) {
@@ -628,6 +644,26 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       const size_t lds = (size_t)S * (8 + 8 * (size_t)nsum);
       int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
       launch_scan_shared(pl.p, sa, scan_blocks(c, N, std::max(per_cu, 1)), lds, st);
+    } else if (pl.mode == kPartitioned) {
+      PartLaunch L{};
+      L.wbits = pl.wbits;
+      L.nparts = (int)((S + (1ull << pl.wbits) - 1) >> pl.wbits);
+      L.blocks = scan_blocks(c, N, 4);
+      const int64_t tiles = (N + kTileRows - 1) / kTileRows;
+      L.rows_per_block = ((tiles + L.blocks - 1) / L.blocks) * kTileRows;
+      L.splits = std::max(1, (2 * c->cu + L.nparts - 1) / L.nparts);
+      L.capacity = (uint64_t)N;
+      const size_t ncounts = (size_t)L.nparts * L.blocks + 1;
+      unsigned char* pb = (unsigned char*)c->prefix.ensure(ncounts * 4 + (size_t)(L.nparts + 1) * 4 +
+                                                           (2 * (ncounts / 1024 + 2) + 4096) * 4 + 1024);
+      L.counts = (uint32_t*)pb;
+      L.part_start = L.counts + ncounts;
+      uint32_t* scan_scratch = L.part_start + L.nparts + 1;
+      unsigned char* eb = (unsigned char*)c->bitmap.ensure((size_t)N * 8 * (1 + std::max(nsum, 0)) + 256);
+      L.meta = (unsigned long long*)eb;
+      L.vals = L.meta + N;
+      HIPCHECK(hipMemsetAsync(L.counts + ncounts - 1, 0, 4, st));
+      launch_partitioned(pl.p, sa, L, scan_scratch, st);
     } else {
       launch_scan_global(pl.p, sa, scan_blocks(c, N, 8), st);
     }
@@ -894,7 +930,6 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     float ms = 0;
     HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
     c->last.scan_ms = ms;
-    c->last.scan_launches = 1;
     HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
     c->last.total_ms = ms;
   }
@@ -1012,7 +1047,7 @@ int bqg_table_create(bqg_ctx* c, int64_t nrows, int32_t ncols, const int32_t* dt
       (void)slot;
     }
     for (Column& col : t->cols) {
-      col.bytes = (((size_t)nrows << dtype_lg(col.dtype)) + 255) / 256 * 256 + 256;  // padded for 4-row loads
+      col.bytes = column_bytes(nrows, col.dtype);
       if (hipMalloc(&col.dev, col.bytes) != hipSuccess) fail(BQG_E_OOM, "device allocation of a column failed");
       HIPCHECK(hipMemsetAsync(col.dev, 0, col.bytes, c->stream));
     }
@@ -1042,7 +1077,7 @@ int bqg_table_add_column(bqg_table* t, int32_t dtype, int32_t* slot_out) {
     if (dtype < BQG_BOOL || dtype > BQG_F64) fail(BQG_E_INVALID, "unknown dtype %d", dtype);
     Column col;
     col.dtype = dtype;
-    col.bytes = (((size_t)t->nrows << dtype_lg(dtype)) + 255) / 256 * 256 + 256;
+    col.bytes = column_bytes(t->nrows, dtype);
     if (hipMalloc(&col.dev, col.bytes) != hipSuccess) fail(BQG_E_OOM, "device allocation of a column failed");
     HIPCHECK(hipMemsetAsync(col.dev, 0, col.bytes, t->ctx->stream));
     t->cols.push_back(col);
@@ -1197,7 +1232,7 @@ int bqg_select_rows(bqg_ctx* c, bqg_table* t, const bqg_query* q, int32_t n_cols
         const Column& col = t->cols[q->mask_col];
         pl.p.cols[pl.p.mask_col] = DevCol{col.dev, col.dtype, 0};
       }
-      mask = (unsigned char*)c->mask.ensure((size_t)N + 256);
+      mask = (unsigned char*)c->mask.ensure(column_bytes(N, BQG_U8));
       unsigned long long* d = (unsigned long long*)c->hdr.ensure(64);
       HIPCHECK(hipMemsetAsync(d, 0, 8, c->stream));
       if (N > 0) launch_where(pl.p, mask, d, scan_blocks(c, N, 8), c->stream);
@@ -1205,7 +1240,7 @@ int bqg_select_rows(bqg_ctx* c, bqg_table* t, const bqg_query* q, int32_t n_cols
       if (t->cols[q->mask_col].dtype != BQG_BOOL) fail(BQG_E_INVALID, "mask must be BOOL");
       mask = t->cols[q->mask_col].dev;
     } else {
-      mask = (unsigned char*)c->mask.ensure((size_t)N + 256);
+      mask = (unsigned char*)c->mask.ensure(column_bytes(N, BQG_U8));
       HIPCHECK(hipMemsetAsync(mask, 1, (size_t)N + 4, c->stream));
     }
     bqg_result* r = new bqg_result();
@@ -1250,6 +1285,30 @@ int bqg_select_rows(bqg_ctx* c, bqg_table* t, const bqg_query* q, int32_t n_cols
     HIPCHECK(hipStreamSynchronize(c->stream));
     for (auto& d : r->data) r->ptrs.push_back(d.data());
     *out = guard_r.release();
+  });
+}
+
+int bqg_hash_partition(bqg_ctx* c, bqg_table* t, int32_t n_keys, const int32_t* key_cols, int32_t nparts,
+                       int32_t out_col, int64_t* counts) {
+  return guard(c, [&] {
+    if (n_keys < 1 || n_keys > kMaxKeys) fail(BQG_E_UNSUPPORTED, "1..%d key columns", kMaxKeys);
+    if (nparts < 1) fail(BQG_E_INVALID, "nparts must be >= 1");
+    if (out_col < 0 || out_col >= (int)t->cols.size() || t->cols[out_col].dtype != BQG_U32)
+      fail(BQG_E_INVALID, "partition output must be a U32 column");
+    PartitionCols k{};
+    k.nkeys = n_keys;
+    for (int i = 0; i < n_keys; ++i) {
+      if (key_cols[i] < 0 || key_cols[i] >= (int)t->cols.size()) fail(BQG_E_INVALID, "key column out of range");
+      const Column& col = t->cols[key_cols[i]];
+      k.cols[i] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
+    }
+    unsigned long long* d = (unsigned long long*)c->misc.ensure((size_t)nparts * 8 + 64);
+    HIPCHECK(hipMemsetAsync(d, 0, (size_t)nparts * 8, c->stream));
+    if (t->nrows > 0) launch_hash_partition(k, t->nrows, (uint32_t)nparts, (uint32_t*)t->cols[out_col].dev, d, c->stream);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(counts, d, (size_t)nparts * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    t->cols[out_col].stats.valid = false;
   });
 }
 

@@ -122,6 +122,31 @@ void launch_select_gather(const unsigned char* mask, int64_t nrows,
                           const unsigned int* tile_offsets, const DevCol* cols, int ncols,
                           void* const* outs, hipStream_t st);
 
+// Partitioned aggregation (large dense slot spaces): count -> scan -> scatter -> aggregate
+struct PartLaunch {
+  int wbits;                 // slots per partition = 2^wbits
+  int nparts;
+  int blocks;                // workgroups of the count / scatter passes
+  int splits;                // aggregate workgroups per partition
+  int64_t rows_per_block;    // contiguous rows per count/scatter workgroup (multiple of 1024)
+  uint64_t capacity;         // entry capacity (>= passing rows)
+  uint32_t* counts;          // [nparts * blocks + 1] -> exclusive offsets in place
+  uint32_t* part_start;      // [nparts + 1]
+  unsigned long long* meta;  // [capacity] (row << 32) | slot_low
+  unsigned long long* vals;  // [nsum][capacity]
+};
+void launch_partitioned(const ScanParams& p, const SlotArrays& s, PartLaunch L, uint32_t* scan_scratch,
+                        hipStream_t st);
+void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipStream_t st);
+
+// cross-rank merge: partition id of every row from its key values
+struct PartitionCols {
+  DevCol cols[kMaxKeys];
+  int nkeys;
+};
+void launch_hash_partition(const PartitionCols& k, int64_t nrows, uint32_t nparts, uint32_t* out,
+                           unsigned long long* counts, hipStream_t st);
+
 int device_cu_count();
 
 }  // namespace bqg

@@ -1,0 +1,140 @@
+"""Cross-GPU merge of per-shard results for ``aggregate=True``.
+
+The reference merges on the client: every shard's finalized table is appended and re-grouped
+with ``sum`` of every column ("we can only sum now", ``bqueryd/rpc.py:164-173``).  For shards
+co-located on one node this module does the same merge across GPU ranks:
+
+  1. local:    each rank sums its own shards' tables by key (GPU groupby-sum);
+  2. partition: rows are assigned to rank ``hash(key values) mod world`` (GPU kernel
+               ``bqg_hash_partition``: a pure function of the key values, identical on every
+               rank, so all partials of one key meet on one rank);
+  3. exchange: one ``all_to_all_single`` per column, raw bytes with per-rank split sizes
+               (``torch.distributed``: RCCL over xGMI on GPUs, gloo on CPU);
+  4. reduce:   each rank sums the rows it received by key (GPU groupby-sum);
+  5. gather:   the reduced partitions travel to rank 0 with the same byte all-to-all.
+
+The protocol is written against a small backend interface (``partition`` / ``reduce``) so the
+CPU test suite can run it under gloo with the oracle as the backend; the product backend is
+``GpuBackend`` (libbqgpu), which has no CPU fallback.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+
+
+def sum_spec(agg_list):
+    """The client's merge aggregation list: ``[[x[2], 'sum', x[2]] for x in agg_list]``."""
+    return [[x[2], 'sum', x[2]] for x in agg_list]
+
+
+def concat_tables(tables, names=None):
+    tables = [t for t in tables if t is not None and not (isinstance(t, str) and t == '')]
+    if not tables:
+        return None
+    names = names or list(tables[0].keys())
+    return OrderedDict((n, np.concatenate([np.asarray(t[n]) for t in tables])) for n in names)
+
+
+class GpuBackend:
+    """partition / reduce on the GPU through libbqgpu."""
+
+    def __init__(self, device=None):
+        from .engine import get_device
+        self.device = device or get_device()
+
+    def reduce(self, table, groupby_cols, agg_list):
+        from .engine import ShardTable
+        t = ShardTable(table, device=self.device)
+        try:
+            out, _ = t.groupby(groupby_cols, sum_spec(agg_list))
+            return out
+        finally:
+            t.close()
+
+    def partition(self, table, groupby_cols, nparts):
+        import ctypes
+        from . import _lib as L
+        from .engine import ShardTable
+        t = ShardTable(table, device=self.device)
+        try:
+            col = t.add_column('__part__', np.uint32)
+            keys = np.array([t.slot(c) for c in groupby_cols], np.int32)
+            counts = np.zeros(nparts, np.int64)
+            self.device.check(L.lib().bqg_hash_partition(self.device.handle, t.handle, len(keys),
+                                                         keys.ctypes.data, nparts, col,
+                                                         counts.ctypes.data))
+            names = list(table.keys())
+            parts = []
+            for p in range(nparts):
+                if counts[p] == 0:
+                    parts.append(OrderedDict((n, np.asarray(table[n])[:0]) for n in names))
+                else:
+                    parts.append(t.select_rows(names, where_terms=[('__part__', '==', p)]))
+            return parts
+        finally:
+            t.close()
+
+
+class Exchange:
+    """Byte all-to-all over torch.distributed (nccl = RCCL on ROCm, or gloo)."""
+
+    def __init__(self, dist, device=None):
+        self.dist = dist
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        self.device = device
+
+    def _tensor(self, arr):
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).copy())
+        return t.to(self.device) if self.device is not None else t
+
+    def counts(self, send_counts):
+        import torch
+        s = torch.tensor(np.asarray(send_counts, np.int64))
+        r = torch.empty(self.world, dtype=torch.int64)
+        if self.device is not None:
+            s, r = s.to(self.device), r.to(self.device)
+        self.dist.all_to_all_single(r, s)
+        return r.cpu().numpy()
+
+    def column(self, parts, dtype, recv_counts):
+        """parts[dst] -> this rank's rows from every source, concatenated in rank order."""
+        import torch
+        dtype = np.dtype(dtype)
+        send = np.concatenate([np.ascontiguousarray(p, dtype=dtype) for p in parts]) if parts else np.zeros(0, dtype)
+        in_split = [int(len(p)) * dtype.itemsize for p in parts]
+        out_split = [int(c) * dtype.itemsize for c in recv_counts]
+        out = torch.empty(sum(out_split), dtype=torch.uint8)
+        if self.device is not None:
+            out = out.to(self.device)
+        self.dist.all_to_all_single(out, self._tensor(send), out_split, in_split)
+        return out.cpu().numpy().view(dtype)
+
+
+def merge_partials(local_tables, groupby_cols, agg_list, dtypes, backend, exchange):
+    """Merge this rank's finalized shard tables with every other rank's; returns the merged
+    table on rank 0 (None elsewhere).  ``dtypes``: name -> dtype of the finalized columns
+    (needed by ranks that hold no shard)."""
+    names = list(groupby_cols) + [x[2] for x in agg_list]
+    local = concat_tables(local_tables, names)
+    if local is not None and len(next(iter(local.values()))):
+        local = backend.reduce(local, groupby_cols, agg_list)
+        parts = backend.partition(local, groupby_cols, exchange.world)
+    else:
+        parts = [OrderedDict((n, np.zeros(0, dtypes[n])) for n in names) for _ in range(exchange.world)]
+    recv_counts = exchange.counts([len(p[names[0]]) for p in parts])
+    mine = OrderedDict((n, exchange.column([p[n] for p in parts], dtypes[n], recv_counts)) for n in names)
+    if len(mine[names[0]]):
+        mine = backend.reduce(mine, groupby_cols, agg_list)
+    # gather to rank 0
+    n_mine = len(mine[names[0]])
+    to_root = [n_mine if dst == 0 else 0 for dst in range(exchange.world)]
+    recv = exchange.counts(to_root)
+    gathered = OrderedDict()
+    for n in names:
+        parts_n = [mine[n] if dst == 0 else np.zeros(0, dtypes[n]) for dst in range(exchange.world)]
+        gathered[n] = exchange.column(parts_n, dtypes[n], recv)
+    return gathered if exchange.rank == 0 else None

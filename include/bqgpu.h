@@ -17,7 +17,7 @@
  *   worker.py:319  bcolz.fromiter(ct[cols].where(bool_arr), ...)   (aggregate=False)
  *                    -> bqg_select_rows
  * and the co-located cross-shard merge that the client does at bqueryd/rpc.py:164-173
- * ("we can only sum now") -> bqg_partition_result / bqg_merge_partials.
+ * ("we can only sum now") -> bqg_hash_partition + the all-to-all of bqueryd_amd/dist.py.
  *
  * Conventions
  *  - Every function returns 0 on success and a negative BQG_E_* code on failure; the
@@ -169,6 +169,13 @@ int bqg_groupby(bqg_ctx* ctx, bqg_table* t, const bqg_query* q, bqg_result** out
 int bqg_select_rows(bqg_ctx* ctx, bqg_table* t, const bqg_query* q, int32_t n_cols,
                     const int32_t* cols, bqg_result** out);
 int bqg_result_view_get(bqg_result* r, bqg_result_view* out);
+
+/* ---------------- co-located merge (replaces the client re-group, rpc.py:164-173) --------
+ * Partition id (hash of the key VALUES mod nparts) of every row into the U32 column
+ * `out_col`; counts[nparts] receives the rows per partition.  Identical on every rank, so
+ * partials of one key meet on one rank after the all-to-all exchange. */
+int bqg_hash_partition(bqg_ctx* ctx, bqg_table* t, int32_t n_keys, const int32_t* key_cols,
+                       int32_t nparts, int32_t out_col, int64_t* counts);
 int bqg_result_free(bqg_result* r);
 
 #ifdef __cplusplus

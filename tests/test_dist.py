@@ -1,0 +1,83 @@
+"""Cross-rank merge protocol (bqueryd_amd/dist.py) under gloo, world_size 2, on CPU.
+
+The per-rank partition/reduce steps use the oracle as the backend (test infrastructure); the
+exchange, the partition bookkeeping and the gather are the product code.  The merged result
+must equal the reference client merge (rpc.py:164-173) of all shards."""
+import os
+import socket
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+
+from bqueryd_amd import dist as bdist
+from bqueryd_amd import synth
+from oracle import bquery_oracle as bo
+from tests.helpers import assert_tables_equal, sort_by_keys
+
+AGGS = [['fare_amount', 'sum', 'fare_sum'], ['fare_amount', 'count', 'n'], ['fare_amount', 'mean', 'fm']]
+KEYS = ['pickup_location', 'vendor_id']
+NSHARDS = 5
+
+
+class OracleBackend:
+    def reduce(self, table, groupby_cols, agg_list):
+        return bo.groupby(table, groupby_cols, bdist.sum_spec(agg_list))
+
+    def partition(self, table, groupby_cols, nparts):
+        h = np.zeros(len(table[groupby_cols[0]]), np.uint64)
+        for c in groupby_cols:
+            h = (h * np.uint64(1000003)) ^ table[c].astype(np.int64).view(np.uint64)
+        p = (h % np.uint64(nparts)).astype(np.int64)
+        return [OrderedDict((n, v[p == i]) for n, v in table.items()) for i in range(nparts)]
+
+
+def shard_results():
+    out = []
+    for i in range(NSHARDS):
+        s = synth.taxi_shard(3000, config_id=5, n_shards=NSHARDS, shard=i,
+                             columns=('pickup_location', 'vendor_id', 'fare_amount'))
+        s['pickup_location'] = (s['pickup_location'] % 300).astype(np.int32)
+        out.append(bo.handle_work(s, KEYS, AGGS, []))
+    return out
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world)
+    try:
+        results = shard_results()
+        mine = [r for i, r in enumerate(results) if i % world == rank]
+        dtypes = OrderedDict((k, v.dtype) for k, v in results[0].items())
+        merged = bdist.merge_partials(mine, KEYS, AGGS, dtypes, OracleBackend(), bdist.Exchange(dist))
+        q.put((rank, None if merged is None else {k: v.tolist() for k, v in merged.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize('world', [2])
+def test_merge_partials_gloo(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[1] is None
+    results = shard_results()
+    ref = bo.client_merge(results, KEYS, AGGS, aggregate=True)
+    merged = OrderedDict((k, np.array(v, dtype=ref[k].dtype)) for k, v in got[0].items())
+    assert_tables_equal(sort_by_keys(merged, KEYS), sort_by_keys(ref, KEYS))
