@@ -28,6 +28,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+MODES = ['private-lds', 'shared-lds', 'global-dense', 'global-hash', 'partitioned']
+KERNELS = ['k_scan_private', 'k_scan_shared', 'k_scan_global', 'k_scan_global<hash>',
+           'k_part_count+scan+scatter+aggregate (timed together)']
 
 
 def _dist_env():
@@ -196,7 +199,7 @@ def main(argv=None):
                 args.config.upper(), rows, cfg['groupby'], [a[1] for a in cfg['aggs']], cfg['where']),
             'rows_per_gpu': rows,
             'parallelism': 'shard-per-rank x%d' % ws,
-            'engine_mode': ['private-lds', 'shared-lds', 'global-dense', 'global-hash'][mode or 0],
+            'engine_mode': MODES[mode or 0],
         },
         'roofline': {
             'bound': 'hbm',
@@ -205,7 +208,7 @@ def main(argv=None):
             'unit': 'GB/s',
             'frac': achieved / HBM_PEAK_GBS,
             'traffic': traffic,
-            'kernel': 'k_scan_private' if (mode or 0) == 0 else 'k_scan_*',
+            'kernel': KERNELS[mode or 0],
             'kernel_avg_ms': scan_avg,
             'algorithmic_bytes_per_launch': bytes_per_launch,
         },

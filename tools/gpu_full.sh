@@ -21,3 +21,5 @@ for c in c3 c4; do
   timeout -k 10 400 python bench.py --config $c --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_$c.json 2> $OUT/bench_$c.err || exit $?
   cat $OUT/bench_$c.json
 done
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_torchrun.json 2> $OUT/bench_torchrun.err || exit $?
+cat $OUT/bench_torchrun.json
