@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -137,11 +138,64 @@ struct bqg_table {
   std::vector<Column> cols;
 };
 
+// A result's columns live in one pinned host block taken from the context's pool (the D2H
+// copies land there directly; Python wraps the columns zero-copy) or, for tiny synthesized
+// results, in `small`.
+struct PinnedBlock {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+struct PinnedPool {
+  std::mutex mu;
+  std::vector<PinnedBlock> free;
+  ~PinnedPool() {
+    for (PinnedBlock& b : free) (void)hipHostFree(b.p);
+  }
+  PinnedBlock get(size_t bytes) {
+    bytes = std::max<size_t>(bytes, 4096);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      size_t best = (size_t)-1;
+      for (size_t i = 0; i < free.size(); ++i)
+        if (free[i].cap >= bytes && (best == (size_t)-1 || free[i].cap < free[best].cap)) best = i;
+      if (best != (size_t)-1) {
+        PinnedBlock b = free[best];
+        free.erase(free.begin() + best);
+        return b;
+      }
+    }
+    size_t cap = 4096;
+    while (cap < bytes) cap <<= 1;
+    PinnedBlock b;
+    if (hipHostMalloc(&b.p, cap, hipHostMallocDefault) != hipSuccess) {
+      b.p = nullptr;
+      throw ApiError{BQG_E_OOM, "pinned result block allocation failed"};
+    }
+    b.cap = cap;
+    return b;
+  }
+  void put(PinnedBlock b) {
+    if (!b.p) return;
+    std::lock_guard<std::mutex> lk(mu);
+    free.push_back(b);
+    while (free.size() > 8) {  // bounded: drop the smallest block
+      size_t sm = 0;
+      for (size_t i = 1; i < free.size(); ++i)
+        if (free[i].cap < free[sm].cap) sm = i;
+      (void)hipHostFree(free[sm].p);
+      free.erase(free.begin() + sm);
+    }
+  }
+};
+
 struct bqg_result {
+  std::shared_ptr<PinnedPool> pool;
+  PinnedBlock block;
   int64_t n_rows = 0;
   int32_t filtered = 0;
   std::vector<int32_t> dtypes;
-  std::vector<std::vector<unsigned char>> data;
+  std::vector<std::vector<unsigned char>> small;
   std::vector<const void*> ptrs;
 };
 
@@ -159,6 +213,10 @@ struct bqg_ctx {
   // scratch
   DevBuf partials, counter, hdr, slots, terms, outcols, lists, bitmap, prefix, cdbuf, scdbuf, mask, misc;
   HostBuf hhdr, hout;
+  // pinned blocks for results (returned by bqg_result_free); shared with outstanding results
+  // so a result may outlive its context
+  std::shared_ptr<PinnedPool> pool = std::make_shared<PinnedPool>();
+  PinnedBlock pool_get(size_t bytes) { return pool->get(bytes); }
   // timing
   bool timing = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -260,8 +318,6 @@ int scan_col(Plan& pl, int tc) {
   pl.tcol.push_back(tc);
   return (int)pl.tcol.size() - 1;
 }
-
-bool is_float_op_input(int dt) { return dtype_is_float(dt); }
 
 uint64_t bits_for(uint64_t range) {  // bits needed to code values 0..range-1
   uint64_t b = 0;
@@ -505,9 +561,24 @@ bqg_result* empty_result(const std::vector<int>& dts, int filtered) {
   r->filtered = filtered;
   for (int dt : dts) {
     r->dtypes.push_back(dt);
-    r->data.emplace_back(8);
+    r->small.emplace_back(8);
   }
-  for (auto& d : r->data) r->ptrs.push_back(d.data());
+  for (auto& d : r->small) r->ptrs.push_back(d.data());
+  return r;
+}
+
+// result over a pinned block: column j at base + offsets[j]
+bqg_result* block_result(bqg_ctx* c, PinnedBlock b, int64_t n, int filtered, const std::vector<int>& dts,
+                         const std::vector<size_t>& offsets) {
+  bqg_result* r = new bqg_result();
+  r->pool = c->pool;
+  r->block = b;
+  r->n_rows = n;
+  r->filtered = filtered;
+  for (size_t j = 0; j < dts.size(); ++j) {
+    r->dtypes.push_back(dts[j]);
+    r->ptrs.push_back((const unsigned char*)b.p + offsets[j]);
+  }
   return r;
 }
 
@@ -531,14 +602,14 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       r->n_rows = 1;
       for (size_t j = 0; j < out_dt.size(); ++j) {
         r->dtypes.push_back(out_dt[j]);
-        r->data.emplace_back(8, 0);
+        r->small.emplace_back(8, 0);
         const bqg_agg& g = q->aggs[j];
         if (g.op == BQG_STD) {
           const double nan = NAN;
-          memcpy(r->data.back().data(), &nan, 8);
+          memcpy(r->small.back().data(), &nan, 8);
         }
       }
-      for (auto& d : r->data) r->ptrs.push_back(d.data());
+      for (auto& d : r->small) r->ptrs.push_back(d.data());
       *out = r;
     } else {
       *out = empty_result(out_dt, 0);
@@ -606,24 +677,18 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     launch_private_finish(F, sa, e, st);
     HIPCHECK(hipGetLastError());
     if (!need_generic) {
-      // one D2H of header + columns
+      // one D2H of header + columns straight into a pooled pinned block
       const size_t colbytes = (size_t)e.ncols * S * 8;
-      unsigned char* h = (unsigned char*)c->hout.ensure(colbytes + 64);
+      PinnedBlock blk = c->pool_get(colbytes + 64);
+      unsigned char* h = (unsigned char*)blk.p;
       HIPCHECK(hipMemcpyAsync(h, F.out_hdr, 16, hipMemcpyDeviceToHost, st));
       if (colbytes) HIPCHECK(hipMemcpyAsync(h + 64, c->outcols.p, colbytes, hipMemcpyDeviceToHost, st));
       if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
       HIPCHECK(hipStreamSynchronize(st));
       const unsigned long long G = ((unsigned long long*)h)[0], total = ((unsigned long long*)h)[1];
-      bqg_result* r = new bqg_result();
-      r->n_rows = (int64_t)G;
-      r->filtered = pl.has_filter && (int64_t)total < N;
-      for (int j = 0; j < e.ncols; ++j) {
-        const size_t isz = dtype_size(out_dt[j]);
-        r->dtypes.push_back(out_dt[j]);
-        r->data.emplace_back(std::max<size_t>(G * isz, 8));
-        memcpy(r->data.back().data(), h + 64 + (size_t)j * S * 8, G * isz);
-      }
-      for (auto& d : r->data) r->ptrs.push_back(d.data());
+      std::vector<size_t> offs;
+      for (int j = 0; j < e.ncols; ++j) offs.push_back(64 + (size_t)j * S * 8);
+      bqg_result* r = block_result(c, blk, (int64_t)G, pl.has_filter && (int64_t)total < N, out_dt, offs);
       if (c->timing) {
         float ms = 0;
         HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
@@ -648,9 +713,10 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       PartLaunch L{};
       L.wbits = pl.wbits;
       L.nparts = (int)((S + (1ull << pl.wbits) - 1) >> pl.wbits);
-      L.blocks = scan_blocks(c, N, 4);
-      const int64_t tiles = (N + kTileRows - 1) / kTileRows;
-      L.rows_per_block = ((tiles + L.blocks - 1) / L.blocks) * kTileRows;
+      const int64_t ptile = 4096;  // rows per 1024-thread count/scatter iteration
+      const int64_t ptiles = (N + ptile - 1) / ptile;
+      L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->cu, ptiles));
+      L.rows_per_block = ((ptiles + L.blocks - 1) / L.blocks) * ptile;
       L.splits = std::max(1, (2 * c->cu + L.nparts - 1) / L.nparts);
       L.capacity = (uint64_t)N;
       const size_t ncounts = (size_t)L.nparts * L.blocks + 1;
@@ -659,9 +725,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.counts = (uint32_t*)pb;
       L.part_start = L.counts + ncounts;
       uint32_t* scan_scratch = L.part_start + L.nparts + 1;
-      unsigned char* eb = (unsigned char*)c->bitmap.ensure((size_t)N * 8 * (1 + std::max(nsum, 0)) + 256);
-      L.meta = (unsigned long long*)eb;
-      L.vals = L.meta + N;
+      L.entries = (unsigned long long*)c->bitmap.ensure((size_t)N * 8 * (1 + std::max(nsum, 0)) + 256);
       HIPCHECK(hipMemsetAsync(L.counts + ncounts - 1, 0, 4, st));
       launch_partitioned(pl.p, sa, L, scan_scratch, st);
     } else {
@@ -845,6 +909,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       d.waves = (int)waves;
       d.chunk_rows = (((int64_t)((N + waves - 1) / waves)) + 63) / 64 * 64;
       d.lds_state = (S * 24 * (kBlock / 64) <= 64 * 1024) ? 1 : 0;
+      d.slot_bits = 0;
+      while (d.slot_bits < 63 && (S - 1) >> d.slot_bits) ++d.slot_bits;
       unsigned char* b = (unsigned char*)c->prefix.ensure(waves * S * 24 + 1024);
       d.st_first = (unsigned long long*)b;
       d.st_last = d.st_first + waves * S;
@@ -865,14 +931,16 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   }
 
   // ---- generic emit
-  unsigned char* lb = (unsigned char*)c->lists.ensure(S * 8 + 256);
+  const uint64_t cblocks = (S + 4095) / 4096 + 1;
+  unsigned char* lb = (unsigned char*)c->lists.ensure(S * 8 + (2 * cblocks + 4096) * 8 + 256);
   uint32_t* list_fst = (uint32_t*)lb;
   uint32_t* list_slot = list_fst + S;
+  uint32_t* compact_scratch = list_slot + S;
   unsigned char* hb = (unsigned char*)c->hdr.ensure(64);
   unsigned int* gcount = (unsigned int*)hb;
   unsigned long long* gtotal = (unsigned long long*)(hb + 8);
   HIPCHECK(hipMemsetAsync(hb, 0, 16, st));
-  launch_compact(sa, S, list_fst, list_slot, gcount, gtotal, st);
+  launch_compact(sa, S, list_fst, list_slot, gcount, gtotal, compact_scratch, st);
   HIPCHECK(hipGetLastError());
   unsigned char* hh = (unsigned char*)c->hhdr.ensure(64);
   HIPCHECK(hipMemcpyAsync(hh, hb, 16, hipMemcpyDeviceToHost, st));
@@ -908,24 +976,19 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   }
   launch_emit(e, sa, order, G, nsum, S, st);
   HIPCHECK(hipGetLastError());
-  unsigned char* h = (unsigned char*)c->hout.ensure(obytes + 64);
-  HIPCHECK(hipMemcpyAsync(h, ob, obytes, hipMemcpyDeviceToHost, st));
+  PinnedBlock blk = c->pool_get(obytes + 64);
+  HIPCHECK(hipMemcpyAsync(blk.p, ob, obytes, hipMemcpyDeviceToHost, st));
   if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
   HIPCHECK(hipStreamSynchronize(st));
-  bqg_result* r = new bqg_result();
-  r->n_rows = G;
-  r->filtered = pl.has_filter && (int64_t)total < N;
+  std::vector<size_t> offs;
   {
     size_t o = 0;
     for (int j = 0; j < e.ncols; ++j) {
-      const size_t nb = (size_t)G * dtype_size(out_dt[j]);
-      r->dtypes.push_back(out_dt[j]);
-      r->data.emplace_back(std::max<size_t>(nb, 8));
-      memcpy(r->data.back().data(), h + o, nb);
-      o += (nb + 255) & ~size_t(255);
+      offs.push_back(o);
+      o += ((size_t)G * dtype_size(out_dt[j]) + 255) & ~size_t(255);
     }
   }
-  for (auto& d : r->data) r->ptrs.push_back(d.data());
+  bqg_result* r = block_result(c, blk, G, pl.has_filter && (int64_t)total < N, out_dt, offs);
   if (c->timing) {
     float ms = 0;
     HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
@@ -990,6 +1053,7 @@ int bqg_destroy(bqg_ctx* c) {
       b->release();
     c->hhdr.release();
     c->hout.release();
+    c->pool.reset();
     for (int i = 0; i < 2; ++i) {
       if (c->stage[i]) (void)hipHostFree(c->stage[i]);
       if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
@@ -1188,7 +1252,8 @@ int bqg_expand_subgroups(bqg_ctx* c, bqg_table* t, int32_t basket_col, int32_t m
     const int64_t N = t->nrows;
     if (N == 0) return;
     const int64_t tiles = (N + kTileRows - 1) / kTileRows;
-    unsigned int* scratch = (unsigned int*)c->misc.ensure((size_t)(tiles + 1) * 4 + (size_t)N + 256);
+    unsigned int* scratch = (unsigned int*)c->misc.ensure((size_t)(tiles + 1) * 4 + (2 * (tiles / 1024 + 2) + 4096) * 4 +
+                                                          (size_t)N + 256);
     const Column& b = t->cols[basket_col];
     DevCol bc{b.dev, b.dtype, dtype_lg(b.dtype)};
     launch_expand_subgroups(bc, t->cols[mask_col].dev, t->cols[out_mask_col].dev, N, 0, scratch, c->stream);
@@ -1245,11 +1310,11 @@ int bqg_select_rows(bqg_ctx* c, bqg_table* t, const bqg_query* q, int32_t n_cols
     }
     bqg_result* r = new bqg_result();
     std::unique_ptr<bqg_result> guard_r(r);
-    unsigned int* tc = (unsigned int*)c->lists.ensure((size_t)(tiles + 1) * 4 + 256);
+    unsigned int* tc = (unsigned int*)c->lists.ensure((size_t)(tiles + 1) * 4 + (2 * (tiles / 1024 + 2) + 4096) * 4 + 256);
     int64_t total = 0;
     if (N > 0) {
       launch_select_count(mask, N, tc, c->stream);
-      launch_select_scan(tc, tiles, c->stream);
+      launch_select_scan(tc, tiles, tc + tiles + 1, c->stream);
       // total = offset of the last tile + its count: recount on host from the mask tail
       unsigned int* hc = (unsigned int*)c->hhdr.ensure(64);
       HIPCHECK(hipMemcpyAsync(hc, tc + tiles - 1, 4, hipMemcpyDeviceToHost, c->stream));
@@ -1275,15 +1340,15 @@ int bqg_select_rows(bqg_ctx* c, bqg_table* t, const bqg_query* q, int32_t n_cols
     for (int i = 0; i < n_cols; ++i) outs.push_back(ob + offs[i]);
     if (total > 0) launch_select_gather(mask, N, tc, dcs.data(), n_cols, outs.data(), c->stream);
     HIPCHECK(hipGetLastError());
-    for (int i = 0; i < n_cols; ++i) {
-      const int dt = t->cols[cols[i]].dtype;
-      const size_t nb = (size_t)total * dtype_size(dt);
-      r->dtypes.push_back(dt);
-      r->data.emplace_back(std::max<size_t>(nb, 8));
-      if (nb) HIPCHECK(hipMemcpyAsync(r->data.back().data(), outs[i], nb, hipMemcpyDeviceToHost, c->stream));
-    }
+    PinnedBlock blk = c->pool_get(obytes + 64);
+    if (obytes) HIPCHECK(hipMemcpyAsync(blk.p, ob, obytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
-    for (auto& d : r->data) r->ptrs.push_back(d.data());
+    r->pool = c->pool;
+    r->block = blk;
+    for (int i = 0; i < n_cols; ++i) {
+      r->dtypes.push_back(t->cols[cols[i]].dtype);
+      r->ptrs.push_back((const unsigned char*)blk.p + offs[i]);
+    }
     *out = guard_r.release();
   });
 }
@@ -1323,6 +1388,8 @@ int bqg_result_view_get(bqg_result* r, bqg_result_view* out) {
 }
 
 int bqg_result_free(bqg_result* r) {
+  if (!r) return BQG_OK;
+  if (r->pool && r->block.p) r->pool->put(r->block);
   delete r;
   return BQG_OK;
 }

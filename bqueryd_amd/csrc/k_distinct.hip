@@ -48,6 +48,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_count_distinct(ScanParams p, Slot
         const uint64_t bit = s * d.vrange + vcode;
         const unsigned int m = 1u << (bit & 31);
         if (d.lds_bitmap_words > 0) {
+          if (lbits[bit >> 5] & m) continue;  // hot pairs: a broadcast read, no atomic
           if (atomicOr(&lbits[bit >> 5], m) & m) continue;
         }
         if (d.bitmap[bit >> 5] & m) continue;
@@ -140,38 +141,40 @@ __global__ __launch_bounds__(kBlock, 4) void k_scd(ScanParams p, SlotArrays sa, 
       }
 #pragma unroll
       for (int c = 0; c < NC; ++c)
-        if (vc == c) {
-          const int dt = p.cols[c].dtype;
-          vb = v[c][0];
-        }
+        if (vc == c) vb = v[c][0];
     }
-    uint64_t active = __ballot(act);
-    while (active) {
-      const int leader = __ffsll((unsigned long long)active) - 1;
-      const uint64_t ls = __shfl(slot, leader, 64);
-      const uint64_t m = __ballot(act && slot == ls) & active;
-      active &= ~m;
-      const bool mine = (m >> lane) & 1ull;
-      const uint64_t below = m & ((1ull << lane) - 1ull);
-      const int pl = below ? 63 - __clzll((long long)below) : lane;
-      const uint64_t pv = __shfl(vb, pl, 64);
-      const bool diff = mine && below != 0 && !scd_equal(vb, pv, isf);
-      unsigned int nchg = (unsigned int)__popcll(__ballot(diff));
-      const int hl = 63 - __clzll((long long)m);
-      const uint64_t lastv = __shfl(vb, hl, 64);
-      const uint64_t firstv = __shfl(vb, leader, 64);
-      const uint32_t firstrow = (uint32_t)__shfl((int)(uint32_t)row, leader, 64);
-      if (lane == 0) {
-        if (fr[ls] == kNoRow) {
-          fr[ls] = firstrow;
-          fv[ls] = firstv;
-        } else if (!scd_equal(lv[ls], firstv, isf)) {
-          ++nchg;
-        }
-        lv[ls] = lastv;
-        ch[ls] += nchg;
+    // Lanes sharing this lane's slot, from one ballot per slot bit (cost independent of how
+    // many distinct slots the 64-row step holds).
+    const uint64_t actm = __ballot(act);
+    uint64_t match = actm;
+    for (int b = 0; b < d.slot_bits; ++b) {
+      const bool bit = (slot >> b) & 1ull;
+      const uint64_t bb = __ballot(act && bit);
+      match &= bit ? bb : ~bb;
+    }
+    const uint64_t self = 1ull << lane;
+    const uint64_t below = match & (self - 1ull);
+    const uint64_t above = match & ~((self - 1ull) | self);
+    const int pl = below ? 63 - __clzll((long long)below) : lane;
+    const uint64_t pv = __shfl(vb, pl, 64);  // previous row of the same slot in this step
+    const bool is_first = act && below == 0;
+    const bool is_last = act && above == 0;
+    bool diff = act && below != 0 && !scd_equal(vb, pv, isf);
+    if (is_first) {
+      // the slot's previous row lies in an earlier step of this chunk (or none)
+      if (fr[slot] == kNoRow) {
+        fr[slot] = (uint32_t)row;
+        fv[slot] = vb;
+      } else {
+        diff = !scd_equal(lv[slot], vb, isf);
       }
     }
+    const uint64_t dm = __ballot(diff);
+    if (is_first) {
+      const unsigned int n = (unsigned int)__popcll(dm & match);
+      if (n) ch[slot] += n;
+    }
+    if (is_last) lv[slot] = vb;  // after every first-lane read of lv (program order)
   }
   if (d.lds_state) {
     for (int i = lane; i < S; i += 64) {

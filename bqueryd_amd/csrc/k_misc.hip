@@ -10,38 +10,73 @@ namespace bqg {
 // ------------------------------------------------------------------------------------
 // Emit: occupied slots -> first-appearance order -> output columns
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_compact(SlotArrays sa, uint64_t nslots, uint32_t* list_fst,
-                                                    uint32_t* list_slot, unsigned int* count,
-                                                    unsigned long long* total) {
-  __shared__ unsigned int s_base;
-  __shared__ unsigned int s_wave[kBlock / 64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < nslots; base += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t s = base + tid;
-    const unsigned long long cs = s < nslots ? sa.cnt[s] : 0ull;
-    const bool occ = cs > 0;
-    const unsigned long long csum = wave_sum_u64(cs);
-    if (lane == 0 && csum) atomicAdd(total, csum);
-    const uint64_t bal = __ballot(occ);
-    const unsigned int before = (unsigned int)__popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) s_wave[wave] = (unsigned int)__popcll(bal);
-    __syncthreads();
-    if (tid == 0) {
-      unsigned int tot = 0;
-      for (int q = 0; q < kBlock / 64; ++q) {
-        const unsigned int t = s_wave[q];
-        s_wave[q] = tot;
-        tot += t;
-      }
-      s_base = tot ? atomicAdd(count, tot) : 0u;
+// Occupied slots -> (first row, slot) list in slot order: per-workgroup counts, an exclusive
+// scan of the counts, then an ordered write (deterministic, no shared counter).
+constexpr int kCompactBlock = 1024;
+constexpr int kCompactSlots = kCompactBlock * 4;
+
+__global__ __launch_bounds__(kCompactBlock) void k_compact_count(SlotArrays sa, uint64_t nslots, uint32_t* block_counts,
+                                                                 unsigned long long* total) {
+  const uint64_t base = (uint64_t)blockIdx.x * kCompactSlots + (uint64_t)threadIdx.x * 4;
+  unsigned int c = 0;
+  unsigned long long rows = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint64_t s = base + r;
+    const unsigned long long n = s < nslots ? sa.cnt[s] : 0ull;
+    c += n > 0 ? 1u : 0u;
+    rows += n;
+  }
+  __shared__ unsigned int wc[kCompactBlock / 64];
+  __shared__ unsigned long long wr[kCompactBlock / 64];
+  const unsigned int cw = (unsigned int)wave_sum_u64(c);
+  const unsigned long long rw = wave_sum_u64(rows);
+  if ((threadIdx.x & 63) == 0) {
+    wc[threadIdx.x >> 6] = cw;
+    wr[threadIdx.x >> 6] = rw;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int t = 0;
+    unsigned long long tr = 0;
+    for (int q = 0; q < kCompactBlock / 64; ++q) {
+      t += wc[q];
+      tr += wr[q];
     }
-    __syncthreads();
-    if (occ) {
-      const unsigned int i = s_base + s_wave[wave] + before;
-      list_fst[i] = sa.fst[s];
-      list_slot[i] = (uint32_t)s;
+    block_counts[blockIdx.x] = t;
+    if (tr) atomicAdd(total, tr);
+  }
+}
+
+__global__ __launch_bounds__(kCompactBlock) void k_compact_write(SlotArrays sa, uint64_t nslots, const uint32_t* block_offsets,
+                                                                 uint32_t* list_fst, uint32_t* list_slot) {
+  const uint64_t base = (uint64_t)blockIdx.x * kCompactSlots + (uint64_t)threadIdx.x * 4;
+  uint32_t occ = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint64_t s = base + r;
+    if (s < nslots && sa.cnt[s] > 0) occ |= 1u << r;
+  }
+  __shared__ unsigned int wsum[kCompactBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned int v = (unsigned int)__popc(occ), incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned int t = (unsigned int)__shfl_up((int)incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  unsigned int before = 0;
+  for (int q = 0; q < wave; ++q) before += wsum[q];
+  unsigned int pos = block_offsets[blockIdx.x] + before + incl - v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (occ & (1u << r)) {
+      list_fst[pos] = sa.fst[base + r];
+      list_slot[pos] = (uint32_t)(base + r);
+      ++pos;
     }
-    __syncthreads();
   }
 }
 
@@ -195,7 +230,19 @@ __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsig
     mx = max(mx, (unsigned long long)__shfl_xor(mx, o, 64));
     nan |= (unsigned long long)__shfl_xor(nan, o, 64);
   }
+  __shared__ unsigned long long smn[kBlock / 64], smx[kBlock / 64], snan[kBlock / 64];
   if ((threadIdx.x & 63) == 0) {
+    smn[threadIdx.x >> 6] = mn;
+    smx[threadIdx.x >> 6] = mx;
+    snan[threadIdx.x >> 6] = nan;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < kBlock / 64; ++q) {
+      mn = min(mn, smn[q]);
+      mx = max(mx, smx[q]);
+      nan |= snan[q];
+    }
     atomicMin(&out[0], mn);
     atomicMax(&out[1], mx);
     if (nan) atomicOr(&out[2], 1ull);
@@ -258,29 +305,6 @@ __global__ __launch_bounds__(kBlock) void k_select_count(const unsigned char* ma
   if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = c;
   __syncthreads();
   if (threadIdx.x == 0) tile_counts[blockIdx.x] = sw[0] + sw[1] + sw[2] + sw[3];
-}
-
-__global__ __launch_bounds__(1024) void k_excl_scan_u32(unsigned int* v, int64_t n) {
-  __shared__ unsigned int sh[1024];
-  __shared__ unsigned int carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int64_t base = 0; base < n; base += 1024) {
-    const int64_t i = base + threadIdx.x;
-    const unsigned int c = i < n ? v[i] : 0u;
-    sh[threadIdx.x] = c;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-      const unsigned int t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
-      __syncthreads();
-      sh[threadIdx.x] += t;
-      __syncthreads();
-    }
-    if (i < n) v[i] = carry + sh[threadIdx.x] - c;
-    __syncthreads();
-    if (threadIdx.x == 1023) carry += sh[1023];
-    __syncthreads();
-  }
 }
 
 struct GatherCols {
@@ -369,11 +393,15 @@ __global__ __launch_bounds__(kBlock) void k_runs_mark(DevCol b, int64_t nrows, c
 }
 
 void launch_compact(const SlotArrays& s, uint64_t nslots, uint32_t* list_fst, uint32_t* list_slot,
-                    unsigned int* count, unsigned long long* total, hipStream_t st) {
-  uint64_t blocks = (nslots + kBlock - 1) / kBlock;
-  if (blocks > 2048) blocks = 2048;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_compact, dim3((unsigned)blocks), dim3(kBlock), 0, st, s, nslots, list_fst, list_slot, count, total);
+                    unsigned int* count, unsigned long long* total, uint32_t* scratch, hipStream_t st) {
+  const uint64_t blocks = std::max<uint64_t>(1, (nslots + kCompactSlots - 1) / kCompactSlots);
+  uint32_t* counts = scratch;  // [blocks + 1], scanned in place; counts[blocks] = groups
+  hipLaunchKernelGGL(k_compact_count, dim3((unsigned)blocks), dim3(kCompactBlock), 0, st, s, nslots, counts, total);
+  (void)hipMemsetAsync(counts + blocks, 0, 4, st);
+  launch_exclusive_scan_u32(counts, blocks + 1, scratch + blocks + 1, st);
+  hipLaunchKernelGGL(k_compact_write, dim3((unsigned)blocks), dim3(kCompactBlock), 0, st, s, nslots, counts, list_fst,
+                     list_slot);
+  (void)hipMemcpyAsync(count, counts + blocks, 4, hipMemcpyDeviceToDevice, st);
 }
 void launch_sort_small(uint32_t* list_fst, uint32_t* list_slot, unsigned int n, uint32_t* order, hipStream_t st) {
   hipLaunchKernelGGL(k_sort_small, dim3(1), dim3(1024), 0, st, list_fst, list_slot, n, order);
@@ -420,7 +448,7 @@ __global__ __launch_bounds__(kBlock) void k_hash_partition(PartitionCols k, int6
 
 void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, hipStream_t st) {
   int64_t blocks = (nrows + kTileRows - 1) / kTileRows;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_stats, dim3((unsigned)blocks), dim3(kBlock), 0, st, c, nrows, out4);
 }
@@ -431,8 +459,8 @@ void launch_select_count(const unsigned char* mask, int64_t nrows, unsigned int*
   const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
   if (tiles > 0) hipLaunchKernelGGL(k_select_count, dim3((unsigned)tiles), dim3(kBlock), 0, st, mask, nrows, tile_counts);
 }
-void launch_select_scan(unsigned int* tile_counts, int64_t ntiles, hipStream_t st) {
-  if (ntiles > 0) hipLaunchKernelGGL(k_excl_scan_u32, dim3(1), dim3(1024), 0, st, tile_counts, ntiles);
+void launch_select_scan(unsigned int* tile_counts, int64_t ntiles, unsigned int* scratch, hipStream_t st) {
+  if (ntiles > 0) launch_exclusive_scan_u32(tile_counts, (uint64_t)ntiles, scratch, st);
 }
 void launch_select_gather(const unsigned char* mask, int64_t nrows, const unsigned int* tile_offsets,
                           const DevCol* cols, int ncols, void* const* outs, hipStream_t st) {
@@ -451,9 +479,11 @@ void launch_expand_subgroups(const DevCol& basket, const unsigned char* mask, un
   const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
   if (tiles <= 0) return;
   unsigned int* tile_counts = scratch;
-  unsigned char* run_any = reinterpret_cast<unsigned char*>(scratch + tiles + 1);
+  unsigned int* scan_scratch = scratch + tiles + 1;
+  const int64_t scan_words = 2 * (tiles / 1024 + 2) + 4096;
+  unsigned char* run_any = reinterpret_cast<unsigned char*>(scan_scratch + scan_words);
   hipLaunchKernelGGL(k_runs_count, dim3((unsigned)tiles), dim3(kBlock), 0, st, basket, nrows, tile_counts);
-  hipLaunchKernelGGL(k_excl_scan_u32, dim3(1), dim3(1024), 0, st, tile_counts, tiles);
+  launch_exclusive_scan_u32(tile_counts, (uint64_t)tiles, scan_scratch, st);
   (void)hipMemsetAsync(run_any, 0, (size_t)nrows, st);
   hipLaunchKernelGGL((k_runs_mark<false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, basket, nrows, tile_counts,
                      mask, out, run_any);

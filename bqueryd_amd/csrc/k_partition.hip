@@ -21,62 +21,87 @@
 
 namespace bqg {
 
+// count / scatter run as one 1024-thread workgroup per CU over a contiguous row range: the
+// (workgroup, partition) regions being filled at any time total ~256 x nparts cache lines,
+// small enough to stay in the XCDs' L2 until each line is complete (write combining).
+constexpr int kPartBlock = 1024;
+constexpr int kPartTile = kPartBlock * kRowsPerThread;
+
 template <int NC>
-__global__ __launch_bounds__(kBlock, 4) void k_part_count(ScanParams p, PartLaunch L) {
+__device__ __forceinline__ uint32_t part_rows(const ScanParams& p, int64_t row0, int64_t end, const Chunk (&raw)[NC],
+                                              uint64_t (&v)[NC][4], uint64_t (&code)[4]) {
+  decode_all<NC, 4>(p, raw, v);
+  uint32_t pass = vals_pass<NC, 4>(p, row0, v);
+  if (end - row0 < 4) pass &= (end - row0 > 0) ? ((1u << (end - row0)) - 1u) : 0u;
+  vals_code<NC, 4>(p, v, code);
+  return pass;
+}
+
+template <int NC>
+__global__ __launch_bounds__(kPartBlock) void k_part_count(ScanParams p, PartLaunch L) {
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
   const int tid = threadIdx.x;
-  for (int i = tid; i < L.nparts; i += kBlock) hist[i] = 0;
+  for (int i = tid; i < L.nparts; i += kPartBlock) hist[i] = 0;
   __syncthreads();
   const int64_t begin = (int64_t)blockIdx.x * L.rows_per_block;
   const int64_t end = std::min<int64_t>(p.nrows, begin + L.rows_per_block);
-  for (int64_t base = begin; base < end; base += kTileRows) {
+  Chunk raw[NC];
+  if (begin < end) load_rows4<NC>(p, begin + (int64_t)tid * kRowsPerThread, raw);
+  for (int64_t base = begin; base < end; base += kPartTile) {
     const int64_t row0 = base + (int64_t)tid * kRowsPerThread;
-    Chunk raw[NC];
-    load_rows4<NC>(p, row0, raw);
-    uint64_t v[NC][4];
+    uint64_t v[NC][4], code[4];
     decode_all<NC, 4>(p, raw, v);
+    if (base + kPartTile < end) load_rows4<NC>(p, row0 + kPartTile, raw);
     uint32_t pass = vals_pass<NC, 4>(p, row0, v);
     if (end - row0 < 4) pass &= (end - row0 > 0) ? ((1u << (end - row0)) - 1u) : 0u;
-    uint64_t code[4];
     vals_code<NC, 4>(p, v, code);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (pass & (1u << r)) atomicAdd(&hist[(uint32_t)(code[r] >> L.wbits)], 1u);
   }
   __syncthreads();
-  for (int i = tid; i < L.nparts; i += kBlock) L.counts[(size_t)i * gridDim.x + blockIdx.x] = hist[i];
+  for (int i = tid; i < L.nparts; i += kPartBlock) L.counts[(size_t)i * gridDim.x + blockIdx.x] = hist[i];
 }
 
+// entries are array-of-structs: {u32 slot_low, u32 row, u64 value[nsum]} (16 bytes for one
+// summed column: a single 16-byte store per passing row)
 template <int NC>
-__global__ __launch_bounds__(kBlock, 4) void k_part_scatter(ScanParams p, PartLaunch L) {
+__global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartLaunch L) {
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t* cursor = reinterpret_cast<uint32_t*>(smem);
   const int tid = threadIdx.x;
-  for (int i = tid; i < L.nparts; i += kBlock) cursor[i] = L.counts[(size_t)i * gridDim.x + blockIdx.x];
+  for (int i = tid; i < L.nparts; i += kPartBlock) cursor[i] = L.counts[(size_t)i * gridDim.x + blockIdx.x];
   __syncthreads();
   const int64_t begin = (int64_t)blockIdx.x * L.rows_per_block;
   const int64_t end = std::min<int64_t>(p.nrows, begin + L.rows_per_block);
   const uint64_t lowmask = (1ull << L.wbits) - 1ull;
   const int nsum = p.nsum;
-  for (int64_t base = begin; base < end; base += kTileRows) {
+  const int words = 1 + nsum;  // 8-byte words per entry
+  Chunk raw[NC];
+  if (begin < end) load_rows4<NC>(p, begin + (int64_t)tid * kRowsPerThread, raw);
+  for (int64_t base = begin; base < end; base += kPartTile) {
     const int64_t row0 = base + (int64_t)tid * kRowsPerThread;
-    Chunk raw[NC];
-    load_rows4<NC>(p, row0, raw);
-    uint64_t v[NC][4];
+    uint64_t v[NC][4], code[4];
     decode_all<NC, 4>(p, raw, v);
+    if (base + kPartTile < end) load_rows4<NC>(p, row0 + kPartTile, raw);
     uint32_t pass = vals_pass<NC, 4>(p, row0, v);
     if (end - row0 < 4) pass &= (end - row0 > 0) ? ((1u << (end - row0)) - 1u) : 0u;
-    uint64_t code[4];
     vals_code<NC, 4>(p, v, code);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (pass & (1u << r)) {
         const uint32_t pos = atomicAdd(&cursor[(uint32_t)(code[r] >> L.wbits)], 1u);
-        L.meta[pos] = ((unsigned long long)(uint32_t)(row0 + r) << 32) | (code[r] & lowmask);
+        const unsigned long long meta = ((unsigned long long)(uint32_t)(row0 + r) << 32) | (code[r] & lowmask);
+        unsigned long long* e = L.entries + (size_t)pos * words;
+        if (nsum == 1) {
+          *reinterpret_cast<ulonglong2*>(e) = make_ulonglong2(meta, v[0][r]);
+        } else {
+          e[0] = meta;
 #pragma unroll
-        for (int s = 0; s < (NC < kMaxSums ? NC : kMaxSums); ++s)
-          if (s < nsum) L.vals[(size_t)s * L.capacity + pos] = v[s][r];
+          for (int s = 0; s < (NC < kMaxSums ? NC : kMaxSums); ++s)
+            if (s < nsum) e[1 + s] = v[s][r];
+        }
       }
     }
   }
@@ -86,6 +111,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   extern __shared__ __align__(16) unsigned char smem[];
   const int W = 1 << L.wbits;
   const int nsum = p.nsum;
+  const int words = 1 + nsum;
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][W]
   uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)nsum * W);    // [W]
   uint32_t* fst = cnt + W;                                                 // [W]
@@ -103,13 +129,22 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   const uint32_t beg = pbeg + (uint32_t)(len * split / L.splits);
   const uint32_t fin = pbeg + (uint32_t)(len * (split + 1) / L.splits);
   for (uint32_t i = beg + tid; i < fin; i += blockDim.x) {
-    const unsigned long long m = L.meta[i];
+    const unsigned long long* e = L.entries + (size_t)i * words;
+    unsigned long long m, x0;
+    if (nsum == 1) {
+      const ulonglong2 t = *reinterpret_cast<const ulonglong2*>(e);
+      m = t.x;
+      x0 = t.y;
+    } else {
+      m = e[0];
+      x0 = nsum ? e[1] : 0ull;
+    }
     const uint32_t s = (uint32_t)(m & 0xFFFFFFFFull);
     const uint32_t row = (uint32_t)(m >> 32);
     atomicAdd(&cnt[s], 1u);
     if (fst[s] > row) atomicMin(&fst[s], row);
     for (int q = 0; q < nsum; ++q) {
-      const unsigned long long x = L.vals[(size_t)q * L.capacity + i];
+      const unsigned long long x = q == 0 ? x0 : e[1 + q];
       if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + s]), value_f64(x, p.sum_conv[q]));
       else atomicAdd(&acc[(size_t)q * W + s], x);
     }
@@ -197,13 +232,13 @@ void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipSt
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, PartLaunch L, uint32_t* scan_scratch,
                         hipStream_t st) {
   const size_t hist_lds = (size_t)L.nparts * 4;
-  BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_count<NC>), dim3(L.blocks), dim3(kBlock), hist_lds, st, p, L));
+  BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_count<NC>), dim3(L.blocks), dim3(kPartBlock), hist_lds, st, p, L));
   // counts has one extra zero word at the end: after the scan it holds the total
   const uint64_t n = (uint64_t)L.nparts * L.blocks + 1;
   launch_exclusive_scan_u32(L.counts, n, scan_scratch, st);
   hipLaunchKernelGGL(k_part_starts, dim3((L.nparts + 256) / 256), dim3(256), 0, st, L.counts, L.nparts, L.blocks,
                      L.part_start);
-  BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC>), dim3(L.blocks), dim3(kBlock), hist_lds, st, p, L));
+  BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC>), dim3(L.blocks), dim3(kPartBlock), hist_lds, st, p, L));
   const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)p.nsum);
   hipLaunchKernelGGL(k_part_aggregate, dim3(L.nparts * L.splits), dim3(1024), agg_lds, st, p, L, s);
 }

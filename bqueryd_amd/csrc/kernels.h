@@ -83,6 +83,7 @@ struct ScdLaunch {
   int waves;                         // number of row chunks (one wave each)
   int64_t chunk_rows;                // rows per chunk (multiple of 64)
   int lds_state;                     // 1: per-wave state staged in LDS
+  int slot_bits;                     // bits of a slot id (ballots per 64-row step)
   uint32_t* st_first_row;            // [waves][nslots]   (kNoRow = absent)
   unsigned long long* st_first;      // [waves][nslots]   first value bits
   unsigned long long* st_last;       // [waves][nslots]
@@ -95,7 +96,7 @@ void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hi
 // emit: occupied slots -> first-appearance order -> finalised output columns
 void launch_compact(const SlotArrays& s, uint64_t nslots, uint32_t* list_fst,
                     uint32_t* list_slot, unsigned int* count, unsigned long long* total,
-                    hipStream_t st);
+                    uint32_t* scratch, hipStream_t st);
 void launch_sort_small(uint32_t* list_fst, uint32_t* list_slot, unsigned int n,
                        uint32_t* order, hipStream_t st);
 void launch_rank_bitmap(const uint32_t* list_fst, const uint32_t* list_slot, unsigned int n,
@@ -117,7 +118,7 @@ void launch_expand_subgroups(const DevCol& basket, const unsigned char* mask,
 // aggregate=False row selection: per-tile pass counts, then ordered compaction
 void launch_select_count(const unsigned char* mask, int64_t nrows, unsigned int* tile_counts,
                          hipStream_t st);
-void launch_select_scan(unsigned int* tile_counts, int64_t ntiles, hipStream_t st);
+void launch_select_scan(unsigned int* tile_counts, int64_t ntiles, unsigned int* scratch, hipStream_t st);
 void launch_select_gather(const unsigned char* mask, int64_t nrows,
                           const unsigned int* tile_offsets, const DevCol* cols, int ncols,
                           void* const* outs, hipStream_t st);
@@ -128,12 +129,11 @@ struct PartLaunch {
   int nparts;
   int blocks;                // workgroups of the count / scatter passes
   int splits;                // aggregate workgroups per partition
-  int64_t rows_per_block;    // contiguous rows per count/scatter workgroup (multiple of 1024)
+  int64_t rows_per_block;    // contiguous rows per count/scatter workgroup (multiple of 4096)
   uint64_t capacity;         // entry capacity (>= passing rows)
   uint32_t* counts;          // [nparts * blocks + 1] -> exclusive offsets in place
   uint32_t* part_start;      // [nparts + 1]
-  unsigned long long* meta;  // [capacity] (row << 32) | slot_low
-  unsigned long long* vals;  // [nsum][capacity]
+  unsigned long long* entries;  // [capacity][1 + nsum]: (row << 32) | slot_low, then values
 };
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, PartLaunch L, uint32_t* scan_scratch,
                         hipStream_t st);

@@ -76,20 +76,38 @@ def get_device(ordinal=None):
     return dev
 
 
+class _ResultHolder:
+    """Owns one bqg_result; freed (its pinned block returned to the pool) when the last numpy
+    view of its columns is garbage-collected."""
+
+    def __init__(self, handle):
+        self.handle = handle
+        self._free = L.lib().bqg_result_free
+
+    def __del__(self):
+        if self.handle:
+            self._free(self.handle)
+            self.handle = None
+
+
 def _result_to_columns(dev, res_handle, names):
+    """Zero-copy numpy views of a result's columns (pinned host memory of the library)."""
     view = L.ResultView()
-    dev.check(L.lib().bqg_result_view_get(res_handle, ctypes.byref(view)))
-    try:
-        n = view.n_rows
-        out = OrderedDict()
-        for j, name in enumerate(names):
-            dt = L.DTYPES[view.dtypes[j]]
-            nbytes = n * dt.itemsize
-            buf = ctypes.string_at(view.cols[j], nbytes) if nbytes else b''
-            out[name] = np.frombuffer(buf, dtype=dt).copy()
-        return out, bool(view.filtered)
-    finally:
-        L.lib().bqg_result_free(res_handle)
+    rc = L.lib().bqg_result_view_get(res_handle, ctypes.byref(view))
+    holder = _ResultHolder(res_handle)
+    dev.check(rc)
+    n = view.n_rows
+    out = OrderedDict()
+    for j, name in enumerate(names):
+        dt = L.DTYPES[view.dtypes[j]]
+        nbytes = n * dt.itemsize
+        if nbytes == 0:
+            out[name] = np.zeros(0, dtype=dt)
+            continue
+        buf = (ctypes.c_char * nbytes).from_address(view.cols[j])
+        buf._bqg_holder = holder
+        out[name] = np.frombuffer(buf, dtype=dt)
+    return out, bool(view.filtered)
 
 
 class ShardTable:
