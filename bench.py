@@ -43,14 +43,19 @@ def _dist_env():
 class _Comm:
     """Barrier / max-reduce across ranks (gloo, CPU only).  Single process: no-ops."""
 
-    def __init__(self, ws):
+    def __init__(self, ws, local=0, nccl=False):
         self.ws = ws
         self.dist = None
+        self.nccl_group = None
         if ws > 1:
+            import torch
             import torch.distributed as dist  # imported before libbqgpu: one HIP runtime
             os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
             dist.init_process_group('gloo')
             self.dist = dist
+            if nccl:  # the data-path exchange of the aggregate=True merge: RCCL over xGMI
+                torch.cuda.set_device(local)
+                self.nccl_group = dist.new_group(backend='nccl')
 
     def barrier(self):
         if self.dist:
@@ -109,54 +114,86 @@ def main(argv=None):
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4'])
+    ap.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5'])
     ap.add_argument('--rows', type=int, default=None, help='override rows per shard')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--variant', default='exact', choices=['exact', 'raw'])
     args = ap.parse_args(argv)
 
     ws, rank, local = _dist_env()
-    comm = _Comm(ws)
+    comm = _Comm(ws, local, nccl=(args.config == 'c5'))
 
     from bqueryd_amd import synth
     from bqueryd_amd.engine import Device, ShardTable
 
     cfg = synth.CONFIGS[args.config]
-    rows = args.rows or cfg['rows']
-    cols = synth.taxi_shard(rows, config_id=synth.CONFIG_ID[args.config], n_shards=max(ws, 1),
-                            shard=rank, variant=args.variant, columns=synth.query_columns(cfg))
     dev = Device(local)
-    table = ShardTable(cols, device=dev)
     npass_expected = None
-    if cfg['where']:
-        npass_expected = int(np.count_nonzero(cols['passenger_count'] >= 2))
+    timings = []
+    phase = []  # C5: (shard queries s, merge s) per step
+    if args.config == 'c5':
+        # 80 shards over 8 GPUs: 10 shards of 12.5 M rows per rank (weak scaling), per-shard
+        # groupby + the cross-rank aggregate=True merge (RCCL all-to-all) in every step
+        from bqueryd_amd import dist as bdist
+        per_rank = max(1, cfg['shards'] // 8)
+        shard_rows = args.rows or cfg['rows'] // cfg['shards']
+        rows = per_rank * shard_rows
+        tables = []
+        for i in range(per_rank):
+            sc = synth.taxi_shard(shard_rows, config_id=5, n_shards=max(cfg['shards'], ws * per_rank),
+                                  shard=rank * per_rank + i, variant=args.variant,
+                                  columns=synth.query_columns(cfg))
+            tables.append(ShardTable(sc, device=dev))
+        probe, _ = tables[0].groupby(cfg['groupby'], cfg['aggs'])
+        dtypes = {n: np.asarray(v).dtype for n, v in probe.items()}
+        if ws > 1:
+            import torch
+            exchange = bdist.Exchange(comm.dist, device=torch.device('cuda', local), group=comm.nccl_group)
+        else:
+            exchange = bdist.LocalExchange()
+        backend = bdist.GpuBackend(dev)
 
-    def step():
-        out, _ = table.groupby(cfg['groupby'], cfg['aggs'], where_terms=cfg['where'])
-        return out
+        def step():
+            per = []
+            t0 = time.perf_counter()
+            for t in tables:
+                out, _ = t.groupby(cfg['groupby'], cfg['aggs'])
+                timings.append(dev.last_timing())
+                per.append(out)
+            t1 = time.perf_counter()
+            merged = bdist.merge_partials(per, cfg['groupby'], cfg['aggs'], dtypes, backend, exchange)
+            phase.append((t1 - t0, time.perf_counter() - t1))
+            return merged
+    else:
+        rows = args.rows or cfg['rows']
+        cols = synth.taxi_shard(rows, config_id=synth.CONFIG_ID[args.config], n_shards=max(ws, 1),
+                                shard=rank, variant=args.variant, columns=synth.query_columns(cfg))
+        table = ShardTable(cols, device=dev)
+        if cfg['where']:
+            npass_expected = int(np.count_nonzero(cols['passenger_count'] >= 2))
+
+        def step():
+            out, _ = table.groupby(cfg['groupby'], cfg['aggs'], where_terms=cfg['where'])
+            timings.append(dev.last_timing())
+            return out
 
     for _ in range(args.warmup):
         out = step()
     cnt_col = [a[2] for a in cfg['aggs'] if a[1] == 'count']
-    if npass_expected is not None and cnt_col:
+    if npass_expected is not None and cnt_col and out is not None:
         got = int(out[cnt_col[0]].sum())
         if got != npass_expected:
             raise SystemExit('sanity check failed: %d != %d passing rows' % (got, npass_expected))
 
     # device timing of the dominant (scan) kernel: HIP events on the library's stream
     dev.enable_timing(True)
-    scan_ms = []
-    bytes_per_launch = 0
-    mode = None
+    del timings[:]
+    del phase[:]
     comm.barrier()
     dev.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        tm = dev.last_timing()
-        scan_ms.append(tm['scan_ms'])
-        bytes_per_launch = tm['bytes']
-        mode = tm['mode']
     dev.synchronize()
     t1 = time.perf_counter()
     comm.barrier()
@@ -165,11 +202,14 @@ def main(argv=None):
     ms_per_step = elapsed / args.steps * 1e3
     value = total_rows / elapsed
 
-    scan_avg = float(np.mean(scan_ms)) if scan_ms else float('nan')
+    scan_avg = float(np.mean([t['scan_ms'] for t in timings])) if timings else float('nan')
+    device_avg = float(np.mean([t['total_ms'] for t in timings])) if timings else float('nan')
+    bytes_per_launch = timings[-1]['bytes'] if timings else 0
+    mode = timings[-1]['mode'] if timings else 0
     achieved = bytes_per_launch / (scan_avg * 1e-3) / 1e9 if scan_avg > 0 else 0.0
 
     cpu = None
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.config != 'c5':
         rate, secs = _cpu_baseline(cols, cfg)
         cpu = {'value': rate, 'unit': 'rows/s', 'cores': 1, 'kind': 'port',
                'sample': 'full %s shard (%d rows), oracle/cbquery.c single-threaded C port of '
@@ -181,6 +221,11 @@ def main(argv=None):
     comm.close()
     if rank != 0:
         return
+    if phase:
+        cfg_extra = {'shard_queries_ms_per_step': 1e3 * float(np.mean([p[0] for p in phase])),
+                     'merge_ms_per_step': 1e3 * float(np.mean([p[1] for p in phase]))}
+    else:
+        cfg_extra = {}
     line = {
         'metric': 'groupby rows/sec (whole node) + achieved HBM GB/s vs peak, 1/2/4/8 GPUs',
         'value': value,
@@ -195,11 +240,15 @@ def main(argv=None):
         'dtype': 'f64',
         'data': 'synthetic taxi-shaped shards (SURVEY.md §8d generator, %s variant), resident in HBM' % args.variant,
         'config': {
-            'workload': '%s: %d rows/shard, 1 shard per GPU, groupby %s, aggs %s, where %s' % (
-                args.config.upper(), rows, cfg['groupby'], [a[1] for a in cfg['aggs']], cfg['where']),
+            'workload': '%s: %d rows per GPU (%s), groupby %s, aggs %s, where %s%s' % (
+                args.config.upper(), rows,
+                '%d shards x %d rows' % (rows // (args.rows or cfg['rows'] // cfg['shards']), args.rows or cfg['rows'] // cfg['shards'])
+                if args.config == 'c5' else '1 shard', cfg['groupby'], [a[1] for a in cfg['aggs']], cfg['where'],
+                ', aggregate=True merge across ranks (RCCL all-to-all)' if args.config == 'c5' else ''),
             'rows_per_gpu': rows,
             'parallelism': 'shard-per-rank x%d' % ws,
             'engine_mode': MODES[mode or 0],
+            **cfg_extra,
         },
         'roofline': {
             'bound': 'hbm',
@@ -211,6 +260,7 @@ def main(argv=None):
             'kernel': KERNELS[mode or 0],
             'kernel_avg_ms': scan_avg,
             'algorithmic_bytes_per_launch': bytes_per_launch,
+            'device_ms_per_query': device_avg,
         },
         'cpu_baseline': cpu,
     }

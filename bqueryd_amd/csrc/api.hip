@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "jit.h"
 
 using namespace bqg;
 
@@ -179,12 +180,25 @@ struct PinnedPool {
     if (!b.p) return;
     std::lock_guard<std::mutex> lk(mu);
     free.push_back(b);
-    while (free.size() > 8) {  // bounded: drop the smallest block
+    // bounded (a multi-shard step keeps one block per shard result alive at once):
+    // at most kMaxBlocks blocks, dropping the smallest, and kMaxBytes, dropping the largest
+    constexpr size_t kMaxBlocks = 32, kMaxBytes = size_t(2) << 30;
+    while (free.size() > kMaxBlocks) {
       size_t sm = 0;
       for (size_t i = 1; i < free.size(); ++i)
         if (free[i].cap < free[sm].cap) sm = i;
       (void)hipHostFree(free[sm].p);
       free.erase(free.begin() + sm);
+    }
+    for (;;) {
+      size_t tot = 0, lg = 0;
+      for (size_t i = 0; i < free.size(); ++i) {
+        tot += free[i].cap;
+        if (free[i].cap > free[lg].cap) lg = i;
+      }
+      if (tot <= kMaxBytes || free.empty()) break;
+      (void)hipHostFree(free[lg].p);
+      free.erase(free.begin() + lg);
     }
   }
 };
@@ -547,6 +561,10 @@ void build_emit(bqg_table* t, const bqg_query* q, const Plan& pl, EmitParams& e,
   e.nsum2 = (int)pl.std_cols.size();
 }
 
+// workgroups per CU for the private-LDS scan (tools/membench.hip: 2-4 per CU stream best
+// with non-temporal loads; the grid still strides over >= 97 k tiles at C2 size)
+constexpr size_t kPrivatePerCu = 4;
+
 int scan_blocks(bqg_ctx* c, int64_t nrows, int per_cu) {
   const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
   int64_t b = (int64_t)c->cu * per_cu;
@@ -649,9 +667,32 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   hipStream_t st = c->stream;
   if (c->timing) HIPCHECK(hipEventRecord(c->ev[0], st));
 
-  if (pl.mode == kPrivate) {
+  // count / distinct-only queries on a small dense slot space: one fused pass
+  // (k_scd_fused) produces rows, first rows, sorted_count_distinct and one count_distinct
+  int ncd = 0, nscd = 0;
+  for (int a = 0; a < q->n_aggs; ++a) ncd += q->aggs[a].op == BQG_COUNT_DISTINCT, nscd += q->aggs[a].op == BQG_SORTED_COUNT_DISTINCT;
+  bool fused = !pl.p.hash && nsum == 0 && nsum2 == 0 && nscd == 1 && ncd <= 1 && N < (int64_t)kNoRow &&
+               (kBlock / 64) * scd_fused_wave_lds(S) <= kScdFusedMaxLds && !getenv("BQGPU_NO_FUSED_SCD");
+  if (fused && ncd == 1) {
+    for (int a = 0; a < q->n_aggs; ++a) {
+      if (q->aggs[a].op != BQG_COUNT_DISTINCT) continue;
+      Column& col = t->cols[q->aggs[a].col];
+      compute_stats(t, q->aggs[a].col);
+      if (dtype_is_float(col.dtype)) {
+        fused = false;
+      } else {
+        const uint64_t vr = col.stats.empty ? 1 : (uint64_t)col.stats.imax - (uint64_t)col.stats.imin + 1;
+        if (vr == 0 || (unsigned __int128)S * vr > ((unsigned __int128)1 << 30)) fused = false;
+      }
+    }
+  }
+
+  if (fused) {
+    // the scan is the fused distinct pass below
+  } else if (pl.mode == kPrivate) {
     const size_t lds = (size_t)S * kBlock * (8 + 8 * (size_t)nsum);
-    int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
+    int per_cu = (int)std::min<size_t>(kPrivatePerCu, (160 * 1024) / std::max<size_t>(lds, 1));
+    if (const char* ev = getenv("BQGPU_PRIVATE_PER_CU")) per_cu = std::min(per_cu, std::max(1, atoi(ev)));
     if (per_cu < 1) per_cu = 1;
     PrivateLaunch L{};
     L.blocks = scan_blocks(c, N, per_cu);
@@ -670,8 +711,16 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       unsigned char* ob = (unsigned char*)c->outcols.ensure((size_t)e.ncols * S * 8 + 256);
       for (int j = 0; j < e.ncols; ++j) e.cols[j].out = ob + (size_t)j * S * 8;
     }
+    hipFunction_t jfn = N >= jit_min_rows() ? jit_function("bq_jit_scan_private", jit_spec(pl.p)) : nullptr;
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
-    launch_scan_private(pl.p, L, st);
+    if (jfn) {
+      void* args[] = {(void*)&pl.p, (void*)&L};
+      HIPCHECK(hipModuleLaunchKernel(jfn, (unsigned)L.blocks, 1, 1, kBlock, 1, 1, (unsigned)L.lds_bytes, st, args,
+                                     nullptr));
+      c->last.specialized = 1;
+    } else {
+      launch_scan_private(pl.p, L, st);
+    }
     HIPCHECK(hipGetLastError());
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));
     launch_private_finish(F, sa, e, st);
@@ -825,8 +874,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   }
 
   // ---- count_distinct
-  int ncd = 0, nscd = 0;
-  for (int a = 0; a < q->n_aggs; ++a) ncd += q->aggs[a].op == BQG_COUNT_DISTINCT, nscd += q->aggs[a].op == BQG_SORTED_COUNT_DISTINCT;
+  DistinctLaunch fused_cd{};
   std::vector<DevBuf> tmp_bufs;  // per-op scratch
   unsigned long long* cd_out = nullptr;
   if (ncd) cd_out = (unsigned long long*)c->cdbuf.ensure((size_t)ncd * S * 8 + (nsum2 ? 0 : 0));
@@ -874,6 +922,12 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         HIPCHECK(hipMemsetAsync(d.set, 0xFF, cap * 8, st));
         HIPCHECK(hipMemsetAsync(d.set_fill, 0, 8, st));
       }
+      if (fused) {
+        fused_cd = d;  // folded into k_scd_fused (bitmap mode: checked above)
+        e.cd[i] = d.out;
+        ++i;
+        continue;
+      }
       launch_count_distinct(pc.p, sa, d, scan_blocks(c, N, 8), st);
       HIPCHECK(hipGetLastError());
       if (d.set) {
@@ -900,30 +954,58 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       d.vcol = scan_col(pc, tc);
       pc.p.ncols = (int)pc.tcol.size();
       pc.p.cols[d.vcol] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
+      if (fused && fused_cd.bitmap) {
+        // the count_distinct column joins this pass's column set
+        for (int b2 = 0; b2 < q->n_aggs; ++b2) {
+          if (q->aggs[b2].op != BQG_COUNT_DISTINCT) continue;
+          const int cc = q->aggs[b2].col;
+          fused_cd.vcol = scan_col(pc, cc);
+          pc.p.ncols = (int)pc.tcol.size();
+          pc.p.cols[fused_cd.vcol] = DevCol{t->cols[cc].dev, t->cols[cc].dtype, dtype_lg(t->cols[cc].dtype)};
+        }
+      }
       const uint64_t budget = 1ull << 30;
       uint64_t waves = (uint64_t)c->cu * 16;
-      const uint64_t need64 = ((uint64_t)N + 63) / 64;
-      if (waves > need64) waves = need64;
-      while (waves > 64 && waves * S * 24 > budget) waves /= 2;
+      const uint64_t grain = fused ? 256 : 64;  // fused: 256-row groups, 4 rows per lane
+      if (fused) {
+        d.fused = 1;
+        d.wave_lds = scd_fused_wave_lds(S);
+        d.cd = fused_cd;
+        const size_t blk_lds = (kBlock / 64) * d.wave_lds + (size_t)fused_cd.lds_bitmap_words * 4;
+        if (blk_lds > kScdFusedMaxLds) d.cd.lds_bitmap_words = 0;  // no LDS pre-filter
+        const size_t lds = (kBlock / 64) * d.wave_lds + (size_t)d.cd.lds_bitmap_words * 4;
+        const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(4, (160 * 1024) / lds));
+        waves = (uint64_t)c->cu * per_cu * (kBlock / 64);
+      }
+      const uint64_t needg = ((uint64_t)N + grain - 1) / grain;
+      if (waves > needg) waves = needg;
+      while (waves > 64 && waves * S * 28 > budget) waves /= 2;
       if (waves < 1) waves = 1;
       d.waves = (int)waves;
-      d.chunk_rows = (((int64_t)((N + waves - 1) / waves)) + 63) / 64 * 64;
+      d.chunk_rows = (((int64_t)((N + waves - 1) / waves)) + grain - 1) / grain * grain;
       d.lds_state = (S * 24 * (kBlock / 64) <= 64 * 1024) ? 1 : 0;
       d.slot_bits = 0;
       while (d.slot_bits < 63 && (S - 1) >> d.slot_bits) ++d.slot_bits;
-      unsigned char* b = (unsigned char*)c->prefix.ensure(waves * S * 24 + 1024);
+      unsigned char* b = (unsigned char*)c->prefix.ensure(waves * S * 28 + 1024);
       d.st_first = (unsigned long long*)b;
       d.st_last = d.st_first + waves * S;
       d.st_first_row = (uint32_t*)(d.st_last + waves * S);
       d.st_changes = d.st_first_row + waves * S;
-      if (!d.lds_state) {
+      d.st_count = fused ? d.st_changes + waves * S : nullptr;
+      if (!d.lds_state && !fused) {
         HIPCHECK(hipMemsetAsync(d.st_first_row, 0xFF, waves * S * 4, st));
         HIPCHECK(hipMemsetAsync(d.st_changes, 0, waves * S * 4, st));
       }
+      if (fused) {
+        d.slot_cnt = sa.cnt;
+        d.slot_fst = sa.fst;
+      }
       d.out_changes = so + (size_t)i * S * 2;
       d.out_first = d.out_changes + S;
+      if (fused && c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
       launch_scd(pc.p, sa, d, st);
       HIPCHECK(hipGetLastError());
+      if (fused && c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));
       e.scd_changes[i] = d.out_changes;
       e.scd_first[i] = d.out_first;
       ++i;
@@ -1149,6 +1231,15 @@ int bqg_table_add_column(bqg_table* t, int32_t dtype, int32_t* slot_out) {
   });
 }
 
+static bool is_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows, int64_t row_offset) {
   bqg_ctx* c = t->ctx;
   return guard(c, [&] {
@@ -1160,6 +1251,13 @@ int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows, i
     const unsigned char* src = (const unsigned char*)host;
     size_t left = (size_t)nrows * isz;
     unsigned char* dst = k.dev + (size_t)row_offset * isz;
+    if (left >= (1u << 20) && is_pinned(src)) {
+      // page-locked source (e.g. another query's result block): one DMA, no staging memcpy;
+      // synchronous like the staged path, so the caller may reuse the buffer on return
+      HIPCHECK(hipMemcpyAsync(dst, src, left, hipMemcpyHostToDevice, c->stream));
+      HIPCHECK(hipStreamSynchronize(c->stream));
+      return;
+    }
     while (left) {
       const size_t n = std::min(left, bqg_ctx::kStage);
       const int i = c->stage_i;

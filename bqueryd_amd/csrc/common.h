@@ -1,8 +1,12 @@
 // common.h -- shared host/device definitions for libbqgpu (gfx950 only).
 #pragma once
 
+#ifndef __HIPCC_RTC__  // the JIT (hiprtc) provides the HIP runtime and fixed-width types
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#else
+typedef struct ihipStream_t* hipStream_t;  // host launchers are declared, never defined, in JIT code
+#endif
 
 #include "../../include/bqgpu.h"
 
@@ -102,11 +106,20 @@ struct Chunk {
 // lane's 4 rows (one global_load_dwordx4; neighbouring lanes share the block, so HBM traffic
 // is unchanged), 8-byte columns read 32 bytes.  A runtime switch on the width here made the
 // compiler split the loads and drain vmcnt at every join.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// Column streams are read once per query: non-temporal 16-byte loads (measured on MI355X,
+// tools/membench.hip: three C2-shaped streams 6.55-6.7 TB/s nt vs 5.8-5.9 TB/s default policy)
+__device__ __forceinline__ uint4 load_stream16(const unsigned char* p) {
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ void load_chunk(Chunk& c, const DevCol& col, int64_t row0) {
   const int64_t off = row0 << col.lg;
   const unsigned char* p = col.ptr + (off & ~int64_t(15));
-  c.a = *reinterpret_cast<const uint4*>(p);
-  if (col.lg == 3) c.b = *reinterpret_cast<const uint4*>(p + 16);
+  c.a = load_stream16(p);
+  if (col.lg == 3) c.b = load_stream16(p + 16);
   c.sh = (uint32_t)(off & 15) >> 2;
 }
 

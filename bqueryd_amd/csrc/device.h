@@ -62,6 +62,20 @@ __device__ __forceinline__ void load_one(Chunk& c, const DevCol& col, int64_t ro
   }
 }
 
+// Branch-free single-row load: the aligned 8-byte word holding the row (any width <= 8; the
+// column allocations are padded, so the word never leaves the buffer).
+__device__ __forceinline__ uint2 load_row_word(const DevCol& col, int64_t row) {
+  const int64_t off = row << col.lg;
+  return *reinterpret_cast<const uint2*>(col.ptr + (off & ~(int64_t)7));
+}
+__device__ __forceinline__ void row_word_to_chunk(Chunk& c, const DevCol& col, int64_t row, uint2 w) {
+  const int64_t off = row << col.lg;
+  const uint64_t x = (((uint64_t)w.y << 32) | w.x) >> ((off & 7) * 8);
+  c.a = make_uint4((uint32_t)x, (uint32_t)(x >> 32), 0u, 0u);
+  c.b = make_uint4(0u, 0u, 0u, 0u);
+  c.sh = 0;
+}
+
 template <int NC>
 __device__ __forceinline__ void load_rows1(const ScanParams& p, int64_t row, Chunk (&raw)[NC]) {
 #pragma unroll

@@ -1,0 +1,21 @@
+// jit_kernels.h -- query-specialised kernel entry points, compiled at run time by hiprtc
+// (jit.hip).  The host prepends `#define BQ_NC <n>` and `#define BQ_SPEC <assignments>`:
+// the query's shape (column dtypes and widths, term columns and operators, key columns,
+// summed-column kinds, mask / hash flags) becomes compile-time constants, so every dtype and
+// operator dispatch of the generic kernels folds away; pointers, values, key minima and
+// strides stay run-time parameters.  The bodies are the precompiled kernels' own
+// (scan_private.h), so both paths compute the same thing.
+#pragma once
+
+#include "scan_private.h"
+
+namespace bqg {
+__device__ __forceinline__ void jit_specialize(ScanParams& p) { BQ_SPEC }
+}  // namespace bqg
+
+extern "C" __global__ __launch_bounds__(256, 4) void bq_jit_scan_private(bqg::ScanParams pin, bqg::PrivateLaunch L) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  bqg::ScanParams p = pin;
+  bqg::jit_specialize(p);
+  bqg::scan_private_body<BQ_NC>(p, L, smem);
+}

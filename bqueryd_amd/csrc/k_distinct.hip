@@ -87,6 +87,8 @@ __device__ __forceinline__ bool scd_equal(uint64_t a, uint64_t b, bool isf) {
   return isf ? (as_f64(a) == as_f64(b)) : (a == b);
 }
 
+constexpr int kScdU = 4;
+
 template <int NC, bool HASH>
 __global__ __launch_bounds__(kBlock, 4) void k_scd(ScanParams p, SlotArrays sa, ScdLaunch d) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -122,59 +124,83 @@ __global__ __launch_bounds__(kBlock, 4) void k_scd(ScanParams p, SlotArrays sa, 
     if (d.vcol == c) vc = c;
   const bool isf = dtype_is_float(p.cols[vc].dtype);
   const uint64_t hmask = p.nslots - 1;
-  for (int64_t base = start; base < end; base += 64) {
-    const int64_t row = base + lane;
-    Chunk raw[NC];
-    bool act = false;
-    uint64_t slot = 0, vb = 0;
-    if (row < end) {
-      load_rows1<NC>(p, row, raw);
-      uint64_t v[NC][1];
-      decode_all<NC, 1>(p, raw, v);
-      act = vals_pass<NC, 1>(p, row, v) & 1u;
-      uint64_t code[1];
-      vals_code<NC, 1>(p, v, code);
-      slot = code[0];
-      if (HASH && act) {
-        slot = hash_slot(sa, hmask, code[0], false);
-        if (slot == kEmpty) act = false;
-      }
+  // Rows are consumed 64 at a time in row order, but loaded kScdU steps (kScdU x 64 rows) at
+  // once and one group ahead, so every wave keeps 2 x kScdU x NC loads in flight instead of
+  // waiting out one HBM round trip per 64-row step.
+  uint2 cur[kScdU][NC], nxt[kScdU][NC];
+  auto issue = [&](int64_t b, uint2 (&dst)[kScdU][NC]) {
 #pragma unroll
-      for (int c = 0; c < NC; ++c)
-        if (vc == c) vb = v[c][0];
+    for (int u = 0; u < kScdU; ++u) {
+      int64_t r = b + 64 * u + lane;
+      r = r < end ? r : (end > start ? end - 1 : start);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dst[u][c] = load_row_word(p.cols[c], r);
     }
-    // Lanes sharing this lane's slot, from one ballot per slot bit (cost independent of how
-    // many distinct slots the 64-row step holds).
-    const uint64_t actm = __ballot(act);
-    uint64_t match = actm;
-    for (int b = 0; b < d.slot_bits; ++b) {
-      const bool bit = (slot >> b) & 1ull;
-      const uint64_t bb = __ballot(act && bit);
-      match &= bit ? bb : ~bb;
-    }
-    const uint64_t self = 1ull << lane;
-    const uint64_t below = match & (self - 1ull);
-    const uint64_t above = match & ~((self - 1ull) | self);
-    const int pl = below ? 63 - __clzll((long long)below) : lane;
-    const uint64_t pv = __shfl(vb, pl, 64);  // previous row of the same slot in this step
-    const bool is_first = act && below == 0;
-    const bool is_last = act && above == 0;
-    bool diff = act && below != 0 && !scd_equal(vb, pv, isf);
-    if (is_first) {
-      // the slot's previous row lies in an earlier step of this chunk (or none)
-      if (fr[slot] == kNoRow) {
-        fr[slot] = (uint32_t)row;
-        fv[slot] = vb;
-      } else {
-        diff = !scd_equal(lv[slot], vb, isf);
+  };
+  if (start < end) issue(start, cur);
+  for (int64_t gbase = start; gbase < end; gbase += 64 * kScdU) {
+    if (gbase + 64 * kScdU < end) issue(gbase + 64 * kScdU, nxt);
+#pragma unroll
+    for (int u = 0; u < kScdU; ++u) {
+      const int64_t row = gbase + 64 * u + lane;
+      bool act = false;
+      uint64_t slot = 0, vb = 0;
+      if (row < end) {
+        Chunk raw[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) row_word_to_chunk(raw[c], p.cols[c], row, cur[u][c]);
+        uint64_t v[NC][1];
+        decode_all<NC, 1>(p, raw, v);
+        act = vals_pass<NC, 1>(p, row, v) & 1u;
+        uint64_t code[1];
+        vals_code<NC, 1>(p, v, code);
+        slot = code[0];
+        if (HASH && act) {
+          slot = hash_slot(sa, hmask, code[0], false);
+          if (slot == kEmpty) act = false;
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+          if (vc == c) vb = v[c][0];
       }
+      // Lanes sharing this lane's slot, from one ballot per slot bit (cost independent of how
+      // many distinct slots the 64-row step holds).
+      const uint64_t actm = __ballot(act);
+      if (actm == 0) continue;
+      uint64_t match = actm;
+      for (int b = 0; b < d.slot_bits; ++b) {
+        const bool bit = (slot >> b) & 1ull;
+        const uint64_t bb = __ballot(act && bit);
+        match &= bit ? bb : ~bb;
+      }
+      const uint64_t self = 1ull << lane;
+      const uint64_t below = match & (self - 1ull);
+      const uint64_t above = match & ~((self - 1ull) | self);
+      const int pl = below ? 63 - __clzll((long long)below) : lane;
+      const uint64_t pv = __shfl(vb, pl, 64);  // previous row of the same slot in this step
+      const bool is_first = act && below == 0;
+      const bool is_last = act && above == 0;
+      bool diff = act && below != 0 && !scd_equal(vb, pv, isf);
+      if (is_first) {
+        // the slot's previous row lies in an earlier step of this chunk (or none)
+        if (fr[slot] == kNoRow) {
+          fr[slot] = (uint32_t)row;
+          fv[slot] = vb;
+        } else {
+          diff = !scd_equal(lv[slot], vb, isf);
+        }
+      }
+      const uint64_t dm = __ballot(diff);
+      if (is_first) {
+        const unsigned int n = (unsigned int)__popcll(dm & match);
+        if (n) ch[slot] += n;
+      }
+      if (is_last) lv[slot] = vb;  // after every first-lane read of lv (program order)
     }
-    const uint64_t dm = __ballot(diff);
-    if (is_first) {
-      const unsigned int n = (unsigned int)__popcll(dm & match);
-      if (n) ch[slot] += n;
-    }
-    if (is_last) lv[slot] = vb;  // after every first-lane read of lv (program order)
+#pragma unroll
+    for (int u = 0; u < kScdU; ++u)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) cur[u][c] = nxt[u][c];
   }
   if (d.lds_state) {
     for (int i = lane; i < S; i += 64) {
@@ -186,9 +212,157 @@ __global__ __launch_bounds__(kBlock, 4) void k_scd(ScanParams p, SlotArrays sa, 
   }
 }
 
+
+// ------------------------------------------------------------------------------------
+// k_scd_fused: sorted_count_distinct for small dense slot spaces, with the per-slot row
+// counts / first rows (so the generic scan can be skipped for count / distinct-only queries)
+// and optionally one count_distinct, in ONE pass over the rows.
+//
+// Each wave owns a contiguous chunk.  It loads 256 rows at a time the coalesced way (4 rows
+// per lane, 16-byte loads, next group prefetched), decodes / filters / codes them once, and
+// transposes (slot, value) through LDS so that it can then walk the 256 rows in row order,
+// 64 at a time.  Inside a 64-row step, the lanes of one slot find each other through an LDS
+// match-mask table (ds_or_b64 of the lane bit, read back): the previous row of a slot is
+// the highest lower lane in the mask, the slot's first lane updates the per-slot state
+// {last value, rows, changes} once for the whole step.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int NC>
+__global__ __launch_bounds__(kBlock, 2) void k_scd_fused(ScanParams p, ScdLaunch d) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int S = (int)p.nslots;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char* wb = smem + (size_t)wave * d.wave_lds;
+  uint4* st = reinterpret_cast<uint4*>(wb);                                   // [S] {last lo, last hi, rows, changes}
+  unsigned long long* tbl = reinterpret_cast<unsigned long long*>(st + S);    // [S] match masks
+  unsigned long long* fv = tbl + S;                                           // [S] first value
+  unsigned long long* vl = fv + S;                                            // [256] transposed values
+  uint32_t* fr = reinterpret_cast<uint32_t*>(vl + 256);                       // [S] first row
+  uint32_t* sl = fr + S;                                                      // [256] transposed slots
+  unsigned int* cdb = reinterpret_cast<unsigned int*>(smem + (size_t)(kBlock / 64) * d.wave_lds);
+  for (int i = lane; i < S; i += 64) {
+    st[i] = make_uint4(0u, 0u, 0u, 0u);
+    tbl[i] = 0ull;
+    fr[i] = kNoRow;
+  }
+  const bool do_cd = d.cd.bitmap != nullptr;
+  for (int i = threadIdx.x; i < d.cd.lds_bitmap_words; i += kBlock) cdb[i] = 0u;
+  __syncthreads();
+  const int w = blockIdx.x * (kBlock / 64) + wave;
+  if (w >= d.waves) return;
+  const int64_t start = (int64_t)w * d.chunk_rows;
+  const int64_t end = min(start + d.chunk_rows, p.nrows);
+  int vc = 0, cc = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (d.vcol == c) vc = c;
+    if (d.cd.vcol == c) cc = c;
+  }
+  const bool isf = dtype_is_float(p.cols[vc].dtype);
+  Chunk raw[NC];
+  if (start < end) load_rows4<NC>(p, start + 4 * lane, raw);
+  for (int64_t gbase = start; gbase < end; gbase += 256) {
+    const int64_t row0 = gbase + 4 * lane;
+    uint64_t v[NC][4];
+    decode_all<NC, 4>(p, raw, v);
+    if (gbase + 256 < end) load_rows4<NC>(p, row0 + 256, raw);
+    uint32_t pass = vals_pass<NC, 4>(p, row0, v);
+    const int64_t rem = end - row0;
+    pass &= rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
+    uint64_t code[4];
+    vals_code<NC, 4>(p, v, code);
+    uint64_t vb[4], vcd[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      vb[r] = 0;
+      vcd[r] = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (vc == c) vb[r] = v[c][r];
+        if (cc == c) vcd[r] = v[c][r];
+      }
+    }
+    if (do_cd) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!(pass & (1u << r))) continue;
+        const uint64_t bit = code[r] * d.cd.vrange + (vcd[r] - (uint64_t)d.cd.vmin);
+        const unsigned int m = 1u << (bit & 31);
+        if (d.cd.lds_bitmap_words > 0) {
+          if (cdb[bit >> 5] & m) continue;
+          if (atomicOr(&cdb[bit >> 5], m) & m) continue;
+        }
+        if (d.cd.bitmap[bit >> 5] & m) continue;
+        if (!(atomicOr(&d.cd.bitmap[bit >> 5], m) & m)) atomicAdd(&d.cd.out[code[r]], 1ull);
+      }
+    }
+    wave_fence();  // the previous group's reads of sl / vl are done
+    *reinterpret_cast<uint4*>(&sl[4 * lane]) =
+        make_uint4((pass & 1u) ? (uint32_t)code[0] : kNoRow, (pass & 2u) ? (uint32_t)code[1] : kNoRow,
+                   (pass & 4u) ? (uint32_t)code[2] : kNoRow, (pass & 8u) ? (uint32_t)code[3] : kNoRow);
+    *reinterpret_cast<ulonglong2*>(&vl[4 * lane]) = make_ulonglong2(vb[0], vb[1]);
+    *reinterpret_cast<ulonglong2*>(&vl[4 * lane + 2]) = make_ulonglong2(vb[2], vb[3]);
+    wave_fence();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t s = sl[64 * u + lane];
+      const unsigned long long x = vl[64 * u + lane];
+      const bool act = s != kNoRow;
+      const unsigned long long self = 1ull << lane;
+      if (act) atomicOr(&tbl[s], self);
+      wave_fence();
+      const unsigned long long match = act ? tbl[s] : 0ull;
+      const unsigned long long below = match & (self - 1ull);
+      const int pl = below ? 63 - __clzll((long long)below) : lane;
+      const int hl = match ? 63 - __clzll((long long)match) : lane;
+      const unsigned long long pv = __shfl(x, pl, 64);     // previous row of the slot in this step
+      const unsigned long long lastv = __shfl(x, hl, 64);  // last row of the slot in this step
+      const bool is_first = act && below == 0;
+      uint4 cur = make_uint4(0u, 0u, 0u, 0u);
+      bool diff = false;
+      if (is_first) {
+        cur = st[s];
+        const unsigned long long lv = ((unsigned long long)cur.y << 32) | cur.x;
+        diff = cur.z != 0u && !scd_equal(lv, x, isf);
+      } else if (act) {
+        diff = !scd_equal(x, pv, isf);
+      }
+      const unsigned long long dm = __ballot(diff);
+      wave_fence();  // every lane has read tbl[s]
+      if (is_first) {
+        if (cur.z == 0u) {
+          fr[s] = (uint32_t)(gbase + 64 * u + lane);
+          fv[s] = x;
+        }
+        cur.x = (uint32_t)lastv;
+        cur.y = (uint32_t)(lastv >> 32);
+        cur.z += (uint32_t)__popcll(match);
+        cur.w += (uint32_t)__popcll(dm & match);
+        st[s] = cur;
+        tbl[s] = 0ull;
+      }
+    }
+  }
+  wave_fence();
+  for (int i = lane; i < S; i += 64) {
+    const uint4 c = st[i];
+    const size_t o = (size_t)w * S + i;
+    d.st_first_row[o] = fr[i];
+    d.st_first[o] = fv[i];
+    d.st_last[o] = ((unsigned long long)c.y << 32) | c.x;
+    d.st_changes[o] = c.w;
+    d.st_count[o] = c.z;
+  }
+}
+
 struct ScdState {
   uint32_t present;
-  unsigned long long first, last, changes;
+  uint32_t first_row;
+  unsigned long long first, last, changes, rows;
 };
 
 __device__ __forceinline__ ScdState scd_combine(const ScdState& a, const ScdState& b, bool isf) {
@@ -196,6 +370,8 @@ __device__ __forceinline__ ScdState scd_combine(const ScdState& a, const ScdStat
   if (!b.present) return a;
   ScdState r;
   r.present = 1;
+  r.first_row = a.first_row;
+  r.rows = a.rows + b.rows;
   r.first = a.first;
   r.last = b.last;
   r.changes = a.changes + b.changes + (scd_equal(a.last, b.first, isf) ? 0ull : 1ull);
@@ -208,29 +384,37 @@ __global__ __launch_bounds__(kBlock) void k_scd_combine(ScdLaunch d, uint64_t ns
   const uint64_t s = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
   if (s >= nslots) return;
   const int per = (d.waves + 63) / 64;
-  ScdState st = {0, 0, 0, 0};
+  ScdState st = {0, kNoRow, 0, 0, 0, 0};
   for (int i = 0; i < per; ++i) {
     const int w = lane * per + i;
     if (w >= d.waves) break;
     const size_t idx = (size_t)w * nslots + s;
     ScdState x;
-    x.present = d.st_first_row[idx] != kNoRow;
+    x.first_row = d.st_first_row[idx];
+    x.present = x.first_row != kNoRow;
     x.first = d.st_first[idx];
     x.last = d.st_last[idx];
     x.changes = d.st_changes[idx];
+    x.rows = d.st_count ? d.st_count[idx] : 0u;
     st = scd_combine(st, x, isf);
   }
   for (int o = 1; o < 64; o <<= 1) {
     ScdState other;
     other.present = __shfl_down(st.present, o, 64);
+    other.first_row = __shfl_down(st.first_row, o, 64);
     other.first = __shfl_down(st.first, o, 64);
     other.last = __shfl_down(st.last, o, 64);
     other.changes = __shfl_down(st.changes, o, 64);
+    other.rows = __shfl_down(st.rows, o, 64);
     if ((lane % (2 * o)) == 0 && lane + o < 64) st = scd_combine(st, other, isf);
   }
   if (lane == 0) {
     d.out_changes[s] = st.changes;
     d.out_first[s] = st.first;
+    if (d.slot_cnt) {
+      d.slot_cnt[s] = st.present ? st.rows : 0ull;
+      d.slot_fst[s] = st.present ? st.first_row : kNoRow;
+    }
   }
 }
 
@@ -245,11 +429,16 @@ void launch_count_distinct(const ScanParams& p, const SlotArrays& s, const Disti
 }
 void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st) {
   const int blocks = (d.waves + (kBlock / 64) - 1) / (kBlock / 64);
-  const size_t lds = d.lds_state ? (size_t)(kBlock / 64) * p.nslots * 24 : 0;
-  if (p.hash) {
-    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd<NC, true>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
+  if (d.fused) {
+    const size_t lds = (kBlock / 64) * d.wave_lds + (size_t)d.cd.lds_bitmap_words * 4;
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd_fused<NC>), dim3(blocks), dim3(kBlock), lds, st, p, d));
   } else {
-    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd<NC, false>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
+    const size_t lds = d.lds_state ? (size_t)(kBlock / 64) * p.nslots * 24 : 0;
+    if (p.hash) {
+      BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd<NC, true>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
+    } else {
+      BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd<NC, false>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
+    }
   }
   int isf = 0;
   for (int c = 0; c < p.ncols; ++c)

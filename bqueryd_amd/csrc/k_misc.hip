@@ -424,17 +424,25 @@ void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order
   const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(k_emit, dim3(g ? g : 1), dim3(256), 0, st, e, s, order, n, nsum, nslots);
 }
+constexpr uint32_t kHashPartLds = 8192;
 // ------------------------------------------------------------------------------------
 // Hash partition of rows by their key VALUES (not codes: codes depend on per-shard
 // statistics), for the cross-rank merge: partition = mix(canonical key bits) mod nparts.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_hash_partition(PartitionCols k, int64_t nrows, uint32_t nparts,
                                                            uint32_t* out, unsigned long long* counts) {
+  // per-workgroup LDS histogram (a single hot partition -- world size 1 or skewed keys --
+  // would otherwise serialize every row on one device atomic)
+  extern __shared__ unsigned int hist[];
+  const bool lds = nparts <= kHashPartLds;
+  if (lds)
+    for (uint32_t i = threadIdx.x; i < nparts; i += kBlock) hist[i] = 0;
+  __syncthreads();
   for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < nrows; row += (int64_t)gridDim.x * kBlock) {
     uint64_t h = 0x243F6A8885A308D3ull;
     for (int j = 0; j < k.nkeys; ++j) {
       Chunk c;
-      load_one(c, k.cols[j], row);
+      row_word_to_chunk(c, k.cols[j], row, load_row_word(k.cols[j], row));
       uint64_t v[1];
       decode<1>(c, k.cols[j].dtype, v);
       const uint64_t bits = dtype_is_float(k.cols[j].dtype) ? canon_f64_bits(v[0]) : v[0];
@@ -442,7 +450,15 @@ __global__ __launch_bounds__(kBlock) void k_hash_partition(PartitionCols k, int6
     }
     const uint32_t p = (uint32_t)(h % nparts);
     out[row] = p;
-    atomicAdd(&counts[p], 1ull);
+    if (lds)
+      atomicAdd(&hist[p], 1u);
+    else
+      atomicAdd(&counts[p], 1ull);
+  }
+  if (lds) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nparts; i += kBlock)
+      if (hist[i]) atomicAdd(&counts[i], (unsigned long long)hist[i]);
   }
 }
 
@@ -504,7 +520,8 @@ void launch_hash_partition(const PartitionCols& k, int64_t nrows, uint32_t npart
   int64_t blocks = (nrows + kBlock - 1) / kBlock;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_hash_partition, dim3((unsigned)blocks), dim3(kBlock), 0, st, k, nrows, nparts, out, counts);
+  const size_t lds = nparts <= kHashPartLds ? (size_t)nparts * 4 : 0;
+  hipLaunchKernelGGL(k_hash_partition, dim3((unsigned)blocks), dim3(kBlock), lds, st, k, nrows, nparts, out, counts);
 }
 
 }  // namespace bqg

@@ -4,105 +4,14 @@
 
 #include <algorithm>
 
-#include "device.h"
+#include "scan_private.h"
 
 namespace bqg {
 
-// Every lane owns a private accumulator row per slot in LDS, laid out [slot][lane] so that
-// the per-row read-modify-writes are conflict-free ds_read/ds_write with no atomics.  Rows
-// of a lane are processed in increasing order, so its first write to a slot is that slot's
-// first row for the lane.  A workgroup streams tiles of 1024 rows (4 per lane, one 16-byte
-// load per 4-byte column) and prefetches the next tile while it aggregates the current one.
 template <int NC>
 __global__ __launch_bounds__(kBlock, 4) void k_scan_private(ScanParams p, PrivateLaunch L) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int S = (int)p.nslots;
-  const int tid = threadIdx.x;
-  const int nsum = p.nsum;
-  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);          // [nsum][S][256]
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)nsum * S * kBlock);   // [S][256]
-  uint32_t* fst = cnt + S * kBlock;                                                // [S][256]
-  for (int s = 0; s < S; ++s) {
-    cnt[s * kBlock + tid] = 0;
-    fst[s * kBlock + tid] = kNoRow;
-  }
-  for (int i = 0; i < nsum * S; ++i) acc[i * kBlock + tid] = 0;
-
-  const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
-  int64_t tile = blockIdx.x;
-  Chunk raw[NC];
-  if (tile < ntiles) load_rows4<NC>(p, tile * kTileRows + (int64_t)tid * kRowsPerThread, raw);
-  for (; tile < ntiles; tile += gridDim.x) {
-    const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
-    uint64_t v[NC][4];
-    decode_all<NC, 4>(p, raw, v);
-    const int64_t next = tile + gridDim.x;
-    if (next < ntiles) load_rows4<NC>(p, next * kTileRows + (int64_t)tid * kRowsPerThread, raw);
-    const uint32_t pass = vals_pass<NC, 4>(p, row0, v);
-    uint64_t code[4];
-    vals_code<NC, 4>(p, v, code);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (pass & (1u << r)) {
-        const int idx = (int)code[r] * kBlock + tid;
-        const uint32_t c0 = cnt[idx];
-        if (c0 == 0) fst[idx] = (uint32_t)(row0 + r);
-        cnt[idx] = c0 + 1;
-#pragma unroll
-        for (int s = 0; s < (NC < kMaxSums ? NC : kMaxSums); ++s) {
-          if (s < nsum) {
-            unsigned long long* a = &acc[(size_t)s * S * kBlock + idx];
-            if (p.sum_is_float[s]) {
-              double x = value_f64(v[s][r], p.sum_conv[s]);
-              if (p.sum_centered[s]) {
-                const double d = x - p.centers[s][code[r]];
-                x = d * d;
-              }
-              *a = as_u64(as_f64(*a) + x);
-            } else {
-              *a += v[s][r];
-            }
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  // workgroup reduction of the lane-private tables -> partials[comp][slot][block]
-  const int wave = tid >> 6, lane = tid & 63;
-  const int nb = gridDim.x, b = blockIdx.x;
-  for (int s = wave; s < S; s += kBlock / 64) {
-    unsigned long long c = 0;
-    uint32_t f = kNoRow;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      c += cnt[s * kBlock + lane + 64 * j];
-      f = min(f, fst[s * kBlock + lane + 64 * j]);
-    }
-    c = wave_sum_u64(c);
-    f = wave_min_u32(f);
-    if (lane == 0) {
-      L.partials[((size_t)0 * S + s) * nb + b] = c;
-      L.partials[((size_t)1 * S + s) * nb + b] = f;
-    }
-    for (int q = 0; q < nsum; ++q) {
-      const unsigned long long* a = &acc[(size_t)q * S * kBlock + s * kBlock];
-      unsigned long long out;
-      if (p.sum_is_float[q]) {
-        double x = 0.0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) x += as_f64(a[lane + 64 * j]);
-        out = as_u64(wave_sum_f64(x));
-      } else {
-        unsigned long long x = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) x += a[lane + 64 * j];
-        out = wave_sum_u64(x);
-      }
-      if (lane == 0) L.partials[((size_t)(2 + q) * S + s) * nb + b] = out;
-    }
-  }
+  scan_private_body<NC>(p, L, smem);
 }
 
 // One workgroup per (component, slot): sums / mins that slot's per-workgroup partials in a

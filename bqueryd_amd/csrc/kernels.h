@@ -90,7 +90,20 @@ struct ScdLaunch {
   uint32_t* st_changes;              // [waves][nslots]
   unsigned long long* out_changes;   // [nslots]
   unsigned long long* out_first;     // [nslots]
+  // fused variant (k_scd_fused: dense slots, small slot space): LDS match masks instead of
+  // slot-bit ballots, per-slot row counts, optional count_distinct folded into the same pass
+  int fused;                         // 1: k_scd_fused
+  size_t wave_lds;                   // bytes of LDS per wave (16-byte multiple)
+  uint32_t* st_count;                // [waves][nslots] rows per chunk (fused)
+  unsigned long long* slot_cnt;      // fused + write_slots: SlotArrays::cnt to fill
+  uint32_t* slot_fst;                // fused + write_slots: SlotArrays::fst to fill
+  DistinctLaunch cd;                 // fused: cd.bitmap != nullptr -> count_distinct too
 };
+// LDS bytes per wave of k_scd_fused for a slot space of nslots
+inline size_t scd_fused_wave_lds(uint64_t nslots) {
+  return ((size_t)nslots * 36 + 256 * 12 + 15) & ~size_t(15);
+}
+constexpr size_t kScdFusedMaxLds = 80 * 1024;  // per workgroup (4 waves + shared cd filter)
 void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st);
 
 // emit: occupied slots -> first-appearance order -> finalised output columns

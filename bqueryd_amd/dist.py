@@ -45,8 +45,11 @@ class GpuBackend:
         self.device = device or get_device()
 
     def reduce(self, table, groupby_cols, agg_list):
+        """``table``: one table or a list of tables (row-concatenated on the device)."""
         from .engine import ShardTable
-        t = ShardTable(table, device=self.device)
+        parts = table if isinstance(table, (list, tuple)) else [table]
+        names = list(groupby_cols) + [x[2] for x in agg_list]
+        t = ShardTable.from_parts(parts, names, device=self.device)
         try:
             out, _ = t.groupby(groupby_cols, sum_spec(agg_list))
             return out
@@ -77,13 +80,26 @@ class GpuBackend:
             t.close()
 
 
+class LocalExchange:
+    """World of one (no torch): the exchange is the identity."""
+    world = 1
+    rank = 0
+
+    def counts(self, send_counts):
+        return np.asarray(send_counts, np.int64)
+
+    def column(self, parts, dtype, recv_counts):
+        return np.ascontiguousarray(parts[0], dtype=np.dtype(dtype))
+
+
 class Exchange:
     """Byte all-to-all over torch.distributed (nccl = RCCL on ROCm, or gloo)."""
 
-    def __init__(self, dist, device=None):
+    def __init__(self, dist, device=None, group=None):
         self.dist = dist
-        self.world = dist.get_world_size()
-        self.rank = dist.get_rank()
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
         self.device = device
 
     def _tensor(self, arr):
@@ -97,7 +113,7 @@ class Exchange:
         r = torch.empty(self.world, dtype=torch.int64)
         if self.device is not None:
             s, r = s.to(self.device), r.to(self.device)
-        self.dist.all_to_all_single(r, s)
+        self.dist.all_to_all_single(r, s, group=self.group)
         return r.cpu().numpy()
 
     def column(self, parts, dtype, recv_counts):
@@ -110,7 +126,7 @@ class Exchange:
         out = torch.empty(sum(out_split), dtype=torch.uint8)
         if self.device is not None:
             out = out.to(self.device)
-        self.dist.all_to_all_single(out, self._tensor(send), out_split, in_split)
+        self.dist.all_to_all_single(out, self._tensor(send), out_split, in_split, group=self.group)
         return out.cpu().numpy().view(dtype)
 
 
@@ -119,9 +135,15 @@ def merge_partials(local_tables, groupby_cols, agg_list, dtypes, backend, exchan
     table on rank 0 (None elsewhere).  ``dtypes``: name -> dtype of the finalized columns
     (needed by ranks that hold no shard)."""
     names = list(groupby_cols) + [x[2] for x in agg_list]
-    local = concat_tables(local_tables, names)
-    if local is not None and len(next(iter(local.values()))):
-        local = backend.reduce(local, groupby_cols, agg_list)
+    local_tables = [t for t in local_tables
+                    if t is not None and not (isinstance(t, str) and t == '') and len(t[names[0]])]
+    if exchange.world == 1:
+        # partition / exchange / gather are the identity: one reduce of everything
+        if not local_tables:
+            return OrderedDict((n, np.zeros(0, dtypes[n])) for n in names)
+        return backend.reduce(local_tables, groupby_cols, agg_list)
+    if local_tables:
+        local = backend.reduce(local_tables, groupby_cols, agg_list)
         parts = backend.partition(local, groupby_cols, exchange.world)
     else:
         parts = [OrderedDict((n, np.zeros(0, dtypes[n])) for n in names) for _ in range(exchange.world)]

@@ -54,7 +54,7 @@ class Device:
         t = L.Timing()
         self.check(self._lib.bqg_last_timing(self.handle, ctypes.byref(t)))
         return {'scan_ms': t.scan_ms, 'scan_launches': t.scan_launches, 'total_ms': t.total_ms,
-                'rows': t.rows, 'bytes': t.bytes, 'mode': t.mode}
+                'rows': t.rows, 'bytes': t.bytes, 'mode': t.mode, 'specialized': bool(t.specialized)}
 
 
 _devices = {}
@@ -139,6 +139,28 @@ class ShardTable:
         for i, a in enumerate(arrays):
             self.push(i, a)
         self.sync()
+
+    @classmethod
+    def from_parts(cls, parts, names=None, device=None):
+        """One table holding the row-concatenation of ``parts`` (mappings name -> array), each
+        part copied straight to its row offset in HBM (no host-side concatenation; parts in
+        page-locked memory -- query results -- go by DMA without staging)."""
+        parts = [p for p in parts if p is not None]
+        names = list(names or parts[0].keys())
+        total = sum(len(p[names[0]]) for p in parts)
+        t = cls(OrderedDict(), device=device, nrows=total)
+        for n in names:
+            t.add_column(n, np.asarray(parts[0][n]).dtype)
+            t.names.append(n)
+        off = 0
+        for p in parts:
+            m = len(p[names[0]])
+            if m:
+                for n in names:
+                    t.push(n, p[n], off)
+            off += m
+        t.sync()
+        return t
 
     # ---- lifecycle
     def close(self):

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BQG_ABI_VERSION 1
+#define BQG_ABI_VERSION 2
 
 /* error codes */
 #define BQG_OK 0
@@ -118,7 +118,9 @@ typedef struct {
   double total_ms;       /* all device work of the last call */
   int64_t rows;          /* input rows scanned */
   int64_t bytes;         /* algorithmic bytes: distinct input columns x itemsize x rows + output */
-  int32_t mode;          /* 0 private-LDS, 1 shared-LDS, 2 global dense, 3 global hash */
+  int32_t mode;          /* 0 private-LDS, 1 shared-LDS, 2 global dense, 3 global hash,
+                            4 partitioned */
+  int32_t specialized;   /* 1: the scan ran a query-specialised (run-time compiled) kernel */
 } bqg_timing;
 
 /* ---------------- lifecycle ---------------- */

@@ -22,6 +22,8 @@ NSHARDS = 5
 
 class OracleBackend:
     def reduce(self, table, groupby_cols, agg_list):
+        if isinstance(table, list):
+            table = bdist.concat_tables(table)
         return bo.groupby(table, groupby_cols, bdist.sum_spec(agg_list))
 
     def partition(self, table, groupby_cols, nparts):
@@ -81,3 +83,15 @@ def test_merge_partials_gloo(world):
     ref = bo.client_merge(results, KEYS, AGGS, aggregate=True)
     merged = OrderedDict((k, np.array(v, dtype=ref[k].dtype)) for k, v in got[0].items())
     assert_tables_equal(sort_by_keys(merged, KEYS), sort_by_keys(ref, KEYS))
+
+
+def test_merge_partials_single_rank():
+    """World of one: the merge is one reduce of every local table, in client order."""
+    results = shard_results()
+    dtypes = OrderedDict((k, v.dtype) for k, v in results[0].items())
+    merged = bdist.merge_partials(results + [''], KEYS, AGGS, dtypes, OracleBackend(), bdist.LocalExchange())
+    ref = bo.client_merge(results, KEYS, AGGS, aggregate=True)
+    # same first-appearance order as the client's appended-then-regrouped table
+    assert_tables_equal(merged, ref)
+    empty = bdist.merge_partials([], KEYS, AGGS, dtypes, OracleBackend(), bdist.LocalExchange())
+    assert all(len(v) == 0 and v.dtype == dtypes[k] for k, v in empty.items())

@@ -200,3 +200,59 @@ def test_partitioned_mode(krange, terms, oracle_c):
              terms, oracle_c, exact=True)
     mask = rng.random(n) < 0.5
     run_both(cols, ['k'], [['v', 'sum', 'vs']], [], oracle_c, exact=True, mask=mask)
+
+
+@pytest.mark.parametrize('n', [1, 255, 257, 70_001, 400_000])
+def test_fused_distinct_pass(n, oracle_c, monkeypatch):
+    """count + count_distinct + sorted_count_distinct on different columns: one fused pass
+    (k_scd_fused), checked against the oracle and against the unfused kernels."""
+    rng = np.random.default_rng(n)
+    cols = OrderedDict(k=rng.integers(0, 50, n).astype(np.int16), a=rng.integers(-5, 40, n).astype(np.int32),
+                       b=np.repeat(rng.integers(0, 4, (n + 9) // 10), 10)[:n].astype(np.int64),
+                       f=rng.integers(0, 9, n).astype(np.uint8))
+    aggs = [['a', 'count', 'n'], ['a', 'count_distinct', 'acd'], ['b', 'sorted_count_distinct', 'bscd']]
+    for terms in ([], [('f', '>', 2)], [('f', 'in', [0, 8])]):
+        got = run_both(cols, ['k'], aggs, terms, oracle_c)
+        monkeypatch.setenv('BQGPU_NO_FUSED_SCD', '1')
+        t = ShardTable(cols)
+        ref, _ = t.groupby(['k'], aggs, where_terms=terms)
+        t.close()
+        monkeypatch.delenv('BQGPU_NO_FUSED_SCD')
+        assert_tables_equal(got, ref)
+    # float value column for the sorted distinct, first row filtered out
+    cols['b'] = (cols['b'] * 0.5).astype(np.float64)
+    cols['f'][0] = 0
+    run_both(cols, ['k'], [['b', 'sorted_count_distinct', 's'], ['b', 'count', 'c']], [('f', '>', 0)], oracle_c)
+
+
+@pytest.mark.parametrize('case', range(6))
+def test_specialised_private_scan(case, oracle_c, monkeypatch):
+    """The run-time specialised (hiprtc) private scan against the oracle, forced on at small
+    sizes; the precompiled generic kernel must give the same table."""
+    monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
+    n = 300_001
+    rng = np.random.default_rng(100 + case)
+    cols = synth.taxi_shard(n, config_id=2, columns=('payment_type', 'passenger_count', 'fare_amount'))
+    cols['k8'] = rng.integers(-3, 4, n).astype(np.int8)
+    cols['u16'] = rng.integers(0, 7, n).astype(np.uint16)
+    cols['i64'] = rng.integers(-2**40, 2**40, n)
+    cols['f32'] = (np.round(rng.normal(size=n) * 16) / 16).astype(np.float32)
+    cases = [
+        (['payment_type'], C2['aggs'], C2['where']),
+        (['k8'], [['fare_amount', 'sum', 's'], ['i64', 'sum', 'i'], ['f32', 'mean', 'm']],
+         [('passenger_count', 'in', [1, 3, 5])]),
+        (['u16'], [['fare_amount', 'std', 'sd'], ['passenger_count', 'count', 'c']], [('fare_amount', '<=', 12.25)]),
+        ([], [['fare_amount', 'sum', 's'], ['k8', 'sum', 'k']], [('k8', '!=', 0), ('u16', '>', 1)]),
+        (['k8'], [['i64', 'mean', 'm'], ['u16', 'sum', 'u']], []),
+        (['payment_type'], [['f32', 'sum', 'f']], [('f32', '>', 0.5), ('passenger_count', 'nin', [2])]),
+    ]
+    keys, aggs, terms = cases[case]
+    got = run_both(cols, keys, aggs, terms, oracle_c)
+    t = ShardTable(cols)
+    t.groupby(keys, aggs, where_terms=terms)
+    assert t.dev.last_timing()['specialized'], 'specialised kernel did not run'
+    monkeypatch.setenv('BQGPU_JIT', '0')
+    ref, _ = t.groupby(keys, aggs, where_terms=terms)
+    assert not t.dev.last_timing()['specialized']
+    t.close()
+    assert_tables_equal(got, ref, exact_float_sums=True)

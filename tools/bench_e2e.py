@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""End-to-end C1 measurement (BASELINE.json configs[0]): the whole bqueryd message path.
+
+C1 = 10 shards x 1 M rows on disk as bcolz ctables, ``groupby(['payment_type'],
+[['fare_amount', 'sum', 'fare_amount']], aggregate=True)``.  One query =
+
+  worker: CalcPath.handle_work per shard (worker.py:269-348: open ctable, groupby, write the
+          result ctable, tar it)  ->  controller: tar of tars (controller.py:146-221)  ->
+  client: rpc.uncompress_groupby_to_df(aggregate=True) (rpc.py:134-179).
+
+Legs (each the best of ``--reps``):
+  gpu_warm   shards resident in HBM (ShardCache hit: the steady state of a worker)
+  gpu_cold   fresh cache: bcolz decode on the host + H2D copy + query (PCIe-inclusive)
+  cpu_port   the same path with the C port of bquery (oracle/cbquery.c) as the calc, on
+             already-decoded columns, ``--cpu-workers`` processes (one shard per task) and the
+             oracle's client merge -- the reference's architecture on this host's cores.
+
+This is a latency-shaped end-to-end figure (per-message Python + file + tar overheads dominate
+at 1 M rows/shard); the headline device throughput is bench.py.  Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import shutil
+import sys
+import tempfile
+import time
+from collections import OrderedDict
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+GROUPBY = ['payment_type']
+AGGS = [['fare_amount', 'sum', 'fare_amount']]
+COLS = ('payment_type', 'fare_amount')
+
+
+def _cpu_task(args):
+    path, = args
+    from bqueryd_amd import bcolz_io
+    from oracle import cbquery
+    cols = bcolz_io.read_ctable(path, columns=list(COLS), nthreads=1)
+    t0 = time.perf_counter()
+    out = cbquery.handle_work(cols, GROUPBY, AGGS, [])
+    return out, time.perf_counter() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--shards', type=int, default=10)
+    ap.add_argument('--rows', type=int, default=1_000_000)
+    ap.add_argument('--reps', type=int, default=5)
+    ap.add_argument('--cpu-workers', type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument('--no-gpu', action='store_true')
+    args = ap.parse_args()
+
+    from bqueryd_amd import bcolz_io, messages, rpc, synth
+    from oracle import bquery_oracle as bo
+    from oracle import cbquery
+    cbquery.build()
+
+    data_dir = tempfile.mkdtemp(prefix='bqgpu_c1_')
+    try:
+        files, shards = [], []
+        for i in range(args.shards):
+            cols = synth.taxi_shard(args.rows, config_id=1, n_shards=args.shards, shard=i, columns=COLS)
+            fn = 'tripdata-%d.bcolzs' % i
+            bcolz_io.write_ctable(os.path.join(data_dir, fn), cols)
+            files.append(fn)
+            shards.append(cols)
+        ref = bo.client_merge([bo.handle_work(s, GROUPBY, AGGS, []) for s in shards], GROUPBY, AGGS,
+                              aggregate=True)
+        ref = dict(zip(ref['payment_type'].tolist(), ref['fare_amount'].tolist()))
+        total_rows = args.shards * args.rows
+        line = {'workload': 'C1 end-to-end: %d bcolz shards x %d rows, groupby %s sum fare_amount, '
+                            'aggregate=True' % (args.shards, args.rows, GROUPBY),
+                'rows': total_rows}
+
+        def check(df):
+            got = dict(zip(df['payment_type'].tolist(), df['fare_amount'].tolist()))
+            assert set(got) == set(ref), (sorted(got), sorted(ref))
+            for k in ref:
+                assert abs(got[k] - ref[k]) <= 1e-12 * max(1.0, abs(ref[k])), (k, got[k], ref[k])
+
+        def msg_for(fn):
+            m = messages.CalcMessage({'payload': 'groupby', 'token': 'ab' * 8, 'filename': fn})
+            m.set_args_kwargs([fn, GROUPBY, AGGS, []], {'aggregate': True})
+            return m
+
+        if not args.no_gpu:
+            from bqueryd_amd.engine import get_device
+            from bqueryd_amd.worker import CalcPath, ShardCache
+            dev = get_device()
+
+            def gpu_query(calc):
+                t0 = time.perf_counter()
+                replies = OrderedDict((fn, calc.handle_work(msg_for(fn))['data']) for fn in files)
+                t1 = time.perf_counter()
+                df = rpc.uncompress_groupby_to_df(rpc.tar_of_tars(replies), GROUPBY, AGGS, [], aggregate=True,
+                                                  device=dev)
+                t2 = time.perf_counter()
+                check(df)
+                return t2 - t0, t1 - t0, t2 - t1
+
+            calc = CalcPath(data_dir, device=dev)
+            gpu_query(calc)  # warm the cache
+            warm = min((gpu_query(calc) for _ in range(args.reps)), key=lambda x: x[0])
+            cold = min((gpu_query(CalcPath(data_dir, device=dev, cache=ShardCache(device=dev)))
+                        for _ in range(args.reps)), key=lambda x: x[0])
+            line['gpu_warm'] = {'s_per_query': warm[0], 'worker_s': warm[1], 'client_merge_s': warm[2],
+                                'rows_per_s': total_rows / warm[0]}
+            line['gpu_cold'] = {'s_per_query': cold[0], 'worker_s': cold[1], 'client_merge_s': cold[2],
+                                'rows_per_s': total_rows / cold[0],
+                                'note': 'includes bcolz decode on the host and the H2D copy'}
+
+        # CPU: the reference's architecture (one calc per shard on a pool of worker processes)
+        ctx = mp.get_context('fork')
+        with ctx.Pool(args.cpu_workers) as pool:
+            pool.map(_cpu_task, [(os.path.join(data_dir, files[0]),)])
+            best = None
+            for _ in range(args.reps):
+                t0 = time.perf_counter()
+                res = pool.map(_cpu_task, [(os.path.join(data_dir, fn),) for fn in files])
+                merged = bo.client_merge([r[0] for r in res], GROUPBY, AGGS, aggregate=True)
+                dt = time.perf_counter() - t0
+                calc_s = sum(r[1] for r in res)
+                if best is None or dt < best[0]:
+                    best = (dt, calc_s)
+            check(merged)
+        line['cpu_port'] = {'s_per_query': best[0], 'rows_per_s': total_rows / best[0],
+                            'calc_core_s': best[1], 'workers': args.cpu_workers, 'kind': 'port',
+                            'note': 'bcolz decode + oracle/cbquery.c calc per shard in worker processes, '
+                                    'oracle client merge'}
+        print(json.dumps(line), flush=True)
+    finally:
+        shutil.rmtree(data_dir, ignore_errors=True)
+
+
+if __name__ == '__main__':
+    main()
