@@ -24,6 +24,7 @@
 
 #include "kernels.h"
 #include "jit.h"
+#include "ingest.h"
 
 using namespace bqg;
 
@@ -109,10 +110,11 @@ struct HostBuf {
 
 size_t dtype_size(int dt) { return size_t(1) << dtype_lg(dt); }
 
-// Column allocations cover whole 1024-row tiles plus 256 bytes: every lane of the last
-// (partial) tile issues its full-width load in bounds, so the scans need no tail branch.
+// Column allocations cover whole 1024-row tiles plus 4096 rows plus 256 bytes: every lane of
+// the last (partial) tile issues its full-width load in bounds, and so does a prefetch of up
+// to 4096 rows that starts before the last row, so the scans need no tail branch.
 size_t column_bytes(int64_t nrows, int dtype) {
-  const size_t rows = ((size_t)nrows + kTileRows - 1) / kTileRows * kTileRows;
+  const size_t rows = ((size_t)nrows + kTileRows - 1) / kTileRows * kTileRows + 4096;
   return (rows << dtype_lg(dtype)) + 256;
 }
 
@@ -461,7 +463,17 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
   for (int i = 0; i < pl.p.ncols; ++i) {
     const Column& col = t->cols[pl.tcol[i]];
     pl.p.cols[i] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
-    pl.alg_bytes += (int64_t)dtype_size(col.dtype) * t->nrows;
+  }
+  // algorithmic bytes: every distinct input column the query reads, once --
+  // keys, where-term / mask columns and aggregated columns (count_distinct and
+  // sorted_count_distinct value columns are not scan columns of the main pass)
+  {
+    std::vector<int> distinct(pl.tcol.begin(), pl.tcol.end());
+    for (int a = 0; a < q->n_aggs; ++a)
+      if ((q->aggs[a].op == BQG_COUNT_DISTINCT || q->aggs[a].op == BQG_SORTED_COUNT_DISTINCT) &&
+          std::find(distinct.begin(), distinct.end(), q->aggs[a].col) == distinct.end())
+        distinct.push_back(q->aggs[a].col);
+    for (int tc : distinct) pl.alg_bytes += (int64_t)dtype_size(t->cols[tc].dtype) * t->nrows;
   }
   pl.p.nrows = t->nrows;
   // 4. mode
@@ -480,8 +492,11 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
         dk.range = 0;
         continue;
       }
+      // the field of a packed key is a power of two wide: emit decodes (code / stride) % range
+      const uint64_t b = bits_for(dk.range);
       dk.stride = 1ull << shift;
-      shift += bits_for(dk.range);
+      dk.range = 1ull << b;
+      shift += b;
     }
     uint64_t est = std::min<uint64_t>((uint64_t)std::max<int64_t>(t->nrows, 1), 1ull << 26);
     uint64_t cap = 1024;
@@ -504,12 +519,23 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
       pl.mode = kPrivate;
     else if (pl.nslots * per_slot_shared <= 64 * 1024) pl.mode = kShared;
     else {
-      // partitioned aggregation: 2^wbits slots of LDS state per partition, <= 8192 partitions
+      // partitioned aggregation: 2^wbits slots of LDS state per partition (64 KiB: two
+      // aggregate workgroups per CU; up to 128 KiB when the slot space needs it), at most
+      // kPartMaxParts partitions
+      const size_t per_slot = 8 + 8 * (size_t)pl.nsum;
       int wbits = 12;
-      while (wbits > 6 && ((size_t)1 << wbits) * (8 + 8 * (size_t)pl.nsum) > 64 * 1024) --wbits;
+      if (const char* ev = getenv("BQGPU_PART_WBITS")) wbits = std::max(6, std::min(13, atoi(ev)));
+      while (wbits > 6 && ((size_t)1 << wbits) * per_slot > 128 * 1024) --wbits;
+      if (!getenv("BQGPU_PART_WBITS") && ((size_t)2 << wbits) * per_slot <= 128 * 1024) ++wbits;  // fewer, longer runs
+      while (((pl.nslots + (1ull << wbits) - 1) >> wbits) > (uint64_t)kPartMaxParts &&
+             ((size_t)2 << wbits) * per_slot <= 128 * 1024)
+        ++wbits;
       pl.wbits = wbits;
       const uint64_t parts = (pl.nslots + (1ull << wbits) - 1) >> wbits;
-      pl.mode = (parts <= 8192 && getenv("BQGPU_NO_PARTITION") == nullptr) ? kPartitioned : kGlobalDense;
+      pl.mode = (parts <= (uint64_t)kPartMaxParts && part_scatter_lds((int)parts, 256, pl.nsum) <= 150 * 1024 &&
+                 getenv("BQGPU_NO_PARTITION") == nullptr)
+                    ? kPartitioned
+                    : kGlobalDense;
     }
   }
   pl.p.nslots = pl.nslots;
@@ -762,21 +788,44 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       PartLaunch L{};
       L.wbits = pl.wbits;
       L.nparts = (int)((S + (1ull << pl.wbits) - 1) >> pl.wbits);
-      const int64_t ptile = 4096;  // rows per 1024-thread count/scatter iteration
+      // scatter workgroup: the widest whose staged tile fits in LDS (BQGPU_PART_THREADS caps it)
+      L.threads = 1024;
+      if (const char* ev = getenv("BQGPU_PART_THREADS")) L.threads = std::max(256, std::min(1024, atoi(ev)));
+      while (L.threads > 256 && part_scatter_lds(L.nparts, L.threads, nsum) > 150 * 1024) L.threads >>= 1;
+      int per_cu = 2;  // count / scatter workgroups per CU (two 58 KiB scatter workgroups share a CU)
+      if (const char* ev = getenv("BQGPU_PART_PER_CU")) per_cu = std::max(1, std::min(8, atoi(ev)));
+      L.load_mask = 0;
+      for (int k = 0; k < pl.p.nkeys; ++k) L.load_mask |= 1u << pl.p.keys[k].col;
+      for (int i = 0; i < pl.p.nterms; ++i) L.load_mask |= 1u << pl.p.terms[i].col;
+      if (pl.p.mask_col >= 0) L.load_mask |= 1u << pl.p.mask_col;
+      // contiguous row ranges, whole 4096-row tiles (a multiple of every scatter tile), at
+      // most 2^(32 - wbits) rows each so that (row - begin) << wbits | slot_low fits 32 bits
+      const int64_t ptile = 4096;
       const int64_t ptiles = (N + ptile - 1) / ptile;
-      L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->cu, ptiles));
+      const int64_t max_tiles_per_block = std::max<int64_t>(1, (int64_t(1) << (32 - pl.wbits)) / ptile);
+      L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, ptiles));
+      L.blocks = (int)std::max<int64_t>(L.blocks, (ptiles + max_tiles_per_block - 1) / max_tiles_per_block);
       L.rows_per_block = ((ptiles + L.blocks - 1) / L.blocks) * ptile;
-      L.splits = std::max(1, (2 * c->cu + L.nparts - 1) / L.nparts);
-      L.capacity = (uint64_t)N;
+      L.splits = std::max(1, std::min(L.blocks, (2 * c->cu + L.nparts - 1) / L.nparts));
+      L.capacity = ((uint64_t)N + 3) & ~3ull;  // 16-byte aligned value arrays
       const size_t ncounts = (size_t)L.nparts * L.blocks + 1;
-      unsigned char* pb = (unsigned char*)c->prefix.ensure(ncounts * 4 + (size_t)(L.nparts + 1) * 4 +
-                                                           (2 * (ncounts / 1024 + 2) + 4096) * 4 + 1024);
+      unsigned char* pb = (unsigned char*)c->prefix.ensure(ncounts * 4 + (2 * (ncounts / 1024 + 2) + 4096) * 4 + 1024);
       L.counts = (uint32_t*)pb;
-      L.part_start = L.counts + ncounts;
-      uint32_t* scan_scratch = L.part_start + L.nparts + 1;
-      L.entries = (unsigned long long*)c->bitmap.ensure((size_t)N * 8 * (1 + std::max(nsum, 0)) + 256);
+      uint32_t* scan_scratch = L.counts + ncounts + 1;
+      const size_t vbytes = ((size_t)L.capacity * 8 * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
+      unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + (size_t)L.capacity * 4 + 512);
+      L.vals = (unsigned long long*)eb;
+      L.meta = (uint32_t*)(eb + vbytes);
       HIPCHECK(hipMemsetAsync(L.counts + ncounts - 1, 0, 4, st));
-      launch_partitioned(pl.p, sa, L, scan_scratch, st);
+      hipFunction_t fc = nullptr, fs = nullptr;
+      if (N >= jit_min_rows()) {
+        const std::string spec = jit_spec(pl.p);
+        fc = jit_function("bq_jit_part_count", spec);
+        fs = fc ? jit_function("bq_jit_part_scatter", spec) : nullptr;
+        if (!fs) fc = nullptr;
+        c->last.specialized = fc ? 1 : 0;
+      }
+      launch_partitioned(pl.p, sa, L, scan_scratch, st, fc, fs);
     } else {
       launch_scan_global(pl.p, sa, scan_blocks(c, N, 8), st);
     }
@@ -1270,6 +1319,28 @@ int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows, i
       dst += n;
       left -= n;
     }
+  });
+}
+
+int bqg_table_load_carray(bqg_table* t, int32_t col, const char* carray_dir, int64_t chunklen, int32_t nthreads) {
+  bqg_ctx* c = t->ctx;
+  return guard(c, [&] {
+    if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
+    if (!carray_dir) fail(BQG_E_INVALID, "null carray directory");
+    if (chunklen <= 0) fail(BQG_E_INVALID, "chunklen must be positive");
+    Column& k = t->cols[col];
+    k.stats.valid = false;
+    HIPCHECK(hipStreamSynchronize(c->stream));  // the column's zero-fill has landed
+    IngestJob job;
+    job.device = c->device;
+    job.dev_dst = k.dev;
+    job.carray_dir = carray_dir;
+    job.nrows = t->nrows;
+    job.itemsize = (int)dtype_size(k.dtype);
+    job.chunklen = chunklen;
+    job.nthreads = nthreads;
+    std::string err;
+    if (ingest_carray(job, nullptr, err) != 0) fail(BQG_E_INVALID, "%s", err.c_str());
   });
 }
 

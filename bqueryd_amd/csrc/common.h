@@ -6,6 +6,7 @@
 #include <stdint.h>
 #else
 typedef struct ihipStream_t* hipStream_t;  // host launchers are declared, never defined, in JIT code
+typedef struct ihipModuleSymbol_t* hipFunction_t;
 #endif
 
 #include "../../include/bqgpu.h"

@@ -10,6 +10,27 @@
 
 namespace bqg {
 
+// Loops over a query's terms / keys: in a query-specialised (JIT) build the bound is the
+// array size and the loop unrolls, so every ScanParams access has a constant index and the
+// specialised parameter copy stays in registers (a dynamic index would put the whole struct
+// in scratch memory and re-read it after every workgroup barrier).
+#ifdef BQ_NC
+#define BQ_LOOP_BOUND(n, maxn) (maxn)
+#else
+#define BQ_LOOP_BOUND(n, maxn) (n)
+#endif
+
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup-scope fence on all
+// address spaces: it waits for every outstanding global load and store (vmcnt(0)), which
+// drains a tile's prefetched loads and streaming stores at each barrier.  Kernels whose
+// workgroups exchange data through LDS only use this instead (s_waitcnt lgkmcnt(0) +
+// s_barrier).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ------------------------------------------------------------------------------------
 // wave64 reductions (fixed butterfly order: bitwise deterministic)
 // ------------------------------------------------------------------------------------
@@ -206,7 +227,9 @@ template <int NC, int R>
 __device__ __forceinline__ uint32_t vals_pass(const ScanParams& p, int64_t row0, const uint64_t (&v)[NC][R]) {
   const int64_t rem = p.nrows - row0;
   uint32_t pass = rem >= R ? ((1u << R) - 1u) : (rem > 0 ? ((1u << rem) - 1u) : 0u);
-  for (int t = 0; t < p.nterms; ++t) {
+#pragma unroll
+  for (int t = 0; t < BQ_LOOP_BOUND(p.nterms, kMaxTerms); ++t) {
+    if (t >= p.nterms) break;
     const DevTerm& tm = p.terms[t];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
@@ -230,7 +253,9 @@ template <int NC, int R>
 __device__ __forceinline__ void vals_code(const ScanParams& p, const uint64_t (&v)[NC][R], uint64_t (&code)[R]) {
 #pragma unroll
   for (int r = 0; r < R; ++r) code[r] = 0;
-  for (int k = 0; k < p.nkeys; ++k) {
+#pragma unroll
+  for (int k = 0; k < BQ_LOOP_BOUND(p.nkeys, kMaxKeys); ++k) {
+    if (k >= p.nkeys) break;
     const DevKey& key = p.keys[k];
 #pragma unroll
     for (int c = 0; c < NC; ++c)

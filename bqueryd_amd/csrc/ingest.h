@@ -1,0 +1,32 @@
+// ingest.h -- host-side bcolz carray -> HBM column loader (ingest.hip), used by
+// bqg_table_load_carray (api.hip).
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+
+namespace bqg {
+
+struct IngestJob {
+  int device;              // HIP device of the destination column
+  void* dev_dst;           // device column (>= nrows * itemsize bytes)
+  std::string carray_dir;  // bcolz carray rootdir (holds data/__<i>.blp)
+  int64_t nrows;           // items of the carray
+  int itemsize;            // bytes per item
+  int64_t chunklen;        // items per chunk (meta/storage "chunklen")
+  int nthreads;            // host decode threads (<= 0: 8)
+};
+
+struct IngestStats {
+  int64_t chunks = 0;
+  int64_t compressed_bytes = 0;
+  int64_t bytes = 0;
+  int threads = 0;
+};
+
+// Decodes every chunk into dev_dst; returns 0, or -1 with a message in err.  Synchronous:
+// the column is complete in HBM when it returns.
+int ingest_carray(const IngestJob& job, IngestStats* stats, std::string& err);
+
+}  // namespace bqg

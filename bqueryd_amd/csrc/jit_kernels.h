@@ -7,6 +7,7 @@
 // (scan_private.h), so both paths compute the same thing.
 #pragma once
 
+#include "partition.h"
 #include "scan_private.h"
 
 namespace bqg {
@@ -18,4 +19,18 @@ extern "C" __global__ __launch_bounds__(256, 4) void bq_jit_scan_private(bqg::Sc
   bqg::ScanParams p = pin;
   bqg::jit_specialize(p);
   bqg::scan_private_body<BQ_NC>(p, L, smem);
+}
+
+extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_count(bqg::ScanParams pin, bqg::PartLaunch L) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  bqg::ScanParams p = pin;
+  bqg::jit_specialize(p);
+  bqg::part_count_body<BQ_NC>(p, L, smem);
+}
+
+extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_scatter(bqg::ScanParams pin, bqg::PartLaunch L) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  bqg::ScanParams p = pin;
+  bqg::jit_specialize(p);
+  bqg::part_scatter_body<BQ_NC>(p, L, smem);
 }

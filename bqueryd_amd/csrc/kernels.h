@@ -137,19 +137,31 @@ void launch_select_gather(const unsigned char* mask, int64_t nrows,
                           void* const* outs, hipStream_t st);
 
 // Partitioned aggregation (large dense slot spaces): count -> scan -> scatter -> aggregate
+constexpr int kPartMaxParts = 4096;
 struct PartLaunch {
   int wbits;                 // slots per partition = 2^wbits
-  int nparts;
+  int nparts;                // <= kPartMaxParts
   int blocks;                // workgroups of the count / scatter passes
-  int splits;                // aggregate workgroups per partition
-  int64_t rows_per_block;    // contiguous rows per count/scatter workgroup (multiple of 4096)
+  int splits;                // aggregate workgroups per partition (block ranges)
+  int threads;               // threads of a scatter workgroup (4 rows each per tile)
+  uint32_t load_mask;        // scan columns the count pass reads (keys, terms, mask)
+  int64_t rows_per_block;    // contiguous rows per count/scatter workgroup: a multiple of the
+                             // scatter tile and <= 2^(32 - wbits) (row-in-block | slot_low
+                             // packs into one 32-bit word)
   uint64_t capacity;         // entry capacity (>= passing rows)
   uint32_t* counts;          // [nparts * blocks + 1] -> exclusive offsets in place
-  uint32_t* part_start;      // [nparts + 1]
-  unsigned long long* entries;  // [capacity][1 + nsum]: (row << 32) | slot_low, then values
+  uint32_t* meta;            // [capacity]: (row - block begin) << wbits | slot_low
+  unsigned long long* vals;  // [nsum][capacity]: summed values (canonical 64-bit)
 };
+// LDS bytes of a scatter workgroup: the staged tile (meta, destination, values), tile
+// counts / offsets, region cursors and two sets of scan totals
+inline size_t part_scatter_lds(int nparts, int threads, int nsum) {
+  return (size_t)threads * 4 * (8 + 8 * (size_t)nsum) + (size_t)nparts * 12 + 2 * 16 * 4;
+}
+// fcount / fscatter: query-specialised (JIT) count / scatter kernels, or nullptr for the
+// precompiled generic ones
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, PartLaunch L, uint32_t* scan_scratch,
-                        hipStream_t st);
+                        hipStream_t st, hipFunction_t fcount = nullptr, hipFunction_t fscatter = nullptr);
 void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipStream_t st);
 
 // cross-rank merge: partition id of every row from its key values

@@ -148,16 +148,21 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
             if n not in self._dtypes:
                 raise KeyError(str(n))
         if self._table is None:
-            self._table = ShardTable(OrderedDict((n, self._host_column(n)) for n in names),
-                                     device=self.device, nrows=self._len)
-        else:
-            missing = [n for n in names if n not in self._table.dtypes]
-            for n in missing:
-                arr = self._host_column(n)
-                self._table.add_column(n, arr.dtype)
-                self._table.push(n, arr)
-            if missing:
-                self._table.sync()
+            self._table = ShardTable(OrderedDict(), device=self.device, nrows=self._len)
+        missing = [n for n in names if n not in self._table.dtypes]
+        for n in missing:
+            self._table.add_column(n, self._dtypes[n])
+            self._table.names.append(n)
+            if n in self._host:
+                self._table.push(n, self._host[n])
+            else:
+                # cold path: the bcolz chunks decode on host threads straight into HBM
+                meta = bcolz_io.CArrayMeta(bcolz_io.ctable_column_dir(self.rootdir, n))
+                if meta.length != self._len:
+                    raise ValueError('column %s has %d rows, table has %d' % (n, meta.length, self._len))
+                self._table.load_carray(n, meta.rootdir, meta.chunklen)
+        if missing:
+            self._table.sync()
         return self._table
 
     def _table_for_terms(self, terms):

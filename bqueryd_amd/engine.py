@@ -190,6 +190,14 @@ class ShardTable:
         self.dev.check(self._lib.bqg_push_chunk(self.handle, self.slot(col), a.ctypes.data,
                                                 len(a), int(row_offset)))
 
+    def load_carray(self, col, carray_dir, chunklen, nthreads=None):
+        """Decode a bcolz carray directory straight into device column ``col`` (host decode
+        threads, pinned double-buffered DMA; statistics follow at the next ``sync``)."""
+        if not nthreads:
+            nthreads = int(os.environ.get('BQGPU_INGEST_THREADS', '0')) or min(16, len(os.sched_getaffinity(0)))
+        self.dev.check(self._lib.bqg_table_load_carray(self.handle, self.slot(col), os.fsencode(carray_dir),
+                                                       int(chunklen), int(nthreads)))
+
     def sync(self):
         self.dev.check(self._lib.bqg_table_sync(self.handle))
 

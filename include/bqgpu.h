@@ -148,6 +148,15 @@ int bqg_table_add_column(bqg_table* t, int32_t dtype, int32_t* slot_out);
 /* Copy rows [row_offset, row_offset + nrows) of column `col` from host memory. */
 int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows,
                    int64_t row_offset);
+/* Cold-path ingest (worker.py:291 bquery.ctable(rootdir) + bcolz's per-chunk blosc decode,
+ * which bqueryd runs on one thread, worker.py:40): decode the bcolz carray directory
+ * `carray_dir` (data/__<i>.blp, one blosc frame of `chunklen` items each) straight into
+ * column `col` -- `nthreads` host threads decompress chunks into page-locked double buffers
+ * and DMA them with hipMemcpyAsync while the next chunk decodes.  The carray must hold the
+ * table's row count of items of the column's dtype.  Synchronous; statistics are recomputed
+ * by the next bqg_table_sync. */
+int bqg_table_load_carray(bqg_table* t, int32_t col, const char* carray_dir, int64_t chunklen,
+                          int32_t nthreads);
 /* Wait for pushes and compute per-column statistics (min / max / has_nan). */
 int bqg_table_sync(bqg_table* t);
 int bqg_table_column_ptr(bqg_table* t, int32_t col, void** dev_ptr);

@@ -86,6 +86,17 @@ def test_hash_mode_wide_keys(oracle_c):
     run_both(cols, ['k'], [['v', 'sum', 'vs']], [('v', '<', 10)], oracle_c)
 
 
+def test_hash_mode_multi_key(oracle_c):
+    """Two keys whose product exceeds the dense slot space: packed power-of-two fields whose
+    ranges (500 000 and 200) are not powers of two."""
+    rng = np.random.default_rng(12)
+    n = 200_000
+    cols = OrderedDict(a=rng.integers(0, 500_000, n).astype(np.int32), b=rng.integers(0, 200, n).astype(np.uint8),
+                       v=np.round(rng.normal(size=n) * 64) / 64)
+    run_both(cols, ['a', 'b'], [['v', 'sum', 's'], ['v', 'count', 'c']], [], oracle_c, exact=True)
+    run_both(cols, ['b', 'a'], [['v', 'mean', 'm']], [('b', '>', 7)], oracle_c)
+
+
 def test_float_key(oracle_c):
     rng = np.random.default_rng(8)
     n = 20_000
@@ -202,6 +213,17 @@ def test_partitioned_mode(krange, terms, oracle_c):
     run_both(cols, ['k'], [['v', 'sum', 'vs']], [], oracle_c, exact=True, mask=mask)
 
 
+def test_partitioned_four_sums(oracle_c):
+    """Four summed columns: the scatter stages a narrower tile (512 threads) in LDS."""
+    rng = np.random.default_rng(7)
+    n = 300_001
+    cols = OrderedDict(k=rng.integers(-700_000, 700_000, n).astype(np.int32),
+                       a=np.round(rng.normal(size=n) * 64) / 64, b=rng.integers(-9, 9, n).astype(np.int8),
+                       c=rng.integers(0, 1 << 40, n).astype(np.uint64), d=rng.random(n).astype(np.float32))
+    run_both(cols, ['k'], [['a', 'sum', 'as'], ['b', 'sum', 'bs'], ['c', 'sum', 'cs'], ['d', 'mean', 'dm'],
+                           ['a', 'count', 'n']], [('b', '!=', 0)], oracle_c, exact=True)
+
+
 @pytest.mark.parametrize('n', [1, 255, 257, 70_001, 400_000])
 def test_fused_distinct_pass(n, oracle_c, monkeypatch):
     """count + count_distinct + sorted_count_distinct on different columns: one fused pass
@@ -251,6 +273,35 @@ def test_specialised_private_scan(case, oracle_c, monkeypatch):
     t = ShardTable(cols)
     t.groupby(keys, aggs, where_terms=terms)
     assert t.dev.last_timing()['specialized'], 'specialised kernel did not run'
+    monkeypatch.setenv('BQGPU_JIT', '0')
+    ref, _ = t.groupby(keys, aggs, where_terms=terms)
+    assert not t.dev.last_timing()['specialized']
+    t.close()
+    assert_tables_equal(got, ref, exact_float_sums=True)
+
+
+@pytest.mark.parametrize('case', range(3))
+def test_specialised_partitioned(case, oracle_c, monkeypatch):
+    """The run-time specialised (hiprtc) partition count / scatter kernels against the oracle,
+    forced on at small sizes; the precompiled generic kernels must give the same table."""
+    monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
+    n = 500_003
+    rng = np.random.default_rng(200 + case)
+    cols = synth.taxi_shard(n, config_id=3, columns=synth.query_columns(C3) + ['passenger_count'])
+    cols['k64'] = rng.integers(-2**20, 2**20, n)
+    cols['u8'] = rng.integers(0, 200, n).astype(np.uint8)
+    cases = [
+        (C3['groupby'], C3['aggs'], C3['where']),
+        (['k64'], [['fare_amount', 'mean', 'm'], ['u8', 'sum', 'u'], ['k64', 'count', 'c']],
+         [('passenger_count', '>=', 2)]),
+        (['pickup_location'], [['fare_amount', 'sum', 's']], [('u8', 'nin', [3, 4, 5])]),
+    ]
+    keys, aggs, terms = cases[case]
+    got = run_both(cols, keys, aggs, terms, oracle_c)
+    t = ShardTable(cols)
+    t.groupby(keys, aggs, where_terms=terms)
+    timing = t.dev.last_timing()
+    assert timing['mode'] == 4 and timing['specialized'], timing
     monkeypatch.setenv('BQGPU_JIT', '0')
     ref, _ = t.groupby(keys, aggs, where_terms=terms)
     assert not t.dev.last_timing()['specialized']
