@@ -1018,12 +1018,21 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       const uint64_t grain = fused ? 256 : 64;  // fused: 256-row groups, 4 rows per lane
       if (fused) {
         d.fused = 1;
-        d.wave_lds = scd_fused_wave_lds(S);
+        // compact 32-bit value codes for integer value columns spanning < 2^32
+        compute_stats(t, tc);
+        if (!dtype_is_float(col.dtype) && !getenv("BQGPU_SCD_WIDE")) {
+          const uint64_t vr = col.stats.empty ? 1 : (uint64_t)col.stats.imax - (uint64_t)col.stats.imin + 1;
+          if (vr != 0 && vr <= 0xFFFFFFFFull) {
+            d.compact = 1;
+            d.vmin = col.stats.empty ? 0 : col.stats.imin;
+          }
+        }
+        d.wave_lds = scd_fused_wave_lds(S, d.compact != 0);
         d.cd = fused_cd;
         const size_t blk_lds = (kBlock / 64) * d.wave_lds + (size_t)fused_cd.lds_bitmap_words * 4;
         if (blk_lds > kScdFusedMaxLds) d.cd.lds_bitmap_words = 0;  // no LDS pre-filter
         const size_t lds = (kBlock / 64) * d.wave_lds + (size_t)d.cd.lds_bitmap_words * 4;
-        const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(4, (160 * 1024) / lds));
+        const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
         waves = (uint64_t)c->cu * per_cu * (kBlock / 64);
       }
       const uint64_t needg = ((uint64_t)N + grain - 1) / grain;
@@ -1051,8 +1060,14 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       }
       d.out_changes = so + (size_t)i * S * 2;
       d.out_first = d.out_changes + S;
+      hipFunction_t sfn = nullptr;
+      if (fused && N >= jit_min_rows()) {
+        const std::string spec = jit_spec(pc.p) + "#define BQ_SLOT_BITS " + std::to_string(d.slot_bits) + "\n";
+        sfn = jit_function(d.compact ? "bq_jit_scd_fused32" : "bq_jit_scd_fused", spec);
+        c->last.specialized = sfn ? 1 : 0;
+      }
       if (fused && c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
-      launch_scd(pc.p, sa, d, st);
+      launch_scd(pc.p, sa, d, st, sfn);
       HIPCHECK(hipGetLastError());
       if (fused && c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));
       e.scd_changes[i] = d.out_changes;

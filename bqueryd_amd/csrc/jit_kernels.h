@@ -8,6 +8,7 @@
 #pragma once
 
 #include "partition.h"
+#include "scd.h"
 #include "scan_private.h"
 
 namespace bqg {
@@ -33,4 +34,18 @@ extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_scatter(bqg::Scan
   bqg::ScanParams p = pin;
   bqg::jit_specialize(p);
   bqg::part_scatter_body<BQ_NC>(p, L, smem);
+}
+
+extern "C" __global__ __launch_bounds__(256) void bq_jit_scd_fused(bqg::ScanParams pin, bqg::ScdLaunch d) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  bqg::ScanParams p = pin;
+  bqg::jit_specialize(p);
+  bqg::scd_fused_body<BQ_NC, false>(p, d, smem);
+}
+
+extern "C" __global__ __launch_bounds__(256) void bq_jit_scd_fused32(bqg::ScanParams pin, bqg::ScdLaunch d) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  bqg::ScanParams p = pin;
+  bqg::jit_specialize(p);
+  bqg::scd_fused_body<BQ_NC, true>(p, d, smem);
 }

@@ -3,7 +3,7 @@
 
 #include <algorithm>
 
-#include "device.h"
+#include "scd.h"
 
 namespace bqg {
 
@@ -48,8 +48,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_count_distinct(ScanParams p, Slot
         const uint64_t bit = s * d.vrange + vcode;
         const unsigned int m = 1u << (bit & 31);
         if (d.lds_bitmap_words > 0) {
-          if (lbits[bit >> 5] & m) continue;  // hot pairs: a broadcast read, no atomic
-          if (atomicOr(&lbits[bit >> 5], m) & m) continue;
+          if (!(lbits[bit >> 5] & m)) atomicOr(&lbits[bit >> 5], m);  // merged into the device bitmap at the end
+          continue;
         }
         if (d.bitmap[bit >> 5] & m) continue;
         if (!(atomicOr(&d.bitmap[bit >> 5], m) & m)) atomicAdd(&d.out[s], 1ull);
@@ -75,6 +75,20 @@ __global__ __launch_bounds__(kBlock, 4) void k_count_distinct(ScanParams p, Slot
       }
     }
   }
+  // merge the workgroup's pair bitmap; every pair bit it sets first counts once for its slot
+  if (d.bitmap && d.lds_bitmap_words > 0) {
+    __syncthreads();
+    for (int i = tid; i < d.lds_bitmap_words; i += kBlock) {
+      const unsigned int word = lbits[i];
+      if (!word) continue;
+      unsigned int fresh = word & ~atomicOr(&d.bitmap[i], word);
+      while (fresh) {
+        const int b = __ffs(fresh) - 1;
+        fresh &= fresh - 1u;
+        atomicAdd(&d.out[((uint64_t)i * 32 + (uint64_t)b) / d.vrange], 1ull);
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -83,9 +97,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_count_distinct(ScanParams p, Slot
 // inside a 64-row step are resolved with ballots, so the whole chunk is processed in row
 // order.  Chunk states are then combined in chunk order (k_scd_combine).
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ bool scd_equal(uint64_t a, uint64_t b, bool isf) {
-  return isf ? (as_f64(a) == as_f64(b)) : (a == b);
-}
 
 constexpr int kScdU = 4;
 
@@ -213,150 +224,12 @@ __global__ __launch_bounds__(kBlock, 4) void k_scd(ScanParams p, SlotArrays sa, 
 }
 
 
-// ------------------------------------------------------------------------------------
-// k_scd_fused: sorted_count_distinct for small dense slot spaces, with the per-slot row
-// counts / first rows (so the generic scan can be skipped for count / distinct-only queries)
-// and optionally one count_distinct, in ONE pass over the rows.
-//
-// Each wave owns a contiguous chunk.  It loads 256 rows at a time the coalesced way (4 rows
-// per lane, 16-byte loads, next group prefetched), decodes / filters / codes them once, and
-// transposes (slot, value) through LDS so that it can then walk the 256 rows in row order,
-// 64 at a time.  Inside a 64-row step, the lanes of one slot find each other through an LDS
-// match-mask table (ds_or_b64 of the lane bit, read back): the previous row of a slot is
-// the highest lower lane in the mask, the slot's first lane updates the per-slot state
-// {last value, rows, changes} once for the whole step.
-// ------------------------------------------------------------------------------------
-__device__ __forceinline__ void wave_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-template <int NC>
-__global__ __launch_bounds__(kBlock, 2) void k_scd_fused(ScanParams p, ScdLaunch d) {
+// k_scd_fused: sorted_count_distinct + per-slot rows / first rows (+ one count_distinct) in
+// one pass -- body in scd.h
+template <int NC, bool COMPACT>
+__global__ __launch_bounds__(kBlock) void k_scd_fused(ScanParams p, ScdLaunch d) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int S = (int)p.nslots;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  unsigned char* wb = smem + (size_t)wave * d.wave_lds;
-  uint4* st = reinterpret_cast<uint4*>(wb);                                   // [S] {last lo, last hi, rows, changes}
-  unsigned long long* tbl = reinterpret_cast<unsigned long long*>(st + S);    // [S] match masks
-  unsigned long long* fv = tbl + S;                                           // [S] first value
-  unsigned long long* vl = fv + S;                                            // [256] transposed values
-  uint32_t* fr = reinterpret_cast<uint32_t*>(vl + 256);                       // [S] first row
-  uint32_t* sl = fr + S;                                                      // [256] transposed slots
-  unsigned int* cdb = reinterpret_cast<unsigned int*>(smem + (size_t)(kBlock / 64) * d.wave_lds);
-  for (int i = lane; i < S; i += 64) {
-    st[i] = make_uint4(0u, 0u, 0u, 0u);
-    tbl[i] = 0ull;
-    fr[i] = kNoRow;
-  }
-  const bool do_cd = d.cd.bitmap != nullptr;
-  for (int i = threadIdx.x; i < d.cd.lds_bitmap_words; i += kBlock) cdb[i] = 0u;
-  __syncthreads();
-  const int w = blockIdx.x * (kBlock / 64) + wave;
-  if (w >= d.waves) return;
-  const int64_t start = (int64_t)w * d.chunk_rows;
-  const int64_t end = min(start + d.chunk_rows, p.nrows);
-  int vc = 0, cc = 0;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    if (d.vcol == c) vc = c;
-    if (d.cd.vcol == c) cc = c;
-  }
-  const bool isf = dtype_is_float(p.cols[vc].dtype);
-  Chunk raw[NC];
-  if (start < end) load_rows4<NC>(p, start + 4 * lane, raw);
-  for (int64_t gbase = start; gbase < end; gbase += 256) {
-    const int64_t row0 = gbase + 4 * lane;
-    uint64_t v[NC][4];
-    decode_all<NC, 4>(p, raw, v);
-    if (gbase + 256 < end) load_rows4<NC>(p, row0 + 256, raw);
-    uint32_t pass = vals_pass<NC, 4>(p, row0, v);
-    const int64_t rem = end - row0;
-    pass &= rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
-    uint64_t code[4];
-    vals_code<NC, 4>(p, v, code);
-    uint64_t vb[4], vcd[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      vb[r] = 0;
-      vcd[r] = 0;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        if (vc == c) vb[r] = v[c][r];
-        if (cc == c) vcd[r] = v[c][r];
-      }
-    }
-    if (do_cd) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (!(pass & (1u << r))) continue;
-        const uint64_t bit = code[r] * d.cd.vrange + (vcd[r] - (uint64_t)d.cd.vmin);
-        const unsigned int m = 1u << (bit & 31);
-        if (d.cd.lds_bitmap_words > 0) {
-          if (cdb[bit >> 5] & m) continue;
-          if (atomicOr(&cdb[bit >> 5], m) & m) continue;
-        }
-        if (d.cd.bitmap[bit >> 5] & m) continue;
-        if (!(atomicOr(&d.cd.bitmap[bit >> 5], m) & m)) atomicAdd(&d.cd.out[code[r]], 1ull);
-      }
-    }
-    wave_fence();  // the previous group's reads of sl / vl are done
-    *reinterpret_cast<uint4*>(&sl[4 * lane]) =
-        make_uint4((pass & 1u) ? (uint32_t)code[0] : kNoRow, (pass & 2u) ? (uint32_t)code[1] : kNoRow,
-                   (pass & 4u) ? (uint32_t)code[2] : kNoRow, (pass & 8u) ? (uint32_t)code[3] : kNoRow);
-    *reinterpret_cast<ulonglong2*>(&vl[4 * lane]) = make_ulonglong2(vb[0], vb[1]);
-    *reinterpret_cast<ulonglong2*>(&vl[4 * lane + 2]) = make_ulonglong2(vb[2], vb[3]);
-    wave_fence();
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t s = sl[64 * u + lane];
-      const unsigned long long x = vl[64 * u + lane];
-      const bool act = s != kNoRow;
-      const unsigned long long self = 1ull << lane;
-      if (act) atomicOr(&tbl[s], self);
-      wave_fence();
-      const unsigned long long match = act ? tbl[s] : 0ull;
-      const unsigned long long below = match & (self - 1ull);
-      const int pl = below ? 63 - __clzll((long long)below) : lane;
-      const int hl = match ? 63 - __clzll((long long)match) : lane;
-      const unsigned long long pv = __shfl(x, pl, 64);     // previous row of the slot in this step
-      const unsigned long long lastv = __shfl(x, hl, 64);  // last row of the slot in this step
-      const bool is_first = act && below == 0;
-      uint4 cur = make_uint4(0u, 0u, 0u, 0u);
-      bool diff = false;
-      if (is_first) {
-        cur = st[s];
-        const unsigned long long lv = ((unsigned long long)cur.y << 32) | cur.x;
-        diff = cur.z != 0u && !scd_equal(lv, x, isf);
-      } else if (act) {
-        diff = !scd_equal(x, pv, isf);
-      }
-      const unsigned long long dm = __ballot(diff);
-      wave_fence();  // every lane has read tbl[s]
-      if (is_first) {
-        if (cur.z == 0u) {
-          fr[s] = (uint32_t)(gbase + 64 * u + lane);
-          fv[s] = x;
-        }
-        cur.x = (uint32_t)lastv;
-        cur.y = (uint32_t)(lastv >> 32);
-        cur.z += (uint32_t)__popcll(match);
-        cur.w += (uint32_t)__popcll(dm & match);
-        st[s] = cur;
-        tbl[s] = 0ull;
-      }
-    }
-  }
-  wave_fence();
-  for (int i = lane; i < S; i += 64) {
-    const uint4 c = st[i];
-    const size_t o = (size_t)w * S + i;
-    d.st_first_row[o] = fr[i];
-    d.st_first[o] = fv[i];
-    d.st_last[o] = ((unsigned long long)c.y << 32) | c.x;
-    d.st_changes[o] = c.w;
-    d.st_count[o] = c.z;
-  }
+  scd_fused_body<NC, COMPACT>(p, d, smem);
 }
 
 struct ScdState {
@@ -427,11 +300,20 @@ void launch_count_distinct(const ScanParams& p, const SlotArrays& s, const Disti
     BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_count_distinct<NC, false>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
   }
 }
-void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st) {
+void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st, hipFunction_t fused_fn) {
   const int blocks = (d.waves + (kBlock / 64) - 1) / (kBlock / 64);
   if (d.fused) {
     const size_t lds = (kBlock / 64) * d.wave_lds + (size_t)d.cd.lds_bitmap_words * 4;
-    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd_fused<NC>), dim3(blocks), dim3(kBlock), lds, st, p, d));
+    if (fused_fn) {
+      void* args[] = {(void*)&p, (void*)&d};
+      (void)hipModuleLaunchKernel(fused_fn, (unsigned)blocks, 1, 1, kBlock, 1, 1, (unsigned)lds, st, args, nullptr);
+    } else {
+      if (d.compact) {
+        BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd_fused<NC, true>), dim3(blocks), dim3(kBlock), lds, st, p, d));
+      } else {
+        BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd_fused<NC, false>), dim3(blocks), dim3(kBlock), lds, st, p, d));
+      }
+    }
   } else {
     const size_t lds = d.lds_state ? (size_t)(kBlock / 64) * p.nslots * 24 : 0;
     if (p.hash) {

@@ -98,13 +98,18 @@ struct ScdLaunch {
   unsigned long long* slot_cnt;      // fused + write_slots: SlotArrays::cnt to fill
   uint32_t* slot_fst;                // fused + write_slots: SlotArrays::fst to fill
   DistinctLaunch cd;                 // fused: cd.bitmap != nullptr -> count_distinct too
+  int compact;                       // fused: 32-bit value codes (integer values, range < 2^32)
+  int64_t vmin;                      // compact: value code = v - vmin
 };
-// LDS bytes per wave of k_scd_fused for a slot space of nslots
-inline size_t scd_fused_wave_lds(uint64_t nslots) {
-  return ((size_t)nslots * 36 + 256 * 12 + 15) & ~size_t(15);
+// LDS bytes per wave of k_scd_fused for a slot space of nslots: a 32-byte state per slot, or
+// 20 bytes with compact (32-bit) value codes
+inline size_t scd_fused_wave_lds(uint64_t nslots, bool compact = false) {
+  return (((size_t)nslots * (compact ? 20 : 32)) + 15) & ~size_t(15);
 }
 constexpr size_t kScdFusedMaxLds = 80 * 1024;  // per workgroup (4 waves + shared cd filter)
-void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st);
+// fused_fn: query-specialised (JIT) k_scd_fused, or nullptr for the precompiled kernel
+void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st,
+                hipFunction_t fused_fn = nullptr);
 
 // emit: occupied slots -> first-appearance order -> finalised output columns
 void launch_compact(const SlotArrays& s, uint64_t nslots, uint32_t* list_fst,

@@ -64,16 +64,18 @@ __device__ __forceinline__ uint32_t block_excl_scan_1b(uint32_t v, uint32_t* wsu
 // count / scatter: workgroups of up to 1024 threads, each over a contiguous row range
 constexpr int kPartBlock = 1024;
 
-// A thread's 4-row chunk of the columns in `mask`, or zeros when the chunk starts at or past
-// `end` (the last workgroup's prefetch must not run past the padded column allocations).
+// A thread's 4-row chunk of the columns in `mask`, loaded unconditionally: a chunk at or past
+// `end` re-reads the block's last chunk (its rows are masked off by the caller), and a column
+// outside `mask` re-reads its own first chunk at `home` (one cache line for the whole wave:
+// no HBM traffic to speak of).  Every path keeps the same number of loads in flight, so the
+// compiler waits for exactly the chunk it consumes (vmcnt(N)) instead of draining the
+// prefetch (vmcnt(0)).
 template <int NC>
-__device__ __forceinline__ void load_rows4_guard(const ScanParams& p, int64_t row0, int64_t end, Chunk (&raw)[NC],
-                                                 uint32_t mask) {
+__device__ __forceinline__ void load_rows4_clamped(const ScanParams& p, int64_t row0, int64_t end, Chunk (&raw)[NC],
+                                                   uint32_t mask, int64_t home) {
+  const int64_t r = row0 < end ? row0 : ((end - 1) & ~(int64_t)(kRowsPerThread - 1));
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    if (((mask >> c) & 1u) && row0 < end) load_chunk(raw[c], p.cols[c], row0);
-    else raw[c] = Chunk{make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u), 0u};
-  }
+  for (int c = 0; c < NC; ++c) load_chunk(raw[c], p.cols[c], ((mask >> c) & 1u) ? r : home);
 }
 
 // Each thread keeps kCountChunks 4-row chunks of the key columns in flight (16 rows), so a
@@ -90,10 +92,15 @@ __device__ __forceinline__ void part_count_body(const ScanParams& p, const PartL
   lds_barrier();
   const int64_t begin = (int64_t)blockIdx.x * L.rows_per_block;
   const int64_t end = (p.nrows < begin + L.rows_per_block ? p.nrows : begin + L.rows_per_block);
+  if (begin >= end) {
+    for (int i = tid; i < L.nparts; i += T) L.counts[(size_t)i * gridDim.x + blockIdx.x] = 0u;
+    return;
+  }
+  const int64_t home = begin;
   Chunk raw[kCountChunks][NC];
 #pragma unroll
   for (int u = 0; u < kCountChunks; ++u)
-    load_rows4_guard<NC>(p, begin + (int64_t)u * step + (int64_t)tid * kRowsPerThread, end, raw[u], L.load_mask);
+    load_rows4_clamped<NC>(p, begin + (int64_t)u * step + (int64_t)tid * kRowsPerThread, end, raw[u], L.load_mask, home);
   for (int64_t base = begin; base < end; base += tile) {
     uint32_t part[kCountChunks][4], pass[kCountChunks];
 #pragma unroll
@@ -110,8 +117,8 @@ __device__ __forceinline__ void part_count_body(const ScanParams& p, const PartL
     }
 #pragma unroll
     for (int u = 0; u < kCountChunks; ++u)
-      load_rows4_guard<NC>(p, base + tile + (int64_t)u * step + (int64_t)tid * kRowsPerThread, end, raw[u],
-                           L.load_mask);
+      load_rows4_clamped<NC>(p, base + tile + (int64_t)u * step + (int64_t)tid * kRowsPerThread, end, raw[u],
+                             L.load_mask, home);
 #pragma unroll
     for (int u = 0; u < kCountChunks; ++u)
 #pragma unroll
@@ -151,13 +158,13 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   const int q1 = min(P, q0 + per);
   const uint32_t all = (1u << NC) - 1u;
   Chunk raw[NC];
-  load_rows4_guard<NC>(p, begin + (int64_t)tid * kRowsPerThread, end, raw, all);
+  if (begin < end) load_rows4_clamped<NC>(p, begin + (int64_t)tid * kRowsPerThread, end, raw, all, begin);
   int parity = 0;
   for (int64_t base = begin; base < end; base += tile, parity ^= 1) {
     const int64_t row0 = base + (int64_t)tid * kRowsPerThread;
     uint64_t v[NC][4], code[4];
     decode_all<NC, 4>(p, raw, v);
-    load_rows4_guard<NC>(p, row0 + tile, end, raw, all);
+    load_rows4_clamped<NC>(p, row0 + tile, end, raw, all, begin);
     uint32_t pass = vals_pass<NC, 4>(p, row0, v);
     if (end - row0 < 4) pass &= (end - row0 > 0) ? ((1u << (end - row0)) - 1u) : 0u;
     vals_code<NC, 4>(p, v, code);

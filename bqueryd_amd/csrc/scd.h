@@ -1,0 +1,223 @@
+// scd.h -- body of the fused sorted_count_distinct pass (config C4), shared by the
+// precompiled kernel (k_distinct.hip) and the query-specialised JIT kernel (jit_kernels.h).
+//
+// sorted_count_distinct counts, per group and in row order, the rows whose value differs
+// from the previous row OF THE SAME GROUP (bquery's `last[g]` loop, with its zero-initialised
+// `last` and first-row rule applied at emit).  Each wave owns a contiguous chunk of rows and
+// consumes it 64 rows per step in row order, one row per lane (coalesced 4- or 8-byte loads,
+// kScdAhead steps in flight).  Inside a step the lanes of one slot find each other with one
+// ballot per slot-id bit (no LDS traffic); the previous row of a slot inside the step is the
+// highest lower lane of its match mask (one bpermute); the slot's first lane in the step
+// folds the whole step into the per-slot state {last, first, rows, changes, first row} in LDS
+// with one read and one write.  Per-slot row counts and first rows come out of the same pass
+// (so count / distinct-only queries need no other scan), and one count_distinct over a small
+// (slot, value) space is folded in through a per-workgroup LDS pair bitmap that is merged
+// into the device-wide bitmap once, at the end of the workgroup.  Chunk states are combined in chunk order by k_scd_combine.
+#pragma once
+
+#include "device.h"
+
+namespace bqg {
+
+// Per-slot chunk state.  Wide: 64-bit value bits (floats, or integer value spaces of 2^32 and
+// more).  Compact: 32-bit value codes (v - vmin), so that a slot's state is 16 bytes plus its
+// first row and twice as many waves fit in LDS.
+struct __align__(16) ScdSlot {
+  unsigned long long last;   // value bits of the slot's last row so far
+  unsigned long long first;  // value bits of the slot's first row in the chunk
+  uint32_t rows;             // rows of the slot in the chunk (0: absent)
+  uint32_t changes;          // value changes between consecutive rows of the slot
+  uint32_t first_row;
+  uint32_t pad;
+};
+struct __align__(16) ScdSlot32 {
+  uint32_t last, first, rows, changes;
+};
+
+constexpr int kScdAhead = 4;  // 64-row steps loaded ahead of the one being folded
+
+__device__ __forceinline__ bool scd_equal(uint64_t a, uint64_t b, bool isf) {
+  return isf ? (as_f64(a) == as_f64(b)) : (a == b);
+}
+
+template <int NC>
+__device__ __forceinline__ void scd_issue(const ScanParams& p, int64_t b, int64_t end, int lane, uint2 (&dst)[NC]) {
+  int64_t r = b + lane;
+  r = r < end ? r : end - 1;  // lanes past the chunk re-read its last row (end > start)
+#pragma unroll
+  for (int c = 0; c < NC; ++c) dst[c] = load_row_word(p.cols[c], r);
+}
+
+template <int NC, bool COMPACT>
+__device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLaunch& d, unsigned char* smem) {
+  const int S = (int)p.nslots;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char* wbase = smem + (size_t)wave * d.wave_lds;
+  ScdSlot* st = reinterpret_cast<ScdSlot*>(wbase);        // wide state [S]
+  ScdSlot32* st32 = reinterpret_cast<ScdSlot32*>(wbase);  // compact state [S] ...
+  uint32_t* fr32 = reinterpret_cast<uint32_t*>(st32 + S); // ... + first rows [S]
+  unsigned int* cdb = reinterpret_cast<unsigned int*>(smem + (size_t)(blockDim.x >> 6) * d.wave_lds);
+  for (int i = lane; i < S; i += 64) {
+    if (COMPACT) {
+      st32[i] = ScdSlot32{0u, 0u, 0u, 0u};
+      fr32[i] = kNoRow;
+    } else {
+      st[i] = ScdSlot{0ull, 0ull, 0u, 0u, kNoRow, 0u};
+    }
+  }
+  const bool do_cd = d.cd.bitmap != nullptr;
+  for (int i = threadIdx.x; i < d.cd.lds_bitmap_words; i += blockDim.x) cdb[i] = 0u;
+  __syncthreads();
+  const int w = blockIdx.x * (blockDim.x >> 6) + wave;
+  const bool live = w < d.waves;  // every wave stays for the block's final count_distinct flush
+  const int64_t start = live ? (int64_t)w * d.chunk_rows : 0;
+  const int64_t end = live ? min(start + d.chunk_rows, p.nrows) : 0;
+  int vc = 0, cc = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (d.vcol == c) vc = c;
+    if (d.cd.vcol == c) cc = c;
+  }
+  const bool isf = !COMPACT && dtype_is_float(p.cols[vc].dtype);
+  const uint64_t lanes_below = (1ull << lane) - 1ull;
+  uint2 ring[kScdAhead][NC];
+  if (start < end) {
+#pragma unroll
+    for (int a = 0; a < kScdAhead; ++a) scd_issue<NC>(p, start + 64 * a, end, lane, ring[a]);
+  }
+  for (int64_t gbase = start; gbase < end; gbase += 64 * kScdAhead) {
+#pragma unroll
+    for (int a = 0; a < kScdAhead; ++a) {
+      const int64_t b = gbase + 64 * a;
+      if (b >= end) break;
+      const int64_t row = b + lane;
+      Chunk raw[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) row_word_to_chunk(raw[c], p.cols[c], row, ring[a][c]);
+      // unconditional (clamped) prefetch: the same number of loads is in flight on every
+      // path, so the compiler waits for exactly the step it consumes (vmcnt(N), not vmcnt(0))
+      scd_issue<NC>(p, b + 64 * kScdAhead, end, lane, ring[a]);
+      uint64_t v[NC][1];
+      decode_all<NC, 1>(p, raw, v);
+      const bool act = row < end && (vals_pass<NC, 1>(p, row, v) & 1u);
+      uint64_t code[1];
+      vals_code<NC, 1>(p, v, code);
+      const uint32_t s = (uint32_t)code[0];
+      uint64_t vb = 0, vcd = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (vc == c) vb = v[c][0];
+        if (cc == c) vcd = v[c][0];
+      }
+      if (COMPACT) vb = (uint32_t)(vb - (uint64_t)d.vmin);
+      if (do_cd && act) {
+        // (slot, value) pair bit: an LDS fire-and-forget OR (merged into the device bitmap once
+        // per workgroup at the end); without an LDS bitmap, the device bitmap directly
+        const uint64_t bit = (uint64_t)s * d.cd.vrange + (vcd - (uint64_t)d.cd.vmin);
+        const unsigned int m = 1u << (bit & 31);
+        if (d.cd.lds_bitmap_words > 0) {
+          // read first: lanes of one word broadcast; only a new pair pays the (serialising)
+          // same-address atomic
+          if (!(cdb[bit >> 5] & m)) atomicOr(&cdb[bit >> 5], m);
+        } else if (!(d.cd.bitmap[bit >> 5] & m) && !(atomicOr(&d.cd.bitmap[bit >> 5], m) & m)) {
+          atomicAdd(&d.cd.out[s], 1ull);
+        }
+      }
+      // lanes of this lane's slot: one ballot per slot-id bit
+      uint64_t match = __ballot(act);
+      if (match == 0) continue;
+#ifdef BQ_SLOT_BITS
+#pragma unroll
+      for (int bit = 0; bit < BQ_SLOT_BITS; ++bit) {  // JIT: slot-id width is a constant
+#else
+      for (int bit = 0; bit < d.slot_bits; ++bit) {
+#endif
+        const bool on = (s >> bit) & 1u;
+        const uint64_t bb = __ballot(act && on);
+        match &= on ? bb : ~bb;
+      }
+      const uint64_t below = match & lanes_below;
+      const int pl = below ? 63 - __clzll((long long)below) : lane;
+      const int hl = (act && match) ? 63 - __clzll((long long)match) : lane;
+      uint64_t pv, lastv;
+      if (COMPACT) {
+        pv = (uint32_t)__shfl((int)(uint32_t)vb, pl, 64);     // previous row of the slot in this step
+        lastv = (uint32_t)__shfl((int)(uint32_t)vb, hl, 64);  // last row of the slot in this step
+      } else {
+        pv = __shfl(vb, pl, 64);
+        lastv = __shfl(vb, hl, 64);
+      }
+      const bool diff = act && below != 0 && !scd_equal(vb, pv, isf);
+      const uint64_t dm = __ballot(diff);
+      if (act && below == 0) {
+        const uint32_t add_rows = (uint32_t)__popcll(match), add_ch = (uint32_t)__popcll(dm & match);
+        if (COMPACT) {
+          ScdSlot32 cur = st32[s];
+          uint32_t ch = cur.changes + add_ch;
+          if (cur.rows == 0) {
+            cur.first = (uint32_t)vb;
+            fr32[s] = (uint32_t)row;
+          } else if (cur.last != (uint32_t)vb) {
+            ch += 1u;
+          }
+          cur.last = (uint32_t)lastv;
+          cur.rows += add_rows;
+          cur.changes = ch;
+          st32[s] = cur;
+        } else {
+          ScdSlot cur = st[s];
+          uint32_t ch = cur.changes + add_ch;
+          if (cur.rows == 0) {
+            cur.first = vb;
+            cur.first_row = (uint32_t)row;
+          } else if (!scd_equal(cur.last, vb, isf)) {
+            ch += 1u;
+          }
+          cur.last = lastv;
+          cur.rows += add_rows;
+          cur.changes = ch;
+          st[s] = cur;
+        }
+      }
+    }
+  }
+  // count_distinct: merge the workgroup's pair bitmap into the device bitmap; every pair bit
+  // this workgroup sets first counts once for its slot
+  if (do_cd && d.cd.lds_bitmap_words > 0) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < d.cd.lds_bitmap_words; i += blockDim.x) {
+      const unsigned int word = cdb[i];
+      if (!word) continue;
+      unsigned int fresh = word & ~atomicOr(&d.cd.bitmap[i], word);
+      while (fresh) {
+        const int b = __ffs(fresh) - 1;
+        fresh &= fresh - 1u;
+        atomicAdd(&d.cd.out[((uint64_t)i * 32 + (uint64_t)b) / d.cd.vrange], 1ull);
+      }
+    }
+  }
+  if (!live) return;
+  // every lane's state writes precede the flush reads (wave-private LDS, program order)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (int i = lane; i < S; i += 64) {
+    const size_t o = (size_t)w * S + i;
+    if (COMPACT) {
+      const ScdSlot32 c = st32[i];
+      d.st_first_row[o] = c.rows ? fr32[i] : kNoRow;
+      d.st_first[o] = (uint64_t)d.vmin + c.first;
+      d.st_last[o] = (uint64_t)d.vmin + c.last;
+      d.st_changes[o] = c.changes;
+      d.st_count[o] = c.rows;
+    } else {
+      const ScdSlot c = st[i];
+      d.st_first_row[o] = c.rows ? c.first_row : kNoRow;
+      d.st_first[o] = c.first;
+      d.st_last[o] = c.last;
+      d.st_changes[o] = c.changes;
+      d.st_count[o] = c.rows;
+    }
+  }
+}
+
+}  // namespace bqg

@@ -224,10 +224,14 @@ def test_partitioned_four_sums(oracle_c):
                            ['a', 'count', 'n']], [('b', '!=', 0)], oracle_c, exact=True)
 
 
+@pytest.mark.parametrize('jit', [False, True])
 @pytest.mark.parametrize('n', [1, 255, 257, 70_001, 400_000])
-def test_fused_distinct_pass(n, oracle_c, monkeypatch):
+def test_fused_distinct_pass(n, jit, oracle_c, monkeypatch):
     """count + count_distinct + sorted_count_distinct on different columns: one fused pass
-    (k_scd_fused), checked against the oracle and against the unfused kernels."""
+    (k_scd_fused; precompiled or run-time specialised), checked against the oracle and against
+    the unfused kernels."""
+    if jit:
+        monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
     rng = np.random.default_rng(n)
     cols = OrderedDict(k=rng.integers(0, 50, n).astype(np.int16), a=rng.integers(-5, 40, n).astype(np.int32),
                        b=np.repeat(rng.integers(0, 4, (n + 9) // 10), 10)[:n].astype(np.int64),
