@@ -28,9 +28,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
-MODES = ['private-lds', 'shared-lds', 'global-dense', 'global-hash', 'partitioned']
+MODES = ['private-lds', 'shared-lds', 'global-dense', 'global-hash', 'partitioned', 'fused-distinct']
 KERNELS = ['k_scan_private', 'k_scan_shared', 'k_scan_global', 'k_scan_global<hash>',
-           'k_part_count+scan+scatter+aggregate (timed together)']
+           'k_part_count+scan+scatter+aggregate (timed together)',
+           'k_scd_fused (rows + count_distinct + sorted_count_distinct in one pass)']
 
 
 def _dist_env():
@@ -148,20 +149,23 @@ def main(argv=None):
         dtypes = {n: np.asarray(v).dtype for n, v in probe.items()}
         if ws > 1:
             import torch
-            exchange = bdist.Exchange(comm.dist, device=torch.device('cuda', local), group=comm.nccl_group)
+            exchange = bdist.DeviceExchange(comm.dist, device=torch.device('cuda', local), group=comm.nccl_group)
         else:
             exchange = bdist.LocalExchange()
         backend = bdist.GpuBackend(dev)
 
         def step():
+            # per-shard results stay in HBM; the merge (local sum, hash partition, RCCL
+            # all-to-all, reduce, gather to rank 0) runs on device buffers
             per = []
             t0 = time.perf_counter()
             for t in tables:
-                out, _ = t.groupby(cfg['groupby'], cfg['aggs'])
+                per.append(t.groupby_table(cfg['groupby'], cfg['aggs']))
                 timings.append(dev.last_timing())
-                per.append(out)
             t1 = time.perf_counter()
-            merged = bdist.merge_partials(per, cfg['groupby'], cfg['aggs'], dtypes, backend, exchange)
+            merged = bdist.merge_partials_device(per, cfg['groupby'], cfg['aggs'], dtypes, backend, exchange)
+            for p in per:
+                p.close()
             phase.append((t1 - t0, time.perf_counter() - t1))
             return merged
     else:
@@ -223,7 +227,8 @@ def main(argv=None):
         return
     if phase:
         cfg_extra = {'shard_queries_ms_per_step': 1e3 * float(np.mean([p[0] for p in phase])),
-                     'merge_ms_per_step': 1e3 * float(np.mean([p[1] for p in phase]))}
+                     'merge_ms_per_step': 1e3 * float(np.mean([p[1] for p in phase])),
+                'merge': 'device-resident: per-shard results in HBM, merged without host copies'}
     else:
         cfg_extra = {}
     line = {

@@ -97,6 +97,10 @@ _PROTOS = {
     'bqg_groupby': ([_P, _P, ctypes.POINTER(Query), ctypes.POINTER(_P)], ctypes.c_int),
     'bqg_select_rows': ([_P, _P, ctypes.POINTER(Query), _I32, _P, ctypes.POINTER(_P)],
                         ctypes.c_int),
+    'bqg_groupby_table': ([_P, _P, ctypes.POINTER(Query), ctypes.POINTER(_P)], ctypes.c_int),
+    'bqg_select_rows_table': ([_P, _P, ctypes.POINTER(Query), _I32, _P, ctypes.POINTER(_P)],
+                              ctypes.c_int),
+    'bqg_table_nrows': ([_P, ctypes.POINTER(_I64)], ctypes.c_int),
     'bqg_result_view_get': ([_P, ctypes.POINTER(ResultView)], ctypes.c_int),
     'bqg_hash_partition': ([_P, _P, _I32, _P, _I32, _I32, _P], ctypes.c_int),
     'bqg_result_free': ([_P], ctypes.c_int),

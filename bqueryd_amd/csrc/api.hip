@@ -17,6 +17,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -215,8 +216,52 @@ struct bqg_result {
   std::vector<const void*> ptrs;
 };
 
+// Column memory of short-lived tables (query results kept in HBM, merge inputs, masks) is
+// recycled instead of hipMalloc/hipFree per table (hipFree synchronises the device): freed
+// blocks wait in size order, at most kMaxIdle bytes of them.
+struct ColumnPool {
+  std::multimap<size_t, void*> idle;  // capacity -> block
+  size_t idle_bytes = 0;
+  static constexpr size_t kMaxIdle = size_t(8) << 30;
+  void* get(size_t bytes, size_t* cap) {
+    auto it = idle.lower_bound(bytes);
+    if (it != idle.end() && it->first <= bytes + bytes / 2 + (size_t(1) << 20)) {
+      void* p = it->second;
+      *cap = it->first;
+      idle_bytes -= it->first;
+      idle.erase(it);
+      return p;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      // release the idle blocks and retry once
+      release();
+      if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    }
+    *cap = bytes;
+    return p;
+  }
+  void put(void* p, size_t cap) {
+    if (!p) return;
+    idle.emplace(cap, p);
+    idle_bytes += cap;
+    while (idle_bytes > kMaxIdle && !idle.empty()) {
+      auto last = std::prev(idle.end());
+      idle_bytes -= last->first;
+      (void)hipFree(last->second);
+      idle.erase(last);
+    }
+  }
+  void release() {
+    for (auto& kv : idle) (void)hipFree(kv.second);
+    idle.clear();
+    idle_bytes = 0;
+  }
+};
+
 struct bqg_ctx {
   int device = 0;
+  ColumnPool colpool;
   int cu = 256;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
@@ -233,6 +278,9 @@ struct bqg_ctx {
   // so a result may outlive its context
   std::shared_ptr<PinnedPool> pool = std::make_shared<PinnedPool>();
   PinnedBlock pool_get(size_t bytes) { return pool->get(bytes); }
+  // set by bqg_groupby_table / bqg_select_rows_table: the result becomes a new device table
+  // (device-to-device copies of the output columns) instead of a host result
+  bqg_table** dev_target = nullptr;
   // timing
   bool timing = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -626,6 +674,57 @@ bqg_result* block_result(bqg_ctx* c, PinnedBlock b, int64_t n, int filtered, con
   return r;
 }
 
+// Column storage from the context's pool; zero_all: zero the whole allocation (public table
+// creation), else only the padding past the last row (the caller fills the rows).
+void alloc_column(bqg_ctx* c, Column& col, int64_t nrows, bool zero_all) {
+  const size_t need = column_bytes(nrows, col.dtype);
+  size_t cap = 0;
+  col.dev = (unsigned char*)c->colpool.get(need, &cap);
+  if (!col.dev) fail(BQG_E_OOM, "device allocation of a column (%zu bytes) failed", need);
+  col.bytes = cap;
+  const size_t used = zero_all ? 0 : (size_t)nrows * dtype_size(col.dtype);
+  HIPCHECK(hipMemsetAsync(col.dev + used, 0, cap - used, c->stream));
+}
+
+// Result as a new device table: device-to-device copies of the output columns (dev_target).
+void table_from_device(bqg_ctx* c, const std::vector<int>& dts, const std::vector<const void*>& src, int64_t n) {
+  std::unique_ptr<bqg_table> t(new bqg_table());
+  t->ctx = c;
+  t->nrows = n;
+  for (int dt : dts) {
+    Column col;
+    col.dtype = dt;
+    t->cols.push_back(col);
+  }
+  struct Undo {
+    bqg_table* t;
+    ~Undo() {
+      if (t)
+        for (Column& col : t->cols) t->ctx->colpool.put(col.dev, col.bytes);
+    }
+  } undo{t.get()};
+  for (Column& col : t->cols) alloc_column(c, col, n, false);
+  for (size_t j = 0; j < dts.size(); ++j)
+    if (n > 0) HIPCHECK(hipMemcpyAsync(t->cols[j].dev, src[j], (size_t)n * dtype_size(dts[j]), hipMemcpyDeviceToDevice, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  undo.t = nullptr;
+  *c->dev_target = t.release();
+}
+
+// Small host result (empty tables, the zero-key 'Total' row) as a new device table.
+void table_from_host_result(bqg_ctx* c, bqg_result* r) {
+  std::unique_ptr<bqg_result> own(r);
+  bqg_table* t = nullptr;
+  const int rc = bqg_table_create(c, r->n_rows, (int32_t)r->dtypes.size(), r->dtypes.data(), &t);
+  if (rc != BQG_OK) throw ApiError{rc, c->err};
+  for (size_t j = 0; j < r->dtypes.size(); ++j)
+    if (r->n_rows > 0)
+      HIPCHECK(hipMemcpyAsync(t->cols[j].dev, r->ptrs[j], (size_t)r->n_rows * dtype_size(r->dtypes[j]), hipMemcpyHostToDevice,
+                              c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  *c->dev_target = t;
+}
+
 // Runs the passes of one groupby; returns the device output columns through `res`.
 void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out) {
   Plan pl;
@@ -715,6 +814,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
 
   if (fused) {
     // the scan is the fused distinct pass below
+    c->last.mode = 5;
   } else if (pl.mode == kPrivate) {
     const size_t lds = (size_t)S * kBlock * (8 + 8 * (size_t)nsum);
     int per_cu = (int)std::min<size_t>(kPrivatePerCu, (160 * 1024) / std::max<size_t>(lds, 1));
@@ -751,6 +851,17 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));
     launch_private_finish(F, sa, e, st);
     HIPCHECK(hipGetLastError());
+    if (!need_generic && c->dev_target) {
+      unsigned long long* hh = (unsigned long long*)c->hhdr.ensure(64);
+      HIPCHECK(hipMemcpyAsync(hh, F.out_hdr, 16, hipMemcpyDeviceToHost, st));
+      if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
+      HIPCHECK(hipStreamSynchronize(st));
+      std::vector<const void*> src;
+      for (int j = 0; j < e.ncols; ++j) src.push_back((const unsigned char*)c->outcols.p + (size_t)j * S * 8);
+      table_from_device(c, out_dt, src, (int64_t)hh[0]);
+      c->last.bytes = pl.alg_bytes + (int64_t)hh[0] * (int64_t)e.ncols * 8;
+      return;
+    }
     if (!need_generic) {
       // one D2H of header + columns straight into a pooled pinned block
       const size_t colbytes = (size_t)e.ncols * S * 8;
@@ -1122,6 +1233,14 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   }
   launch_emit(e, sa, order, G, nsum, S, st);
   HIPCHECK(hipGetLastError());
+  if (c->dev_target) {
+    if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
+    std::vector<const void*> src;
+    for (int j = 0; j < e.ncols; ++j) src.push_back(e.cols[j].out);
+    table_from_device(c, out_dt, src, (int64_t)G);
+    c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
+    return;
+  }
   PinnedBlock blk = c->pool_get(obytes + 64);
   HIPCHECK(hipMemcpyAsync(blk.p, ob, obytes, hipMemcpyDeviceToHost, st));
   if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
@@ -1199,6 +1318,7 @@ int bqg_destroy(bqg_ctx* c) {
       b->release();
     c->hhdr.release();
     c->hout.release();
+    c->colpool.release();
     c->pool.reset();
     for (int i = 0; i < 2; ++i) {
       if (c->stage[i]) (void)hipHostFree(c->stage[i]);
@@ -1256,16 +1376,11 @@ int bqg_table_create(bqg_ctx* c, int64_t nrows, int32_t ncols, const int32_t* dt
       t->cols.push_back(col);
       (void)slot;
     }
-    for (Column& col : t->cols) {
-      col.bytes = column_bytes(nrows, col.dtype);
-      if (hipMalloc(&col.dev, col.bytes) != hipSuccess) fail(BQG_E_OOM, "device allocation of a column failed");
-      HIPCHECK(hipMemsetAsync(col.dev, 0, col.bytes, c->stream));
-    }
+    for (Column& col : t->cols) alloc_column(c, col, nrows, true);
     *out = t;
   });
   if (rc != BQG_OK && t) {
-    for (Column& col : t->cols)
-      if (col.dev) (void)hipFree(col.dev);
+    for (Column& col : t->cols) c->colpool.put(col.dev, col.bytes);
     delete t;
   }
   return rc;
@@ -1275,8 +1390,7 @@ int bqg_table_destroy(bqg_table* t) {
   if (!t) return BQG_OK;
   int rc = guard(t->ctx, [&] {
     HIPCHECK(hipStreamSynchronize(t->ctx->stream));
-    for (Column& col : t->cols)
-      if (col.dev) HIPCHECK(hipFree(col.dev));
+    for (Column& col : t->cols) t->ctx->colpool.put(col.dev, col.bytes);
   });
   delete t;
   return rc;
@@ -1287,21 +1401,20 @@ int bqg_table_add_column(bqg_table* t, int32_t dtype, int32_t* slot_out) {
     if (dtype < BQG_BOOL || dtype > BQG_F64) fail(BQG_E_INVALID, "unknown dtype %d", dtype);
     Column col;
     col.dtype = dtype;
-    col.bytes = column_bytes(t->nrows, dtype);
-    if (hipMalloc(&col.dev, col.bytes) != hipSuccess) fail(BQG_E_OOM, "device allocation of a column failed");
-    HIPCHECK(hipMemsetAsync(col.dev, 0, col.bytes, t->ctx->stream));
+    alloc_column(t->ctx, col, t->nrows, true);
     t->cols.push_back(col);
     *slot_out = (int32_t)t->cols.size() - 1;
   });
 }
 
-static bool is_pinned(const void* p) {
+// 0: pageable host memory, 1: page-locked host memory, 2: device memory
+static int mem_kind(const void* p) {
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();
-    return false;
+    return 0;
   }
-  return a.type == hipMemoryTypeHost;
+  return a.type == hipMemoryTypeDevice ? 2 : (a.type == hipMemoryTypeHost ? 1 : 0);
 }
 
 int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows, int64_t row_offset) {
@@ -1315,7 +1428,14 @@ int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows, i
     const unsigned char* src = (const unsigned char*)host;
     size_t left = (size_t)nrows * isz;
     unsigned char* dst = k.dev + (size_t)row_offset * isz;
-    if (left >= (1u << 20) && is_pinned(src)) {
+    const int kind = mem_kind(src);
+    if (kind == 2) {
+      // device memory (another table's column, a collective's receive buffer): D2D copy,
+      // stream-ordered; complete by the next bqg_table_sync / synchronising call
+      HIPCHECK(hipMemcpyAsync(dst, src, left, hipMemcpyDeviceToDevice, c->stream));
+      return;
+    }
+    if (left >= (1u << 20) && kind == 1) {
       // page-locked source (e.g. another query's result block): one DMA, no staging memcpy;
       // synchronous like the staged path, so the caller may reuse the buffer on return
       HIPCHECK(hipMemcpyAsync(dst, src, left, hipMemcpyHostToDevice, c->stream));
@@ -1366,6 +1486,10 @@ int bqg_table_sync(bqg_table* t) {
   });
 }
 
+int bqg_table_nrows(bqg_table* t, int64_t* nrows) {
+  return guard(t->ctx, [&] { *nrows = t->nrows; });
+}
+
 int bqg_table_column_ptr(bqg_table* t, int32_t col, void** dev_ptr) {
   return guard(t->ctx, [&] {
     if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
@@ -1393,7 +1517,7 @@ int bqg_table_read(bqg_table* t, int32_t col, void* host, int64_t nrows, int64_t
     if (row_offset < 0 || nrows < 0 || row_offset + nrows > t->nrows) fail(BQG_E_INVALID, "rows out of range");
     const size_t isz = dtype_size(t->cols[col].dtype);
     HIPCHECK(hipMemcpyAsync(host, t->cols[col].dev + (size_t)row_offset * isz, (size_t)nrows * isz,
-                            hipMemcpyDeviceToHost, t->ctx->stream));
+                            mem_kind(host) == 2 ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, t->ctx->stream));
     HIPCHECK(hipStreamSynchronize(t->ctx->stream));
   });
 }
@@ -1451,8 +1575,36 @@ int bqg_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out) 
   return guard(c, [&] {
     if (!q || !out) fail(BQG_E_INVALID, "null query/output");
     *out = nullptr;
+    c->dev_target = nullptr;
     run_groupby(c, t, q, out);
   });
+}
+
+int bqg_groupby_table(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_table** out) {
+  return guard(c, [&] {
+    if (!q || !out) fail(BQG_E_INVALID, "null query/output");
+    *out = nullptr;
+    struct Reset {
+      bqg_ctx* c;
+      ~Reset() { c->dev_target = nullptr; }
+    } reset{c};
+    c->dev_target = out;
+    bqg_result* r = nullptr;
+    run_groupby(c, t, q, &r);
+    if (r) table_from_host_result(c, r);  // empty / synthesized results: host-built
+  });
+}
+
+int bqg_select_rows_table(bqg_ctx* c, bqg_table* t, const bqg_query* q, int32_t n_cols, const int32_t* cols,
+                          bqg_table** out) {
+  if (!out) return guard(c, [&] { fail(BQG_E_INVALID, "null output"); });
+  *out = nullptr;
+  c->dev_target = out;
+  bqg_result* r = nullptr;
+  const int rc = bqg_select_rows(c, t, q, n_cols, cols, &r);
+  c->dev_target = nullptr;
+  if (r) bqg_result_free(r);
+  return rc;
 }
 
 int bqg_select_rows(bqg_ctx* c, bqg_table* t, const bqg_query* q, int32_t n_cols, const int32_t* cols,
@@ -1524,6 +1676,16 @@ int bqg_select_rows(bqg_ctx* c, bqg_table* t, const bqg_query* q, int32_t n_cols
     for (int i = 0; i < n_cols; ++i) outs.push_back(ob + offs[i]);
     if (total > 0) launch_select_gather(mask, N, tc, dcs.data(), n_cols, outs.data(), c->stream);
     HIPCHECK(hipGetLastError());
+    if (c->dev_target) {
+      std::vector<int> dts;
+      std::vector<const void*> src;
+      for (int i = 0; i < n_cols; ++i) {
+        dts.push_back(t->cols[cols[i]].dtype);
+        src.push_back(outs[i]);
+      }
+      table_from_device(c, dts, src, total);
+      return;
+    }
     PinnedBlock blk = c->pool_get(obytes + 64);
     if (obytes) HIPCHECK(hipMemcpyAsync(blk.p, ob, obytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));

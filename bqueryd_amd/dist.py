@@ -44,17 +44,51 @@ class GpuBackend:
         from .engine import get_device
         self.device = device or get_device()
 
-    def reduce(self, table, groupby_cols, agg_list):
-        """``table``: one table or a list of tables (row-concatenated on the device)."""
+    def reduce(self, table, groupby_cols, agg_list, on_device=False):
+        """``table``: one table or a list of tables -- host mappings or device ShardTables --
+        row-concatenated on the device and summed by key.  ``on_device``: the result stays in
+        HBM (a ShardTable) instead of coming back as numpy arrays."""
         from .engine import ShardTable
         parts = table if isinstance(table, (list, tuple)) else [table]
         names = list(groupby_cols) + [x[2] for x in agg_list]
         t = ShardTable.from_parts(parts, names, device=self.device)
         try:
+            if on_device:
+                return t.groupby_table(groupby_cols, sum_spec(agg_list))
             out, _ = t.groupby(groupby_cols, sum_spec(agg_list))
             return out
         finally:
             t.close()
+
+    def partition_device(self, table, groupby_cols, nparts):
+        """Device ShardTable -> ``nparts`` device ShardTables, rows split by the hash of their
+        key values (the same function on every rank)."""
+        import ctypes
+        from . import _lib as L
+        names = list(table.names)
+        col = table.add_column('__part__', np.uint32)
+        keys = np.array([table.slot(c) for c in groupby_cols], np.int32)
+        counts = np.zeros(nparts, np.int64)
+        self.device.check(L.lib().bqg_hash_partition(self.device.handle, table.handle, len(keys),
+                                                     keys.ctypes.data, nparts, col, counts.ctypes.data))
+        return [table.select_rows_table(names, where_terms=[('__part__', '==', p)]) for p in range(nparts)]
+
+    def empty_table(self, names, dtypes):
+        from .engine import ShardTable
+        return ShardTable(OrderedDict((n, np.zeros(0, dtypes[n])) for n in names), device=self.device)
+
+    def table_from_buffers(self, names, dtypes, bufs, nrows):
+        """A device ShardTable whose columns are copied (device to device) from ``bufs``
+        (name -> device address)."""
+        from .engine import ShardTable
+        t = ShardTable(OrderedDict(), device=self.device, nrows=nrows)
+        for n in names:
+            t.add_column(n, dtypes[n])
+            t.names.append(n)
+            if nrows:
+                t.push_device(n, bufs[n], nrows)
+        t.sync()
+        return t
 
     def partition(self, table, groupby_cols, nparts):
         import ctypes
@@ -128,6 +162,87 @@ class Exchange:
             out = out.to(self.device)
         self.dist.all_to_all_single(out, self._tensor(send), out_split, in_split, group=self.group)
         return out.cpu().numpy().view(dtype)
+
+
+class DeviceExchange(Exchange):
+    """Byte all-to-all of device-resident columns: RCCL over xGMI (``torch.distributed`` with
+    the nccl backend), no host copies.  Columns of ShardTables are packed into one torch
+    device buffer per column with device-to-device copies."""
+
+    def column_device(self, parts, name, dtype, recv_counts):
+        """parts[dst]: ShardTables on this GPU -> (device address, torch buffer) of this rank's
+        rows of column ``name`` from every source, concatenated in rank order."""
+        import torch
+        dtype = np.dtype(dtype)
+        in_split = [int(p.nrows) * dtype.itemsize for p in parts]
+        out_split = [int(c) * dtype.itemsize for c in recv_counts]
+        stream = torch.cuda.current_stream(self.device)
+        send = torch.empty(max(1, sum(in_split)), dtype=torch.uint8, device=self.device)
+        out = torch.empty(max(1, sum(out_split)), dtype=torch.uint8, device=self.device)
+        stream.synchronize()  # the fresh buffers are idle before another stream writes them
+        off = 0
+        for p, nb in zip(parts, in_split):
+            if nb:
+                p.read_device(name, send.data_ptr() + off)  # synchronous on libbqgpu's stream
+            off += nb
+        self.dist.all_to_all_single(out[:sum(out_split)], send[:sum(in_split)], out_split, in_split,
+                                    group=self.group)
+        stream.synchronize()  # received bytes are complete before libbqgpu reads them
+        return out.data_ptr(), out
+
+    def host_bytes(self, buf, nbytes):
+        """The first ``nbytes`` of a buffer returned by ``column_device``, in host memory."""
+        return buf[:nbytes].cpu().numpy()
+
+
+def merge_partials_device(local_tables, groupby_cols, agg_list, dtypes, backend, exchange):
+    """``merge_partials`` with every step in HBM: ``local_tables`` are this rank's finalized
+    shard tables as device ShardTables (``ShardTable.groupby_table``), the reduce, partition,
+    all-to-all and gather run on device buffers, and only the merged table comes back to host
+    memory (rank 0; None elsewhere)."""
+    names = list(groupby_cols) + [x[2] for x in agg_list]
+    local_tables = [t for t in local_tables if t is not None and t.nrows]
+    if exchange.world == 1:
+        if not local_tables:
+            return OrderedDict((n, np.zeros(0, dtypes[n])) for n in names)
+        return backend.reduce(local_tables, groupby_cols, agg_list)
+    if local_tables:
+        local = backend.reduce(local_tables, groupby_cols, agg_list, on_device=True)
+        try:
+            parts = backend.partition_device(local, groupby_cols, exchange.world)
+        finally:
+            local.close()
+    else:
+        parts = [backend.empty_table(names, dtypes) for _ in range(exchange.world)]
+    recv_counts = exchange.counts([p.nrows for p in parts])
+    n_recv = int(np.sum(recv_counts))
+    keep = []
+    bufs = OrderedDict()
+    for n in names:
+        ptr, buf = exchange.column_device(parts, n, dtypes[n], recv_counts)
+        bufs[n] = ptr
+        keep.append(buf)
+    for p in parts:
+        p.close()
+    mine = backend.table_from_buffers(names, dtypes, bufs, n_recv)
+    del keep[:]
+    if n_recv:
+        reduced = backend.reduce([mine], groupby_cols, agg_list, on_device=True)
+        mine.close()
+        mine = reduced
+    # gather the disjoint reduced partitions to rank 0
+    empty = backend.empty_table(names, dtypes)
+    to_root = [mine.nrows if dst == 0 else 0 for dst in range(exchange.world)]
+    recv = exchange.counts(to_root)
+    gathered = OrderedDict()
+    for n in names:
+        ptr, buf = exchange.column_device([mine if dst == 0 else empty for dst in range(exchange.world)], n,
+                                          dtypes[n], recv)
+        nbytes = int(np.sum(recv)) * np.dtype(dtypes[n]).itemsize
+        gathered[n] = exchange.host_bytes(buf, nbytes).view(np.dtype(dtypes[n])) if exchange.rank == 0 else None
+    mine.close()
+    empty.close()
+    return gathered if exchange.rank == 0 else None
 
 
 def merge_partials(local_tables, groupby_cols, agg_list, dtypes, backend, exchange):

@@ -141,23 +141,50 @@ class ShardTable:
         self.sync()
 
     @classmethod
+    def _wrap(cls, handle, names, dtypes, device):
+        """A ShardTable around a table the library created (a device-resident result)."""
+        t = cls.__new__(cls)
+        t.dev = device
+        t._lib = L.lib()
+        t.handle = handle
+        n = ctypes.c_int64()
+        device.check(t._lib.bqg_table_nrows(handle, ctypes.byref(n)))
+        t.nrows = n.value
+        t.names = list(names)
+        t.dtypes = OrderedDict((nm, np.dtype(dt)) for nm, dt in zip(names, dtypes))
+        t._slot = {nm: i for i, nm in enumerate(names)}
+        t._scratch = []
+        return t
+
+    @classmethod
     def from_parts(cls, parts, names=None, device=None):
-        """One table holding the row-concatenation of ``parts`` (mappings name -> array), each
-        part copied straight to its row offset in HBM (no host-side concatenation; parts in
-        page-locked memory -- query results -- go by DMA without staging)."""
+        """One table holding the row-concatenation of ``parts`` -- mappings name -> array, or
+        device-resident ShardTables -- each part copied straight to its row offset in HBM (no
+        host-side concatenation; page-locked parts go by DMA without staging, device parts
+        by device-to-device copies)."""
         parts = [p for p in parts if p is not None]
-        names = list(names or parts[0].keys())
-        total = sum(len(p[names[0]]) for p in parts)
+        names = list(names or (parts[0].names if isinstance(parts[0], ShardTable) else parts[0].keys()))
+
+        def rows(p):
+            return p.nrows if isinstance(p, ShardTable) else len(p[names[0]])
+
+        def dtype(p, n):
+            return p.dtypes[n] if isinstance(p, ShardTable) else np.asarray(p[n]).dtype
+
+        total = sum(rows(p) for p in parts)
         t = cls(OrderedDict(), device=device, nrows=total)
         for n in names:
-            t.add_column(n, np.asarray(parts[0][n]).dtype)
+            t.add_column(n, dtype(parts[0], n))
             t.names.append(n)
         off = 0
         for p in parts:
-            m = len(p[names[0]])
+            m = rows(p)
             if m:
                 for n in names:
-                    t.push(n, p[n], off)
+                    if isinstance(p, ShardTable):
+                        t.push_device(n, p.column_ptr(n), m, off)
+                    else:
+                        t.push(n, p[n], off)
             off += m
         t.sync()
         return t
@@ -189,6 +216,22 @@ class ShardTable:
         a = np.ascontiguousarray(array)
         self.dev.check(self._lib.bqg_push_chunk(self.handle, self.slot(col), a.ctypes.data,
                                                 len(a), int(row_offset)))
+
+    def push_device(self, col, dev_ptr, nrows, row_offset=0):
+        """Device-to-device copy of ``nrows`` elements at ``dev_ptr`` into column ``col``."""
+        self.dev.check(self._lib.bqg_push_chunk(self.handle, self.slot(col), ctypes.c_void_p(int(dev_ptr)),
+                                                int(nrows), int(row_offset)))
+
+    def read_device(self, col, dev_ptr, nrows=None, row_offset=0):
+        """Device-to-device copy of column ``col`` into the device buffer at ``dev_ptr``."""
+        n = self.nrows - row_offset if nrows is None else nrows
+        self.dev.check(self._lib.bqg_table_read(self.handle, self.slot(col), ctypes.c_void_p(int(dev_ptr)),
+                                                int(n), int(row_offset)))
+
+    def column_ptr(self, col):
+        p = ctypes.c_void_p()
+        self.dev.check(self._lib.bqg_table_column_ptr(self.handle, self.slot(col), ctypes.byref(p)))
+        return p.value or 0
 
     def load_carray(self, col, carray_dir, chunklen, nthreads=None):
         """Decode a bcolz carray directory straight into device column ``col`` (host decode
@@ -312,6 +355,37 @@ class ShardTable:
             if out[out_col].dtype != dt:
                 out[out_col] = out[out_col].astype(dt)
         return out, filtered
+
+    def groupby_table(self, groupby_cols, agg_list, where_terms=None, mask=None):
+        """``groupby`` whose result stays in HBM: a new ShardTable (keys, then aggregations)."""
+        groupby_cols = list(groupby_cols)
+        for c in groupby_cols:
+            self.slot(c)
+        ops = parse_agg_list(self.dtypes, agg_list)
+        names = groupby_cols + [o[1] for o in ops]
+        if len(set(names)) != len(names):
+            raise ValueError('duplicate output column names: %s' % names)
+        keep = []
+        q = self._query(groupby_cols, [(o[0], o[2]) for o in ops], where_terms, mask, keep)
+        h = ctypes.c_void_p()
+        self.dev.check(self._lib.bqg_groupby_table(self.dev.handle, self.handle, ctypes.byref(q), ctypes.byref(h)))
+        dts = [self.dtypes[c] for c in groupby_cols] + [o[3] for o in ops]
+        return ShardTable._wrap(h, names, dts, self.dev)
+
+    def select_rows_table(self, cols, where_terms=None, mask=None):
+        """``select_rows`` whose result stays in HBM: a new ShardTable."""
+        cols = list(cols)
+        keep = []
+        q = self._query([], [], where_terms, mask, keep)
+        sel = np.array([self.slot(c) for c in cols] or [0], np.int32)
+        h = ctypes.c_void_p()
+        self.dev.check(self._lib.bqg_select_rows_table(self.dev.handle, self.handle, ctypes.byref(q), len(cols),
+                                                       sel.ctypes.data, ctypes.byref(h)))
+        return ShardTable._wrap(h, cols, [self.dtypes[c] for c in cols], self.dev)
+
+    def to_host(self, cols=None):
+        """The table's columns as numpy arrays."""
+        return OrderedDict((c, self.read(c)) for c in (cols or self.names))
 
     def select_rows(self, cols, where_terms=None, mask=None):
         """aggregate=False: the passing rows of ``cols`` in row order."""

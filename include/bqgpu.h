@@ -119,7 +119,7 @@ typedef struct {
   int64_t rows;          /* input rows scanned */
   int64_t bytes;         /* algorithmic bytes: distinct input columns x itemsize x rows + output */
   int32_t mode;          /* 0 private-LDS, 1 shared-LDS, 2 global dense, 3 global hash,
-                            4 partitioned */
+                            4 partitioned, 5 fused distinct pass (sorted_count_distinct) */
   int32_t specialized;   /* 1: the scan ran a query-specialised (run-time compiled) kernel */
 } bqg_timing;
 
@@ -145,7 +145,10 @@ int bqg_table_create(bqg_ctx* ctx, int64_t nrows, int32_t ncols, const int32_t* 
                      bqg_table** out);
 int bqg_table_destroy(bqg_table* t);
 int bqg_table_add_column(bqg_table* t, int32_t dtype, int32_t* slot_out);
-/* Copy rows [row_offset, row_offset + nrows) of column `col` from host memory. */
+/* Copy rows [row_offset, row_offset + nrows) of column `col` from host memory (or from
+ * device memory: another table's column, a collective's receive buffer -- a D2D copy that
+ * is stream-ordered and complete at the next bqg_table_sync; keep the source alive until
+ * then). */
 int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows,
                    int64_t row_offset);
 /* Cold-path ingest (worker.py:291 bquery.ctable(rootdir) + bcolz's per-chunk blosc decode,
@@ -162,8 +165,9 @@ int bqg_table_sync(bqg_table* t);
 int bqg_table_column_ptr(bqg_table* t, int32_t col, void** dev_ptr);
 int bqg_table_stats(bqg_table* t, int32_t col, int64_t* imin, int64_t* imax, double* fmin,
                     double* fmax, int32_t* has_nan);
-/* Copy rows of a device column back to host memory. */
+/* Copy rows of a device column back to host memory (or into device memory). */
 int bqg_table_read(bqg_table* t, int32_t col, void* host, int64_t nrows, int64_t row_offset);
+int bqg_table_nrows(bqg_table* t, int64_t* nrows);
 
 /* ---------------- calc path ---------------- */
 /* where_terms: AND of the terms -> BOOL column `out_mask_col` (device); *n_pass receives the
@@ -179,6 +183,12 @@ int bqg_groupby(bqg_ctx* ctx, bqg_table* t, const bqg_query* q, bqg_result** out
 /* aggregate=False: the passing rows of `cols`, in row order.  (worker.py:316-323) */
 int bqg_select_rows(bqg_ctx* ctx, bqg_table* t, const bqg_query* q, int32_t n_cols,
                     const int32_t* cols, bqg_result** out);
+/* The same two calls with the result kept in HBM as a new table (columns as in
+ * bqg_result_view; free with bqg_table_destroy): the co-located aggregate=True merge
+ * (rpc.py:164-173 restated on the GPU, bqueryd_amd/dist.py) chains them without host copies. */
+int bqg_groupby_table(bqg_ctx* ctx, bqg_table* t, const bqg_query* q, bqg_table** out);
+int bqg_select_rows_table(bqg_ctx* ctx, bqg_table* t, const bqg_query* q, int32_t n_cols,
+                          const int32_t* cols, bqg_table** out);
 int bqg_result_view_get(bqg_result* r, bqg_result_view* out);
 
 /* ---------------- co-located merge (replaces the client re-group, rpc.py:164-173) --------
