@@ -216,8 +216,14 @@ def read_ctable(rootdir, columns=None, nthreads=None):
         if c not in names:
             raise KeyError(str(c))
     nthreads = nthreads or min(16, os.cpu_count() or 1)
+    # small tables (query results: a few chunks) decode inline -- a thread pool costs more
+    nchunks = sum(len(CArrayMeta(ctable_column_dir(rootdir, c)).chunk_files) for c in columns)
     out = OrderedDict()
-    with ThreadPoolExecutor(max_workers=nthreads) as pool:
+    if nthreads <= 1 or nchunks <= 2 * len(columns):
+        for c in columns:
+            out[c] = read_carray(ctable_column_dir(rootdir, c))
+        return out
+    with ThreadPoolExecutor(max_workers=min(nthreads, nchunks)) as pool:
         for c in columns:
             out[c] = read_carray(ctable_column_dir(rootdir, c), pool=pool)
     return out

@@ -262,6 +262,7 @@ struct ColumnPool {
 struct bqg_ctx {
   int device = 0;
   ColumnPool colpool;
+  IngestPool ingest;  // cold-path staging: streams + pinned double buffers per decode thread
   int cu = 256;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
@@ -859,6 +860,14 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       std::vector<const void*> src;
       for (int j = 0; j < e.ncols; ++j) src.push_back((const unsigned char*)c->outcols.p + (size_t)j * S * 8);
       table_from_device(c, out_dt, src, (int64_t)hh[0]);
+      if (c->timing) {
+        float ms = 0;
+        HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+        c->last.scan_ms = ms;
+        c->last.scan_launches = 1;
+        HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+        c->last.total_ms = ms;
+      }
       c->last.bytes = pl.alg_bytes + (int64_t)hh[0] * (int64_t)e.ncols * 8;
       return;
     }
@@ -1238,6 +1247,13 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     std::vector<const void*> src;
     for (int j = 0; j < e.ncols; ++j) src.push_back(e.cols[j].out);
     table_from_device(c, out_dt, src, (int64_t)G);
+    if (c->timing) {
+      float ms = 0;
+      HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+      c->last.scan_ms = ms;
+      HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+      c->last.total_ms = ms;
+    }
     c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
     return;
   }
@@ -1475,7 +1491,7 @@ int bqg_table_load_carray(bqg_table* t, int32_t col, const char* carray_dir, int
     job.chunklen = chunklen;
     job.nthreads = nthreads;
     std::string err;
-    if (ingest_carray(job, nullptr, err) != 0) fail(BQG_E_INVALID, "%s", err.c_str());
+    if (ingest_carray(job, c->ingest, nullptr, err) != 0) fail(BQG_E_INVALID, "%s", err.c_str());
   });
 }
 

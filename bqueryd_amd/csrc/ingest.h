@@ -4,7 +4,10 @@
 
 #include <stdint.h>
 
+#include <hip/hip_runtime.h>
+
 #include <string>
+#include <vector>
 
 namespace bqg {
 
@@ -18,6 +21,20 @@ struct IngestJob {
   int nthreads;            // host decode threads (<= 0: 8)
 };
 
+// Reusable per-worker resources (HIP stream, two page-locked staging buffers, their events):
+// created on first use and kept by the context, so repeated ingests pay no pinned allocation.
+struct IngestWorker {
+  hipStream_t stream = nullptr;
+  void* pinned[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  size_t cap = 0;
+};
+struct IngestPool {
+  int device = -1;
+  std::vector<IngestWorker> workers;
+  ~IngestPool();
+};
+
 struct IngestStats {
   int64_t chunks = 0;
   int64_t compressed_bytes = 0;
@@ -27,6 +44,6 @@ struct IngestStats {
 
 // Decodes every chunk into dev_dst; returns 0, or -1 with a message in err.  Synchronous:
 // the column is complete in HBM when it returns.
-int ingest_carray(const IngestJob& job, IngestStats* stats, std::string& err);
+int ingest_carray(const IngestJob& job, IngestPool& pool, IngestStats* stats, std::string& err);
 
 }  // namespace bqg

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -96,7 +97,58 @@ bool read_file(const std::string& path, std::vector<unsigned char>& buf, std::st
 
 }  // namespace
 
-int ingest_carray(const IngestJob& job, IngestStats* stats, std::string& err) {
+IngestPool::~IngestPool() {
+  for (IngestWorker& w : workers) {
+    if (w.stream) (void)hipStreamSynchronize(w.stream);
+    for (int k = 0; k < 2; ++k) {
+      if (w.ev[k]) (void)hipEventDestroy(w.ev[k]);
+      if (w.pinned[k]) (void)hipHostFree(w.pinned[k]);
+    }
+    if (w.stream) (void)hipStreamDestroy(w.stream);
+  }
+}
+
+namespace {
+// worker resources with staging buffers of at least `bytes` (called on the calling thread)
+bool prepare_workers(IngestPool& pool, int device, int n, size_t bytes, std::string& err) {
+  if (pool.device != device) {
+    pool.workers.clear();
+    pool.device = device;
+  }
+  while ((int)pool.workers.size() < n) pool.workers.emplace_back();
+  for (int i = 0; i < n; ++i) {
+    IngestWorker& w = pool.workers[i];
+    if (!w.stream && hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess) {
+      err = "ingest: HIP stream creation failed";
+      return false;
+    }
+    for (int k = 0; k < 2; ++k)
+      if (!w.ev[k] && hipEventCreateWithFlags(&w.ev[k], hipEventDisableTiming) != hipSuccess) {
+        err = "ingest: HIP event creation failed";
+        return false;
+      }
+    if (w.cap < bytes) {
+      for (int k = 0; k < 2; ++k) {
+        if (w.pinned[k]) {
+          (void)hipEventSynchronize(w.ev[k]);
+          (void)hipHostFree(w.pinned[k]);
+          w.pinned[k] = nullptr;
+        }
+        if (hipHostMalloc(&w.pinned[k], bytes, hipHostMallocDefault) != hipSuccess) {
+          w.pinned[k] = nullptr;
+          w.cap = 0;
+          err = "ingest: pinned staging allocation failed";
+          return false;
+        }
+      }
+      w.cap = bytes;
+    }
+  }
+  return true;
+}
+}  // namespace
+
+int ingest_carray(const IngestJob& job, IngestPool& pool, IngestStats* stats, std::string& err) {
   const BloscApi& bl = blosc_api();
   if (!bl.err.empty()) {
     err = bl.err;
@@ -112,6 +164,8 @@ int ingest_carray(const IngestJob& job, IngestStats* stats, std::string& err) {
   int nthreads = job.nthreads > 0 ? job.nthreads : 8;
   nthreads = (int)std::min<int64_t>(nthreads, nchunks);
 
+  if (!prepare_workers(pool, job.device, nthreads, chunk_bytes + kBloscHeader, err)) return -1;
+
   std::atomic<int64_t> next{0};
   std::atomic<bool> failed{false};
   std::atomic<int64_t> comp_bytes{0};
@@ -123,23 +177,13 @@ int ingest_carray(const IngestJob& job, IngestStats* stats, std::string& err) {
     failed = true;
   };
 
-  auto worker = [&]() {
-    hipStream_t s = nullptr;
-    void* pinned[2] = {nullptr, nullptr};
-    hipEvent_t ev[2] = {nullptr, nullptr};
+  auto worker = [&](IngestWorker& res) {
+    hipStream_t s = res.stream;
     std::vector<unsigned char> file;
     std::string e;
-    if (hipSetDevice(job.device) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
-      set_err("ingest: HIP stream creation failed");
+    if (hipSetDevice(job.device) != hipSuccess) {
+      set_err("ingest: hipSetDevice failed");
       return;
-    }
-    for (int k = 0; k < 2; ++k) {
-      if (hipHostMalloc(&pinned[k], chunk_bytes + kBloscHeader, hipHostMallocDefault) != hipSuccess ||
-          hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
-        set_err("ingest: pinned staging allocation failed");
-        break;
-      }
-      (void)hipEventRecord(ev[k], s);
     }
     int slot = 0;
     while (!failed.load(std::memory_order_relaxed)) {
@@ -166,36 +210,31 @@ int ingest_carray(const IngestJob& job, IngestStats* stats, std::string& err) {
         break;
       }
       // the staging buffer's previous copy must have drained before it is overwritten
-      if (hipEventSynchronize(ev[slot]) != hipSuccess) {
+      if (hipEventSynchronize(res.ev[slot]) != hipSuccess) {
         set_err("ingest: HIP event wait failed");
         break;
       }
-      const int got = bl.decompress_ctx(frame, pinned[slot], chunk_bytes + kBloscHeader, 1);
+      const int got = bl.decompress_ctx(frame, res.pinned[slot], chunk_bytes + kBloscHeader, 1);
       if (got < 0 || (size_t)got != nbytes) {
         set_err("ingest: blosc decompression of chunk " + std::to_string(i) + " of " + job.carray_dir + " failed");
         break;
       }
       unsigned char* dst = static_cast<unsigned char*>(job.dev_dst) + (size_t)i * chunk_bytes;
-      if (hipMemcpyAsync(dst, pinned[slot], want, hipMemcpyHostToDevice, s) != hipSuccess ||
-          hipEventRecord(ev[slot], s) != hipSuccess) {
+      if (hipMemcpyAsync(dst, res.pinned[slot], want, hipMemcpyHostToDevice, s) != hipSuccess ||
+          hipEventRecord(res.ev[slot], s) != hipSuccess) {
         set_err("ingest: host-to-device copy failed");
         break;
       }
       comp_bytes += (int64_t)file.size();
       slot ^= 1;
     }
-    if (s) (void)hipStreamSynchronize(s);
-    for (int k = 0; k < 2; ++k) {
-      if (ev[k]) (void)hipEventDestroy(ev[k]);
-      if (pinned[k]) (void)hipHostFree(pinned[k]);
-    }
-    if (s) (void)hipStreamDestroy(s);
+    (void)hipStreamSynchronize(s);
   };
 
-  std::vector<std::thread> pool;
-  pool.reserve(nthreads);
-  for (int t = 0; t < nthreads; ++t) pool.emplace_back(worker);
-  for (std::thread& t : pool) t.join();
+  std::vector<std::thread> threads;
+  threads.reserve(nthreads);
+  for (int t = 0; t < nthreads; ++t) threads.emplace_back(worker, std::ref(pool.workers[t]));
+  for (std::thread& t : threads) t.join();
   if (failed) {
     err = first_err;
     return -1;

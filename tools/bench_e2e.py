@@ -41,13 +41,24 @@ COLS = ('payment_type', 'fare_amount')
 
 
 def _cpu_task(args):
+    """One reference-shaped worker message on the CPU: decode the shard (one thread,
+    worker.py:40), the C port of bquery's groupby, then the result ctable + tar reply exactly
+    as the GPU worker writes it (worker.py:335-346)."""
     path, = args
     from bqueryd_amd import bcolz_io
+    from bqueryd_amd.worker import rm_file_or_dir, tar_directory
     from oracle import cbquery
-    cols = bcolz_io.read_ctable(path, columns=list(COLS), nthreads=1)
     t0 = time.perf_counter()
+    cols = bcolz_io.read_ctable(path, columns=list(COLS), nthreads=1)
     out = cbquery.handle_work(cols, GROUPBY, AGGS, [])
-    return out, time.perf_counter() - t0
+    tmp_dir = tempfile.mkdtemp(prefix='result_')
+    try:
+        rm_file_or_dir(tmp_dir)
+        bcolz_io.write_ctable(tmp_dir, out)
+        data = tar_directory(tmp_dir)
+    finally:
+        rm_file_or_dir(tmp_dir)
+    return data, time.perf_counter() - t0
 
 
 def main():
@@ -126,7 +137,8 @@ def main():
             for _ in range(args.reps):
                 t0 = time.perf_counter()
                 res = pool.map(_cpu_task, [(os.path.join(data_dir, fn),) for fn in files])
-                merged = bo.client_merge([r[0] for r in res], GROUPBY, AGGS, aggregate=True)
+                reply = rpc.tar_of_tars(OrderedDict((fn, r[0]) for fn, r in zip(files, res)))
+                merged = bo.client_merge(rpc.read_shard_results(reply), GROUPBY, AGGS, aggregate=True)
                 dt = time.perf_counter() - t0
                 calc_s = sum(r[1] for r in res)
                 if best is None or dt < best[0]:
@@ -134,8 +146,8 @@ def main():
             check(merged)
         line['cpu_port'] = {'s_per_query': best[0], 'rows_per_s': total_rows / best[0],
                             'calc_core_s': best[1], 'workers': args.cpu_workers, 'kind': 'port',
-                            'note': 'bcolz decode + oracle/cbquery.c calc per shard in worker processes, '
-                                    'oracle client merge'}
+                            'note': 'per shard in worker processes: bcolz decode (1 thread) + oracle/cbquery.c '
+                                    'calc + result ctable + tar; tar of tars; client untar + oracle merge'}
         print(json.dumps(line), flush=True)
     finally:
         shutil.rmtree(data_dir, ignore_errors=True)
