@@ -189,9 +189,14 @@ hipFunction_t jit_function(const char* kernel, const std::string& spec) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   const std::string src = spec + "#include \"jit_kernels.h\"\n";
-  uint64_t h = fnv1a(src);
-  for (int i = 0; i < kJitHeaderCount; ++i) h = fnv1a(kJitHeaderTexts[i], h);
-  for (const char* o : kOptions) h = fnv1a(o, h);
+  // the embedded headers and options hash once per process (~100 KB of text), the spec per call
+  static const uint64_t kSourceHash = [] {
+    uint64_t hh = 1469598103934665603ull;
+    for (int i = 0; i < kJitHeaderCount; ++i) hh = fnv1a(kJitHeaderTexts[i], hh);
+    for (const char* o : kOptions) hh = fnv1a(o, hh);
+    return hh;
+  }();
+  const uint64_t h = fnv1a(src, kSourceHash);
   char hex[17];
   snprintf(hex, sizeof(hex), "%016llx", (unsigned long long)h);
   const std::string key = std::to_string(dev) + ":" + kernel + ":" + hex;

@@ -251,25 +251,35 @@ __device__ __forceinline__ ScdState scd_combine(const ScdState& a, const ScdStat
   return r;
 }
 
-// one wave per slot; lanes take contiguous ranges of chunks, then an ordered tree
+// One workgroup per slot: each of its 4 waves takes a contiguous quarter of the chunks, each
+// lane a contiguous run of that quarter (loads clamped, not branched, so they pipeline), an
+// ordered shuffle tree folds the lanes, and the 4 wave results are folded in order.
 __global__ __launch_bounds__(kBlock) void k_scd_combine(ScdLaunch d, uint64_t nslots, int isf) {
+  __shared__ ScdState part[kBlock / 64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t s = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
-  if (s >= nslots) return;
-  const int per = (d.waves + 63) / 64;
+  const int nw = kBlock / 64;
+  for (uint64_t s = blockIdx.x; s < nslots; s += gridDim.x) {
+  const int wbeg = (int)((int64_t)d.waves * wave / nw), wend = (int)((int64_t)d.waves * (wave + 1) / nw);
+  const int span = wend - wbeg;
+  const int per = (span + 63) / 64;
+  const int lbeg = wbeg + min(span, lane * per), lend = wbeg + min(span, (lane + 1) * per);
   ScdState st = {0, kNoRow, 0, 0, 0, 0};
-  for (int i = 0; i < per; ++i) {
-    const int w = lane * per + i;
-    if (w >= d.waves) break;
-    const size_t idx = (size_t)w * nslots + s;
-    ScdState x;
-    x.first_row = d.st_first_row[idx];
-    x.present = x.first_row != kNoRow;
-    x.first = d.st_first[idx];
-    x.last = d.st_last[idx];
-    x.changes = d.st_changes[idx];
-    x.rows = d.st_count ? d.st_count[idx] : 0u;
-    st = scd_combine(st, x, isf);
+  constexpr int kU = 8;  // chunk states loaded per round (clamped, all in flight at once)
+  for (int w0 = lbeg; w0 < lend; w0 += kU) {
+    ScdState x[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const int w = min(w0 + k, lend - 1);
+      const size_t idx = (size_t)w * nslots + s;
+      x[k].first_row = d.st_first_row[idx];
+      x[k].present = (w0 + k < lend) && x[k].first_row != kNoRow;
+      x[k].first = d.st_first[idx];
+      x[k].last = d.st_last[idx];
+      x[k].changes = d.st_changes[idx];
+      x[k].rows = d.st_count ? d.st_count[idx] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kU; ++k) st = scd_combine(st, x[k], isf);
   }
   for (int o = 1; o < 64; o <<= 1) {
     ScdState other;
@@ -281,13 +291,19 @@ __global__ __launch_bounds__(kBlock) void k_scd_combine(ScdLaunch d, uint64_t ns
     other.rows = __shfl_down(st.rows, o, 64);
     if ((lane % (2 * o)) == 0 && lane + o < 64) st = scd_combine(st, other, isf);
   }
-  if (lane == 0) {
-    d.out_changes[s] = st.changes;
-    d.out_first[s] = st.first;
+  if (lane == 0) part[wave] = st;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ScdState t = part[0];
+    for (int q = 1; q < nw; ++q) t = scd_combine(t, part[q], isf);
+    d.out_changes[s] = t.changes;
+    d.out_first[s] = t.first;
     if (d.slot_cnt) {
-      d.slot_cnt[s] = st.present ? st.rows : 0ull;
-      d.slot_fst[s] = st.present ? st.first_row : kNoRow;
+      d.slot_cnt[s] = t.present ? t.rows : 0ull;
+      d.slot_fst[s] = t.present ? t.first_row : kNoRow;
     }
+  }
+  __syncthreads();  // part[] is rewritten for the next slot
   }
 }
 
@@ -325,7 +341,7 @@ void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hi
   int isf = 0;
   for (int c = 0; c < p.ncols; ++c)
     if (c == d.vcol) isf = dtype_is_float(p.cols[c].dtype);
-  const uint64_t cblocks = (p.nslots + (kBlock / 64) - 1) / (kBlock / 64);
+  const uint64_t cblocks = p.nslots < 65536 ? p.nslots : 65536;  // grid-stride over slots beyond
   hipLaunchKernelGGL(k_scd_combine, dim3((unsigned)cblocks), dim3(kBlock), 0, st, d, p.nslots, isf);
 }
 }  // namespace bqg

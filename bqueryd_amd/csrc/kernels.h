@@ -101,10 +101,11 @@ struct ScdLaunch {
   int compact;                       // fused: 32-bit value codes (integer values, range < 2^32)
   int64_t vmin;                      // compact: value code = v - vmin
 };
-// LDS bytes per wave of k_scd_fused for a slot space of nslots: a 32-byte state per slot, or
-// 20 bytes with compact (32-bit) value codes
+// LDS bytes per wave of k_scd_fused for a slot space of nslots: a 32-byte state per slot (20
+// bytes with compact 32-bit value codes) plus an 8-byte lane mask per slot
 inline size_t scd_fused_wave_lds(uint64_t nslots, bool compact = false) {
-  return (((size_t)nslots * (compact ? 20 : 32)) + 15) & ~size_t(15);
+  const size_t state = compact ? (((size_t)nslots * 20 + 7) & ~size_t(7)) : (size_t)nslots * 32;
+  return (state + (size_t)nslots * 8 + 15) & ~size_t(15);
 }
 constexpr size_t kScdFusedMaxLds = 80 * 1024;  // per workgroup (4 waves + shared cd filter)
 // fused_fn: query-specialised (JIT) k_scd_fused, or nullptr for the precompiled kernel

@@ -56,8 +56,12 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
   ScdSlot* st = reinterpret_cast<ScdSlot*>(wbase);        // wide state [S]
   ScdSlot32* st32 = reinterpret_cast<ScdSlot32*>(wbase);  // compact state [S] ...
   uint32_t* fr32 = reinterpret_cast<uint32_t*>(st32 + S); // ... + first rows [S]
+  // per-slot lane masks of the current step (after the wide or compact state, 8-aligned)
+  unsigned long long* tbl = reinterpret_cast<unsigned long long*>(
+      wbase + (COMPACT ? (((size_t)S * 20 + 7) & ~size_t(7)) : (size_t)S * 32));
   unsigned int* cdb = reinterpret_cast<unsigned int*>(smem + (size_t)(blockDim.x >> 6) * d.wave_lds);
   for (int i = lane; i < S; i += 64) {
+    tbl[i] = 0ull;
     if (COMPACT) {
       st32[i] = ScdSlot32{0u, 0u, 0u, 0u};
       fr32[i] = kNoRow;
@@ -110,6 +114,7 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         if (cc == c) vcd = v[c][0];
       }
       if (COMPACT) vb = (uint32_t)(vb - (uint64_t)d.vmin);
+#ifndef BQ_SCD_SKIP_CD
       if (do_cd && act) {
         // (slot, value) pair bit: an LDS fire-and-forget OR (merged into the device bitmap once
         // per workgroup at the end); without an LDS bitmap, the device bitmap directly
@@ -123,12 +128,15 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
           atomicAdd(&d.cd.out[s], 1ull);
         }
       }
+#endif
       // lanes of this lane's slot: one ballot per slot-id bit
       uint64_t match = __ballot(act);
       if (match == 0) continue;
+#ifdef BQ_SCD_BALLOT_MATCH
+      // (alternative) one ballot per slot-id bit
 #ifdef BQ_SLOT_BITS
 #pragma unroll
-      for (int bit = 0; bit < BQ_SLOT_BITS; ++bit) {  // JIT: slot-id width is a constant
+      for (int bit = 0; bit < BQ_SLOT_BITS; ++bit) {
 #else
       for (int bit = 0; bit < d.slot_bits; ++bit) {
 #endif
@@ -136,6 +144,13 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         const uint64_t bb = __ballot(act && on);
         match &= on ? bb : ~bb;
       }
+#else
+      // lanes of this lane's slot: every lane ORs its bit into the slot's LDS mask word, then
+      // reads the word back (a wave's LDS instructions execute in program order; OR does not
+      // depend on the order of the lanes); the slot's first lane clears it below
+      if (act) atomicOr(&tbl[s], 1ull << lane);
+      match = act ? tbl[s] : 0ull;
+#endif
       const uint64_t below = match & lanes_below;
       const int pl = below ? 63 - __clzll((long long)below) : lane;
       const int hl = (act && match) ? 63 - __clzll((long long)match) : lane;
@@ -149,7 +164,14 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       }
       const bool diff = act && below != 0 && !scd_equal(vb, pv, isf);
       const uint64_t dm = __ballot(diff);
+#ifdef BQ_SCD_SKIP_STATE
+      if (act && below == 0 && dm == 0x1234567ull) {
+#else
       if (act && below == 0) {
+#endif
+#ifndef BQ_SCD_BALLOT_MATCH
+        tbl[s] = 0ull;  // after every lane's read of the mask (program order)
+#endif
         const uint32_t add_rows = (uint32_t)__popcll(match), add_ch = (uint32_t)__popcll(dm & match);
         if (COMPACT) {
           ScdSlot32 cur = st32[s];
