@@ -1197,6 +1197,54 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     }
   }
 
+  // ---- small slot spaces: compaction + ordering + emit in one workgroup; the header and the
+  // columns (capacity S) come back in one copy, with no host round trip in between
+  if (S <= kSmallEmitSlots && !getenv("BQGPU_NO_SMALL_EMIT")) {
+    std::vector<size_t> offs;
+    size_t obytes = 256;  // header: groups, passing rows
+    for (int j = 0; j < e.ncols; ++j) {
+      offs.push_back(obytes);
+      obytes += ((size_t)S * dtype_size(out_dt[j]) + 255) & ~size_t(255);
+    }
+    unsigned char* ob = (unsigned char*)c->outcols.ensure(obytes + 256);
+    for (int j = 0; j < e.ncols; ++j) e.cols[j].out = ob + offs[j];
+    launch_emit_small(e, sa, (uint32_t)S, nsum, (unsigned long long*)ob, st);
+    HIPCHECK(hipGetLastError());
+    PinnedBlock blk{};
+    const unsigned long long* hh;
+    if (c->dev_target) {
+      hh = (const unsigned long long*)c->hhdr.ensure(64);
+      HIPCHECK(hipMemcpyAsync((void*)hh, ob, 16, hipMemcpyDeviceToHost, st));
+    } else {
+      blk = c->pool_get(obytes + 64);
+      hh = (const unsigned long long*)blk.p;
+      HIPCHECK(hipMemcpyAsync(blk.p, ob, obytes, hipMemcpyDeviceToHost, st));
+    }
+    if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
+    HIPCHECK(hipStreamSynchronize(st));
+    const int64_t G = (int64_t)hh[0];
+    const int filtered = pl.has_filter && (int64_t)hh[1] < N;
+    if (c->timing) {
+      float ms = 0;
+      HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+      c->last.scan_ms = ms;
+      HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+      c->last.total_ms = ms;
+    }
+    c->last.bytes = pl.alg_bytes + G * (int64_t)e.ncols * 8;
+    if (G == 0) {
+      if (blk.p) c->pool->put(blk);
+      *out = empty_result(out_dt, filtered);
+    } else if (c->dev_target) {
+      std::vector<const void*> src;
+      for (int j = 0; j < e.ncols; ++j) src.push_back(e.cols[j].out);
+      table_from_device(c, out_dt, src, G);
+    } else {
+      *out = block_result(c, blk, G, filtered, out_dt, offs);
+    }
+    return;
+  }
+
   // ---- generic emit
   const uint64_t cblocks = (S + 4095) / 4096 + 1;
   unsigned char* lb = (unsigned char*)c->lists.ensure(S * 8 + (2 * cblocks + 4096) * 8 + 256);

@@ -251,33 +251,77 @@ __device__ __forceinline__ ScdState scd_combine(const ScdState& a, const ScdStat
   return r;
 }
 
-// One workgroup per slot: each of its 4 waves takes a contiguous quarter of the chunks, each
-// lane a contiguous run of that quarter (loads clamped, not branched, so they pipeline), an
-// ordered shuffle tree folds the lanes, and the 4 wave results are folded in order.
-__global__ __launch_bounds__(kBlock) void k_scd_combine(ScdLaunch d, uint64_t nslots, int isf) {
+__device__ __forceinline__ ScdState scd_load(const ScdLaunch& d, size_t idx, bool valid) {
+  ScdState x;
+  x.first_row = d.st_first_row[idx];
+  x.present = valid && x.first_row != kNoRow;
+  x.first = d.st_first[idx];
+  x.last = d.st_last[idx];
+  x.changes = d.st_changes[idx];
+  x.rows = d.st_count ? d.st_count[idx] : 0u;
+  return x;
+}
+
+__device__ __forceinline__ void scd_store_final(const ScdLaunch& d, uint64_t s, const ScdState& t) {
+  d.out_changes[s] = t.changes;
+  d.out_first[s] = t.first;
+  if (d.slot_cnt) {
+    d.slot_cnt[s] = t.present ? t.rows : 0ull;
+    d.slot_fst[s] = t.present ? t.first_row : kNoRow;
+  }
+}
+
+// Stage 1 of the chunk combine: one thread per (slot, run of `per` consecutive chunks);
+// consecutive threads take consecutive slots, so every load of a wave is one coalesced row
+// segment of the [chunk][slot] state arrays.  The run's combined state is written back in
+// place over the run's first chunk (no other thread reads that run).
+__global__ __launch_bounds__(kBlock) void k_scd_combine_runs(ScdLaunch d, uint64_t nslots, int per, int runs,
+                                                          int isf) {
+  const uint64_t item = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (item >= nslots * (uint64_t)runs) return;
+  const uint64_t s = item % nslots;
+  const int g = (int)(item / nslots);
+  const int beg = g * per, end = min(d.waves, beg + per);
+  ScdState st = {0, kNoRow, 0, 0, 0, 0};
+  constexpr int kU = 8;
+  for (int w0 = beg; w0 < end; w0 += kU) {
+    ScdState x[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) x[k] = scd_load(d, (size_t)min(w0 + k, end - 1) * nslots + s, w0 + k < end);
+#pragma unroll
+    for (int k = 0; k < kU; ++k) st = scd_combine(st, x[k], isf);
+  }
+  if (runs == 1) {  // the run is the whole slot: final values
+    scd_store_final(d, s, st);
+    return;
+  }
+  const size_t o = (size_t)beg * nslots + s;
+  d.st_first_row[o] = st.present ? st.first_row : kNoRow;
+  d.st_first[o] = st.first;
+  d.st_last[o] = st.last;
+  d.st_changes[o] = (uint32_t)st.changes;
+  if (d.st_count) d.st_count[o] = (uint32_t)st.rows;
+}
+
+// Stage 2: one workgroup per slot over the `runs` run states (chunk rows 0, per, 2 per, ...):
+// each of its 4 waves takes a contiguous quarter, each lane a contiguous part of that quarter
+// (loads clamped, not branched, so they pipeline), an ordered shuffle tree folds the lanes,
+// and the 4 wave results are folded in order.
+__global__ __launch_bounds__(kBlock) void k_scd_combine(ScdLaunch d, uint64_t nslots, int per, int runs, int isf) {
   __shared__ ScdState part[kBlock / 64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nw = kBlock / 64;
   for (uint64_t s = blockIdx.x; s < nslots; s += gridDim.x) {
-  const int wbeg = (int)((int64_t)d.waves * wave / nw), wend = (int)((int64_t)d.waves * (wave + 1) / nw);
+  const int wbeg = (int)((int64_t)runs * wave / nw), wend = (int)((int64_t)runs * (wave + 1) / nw);
   const int span = wend - wbeg;
-  const int per = (span + 63) / 64;
-  const int lbeg = wbeg + min(span, lane * per), lend = wbeg + min(span, (lane + 1) * per);
+  const int lper = (span + 63) / 64;
+  const int lbeg = wbeg + min(span, lane * lper), lend = wbeg + min(span, (lane + 1) * lper);
   ScdState st = {0, kNoRow, 0, 0, 0, 0};
-  constexpr int kU = 8;  // chunk states loaded per round (clamped, all in flight at once)
+  constexpr int kU = 4;  // run states loaded per round (clamped, all in flight at once)
   for (int w0 = lbeg; w0 < lend; w0 += kU) {
     ScdState x[kU];
 #pragma unroll
-    for (int k = 0; k < kU; ++k) {
-      const int w = min(w0 + k, lend - 1);
-      const size_t idx = (size_t)w * nslots + s;
-      x[k].first_row = d.st_first_row[idx];
-      x[k].present = (w0 + k < lend) && x[k].first_row != kNoRow;
-      x[k].first = d.st_first[idx];
-      x[k].last = d.st_last[idx];
-      x[k].changes = d.st_changes[idx];
-      x[k].rows = d.st_count ? d.st_count[idx] : 0u;
-    }
+    for (int k = 0; k < kU; ++k) x[k] = scd_load(d, (size_t)min(w0 + k, lend - 1) * per * nslots + s, w0 + k < lend);
 #pragma unroll
     for (int k = 0; k < kU; ++k) st = scd_combine(st, x[k], isf);
   }
@@ -296,12 +340,7 @@ __global__ __launch_bounds__(kBlock) void k_scd_combine(ScdLaunch d, uint64_t ns
   if (threadIdx.x == 0) {
     ScdState t = part[0];
     for (int q = 1; q < nw; ++q) t = scd_combine(t, part[q], isf);
-    d.out_changes[s] = t.changes;
-    d.out_first[s] = t.first;
-    if (d.slot_cnt) {
-      d.slot_cnt[s] = t.present ? t.rows : 0ull;
-      d.slot_fst[s] = t.present ? t.first_row : kNoRow;
-    }
+    scd_store_final(d, s, t);
   }
   __syncthreads();  // part[] is rewritten for the next slot
   }
@@ -341,7 +380,20 @@ void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hi
   int isf = 0;
   for (int c = 0; c < p.ncols; ++c)
     if (c == d.vcol) isf = dtype_is_float(p.cols[c].dtype);
-  const uint64_t cblocks = p.nslots < 65536 ? p.nslots : 65536;  // grid-stride over slots beyond
-  hipLaunchKernelGGL(k_scd_combine, dim3((unsigned)cblocks), dim3(kBlock), 0, st, d, p.nslots, isf);
+  // stage 1: ~2 threads per CU lane over (slot, run of chunks); stage 2 folds the runs per slot
+  const uint64_t S = p.nslots;
+  const uint64_t target = (uint64_t)device_cu_count() * kBlock * 2;
+  uint64_t want = (target + S - 1) / S;
+  if (want > (uint64_t)d.waves) want = (uint64_t)d.waves;
+  if (want < 1) want = 1;
+  const int per = (int)(((uint64_t)d.waves + want - 1) / want);
+  const int runs = (int)(((uint64_t)d.waves + per - 1) / per);
+  const uint64_t items = S * (uint64_t)runs;
+  hipLaunchKernelGGL(k_scd_combine_runs, dim3((unsigned)((items + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, d, S,
+                     per, runs, isf);
+  if (runs > 1) {
+    const uint64_t cblocks = S < 65536 ? S : 65536;  // grid-stride over slots beyond
+    hipLaunchKernelGGL(k_scd_combine, dim3((unsigned)cblocks), dim3(kBlock), 0, st, d, S, per, runs, isf);
+  }
 }
 }  // namespace bqg

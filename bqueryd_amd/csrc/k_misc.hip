@@ -190,6 +190,109 @@ __global__ void k_emit(EmitParams e, SlotArrays sa, const uint32_t* order, unsig
   }
 }
 
+// Small slot spaces (<= kSmallEmitSlots): compaction, first-appearance ordering and emit in
+// one workgroup, with the group count and passing rows written to hdr[0], hdr[1] -- no host
+// round trip between the compaction and the emit.  Up to 1024 groups are ranked by counting
+// (each thread compares its group's first row with every other one, LDS broadcast reads);
+// more are bitonic-sorted in LDS.
+__global__ __launch_bounds__(1024) void k_emit_small(EmitParams e, SlotArrays sa, uint32_t nslots, int nsum,
+                                                     unsigned long long* hdr) {
+  __shared__ uint32_t kf[kSmallEmitSlots];
+  __shared__ uint32_t ks[kSmallEmitSlots];
+  __shared__ unsigned int wsum[16];
+  __shared__ unsigned long long wrows[16];
+  constexpr int kPer = kSmallEmitSlots / 1024;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t occ = 0;
+  unsigned long long rows = 0;
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const uint32_t s = threadIdx.x * kPer + r;
+    const unsigned long long n = s < nslots ? sa.cnt[s] : 0ull;
+    occ |= (n > 0 ? 1u : 0u) << r;
+    rows += n;
+  }
+  const unsigned int v = (unsigned int)__popc(occ);
+  unsigned int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned int t = (unsigned int)__shfl_up((int)incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  const unsigned long long rw = wave_sum_u64(rows);
+  if (lane == 63) wsum[wave] = incl;
+  if (lane == 0) wrows[wave] = rw;
+  __syncthreads();
+  unsigned int before = 0, G = 0;
+  unsigned long long total = 0;
+  for (int q = 0; q < 16; ++q) {
+    before += q < wave ? wsum[q] : 0u;
+    G += wsum[q];
+    total += wrows[q];
+  }
+  unsigned int pos = before + incl - v;
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    if (occ & (1u << r)) {
+      const uint32_t s = threadIdx.x * kPer + r;
+      kf[pos] = sa.fst[s];
+      ks[pos] = s;
+      ++pos;
+    }
+  }
+  if (threadIdx.x == 0) {
+    hdr[0] = G;
+    hdr[1] = total;
+  }
+  const int nsum2 = e.nsum2;
+  auto emit_one = [&](uint32_t s, unsigned int row) {
+    SlotTotals t;
+    t.cnt = sa.cnt[s];
+    t.fst = sa.fst[s];
+#pragma unroll
+    for (int q = 0; q < kMaxSums; ++q) {
+      t.acc[q] = q < nsum ? sa.acc[(size_t)q * nslots + s] : 0ull;
+      t.acc2[q] = (sa.acc2 && q < nsum2) ? sa.acc2[(size_t)q * nslots + s] : 0ull;
+    }
+    const uint64_t code = e.hash ? (uint64_t)sa.keys[s] : (uint64_t)s;
+    emit_slot(e, s, code, row, t);
+  };
+  if (G <= 1024) {
+    // the first rows of distinct groups are distinct: rank = groups whose first row is earlier
+    __syncthreads();
+    uint32_t f = kNoRow, s = 0;
+    if (threadIdx.x < G) {
+      f = kf[threadIdx.x];
+      s = ks[threadIdx.x];
+    }
+    unsigned int rank = 0;
+    for (unsigned int j = 0; j < G; ++j) rank += kf[j] < f ? 1u : 0u;
+    if (threadIdx.x < G) emit_one(s, rank);
+    return;
+  }
+  unsigned int m = 1;
+  while (m < G) m <<= 1;
+  for (unsigned int i = G + threadIdx.x; i < m; i += blockDim.x) kf[i] = kNoRow;
+  __syncthreads();
+  for (unsigned int k = 2; k <= m; k <<= 1) {
+    for (unsigned int j = k >> 1; j > 0; j >>= 1) {
+      for (unsigned int i = threadIdx.x; i < m; i += blockDim.x) {
+        const unsigned int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const uint32_t a = kf[i], b = kf[ixj];
+          if ((a > b) == up) {
+            kf[i] = b; kf[ixj] = a;
+            const uint32_t t = ks[i]; ks[i] = ks[ixj]; ks[ixj] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (unsigned int i = threadIdx.x; i < G; i += blockDim.x) emit_one(ks[i], i);
+}
+
 // ------------------------------------------------------------------------------------
 // Column statistics: order-preserving 64-bit keys, min/max by atomics
 // ------------------------------------------------------------------------------------
@@ -423,6 +526,10 @@ void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order
                  uint64_t nslots, hipStream_t st) {
   const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(k_emit, dim3(g ? g : 1), dim3(256), 0, st, e, s, order, n, nsum, nslots);
+}
+void launch_emit_small(const EmitParams& e, const SlotArrays& s, uint32_t nslots, int nsum, unsigned long long* hdr,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(k_emit_small, dim3(1), dim3(1024), 0, st, e, s, nslots, nsum, hdr);
 }
 constexpr uint32_t kHashPartLds = 8192;
 // ------------------------------------------------------------------------------------

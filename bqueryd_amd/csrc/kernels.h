@@ -123,6 +123,11 @@ void launch_rank_bitmap(const uint32_t* list_fst, const uint32_t* list_slot, uns
                         unsigned int* block_prefix, uint32_t* order, hipStream_t st);
 void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order,
                  unsigned int n, int nsum, uint64_t nslots, hipStream_t st);
+// slot spaces up to kSmallEmitSlots: compaction + ordering + emit in one workgroup (output
+// columns of capacity nslots); hdr[0] = groups, hdr[1] = passing rows
+constexpr uint32_t kSmallEmitSlots = 8192;
+void launch_emit_small(const EmitParams& e, const SlotArrays& s, uint32_t nslots, int nsum,
+                       unsigned long long* hdr, hipStream_t st);
 
 // column statistics (min / max / nan) of one column
 void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, hipStream_t st);

@@ -5,8 +5,9 @@
 // from the previous row OF THE SAME GROUP (bquery's `last[g]` loop, with its zero-initialised
 // `last` and first-row rule applied at emit).  Each wave owns a contiguous chunk of rows and
 // consumes it 64 rows per step in row order, one row per lane (coalesced 4- or 8-byte loads,
-// kScdAhead steps in flight).  Inside a step the lanes of one slot find each other with one
-// ballot per slot-id bit (no LDS traffic); the previous row of a slot inside the step is the
+// kScdAhead steps in flight).  Inside a step the lanes of one slot find each other through a
+// per-slot 64-bit lane mask in wave-private LDS (every lane ORs its bit, then reads the word
+// back; BQ_SCD_BALLOT_MATCH selects one ballot per slot-id bit instead); the previous row of a slot inside the step is the
 // highest lower lane of its match mask (one bpermute); the slot's first lane in the step
 // folds the whole step into the per-slot state {last, first, rows, changes, first row} in LDS
 // with one read and one write.  Per-slot row counts and first rows come out of the same pass

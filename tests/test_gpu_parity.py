@@ -184,6 +184,18 @@ def test_count_distinct_hash_set(oracle_c):
     run_both(cols, ['k'], [['v', 'count_distinct', 'cd'], ['v', 'sorted_count_distinct', 'scd']], [], oracle_c)
 
 
+@pytest.mark.parametrize('krange', [300, 20_000, 400_000])
+def test_sorted_count_distinct_slot_spaces(krange, oracle_c):
+    """Chunk-state combine over small, medium and large slot spaces (many runs of chunks per
+    slot, a few, and one run per slot)."""
+    rng = np.random.default_rng(krange)
+    n = 600_000
+    cols = OrderedDict(k=rng.integers(0, krange, n).astype(np.int32),
+                       v=np.repeat(rng.integers(0, 3, n // 4 + 1), 4)[:n].astype(np.int64))
+    run_both(cols, ['k'], [['v', 'sorted_count_distinct', 's'], ['v', 'sum', 'vs']], [], oracle_c)
+    run_both(cols, ['k'], [['v', 'sorted_count_distinct', 's']], [], oracle_c)
+
+
 def test_select_rows_and_expand(oracle_c):
     cols = synth.taxi_shard(50_000, config_id=2, columns=('payment_type', 'passenger_count', 'fare_amount'))
     terms = [('passenger_count', '>=', 2)]
