@@ -148,6 +148,7 @@ struct bqg_table {
 struct PinnedBlock {
   void* p = nullptr;
   size_t cap = 0;
+  void* dev = nullptr;  // the block's device address (kernels write results into it directly)
 };
 
 struct PinnedPool {
@@ -177,6 +178,10 @@ struct PinnedPool {
       throw ApiError{BQG_E_OOM, "pinned result block allocation failed"};
     }
     b.cap = cap;
+    if (hipHostGetDevicePointer(&b.dev, b.p, 0) != hipSuccess || !b.dev) {
+      (void)hipHostFree(b.p);
+      throw ApiError{BQG_E_HIP, "pinned result block is not device-mapped"};
+    }
     return b;
   }
   void put(PinnedBlock b) {
@@ -273,7 +278,7 @@ struct bqg_ctx {
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
   int stage_i = 0;
   // scratch
-  DevBuf partials, counter, hdr, slots, terms, outcols, lists, bitmap, prefix, cdbuf, scdbuf, mask, misc;
+  DevBuf partials, counter, hdr, slots, terms, outcols, lists, bitmap, prefix, cdbuf, scdbuf, mask, misc, done;
   HostBuf hhdr, hout;
   // pinned blocks for results (returned by bqg_result_free); shared with outstanding results
   // so a result may outlive its context
@@ -833,12 +838,30 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     F.partials = L.partials;
     F.out_hdr = (unsigned long long*)c->hdr.ensure(64);
     F.totals = (unsigned long long*)c->counter.ensure((size_t)(2 + kMaxSums) * kMaxPrivateSlots * 8);
+    F.done = (unsigned int*)c->done.p;
     F.emit_inline = need_generic ? 0 : 1;
+    // host result: the finish step writes [64-byte header | columns of S rows] straight into
+    // a pooled pinned block (device-mapped host memory: no copy); device result: into HBM
+    PinnedBlock hblk{};
+    const size_t colbytes = (size_t)e.ncols * S * 8;
     if (F.emit_inline) {
-      unsigned char* ob = (unsigned char*)c->outcols.ensure((size_t)e.ncols * S * 8 + 256);
-      for (int j = 0; j < e.ncols; ++j) e.cols[j].out = ob + (size_t)j * S * 8;
+      unsigned char* ob;
+      if (!c->dev_target) {
+        hblk = c->pool_get(colbytes + 64);
+        ob = (unsigned char*)hblk.dev;
+      } else {
+        ob = (unsigned char*)c->outcols.ensure(64 + colbytes + 256);
+      }
+      F.out_hdr = (unsigned long long*)ob;
+      for (int j = 0; j < e.ncols; ++j) e.cols[j].out = ob + 64 + (size_t)j * S * 8;
     }
-    hipFunction_t jfn = N >= jit_min_rows() ? jit_function("bq_jit_scan_private", jit_spec(pl.p)) : nullptr;
+    hipFunction_t jfn = nullptr;
+    if (N >= jit_min_rows()) {
+      std::string spec = jit_spec(pl.p);
+      // tiles in flight per workgroup (profiling knob; default in scan_private.h)
+      if (const char* ev = getenv("BQGPU_PRIV_AHEAD")) spec += std::string("#define BQ_PRIV_AHEAD ") + std::to_string(std::max(1, std::min(4, atoi(ev)))) + "\n";
+      jfn = jit_function("bq_jit_scan_private", spec);
+    }
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
     if (jfn) {
       void* args[] = {(void*)&pl.p, (void*)&L};
@@ -858,7 +881,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
       HIPCHECK(hipStreamSynchronize(st));
       std::vector<const void*> src;
-      for (int j = 0; j < e.ncols; ++j) src.push_back((const unsigned char*)c->outcols.p + (size_t)j * S * 8);
+      for (int j = 0; j < e.ncols; ++j) src.push_back(e.cols[j].out);
       table_from_device(c, out_dt, src, (int64_t)hh[0]);
       if (c->timing) {
         float ms = 0;
@@ -872,12 +895,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       return;
     }
     if (!need_generic) {
-      // one D2H of header + columns straight into a pooled pinned block
-      const size_t colbytes = (size_t)e.ncols * S * 8;
-      PinnedBlock blk = c->pool_get(colbytes + 64);
+      PinnedBlock blk = hblk;
       unsigned char* h = (unsigned char*)blk.p;
-      HIPCHECK(hipMemcpyAsync(h, F.out_hdr, 16, hipMemcpyDeviceToHost, st));
-      if (colbytes) HIPCHECK(hipMemcpyAsync(h + 64, c->outcols.p, colbytes, hipMemcpyDeviceToHost, st));
       if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
       HIPCHECK(hipStreamSynchronize(st));
       const unsigned long long G = ((unsigned long long*)h)[0], total = ((unsigned long long*)h)[1];
@@ -1024,6 +1043,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       F.partials = L.partials;
       F.out_hdr = (unsigned long long*)c->hdr.ensure(64);
       F.totals = (unsigned long long*)c->counter.ensure((size_t)(2 + kMaxSums) * kMaxPrivateSlots * 8);
+      F.done = (unsigned int*)c->done.p;
       F.emit_inline = 0;
       launch_scan_private(q2, L, st);
       launch_private_finish(F, sa2, e, st);
@@ -1206,19 +1226,19 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       offs.push_back(obytes);
       obytes += ((size_t)S * dtype_size(out_dt[j]) + 255) & ~size_t(255);
     }
-    unsigned char* ob = (unsigned char*)c->outcols.ensure(obytes + 256);
+    // host result: written straight into a pooled pinned block (device-mapped, no copy)
+    PinnedBlock blk{};
+    if (!c->dev_target) blk = c->pool_get(obytes + 64);
+    unsigned char* ob = c->dev_target ? (unsigned char*)c->outcols.ensure(obytes + 256) : (unsigned char*)blk.dev;
     for (int j = 0; j < e.ncols; ++j) e.cols[j].out = ob + offs[j];
     launch_emit_small(e, sa, (uint32_t)S, nsum, (unsigned long long*)ob, st);
     HIPCHECK(hipGetLastError());
-    PinnedBlock blk{};
     const unsigned long long* hh;
     if (c->dev_target) {
       hh = (const unsigned long long*)c->hhdr.ensure(64);
       HIPCHECK(hipMemcpyAsync((void*)hh, ob, 16, hipMemcpyDeviceToHost, st));
     } else {
-      blk = c->pool_get(obytes + 64);
       hh = (const unsigned long long*)blk.p;
-      HIPCHECK(hipMemcpyAsync(blk.p, ob, obytes, hipMemcpyDeviceToHost, st));
     }
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -1364,7 +1384,10 @@ int bqg_create(int device_ordinal, bqg_ctx** out) {
       HIPCHECK(hipHostMalloc(&c->stage[i], bqg_ctx::kStage, hipHostMallocDefault));
       HIPCHECK(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
     }
-    for (int i = 0; i < 4; ++i) HIPCHECK(hipEventCreate(&c->ev[i]));
+    // timing-only events: no system-scope fence (cache writeback) at each record
+    for (int i = 0; i < 4; ++i) HIPCHECK(hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence));
+    // last-workgroup-done counters of the finish kernels (each reset by its last workgroup)
+    HIPCHECK(hipMemset(c->done.ensure(256), 0, 256));
     *out = c;
   });
   if (rc != BQG_OK && c) {
@@ -1379,7 +1402,7 @@ int bqg_destroy(bqg_ctx* c) {
   int rc = guard(c, [&] {
     HIPCHECK(hipStreamSynchronize(c->stream));
     for (DevBuf* b : {&c->partials, &c->counter, &c->hdr, &c->slots, &c->terms, &c->outcols, &c->lists,
-                      &c->bitmap, &c->prefix, &c->cdbuf, &c->scdbuf, &c->mask, &c->misc})
+                      &c->bitmap, &c->prefix, &c->cdbuf, &c->scdbuf, &c->mask, &c->misc, &c->done})
       b->release();
     c->hhdr.release();
     c->hout.release();

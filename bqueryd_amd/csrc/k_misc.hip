@@ -268,6 +268,7 @@ __global__ __launch_bounds__(1024) void k_emit_small(EmitParams e, SlotArrays sa
     unsigned int rank = 0;
     for (unsigned int j = 0; j < G; ++j) rank += kf[j] < f ? 1u : 0u;
     if (threadIdx.x < G) emit_one(s, rank);
+    __threadfence_system();  // outputs may live in device-mapped host memory
     return;
   }
   unsigned int m = 1;
@@ -291,6 +292,7 @@ __global__ __launch_bounds__(1024) void k_emit_small(EmitParams e, SlotArrays sa
     }
   }
   for (unsigned int i = threadIdx.x; i < G; i += blockDim.x) emit_one(ks[i], i);
+  __threadfence_system();
 }
 
 // ------------------------------------------------------------------------------------

@@ -14,9 +14,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_private(ScanParams p, Privat
   scan_private_body<NC>(p, L, smem);
 }
 
+__device__ void private_finish_body(const FinishParams& f, const SlotArrays& sa, const EmitParams& e, int tid);
+
 // One workgroup per (component, slot): sums / mins that slot's per-workgroup partials in a
-// fixed order (coalesced reads, fixed LDS tree: bitwise deterministic).
-__global__ __launch_bounds__(kBlock) void k_private_reduce(FinishParams f) {
+// fixed order (coalesced reads, fixed LDS tree: bitwise deterministic).  The last workgroup
+// to finish (device-scope counter) runs the finish step, so a query is one launch after the
+// scan.
+__global__ __launch_bounds__(kBlock) void k_private_reduce(FinishParams f, SlotArrays sa, EmitParams e) {
   __shared__ unsigned long long red[kBlock];
   const int pair = blockIdx.x, tid = threadIdx.x;
   const int S = f.nslots, nb = f.blocks;
@@ -48,13 +52,22 @@ __global__ __launch_bounds__(kBlock) void k_private_reduce(FinishParams f) {
     }
     __syncthreads();
   }
-  if (tid == 0) f.totals[pair] = red[0];
+  __shared__ bool last;
+  if (tid == 0) {
+    f.totals[pair] = red[0];
+    __threadfence();  // release the total before counting this workgroup done
+    last = atomicAdd(f.done, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // acquire every workgroup's total
+  if (tid < 64) private_finish_body(f, sa, e, tid);
+  if (tid == 0) *f.done = 0u;  // ready for the next launch (stream order)
 }
 
 // Emits the groups in first-appearance order (S is small: rank by counting), or stores the
 // per-slot totals for the generic emit path.
-__global__ __launch_bounds__(64) void k_private_finish(FinishParams f, SlotArrays sa, EmitParams e) {
-  const int tid = threadIdx.x;
+__device__ void private_finish_body(const FinishParams& f, const SlotArrays& sa, const EmitParams& e, int tid) {
   const int S = f.nslots, nsum = f.nsum;
   const int P = (2 + nsum) * S;
   const unsigned long long* tot = f.totals;
@@ -94,6 +107,8 @@ __global__ __launch_bounds__(64) void k_private_finish(FinishParams f, SlotArray
     f.out_hdr[0] = g;
     f.out_hdr[1] = total;
   }
+  // the outputs may live in device-mapped host memory: make them visible at system scope
+  __threadfence_system();
 }
 
 void launch_scan_private(const ScanParams& p, const PrivateLaunch& l, hipStream_t st) {
@@ -101,8 +116,7 @@ void launch_scan_private(const ScanParams& p, const PrivateLaunch& l, hipStream_
 }
 
 void launch_private_finish(const FinishParams& f, const SlotArrays& s, const EmitParams& e, hipStream_t st) {
-  hipLaunchKernelGGL(k_private_reduce, dim3((2 + f.nsum) * f.nslots), dim3(kBlock), 0, st, f);
-  hipLaunchKernelGGL(k_private_finish, dim3(1), dim3(64), 0, st, f, s, e);
+  hipLaunchKernelGGL(k_private_reduce, dim3((2 + f.nsum) * f.nslots), dim3(kBlock), 0, st, f, s, e);
 }
 
 }  // namespace bqg

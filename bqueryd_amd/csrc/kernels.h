@@ -51,6 +51,7 @@ struct FinishParams {
   const unsigned long long* partials;
   unsigned long long* totals;     // [(2 + nsum) * nslots] scratch
   unsigned long long* out_hdr;    // [0] = groups, [1] = passing rows
+  unsigned int* done;             // zero-initialised counter: the last reduce workgroup finishes
 };
 
 void launch_scan_private(const ScanParams& p, const PrivateLaunch& l, hipStream_t st);

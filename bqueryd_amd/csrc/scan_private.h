@@ -6,6 +6,11 @@
 
 namespace bqg {
 
+#ifndef BQ_PRIV_AHEAD
+#define BQ_PRIV_AHEAD 1
+#endif
+constexpr int kPrivAhead = BQ_PRIV_AHEAD;  // tiles loaded ahead of the one being aggregated
+
 // Every lane owns a private accumulator row per slot in LDS, laid out [slot][lane] so that
 // the per-row read-modify-writes are conflict-free ds_read/ds_write with no atomics.  Rows
 // of a lane are processed in increasing order, so its first write to a slot is that slot's
@@ -26,15 +31,30 @@ __device__ __forceinline__ void scan_private_body(const ScanParams& p, const Pri
   for (int i = 0; i < nsum * S; ++i) acc[i * kBlock + tid] = 0;
 
   const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
-  int64_t tile = blockIdx.x;
-  Chunk raw[NC];
-  if (tile < ntiles) load_rows4<NC>(p, tile * kTileRows + (int64_t)tid * kRowsPerThread, raw);
-  for (; tile < ntiles; tile += gridDim.x) {
-    const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
+  const int64_t grid = gridDim.x;
+  const int64_t lane_row = (int64_t)tid * kRowsPerThread;
+  // kPrivAhead tiles in flight per workgroup while one is aggregated (a ring of registers).
+  // Loads are unconditional: past the last tile a lane re-reads the tile it is consuming (an
+  // L2 hit), so every path has the same loads in flight and the compiler waits with
+  // vmcnt(N) for exactly the oldest tile.
+  Chunk ring[kPrivAhead][NC];
+  if (blockIdx.x < ntiles) {
+#pragma unroll
+    for (int a = 0; a < kPrivAhead; ++a) {
+      const int64_t t = blockIdx.x + a * grid;
+      load_rows4<NC>(p, (t < ntiles ? t : (int64_t)blockIdx.x) * kTileRows + lane_row, ring[a]);
+    }
+  }
+  for (int64_t tbase = blockIdx.x; tbase < ntiles; tbase += kPrivAhead * grid) {
+#pragma unroll
+  for (int a = 0; a < kPrivAhead; ++a) {
+    const int64_t tile = tbase + a * grid;
+    if (tile >= ntiles) break;
+    const int64_t row0 = tile * kTileRows + lane_row;
     uint64_t v[NC][4];
-    decode_all<NC, 4>(p, raw, v);
-    const int64_t next = tile + gridDim.x;
-    if (next < ntiles) load_rows4<NC>(p, next * kTileRows + (int64_t)tid * kRowsPerThread, raw);
+    decode_all<NC, 4>(p, ring[a], v);
+    const int64_t next = tile + kPrivAhead * grid;
+    load_rows4<NC>(p, (next < ntiles ? next : tile) * kTileRows + lane_row, ring[a]);
     const uint32_t pass = vals_pass<NC, 4>(p, row0, v);
     uint64_t code[4];
     vals_code<NC, 4>(p, v, code);
@@ -63,6 +83,7 @@ __device__ __forceinline__ void scan_private_body(const ScanParams& p, const Pri
         }
       }
     }
+  }
   }
   __syncthreads();
 
