@@ -70,7 +70,15 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       st[i] = ScdSlot{0ull, 0ull, 0u, 0u, kNoRow, 0u};
     }
   }
-  const bool do_cd = d.cd.bitmap != nullptr;
+  // count_distinct mode: 0 none, 1 LDS pair bitmap (merged at the end), 2 device bitmap.  The
+  // JIT build fixes it at compile time: a device-bitmap branch in the loop (a load and a
+  // returning atomic) would make the compiler drain every prefetched load at each step.
+#ifdef BQ_SCD_CD
+  constexpr int cd_mode = BQ_SCD_CD;
+#else
+  const int cd_mode = d.cd.bitmap == nullptr ? 0 : (d.cd.lds_bitmap_words > 0 ? 1 : 2);
+#endif
+  const bool do_cd = cd_mode != 0;
   for (int i = threadIdx.x; i < d.cd.lds_bitmap_words; i += blockDim.x) cdb[i] = 0u;
   __syncthreads();
   const int w = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -94,16 +102,22 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
 #pragma unroll
     for (int a = 0; a < kScdAhead; ++a) {
       const int64_t b = gbase + 64 * a;
-      if (b >= end) break;
       const int64_t row = b + lane;
       Chunk raw[NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c) row_word_to_chunk(raw[c], p.cols[c], row, ring[a][c]);
-      // unconditional (clamped) prefetch: the same number of loads is in flight on every
-      // path, so the compiler waits for exactly the step it consumes (vmcnt(N), not vmcnt(0))
-      scd_issue<NC>(p, b + 64 * kScdAhead, end, lane, ring[a]);
       uint64_t v[NC][1];
       decode_all<NC, 1>(p, raw, v);
+      // the step's values are out of ring[a] before its refill is issued: without this
+      // scheduling fence the compiler hoists the refill above the decode into fresh registers
+      // and copies them back at the loop latch, behind an s_waitcnt vmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+      // unconditional (clamped) prefetch: the same number of loads is in flight on every
+      // path, so the compiler waits for exactly the step it consumes (vmcnt(N), not vmcnt(0));
+      // steps past the chunk end skip their work but not their loads (no `break`, whose exit
+      // edge would merge a shorter load history into the loop header)
+      scd_issue<NC>(p, b + 64 * kScdAhead, end, lane, ring[a]);
+      if (b >= end) continue;
       const bool act = row < end && (vals_pass<NC, 1>(p, row, v) & 1u);
       uint64_t code[1];
       vals_code<NC, 1>(p, v, code);
@@ -117,11 +131,12 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       if (COMPACT) vb = (uint32_t)(vb - (uint64_t)d.vmin);
 #ifndef BQ_SCD_SKIP_CD
       if (do_cd && act) {
-        // (slot, value) pair bit: an LDS fire-and-forget OR (merged into the device bitmap once
-        // per workgroup at the end); without an LDS bitmap, the device bitmap directly
-        const uint64_t bit = (uint64_t)s * d.cd.vrange + (vcd - (uint64_t)d.cd.vmin);
+        // (slot, value) pair bit (the planner fuses pair spaces < 2^30 only): an LDS
+        // fire-and-forget OR (merged into the device bitmap once per workgroup at the end);
+        // without an LDS bitmap, the device bitmap directly
+        const uint32_t bit = s * (uint32_t)d.cd.vrange + (uint32_t)(vcd - (uint64_t)d.cd.vmin);
         const unsigned int m = 1u << (bit & 31);
-        if (d.cd.lds_bitmap_words > 0) {
+        if (cd_mode == 1) {
           // read first: lanes of one word broadcast; only a new pair pays the (serialising)
           // same-address atomic
           if (!(cdb[bit >> 5] & m)) atomicOr(&cdb[bit >> 5], m);
@@ -206,7 +221,7 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
   }
   // count_distinct: merge the workgroup's pair bitmap into the device bitmap; every pair bit
   // this workgroup sets first counts once for its slot
-  if (do_cd && d.cd.lds_bitmap_words > 0) {
+  if (cd_mode == 1) {
     __syncthreads();
     for (int i = threadIdx.x; i < d.cd.lds_bitmap_words; i += blockDim.x) {
       const unsigned int word = cdb[i];
