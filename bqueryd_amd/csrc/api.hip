@@ -1210,9 +1210,9 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         c->last.specialized = sfn ? 1 : 0;
       }
       if (fused && c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
-      launch_scd(pc.p, sa, d, st, sfn);
+      // timing brackets the pass itself (the chunk combine follows it)
+      launch_scd(pc.p, sa, d, st, sfn, fused && c->timing ? c->ev[2] : nullptr);
       HIPCHECK(hipGetLastError());
-      if (fused && c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));
       e.scd_changes[i] = d.out_changes;
       e.scd_first[i] = d.out_first;
       ++i;

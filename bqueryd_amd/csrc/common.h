@@ -7,6 +7,7 @@
 #else
 typedef struct ihipStream_t* hipStream_t;  // host launchers are declared, never defined, in JIT code
 typedef struct ihipModuleSymbol_t* hipFunction_t;
+typedef struct ihipEvent_t* hipEvent_t;
 #endif
 
 #include "../../include/bqgpu.h"

@@ -355,7 +355,8 @@ void launch_count_distinct(const ScanParams& p, const SlotArrays& s, const Disti
     BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_count_distinct<NC, false>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
   }
 }
-void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st, hipFunction_t fused_fn) {
+void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st, hipFunction_t fused_fn,
+                hipEvent_t pass_done) {
   const int blocks = (d.waves + (kBlock / 64) - 1) / (kBlock / 64);
   if (d.fused) {
     const size_t lds = (kBlock / 64) * d.wave_lds + (size_t)d.cd.lds_bitmap_words * 4;
@@ -377,6 +378,7 @@ void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hi
       BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd<NC, false>), dim3(blocks), dim3(kBlock), lds, st, p, s, d));
     }
   }
+  if (pass_done) (void)hipEventRecord(pass_done, st);
   int isf = 0;
   for (int c = 0; c < p.ncols; ++c)
     if (c == d.vcol) isf = dtype_is_float(p.cols[c].dtype);

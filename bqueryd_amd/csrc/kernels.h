@@ -110,8 +110,9 @@ inline size_t scd_fused_wave_lds(uint64_t nslots, bool compact = false) {
 }
 constexpr size_t kScdFusedMaxLds = 80 * 1024;  // per workgroup (4 waves + shared cd filter)
 // fused_fn: query-specialised (JIT) k_scd_fused, or nullptr for the precompiled kernel
+// pass_done (optional): recorded between the pass and the chunk combine (kernel timing)
 void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hipStream_t st,
-                hipFunction_t fused_fn = nullptr);
+                hipFunction_t fused_fn = nullptr, hipEvent_t pass_done = nullptr);
 
 // emit: occupied slots -> first-appearance order -> finalised output columns
 void launch_compact(const SlotArrays& s, uint64_t nslots, uint32_t* list_fst,
