@@ -92,6 +92,7 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
     if (d.cd.vcol == c) cc = c;
   }
   const bool isf = !COMPACT && dtype_is_float(p.cols[vc].dtype);
+  const bool cd_runs = cc == vc;  // count_distinct of the sorted_count_distinct column
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   uint2 ring[kScdAhead][NC];
   if (start < end) {
@@ -129,22 +130,6 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         if (cc == c) vcd = v[c][0];
       }
       if (COMPACT) vb = (uint32_t)(vb - (uint64_t)d.vmin);
-#ifndef BQ_SCD_SKIP_CD
-      if (do_cd && act) {
-        // (slot, value) pair bit (the planner fuses pair spaces < 2^30 only): an LDS
-        // fire-and-forget OR (merged into the device bitmap once per workgroup at the end);
-        // without an LDS bitmap, the device bitmap directly
-        const uint32_t bit = s * (uint32_t)d.cd.vrange + (uint32_t)(vcd - (uint64_t)d.cd.vmin);
-        const unsigned int m = 1u << (bit & 31);
-        if (cd_mode == 1) {
-          // read first: lanes of one word broadcast; only a new pair pays the (serialising)
-          // same-address atomic
-          if (!(cdb[bit >> 5] & m)) atomicOr(&cdb[bit >> 5], m);
-        } else if (!(d.cd.bitmap[bit >> 5] & m) && !(atomicOr(&d.cd.bitmap[bit >> 5], m) & m)) {
-          atomicAdd(&d.cd.out[s], 1ull);
-        }
-      }
-#endif
       // lanes of this lane's slot: one ballot per slot-id bit
       uint64_t match = __ballot(act);
       if (match == 0) continue;
@@ -180,6 +165,7 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       }
       const bool diff = act && below != 0 && !scd_equal(vb, pv, isf);
       const uint64_t dm = __ballot(diff);
+      bool run_start = diff;  // first row of a value run of its slot (set below for first lanes)
 #ifdef BQ_SCD_SKIP_STATE
       if (act && below == 0 && dm == 0x1234567ull) {
 #else
@@ -195,8 +181,10 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
           if (cur.rows == 0) {
             cur.first = (uint32_t)vb;
             fr32[s] = (uint32_t)row;
+            run_start = true;
           } else if (cur.last != (uint32_t)vb) {
             ch += 1u;
+            run_start = true;
           }
           cur.last = (uint32_t)lastv;
           cur.rows += add_rows;
@@ -208,8 +196,10 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
           if (cur.rows == 0) {
             cur.first = vb;
             cur.first_row = (uint32_t)row;
+            run_start = true;
           } else if (!scd_equal(cur.last, vb, isf)) {
             ch += 1u;
+            run_start = true;
           }
           cur.last = lastv;
           cur.rows += add_rows;
@@ -217,6 +207,25 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
           st[s] = cur;
         }
       }
+#ifndef BQ_SCD_SKIP_CD
+      // count_distinct of the same column: only the first row of a value run of its slot can
+      // add a (slot, value) pair (every later row of the run repeats one already added), so
+      // the pair check runs at run starts only (most rows of a sorted column skip it)
+      if (do_cd && (cd_runs ? run_start : act)) {
+        // (slot, value) pair bit (the planner fuses pair spaces < 2^30 only): an LDS
+        // fire-and-forget OR (merged into the device bitmap once per workgroup at the end);
+        // without an LDS bitmap, the device bitmap directly
+        const uint32_t bit = s * (uint32_t)d.cd.vrange + (uint32_t)(vcd - (uint64_t)d.cd.vmin);
+        const unsigned int m = 1u << (bit & 31);
+        if (cd_mode == 1) {
+          // read first: lanes of one word broadcast; only a new pair pays the (serialising)
+          // same-address atomic
+          if (!(cdb[bit >> 5] & m)) atomicOr(&cdb[bit >> 5], m);
+        } else if (!(d.cd.bitmap[bit >> 5] & m) && !(atomicOr(&d.cd.bitmap[bit >> 5], m) & m)) {
+          atomicAdd(&d.cd.out[s], 1ull);
+        }
+      }
+#endif
     }
   }
   // count_distinct: merge the workgroup's pair bitmap into the device bitmap; every pair bit
