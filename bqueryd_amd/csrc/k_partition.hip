@@ -64,16 +64,42 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   const uint32_t lo = pbeg + (uint32_t)(len * split / L.splits);
   const uint32_t hi = pbeg + (uint32_t)(len * (split + 1) / L.splits);
   const uint32_t lowmask = (uint32_t)W - 1u;
-  for (uint32_t c4 = (lo >> 2) + tid; c4 < ((hi + 3u) >> 2); c4 += blockDim.x) {
-    const uint32_t i0 = c4 << 2;
-    const uint4 m4 = load_stream16(reinterpret_cast<const unsigned char*>(L.meta + i0));
-    const uint32_t key = max(i0, lo);
-    int b = 0, e = B - 1;  // largest b with rs[b] <= key
+  const uint32_t c4e = (hi + 3u) >> 2;
+  uint32_t c4 = (lo >> 2) + tid;
+  // entries are visited in increasing order: the region of a thread's next entry is found by
+  // walking forward from its last one (a few LDS reads), falling back to a binary search
+  int b = 0;
+  auto region_of = [&](uint32_t key) {  // largest b with rs[b] <= key
+    for (int k = 0; k < 8; ++k) {
+      if (rs[b + 1] > key) return;
+      ++b;
+    }
+    int e = B - 1;
     while (b < e) {
       const int mid = (b + e + 1) >> 1;
       if (rs[mid] <= key) b = mid;
       else e = mid - 1;
     }
+  };
+  // one iteration's meta and first summed column are loaded while the previous one is
+  // aggregated (clamped to the last group of the range: the same loads on every path)
+  const bool pre_v = nsum > 0;
+  const unsigned char* v0 = reinterpret_cast<const unsigned char*>(L.vals);
+  uint4 pm = {0, 0, 0, 0}, pv01 = {0, 0, 0, 0}, pv23 = {0, 0, 0, 0};
+  auto fetch = [&](uint32_t cc) {
+    cc = cc < c4e ? cc : c4e - 1u;
+    pm = load_stream16(reinterpret_cast<const unsigned char*>(L.meta + ((size_t)cc << 2)));
+    if (pre_v) {
+      pv01 = load_stream16(v0 + ((size_t)cc << 5));
+      pv23 = load_stream16(v0 + ((size_t)cc << 5) + 16);
+    }
+  };
+  if (c4 < c4e) fetch(c4);
+  for (; c4 < c4e; c4 += blockDim.x) {
+    const uint32_t i0 = c4 << 2;
+    const uint4 m4 = pm, f01 = pv01, f23 = pv23;
+    fetch(c4 + blockDim.x);
+    region_of(max(i0, lo));
     const uint32_t mm[4] = {m4.x, m4.y, m4.z, m4.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -87,7 +113,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     }
     for (int q = 0; q < nsum; ++q) {
       const unsigned char* vp = reinterpret_cast<const unsigned char*>(L.vals + (size_t)q * L.capacity + i0);
-      const uint4 x01 = load_stream16(vp), x23 = load_stream16(vp + 16);
+      const uint4 x01 = q == 0 ? f01 : load_stream16(vp), x23 = q == 0 ? f23 : load_stream16(vp + 16);
       const unsigned long long xs[4] = {((unsigned long long)x01.y << 32) | x01.x, ((unsigned long long)x01.w << 32) | x01.z,
                                         ((unsigned long long)x23.y << 32) | x23.x, ((unsigned long long)x23.w << 32) | x23.z};
 #pragma unroll
