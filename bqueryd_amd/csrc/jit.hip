@@ -152,6 +152,8 @@ bool jit_disabled() {
 
 std::string jit_spec(const ScanParams& p) {
   std::ostringstream s;
+  // experiment hook: BQGPU_JIT_DEFS=NAME adds `#define NAME 1` (part of the cache key)
+  if (const char* e = getenv("BQGPU_JIT_DEFS")) s << "#define " << e << " 1\n";
   s << "#define BQ_NC " << p.ncols << "\n#define BQ_SPEC ";
   s << "p.ncols=" << p.ncols << ";";
   for (int c = 0; c < p.ncols; ++c)

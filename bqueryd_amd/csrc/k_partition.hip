@@ -81,26 +81,32 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       else e = mid - 1;
     }
   };
-  // one iteration's meta and first summed column are loaded while the previous one is
-  // aggregated (clamped to the last group of the range: the same loads on every path)
+  // two iterations' meta and first summed column are in flight while one is aggregated
+  // (clamped to the last group of the range: the same loads on every path, so the compiler
+  // waits for the oldest group with vmcnt(N) instead of draining)
   const bool pre_v = nsum > 0;
   const unsigned char* v0 = reinterpret_cast<const unsigned char*>(L.vals);
-  uint4 pm = {0, 0, 0, 0}, pv01 = {0, 0, 0, 0}, pv23 = {0, 0, 0, 0};
-  auto fetch = [&](uint32_t cc) {
-    cc = cc < c4e ? cc : c4e - 1u;
-    pm = load_stream16(reinterpret_cast<const unsigned char*>(L.meta + ((size_t)cc << 2)));
-    if (pre_v) {
-      pv01 = load_stream16(v0 + ((size_t)cc << 5));
-      pv23 = load_stream16(v0 + ((size_t)cc << 5) + 16);
-    }
+  struct Grp {
+    uint4 m, v01, v23;
   };
-  if (c4 < c4e) fetch(c4);
-  for (; c4 < c4e; c4 += blockDim.x) {
-    const uint32_t i0 = c4 << 2;
-    const uint4 m4 = pm, f01 = pv01, f23 = pv23;
-    fetch(c4 + blockDim.x);
+  auto fetch = [&](uint32_t cc) {
+    Grp g;
+    cc = cc < c4e ? cc : (c4e > 0u ? c4e - 1u : 0u);
+    g.m = load_stream16(reinterpret_cast<const unsigned char*>(L.meta + ((size_t)cc << 2)));
+    if (pre_v) {
+      g.v01 = load_stream16(v0 + ((size_t)cc << 5));
+      g.v23 = load_stream16(v0 + ((size_t)cc << 5) + 16);
+    } else {
+      g.v01 = g.m;
+      g.v23 = g.m;
+    }
+    return g;
+  };
+  auto consume = [&](const Grp& g, uint32_t cc) {
+    const uint32_t i0 = cc << 2;
+    if (i0 >= hi) return;
     region_of(max(i0, lo));
-    const uint32_t mm[4] = {m4.x, m4.y, m4.z, m4.w};
+    const uint32_t mm[4] = {g.m.x, g.m.y, g.m.z, g.m.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t i = i0 + k;
@@ -113,7 +119,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     }
     for (int q = 0; q < nsum; ++q) {
       const unsigned char* vp = reinterpret_cast<const unsigned char*>(L.vals + (size_t)q * L.capacity + i0);
-      const uint4 x01 = q == 0 ? f01 : load_stream16(vp), x23 = q == 0 ? f23 : load_stream16(vp + 16);
+      const uint4 x01 = q == 0 ? g.v01 : load_stream16(vp), x23 = q == 0 ? g.v23 : load_stream16(vp + 16);
       const unsigned long long xs[4] = {((unsigned long long)x01.y << 32) | x01.x, ((unsigned long long)x01.w << 32) | x01.z,
                                         ((unsigned long long)x23.y << 32) | x23.x, ((unsigned long long)x23.w << 32) | x23.z};
 #pragma unroll
@@ -124,6 +130,18 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
         if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + s]), value_f64(xs[k], p.sum_conv[q]));
         else atomicAdd(&acc[(size_t)q * W + s], xs[k]);
       }
+    }
+  };
+  if (c4 < c4e) {
+    const uint32_t T = blockDim.x;
+    Grp ga = fetch(c4), gb = fetch(c4 + T);
+    for (; c4 < c4e; c4 += 2u * T) {
+      const Grp a = ga;
+      ga = fetch(c4 + 2u * T);
+      consume(a, c4);
+      const Grp bb = gb;
+      gb = fetch(c4 + 3u * T);
+      consume(bb, c4 + T);
     }
   }
   __syncthreads();

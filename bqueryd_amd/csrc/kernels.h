@@ -167,9 +167,9 @@ struct PartLaunch {
   unsigned long long* vals;  // [nsum][capacity]: summed values (canonical 64-bit)
 };
 // LDS bytes of a scatter workgroup: the staged tile (meta, destination, values), tile
-// counts / offsets, region cursors and two sets of scan totals
+// counts (two buffers) / offsets, region cursors and two sets of scan totals
 inline size_t part_scatter_lds(int nparts, int threads, int nsum) {
-  return (size_t)threads * 4 * (8 + 8 * (size_t)nsum) + (size_t)nparts * 12 + 2 * 16 * 4;
+  return (size_t)threads * 4 * (8 + 8 * (size_t)nsum) + (size_t)nparts * 16 + 2 * 16 * 4;
 }
 // fcount / fscatter: query-specialised (JIT) count / scatter kernels, or nullptr for the
 // precompiled generic ones

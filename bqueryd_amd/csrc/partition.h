@@ -141,12 +141,13 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   unsigned long long* sval = reinterpret_cast<unsigned long long*>(smem);             // [nsum][tile]
   uint32_t* smeta = reinterpret_cast<uint32_t*>(sval + (size_t)nsum * tile);          // [tile]
   uint32_t* sdst = smeta + tile;                                                       // [tile] destinations
-  uint32_t* hist = sdst + tile;                                                        // [P] tile counts
-  uint32_t* toff = hist + P;                                                           // [P] tile offsets
+  uint32_t* hist2 = sdst + tile;                                                       // [2][P] tile counts
+  uint32_t* toff = hist2 + 2 * P;                                                      // [P] tile offsets
   uint32_t* cur = toff + P;                                                            // [P] region cursors
   uint32_t* wsum2 = cur + P;                                                           // [2][16] scan totals
   for (int i = tid; i < P; i += T) {
-    hist[i] = 0;
+    hist2[i] = 0;
+    hist2[P + i] = 0;
     cur[i] = L.counts[(size_t)i * gridDim.x + blockIdx.x];
   }
   lds_barrier();
@@ -161,6 +162,10 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   if (begin < end) load_rows4_clamped<NC>(p, begin + (int64_t)tid * kRowsPerThread, end, raw, all, begin);
   int parity = 0;
   for (int64_t base = begin; base < end; base += tile, parity ^= 1) {
+    // the tile histogram alternates between two buffers: the one this tile zeroes at its end
+    // is next counted into two tiles later, past this tile's barriers, so the loop needs no
+    // trailing barrier (tile t+1's first phase touches neither the staging area nor `cur`)
+    uint32_t* hist = hist2 + parity * P;
     const int64_t row0 = base + (int64_t)tid * kRowsPerThread;
     uint64_t v[NC][4], code[4];
     decode_all<NC, 4>(p, raw, v);
@@ -213,7 +218,6 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
       cur[i] += hist[i];
       hist[i] = 0;
     }
-    lds_barrier();
   }
 }
 
