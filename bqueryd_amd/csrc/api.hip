@@ -929,6 +929,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.nparts = (int)((S + (1ull << pl.wbits) - 1) >> pl.wbits);
       // scatter workgroup: the widest whose staged tile fits in LDS (BQGPU_PART_THREADS caps it)
       L.threads = 1024;
+      L.chunks = 1;
       if (const char* ev = getenv("BQGPU_PART_THREADS")) L.threads = std::max(256, std::min(1024, atoi(ev)));
       while (L.threads > 256 && part_scatter_lds(L.nparts, L.threads, nsum) > 150 * 1024) L.threads >>= 1;
       int per_cu = 2;  // count / scatter workgroups per CU (two 58 KiB scatter workgroups share a CU)
@@ -965,10 +966,16 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       HIPCHECK(hipMemsetAsync(L.counts + ncounts - 1, 0, 4, st));
       hipFunction_t fc = nullptr, fs = nullptr;
       if (N >= jit_min_rows()) {
-        const std::string spec = jit_spec(pl.p);
+        // JIT scatter: CH 4-row chunks per thread per tile when the staging still fits
+        int chunks = 1;
+        if (const char* ev = getenv("BQGPU_PART_CHUNKS")) chunks = std::max(1, std::min(2, atoi(ev)));
+        if (chunks > 1 && part_scatter_lds(L.nparts, L.threads, nsum, chunks) > 150 * 1024) chunks = 1;
+        std::string spec = jit_spec(pl.p);
+        const std::string sspec = chunks > 1 ? "#define BQ_PART_CHUNKS " + std::to_string(chunks) + "\n" + spec : spec;
         fc = jit_function("bq_jit_part_count", spec);
-        fs = fc ? jit_function("bq_jit_part_scatter", spec) : nullptr;
+        fs = fc ? jit_function("bq_jit_part_scatter", sspec) : nullptr;
         if (!fs) fc = nullptr;
+        L.chunks = fs ? chunks : 1;
         c->last.specialized = fc ? 1 : 0;
       }
       launch_partitioned(pl.p, sa, L, scan_scratch, st, fc, fs);

@@ -203,7 +203,7 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, PartLaunch L, 
   // counts has one extra zero word at the end: after the scan it holds the total
   const uint64_t n = (uint64_t)L.nparts * L.blocks + 1;
   launch_exclusive_scan_u32(L.counts, n, scan_scratch, st);
-  const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum);
+  const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum, fscatter ? L.chunks : 1);
   if (fscatter) {
     (void)hipModuleLaunchKernel(fscatter, (unsigned)L.blocks, 1, 1, (unsigned)L.threads, 1, 1, (unsigned)scatter_lds,
                                 st, args, nullptr);

@@ -157,6 +157,7 @@ struct PartLaunch {
   int blocks;                // workgroups of the count / scatter passes
   int splits;                // aggregate workgroups per partition (block ranges)
   int threads;               // threads of a scatter workgroup (4 rows each per tile)
+  int chunks;                // 4-row chunks per scatter thread per tile (JIT scatter only)
   uint32_t load_mask;        // scan columns the count pass reads (keys, terms, mask)
   int64_t rows_per_block;    // contiguous rows per count/scatter workgroup: a multiple of the
                              // scatter tile and <= 2^(32 - wbits) (row-in-block | slot_low
@@ -168,8 +169,8 @@ struct PartLaunch {
 };
 // LDS bytes of a scatter workgroup: the staged tile (meta, destination, values), tile
 // counts (two buffers) / offsets, region cursors and two sets of scan totals
-inline size_t part_scatter_lds(int nparts, int threads, int nsum) {
-  return (size_t)threads * 4 * (8 + 8 * (size_t)nsum) + (size_t)nparts * 16 + 2 * 16 * 4;
+inline size_t part_scatter_lds(int nparts, int threads, int nsum, int chunks = 1) {
+  return (size_t)threads * 4 * (size_t)chunks * (8 + 8 * (size_t)nsum) + (size_t)nparts * 16 + 2 * 16 * 4;
 }
 // fcount / fscatter: query-specialised (JIT) count / scatter kernels, or nullptr for the
 // precompiled generic ones

@@ -129,14 +129,17 @@ __device__ __forceinline__ void part_count_body(const ScanParams& p, const PartL
   for (int i = tid; i < L.nparts; i += T) L.counts[(size_t)i * gridDim.x + blockIdx.x] = hist[i];
 }
 
-// Single-buffered tile staging (58 KiB for one summed column at 1024 threads: two scatter
-// workgroups fit on a CU, which measured faster than double buffering at one per CU); the
-// scan's wave totals alternate between two buffers so the scan needs one barrier.
-template <int NC>
+// Single-buffered tile staging (64 KiB for one summed column at 1024 threads and CH = 1: two
+// scatter workgroups fit on a CU, which measured faster than double buffering at one per CU);
+// the scan's wave totals alternate between two buffers so the scan needs one barrier.  CH
+// 4-row chunks per thread make a tile of CH * 4 * T rows (each chunk slice coalesced): longer
+// runs per partition and fewer barriers per row, at CH times the staging LDS.
+template <int NC, int CH = 1>
 __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const PartLaunch& L, unsigned char* smem) {
   const int T = blockDim.x, tid = threadIdx.x;
   const int P = L.nparts;
-  const int tile = T * kRowsPerThread;
+  const int slice = T * kRowsPerThread;
+  const int tile = slice * CH;
   const int nsum = p.nsum;
   unsigned long long* sval = reinterpret_cast<unsigned long long*>(smem);             // [nsum][tile]
   uint32_t* smeta = reinterpret_cast<uint32_t*>(sval + (size_t)nsum * tile);          // [tile]
@@ -158,27 +161,43 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   const int q0 = tid * per;
   const int q1 = min(P, q0 + per);
   const uint32_t all = (1u << NC) - 1u;
-  Chunk raw[NC];
-  if (begin < end) load_rows4_clamped<NC>(p, begin + (int64_t)tid * kRowsPerThread, end, raw, all, begin);
+  constexpr int NS = NC < kMaxSums ? NC : kMaxSums;
+  Chunk raw[CH][NC];
+  if (begin < end) {
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      load_rows4_clamped<NC>(p, begin + (int64_t)u * slice + (int64_t)tid * kRowsPerThread, end, raw[u], all, begin);
+  }
   int parity = 0;
   for (int64_t base = begin; base < end; base += tile, parity ^= 1) {
     // the tile histogram alternates between two buffers: the one this tile zeroes at its end
     // is next counted into two tiles later, past this tile's barriers, so the loop needs no
     // trailing barrier (tile t+1's first phase touches neither the staging area nor `cur`)
     uint32_t* hist = hist2 + parity * P;
-    const int64_t row0 = base + (int64_t)tid * kRowsPerThread;
-    uint64_t v[NC][4], code[4];
-    decode_all<NC, 4>(p, raw, v);
-    load_rows4_clamped<NC>(p, row0 + tile, end, raw, all, begin);
-    uint32_t pass = vals_pass<NC, 4>(p, row0, v);
-    if (end - row0 < 4) pass &= (end - row0 > 0) ? ((1u << (end - row0)) - 1u) : 0u;
-    vals_code<NC, 4>(p, v, code);
-    uint32_t part[4], rank[4];
+    uint32_t pass[CH], part[CH][4], rank[CH][4], low[CH][4];
+    uint64_t sv[CH][NS][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      part[r] = (uint32_t)(code[r] >> L.wbits);
-      rank[r] = (pass & (1u << r)) ? atomicAdd(&hist[part[r]], 1u) : 0u;
+    for (int u = 0; u < CH; ++u) {
+      const int64_t row0 = base + (int64_t)u * slice + (int64_t)tid * kRowsPerThread;
+      uint64_t v[NC][4], code[4];
+      decode_all<NC, 4>(p, raw[u], v);
+      load_rows4_clamped<NC>(p, row0 + tile, end, raw[u], all, begin);
+      pass[u] = vals_pass<NC, 4>(p, row0, v);
+      const int64_t rem = end - row0;
+      pass[u] &= rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
+      vals_code<NC, 4>(p, v, code);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        part[u][r] = (uint32_t)(code[r] >> L.wbits);
+        low[u][r] = (uint32_t)(code[r] & lowmask);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) sv[u][s][r] = v[s][r];
+      }
     }
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rank[u][r] = (pass[u] & (1u << r)) ? atomicAdd(&hist[part[u][r]], 1u) : 0u;
     lds_barrier();
     // tile offsets: exclusive scan of the tile histogram
     uint32_t local = 0;
@@ -192,25 +211,29 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
     lds_barrier();
     // stage the tile sorted by partition, with each entry's destination (region cursor + rank)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (!(pass & (1u << r))) continue;
-      const uint32_t pos = toff[part[r]] + rank[r];
-      smeta[pos] = ((uint32_t)(row0 + r - begin) << L.wbits) | (uint32_t)(code[r] & lowmask);
-      sdst[pos] = cur[part[r]] + rank[r];
+    for (int u = 0; u < CH; ++u) {
+      const int64_t row0 = base + (int64_t)u * slice + (int64_t)tid * kRowsPerThread;
 #pragma unroll
-      for (int s = 0; s < (NC < kMaxSums ? NC : kMaxSums); ++s)
-        if (s < nsum) sval[(size_t)s * tile + pos] = v[s][r];
+      for (int r = 0; r < 4; ++r) {
+        if (!(pass[u] & (1u << r))) continue;
+        const uint32_t pos = toff[part[u][r]] + rank[u][r];
+        smeta[pos] = ((uint32_t)(row0 + r - begin) << L.wbits) | low[u][r];
+        sdst[pos] = cur[part[u][r]] + rank[u][r];
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          if (s < nsum) sval[(size_t)s * tile + pos] = sv[u][s][r];
+      }
     }
     lds_barrier();
     // copy out: consecutive lanes -> consecutive entries of one region (whole lines)
 #pragma unroll
-    for (int k = 0; k < kRowsPerThread; ++k) {
+    for (int k = 0; k < kRowsPerThread * CH; ++k) {
       const uint32_t i = (uint32_t)(tid + k * T);
       if (i < n_tile) {
         const uint32_t dst = sdst[i];
         L.meta[dst] = smeta[i];
 #pragma unroll
-        for (int s = 0; s < (NC < kMaxSums ? NC : kMaxSums); ++s)
+        for (int s = 0; s < NS; ++s)
           if (s < nsum) L.vals[(size_t)s * L.capacity + dst] = sval[(size_t)s * tile + i];
       }
     }
