@@ -116,6 +116,8 @@ def main(argv=None):
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5'])
+    ap.add_argument('--c5-per-shard', action='store_true',
+                    help='C5: one groupby per shard + local re-group instead of one pass over the rank\'s shards')
     ap.add_argument('--rows', type=int, default=None, help='override rows per shard')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--variant', default='exact', choices=['exact', 'raw'])
@@ -153,17 +155,27 @@ def main(argv=None):
         else:
             exchange = bdist.LocalExchange()
         backend = bdist.GpuBackend(dev)
+        colo = bdist.ColocatedShards(tables)
+        fused = not args.c5_per_shard and bdist.decomposable(cfg['aggs'])
+        if fused:
+            colo.union(synth.query_columns(cfg))  # the rank's shard set, resident once (untimed, like the load)
 
         def step():
-            # per-shard results stay in HBM; the merge (local sum, hash partition, RCCL
-            # all-to-all, reduce, gather to rank 0) runs on device buffers
-            per = []
+            # results stay in HBM; the merge (hash partition, RCCL all-to-all, reduce, gather
+            # to rank 0) runs on device buffers.  Fused: the rank's shards in one pass
+            # (sum / count are decomposable); per-shard: one groupby per shard + local re-group
             t0 = time.perf_counter()
-            for t in tables:
-                per.append(t.groupby_table(cfg['groupby'], cfg['aggs']))
+            if fused:
+                per, reduced = colo.groupby_tables(cfg['groupby'], cfg['aggs'])
                 timings.append(dev.last_timing())
+            else:
+                per, reduced = [], False
+                for t in tables:
+                    per.append(t.groupby_table(cfg['groupby'], cfg['aggs']))
+                    timings.append(dev.last_timing())
             t1 = time.perf_counter()
-            merged = bdist.merge_partials_device(per, cfg['groupby'], cfg['aggs'], dtypes, backend, exchange)
+            merged = bdist.merge_partials_device(per, cfg['groupby'], cfg['aggs'], dtypes, backend, exchange,
+                                                 reduced=reduced)
             for p in per:
                 p.close()
             phase.append((t1 - t0, time.perf_counter() - t1))
@@ -228,7 +240,10 @@ def main(argv=None):
     if phase:
         cfg_extra = {'shard_queries_ms_per_step': 1e3 * float(np.mean([p[0] for p in phase])),
                      'merge_ms_per_step': 1e3 * float(np.mean([p[1] for p in phase])),
-                'merge': 'device-resident: per-shard results in HBM, merged without host copies'}
+                     'merge': 'device-resident: results in HBM, merged without host copies',
+                     'shard_pass': ('fused: the rank\'s shards aggregated in one pass (sum / count are '
+                                    'decomposable; dist.ColocatedShards)' if fused else
+                                    'per-shard groupby + local re-group')}
     else:
         cfg_extra = {}
     line = {

@@ -195,23 +195,28 @@ class DeviceExchange(Exchange):
         return buf[:nbytes].cpu().numpy()
 
 
-def merge_partials_device(local_tables, groupby_cols, agg_list, dtypes, backend, exchange):
+def merge_partials_device(local_tables, groupby_cols, agg_list, dtypes, backend, exchange, reduced=False):
     """``merge_partials`` with every step in HBM: ``local_tables`` are this rank's finalized
     shard tables as device ShardTables (``ShardTable.groupby_table``), the reduce, partition,
     all-to-all and gather run on device buffers, and only the merged table comes back to host
-    memory (rank 0; None elsewhere)."""
+    memory (rank 0; None elsewhere).  ``reduced``: ``local_tables`` is ONE table whose keys are
+    already unique (a co-located groupby, ``ColocatedShards``), so the local re-group is skipped."""
     names = list(groupby_cols) + [x[2] for x in agg_list]
     local_tables = [t for t in local_tables if t is not None and t.nrows]
+    reduced = reduced and len(local_tables) == 1
     if exchange.world == 1:
         if not local_tables:
             return OrderedDict((n, np.zeros(0, dtypes[n])) for n in names)
+        if reduced:
+            return OrderedDict((n, local_tables[0].read(n)) for n in names)
         return backend.reduce(local_tables, groupby_cols, agg_list)
     if local_tables:
-        local = backend.reduce(local_tables, groupby_cols, agg_list, on_device=True)
+        local = local_tables[0] if reduced else backend.reduce(local_tables, groupby_cols, agg_list, on_device=True)
         try:
             parts = backend.partition_device(local, groupby_cols, exchange.world)
         finally:
-            local.close()
+            if not reduced:
+                local.close()
     else:
         parts = [backend.empty_table(names, dtypes) for _ in range(exchange.world)]
     recv_counts = exchange.counts([p.nrows for p in parts])
@@ -275,3 +280,69 @@ def merge_partials(local_tables, groupby_cols, agg_list, dtypes, backend, exchan
         parts_n = [mine[n] if dst == 0 else np.zeros(0, dtypes[n]) for dst in range(exchange.world)]
         gathered[n] = exchange.column(parts_n, dtypes[n], recv)
     return gathered if exchange.rank == 0 else None
+
+
+# aggregations whose client-side merge (a sum of the per-shard finalized values, rpc.py:170-172)
+# equals the aggregation over the union of the shards' rows
+DECOMPOSABLE = frozenset(['sum', 'count'])
+
+
+def decomposable(agg_list):
+    """True when every aggregation of ``agg_list`` (3-element specs, as ``aggregate=True``
+    requires, rpc.py:171) merges by summing: then Σ over shards of the per-shard result equals
+    the result over the union of the rows -- exactly for counts and integer sums (integer sums
+    wrap to the input width either way), within float rounding for float sums -- and the group
+    order agrees too: first appearance in the concatenation of per-shard tables, each in its
+    shard's first-appearance order, is first appearance in the concatenated rows."""
+    return all(isinstance(x, (list, tuple)) and len(x) == 3 and x[1] in DECOMPOSABLE for x in agg_list)
+
+
+class ColocatedShards:
+    """The shards one rank holds for an ``aggregate=True`` query (controller.py:494-506 fans
+    out one calc per shard).  For decomposable aggregations the rank's shards
+    are aggregated in ONE pass over their rows -- the shards' columns concatenated once in HBM
+    (device-to-device copies, kept while the shard set is resident) -- instead of one groupby
+    per shard followed by a local re-group; other aggregations (mean, std, count_distinct,
+    sorted_count_distinct: their client merge sums per-shard finalized values, which is not
+    the value over the union) keep the per-shard path."""
+
+    def __init__(self, tables):
+        self.tables = [t for t in tables if t is not None]
+        self._union = None
+        self._union_cols = ()
+
+    def union(self, cols):
+        from .engine import ShardTable
+        cols = tuple(cols)
+        if self._union is None or not set(cols) <= set(self._union_cols):
+            if self._union is not None:
+                self._union.close()
+            self._union = ShardTable.from_parts(self.tables, list(cols), device=self.tables[0].dev)
+            self._union_cols = cols
+        return self._union
+
+    def close(self):
+        if self._union is not None:
+            self._union.close()
+            self._union = None
+
+    def groupby_tables(self, groupby_cols, agg_list, where_terms=None):
+        """(device result tables, reduced): one table over the union for decomposable
+        aggregations, else one per shard."""
+        if not self.tables:
+            return [], False
+        if decomposable(agg_list):
+            cols = list(dict.fromkeys(list(groupby_cols) + [x[0] for x in agg_list] +
+                                      [t[0] for t in (where_terms or [])]))
+            u = self.union(cols)
+            return [u.groupby_table(groupby_cols, agg_list, where_terms=where_terms)], True
+        return [t.groupby_table(groupby_cols, agg_list, where_terms=where_terms) for t in self.tables], False
+
+    def groupby_merged(self, groupby_cols, agg_list, dtypes, backend, exchange, where_terms=None):
+        """The ``aggregate=True`` answer over every rank's shards (rank 0; None elsewhere)."""
+        per, reduced = self.groupby_tables(groupby_cols, agg_list, where_terms)
+        try:
+            return merge_partials_device(per, groupby_cols, agg_list, dtypes, backend, exchange, reduced=reduced)
+        finally:
+            for p in per:
+                p.close()

@@ -95,3 +95,15 @@ def test_merge_partials_single_rank():
     assert_tables_equal(merged, ref)
     empty = bdist.merge_partials([], KEYS, AGGS, dtypes, OracleBackend(), bdist.LocalExchange())
     assert all(len(v) == 0 and v.dtype == dtypes[k] for k, v in empty.items())
+
+
+def test_decomposable_aggregations():
+    from bqueryd_amd.dist import decomposable
+    assert decomposable([['f', 'sum', 'a'], ['f', 'count', 'b']])
+    assert decomposable([])
+    assert not decomposable([['f', 'sum', 'a'], ['f', 'mean', 'b']])
+    assert not decomposable([['f', 'count_distinct', 'a']])
+    assert not decomposable([['f', 'sorted_count_distinct', 'a']])
+    assert not decomposable([['f', 'std', 'a']])
+    assert not decomposable(['f'])  # aggregate=True needs 3-element specs (rpc.py:171)
+    assert not decomposable([['f', 'sum']])

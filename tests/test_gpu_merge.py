@@ -162,3 +162,63 @@ def test_device_merge_protocol_two_ranks_as_threads():
     assert results[1] is None
     ref = bo.client_merge([bo.handle_work(s, KEYS, AGGS_SC, []) for s in shards], KEYS, AGGS_SC, aggregate=True)
     assert_tables_equal(sort_by_keys(results[0], KEYS), sort_by_keys(ref, KEYS))
+
+
+@pytest.mark.parametrize('aggs, where', [
+    (AGGS_SC, []),
+    (AGGS_SC, [('vendor_id', '==', 2)]),
+    ([['fare_amount', 'mean', 'fm'], ['fare_amount', 'count', 'n']], []),  # not decomposable: per shard
+])
+def test_colocated_shards_single_rank(aggs, where):
+    """A rank's shards aggregated in one pass over their union (sum / count) or per shard
+    (anything else): the reference client merge of the per-shard results, in its group order
+    (rpc.py:164-173)."""
+    shards = _shards(5, 120_000, 30_000)
+    tables = [ShardTable(s) for s in shards]
+    colo = bdist.ColocatedShards(tables)
+    per, reduced = colo.groupby_tables(KEYS, aggs, where_terms=where)
+    assert reduced == bdist.decomposable(aggs)
+    dtypes = OrderedDict((k, per[0].dtypes[k]) for k in per[0].names)
+    for p in per:
+        p.close()
+    merged = colo.groupby_merged(KEYS, aggs, dtypes, bdist.GpuBackend(), bdist.LocalExchange(), where_terms=where)
+    colo.close()
+    for t in tables:
+        t.close()
+    ref = bo.client_merge([bo.handle_work(s, KEYS, aggs, where) for s in shards], KEYS, aggs, aggregate=True)
+    assert_tables_equal(merged, ref)
+
+
+def test_colocated_shards_two_ranks_as_threads():
+    import threading
+    from bqueryd_amd.engine import Device
+    shards = _shards(6, 50_000, 9_000)
+    world = 2
+    shared = {'barrier': threading.Barrier(world), 'counts': [None] * world, 'cols': [None] * world}
+    results, errors = [None] * world, []
+    dtypes = OrderedDict([('pickup_location', np.dtype(np.int32)), ('vendor_id', np.dtype(np.int32)),
+                          ('fare_sum', np.dtype(np.float64)), ('n', np.dtype(np.int64))])
+
+    def rank_main(rank):
+        try:
+            dev = Device(0)
+            tables = [ShardTable(s, device=dev) for i, s in enumerate(shards) if i % world == rank]
+            colo = bdist.ColocatedShards(tables)
+            results[rank] = colo.groupby_merged(KEYS, AGGS_SC, dtypes, bdist.GpuBackend(dev),
+                                                _ThreadExchange(rank, world, shared))
+            colo.close()
+            for t in tables:
+                t.close()
+        except Exception as e:  # noqa: BLE001 -- re-raised in the main thread
+            errors.append(e)
+            shared['barrier'].abort()
+
+    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not errors, errors
+    assert results[1] is None
+    ref = bo.client_merge([bo.handle_work(s, KEYS, AGGS_SC, []) for s in shards], KEYS, AGGS_SC, aggregate=True)
+    assert_tables_equal(sort_by_keys(results[0], KEYS), sort_by_keys(ref, KEYS))
