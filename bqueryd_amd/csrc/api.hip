@@ -1302,17 +1302,10 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     *out = empty_result(out_dt, pl.has_filter && (int64_t)total < N);
     return;
   }
-  uint32_t* order = (uint32_t*)c->misc.ensure((size_t)G * 4 + 256);
+  uint32_t* order = nullptr;
   if (G <= 8192) {
+    order = (uint32_t*)c->misc.ensure((size_t)G * 4 + 256);
     launch_sort_small(list_fst, list_slot, G, order, st);
-  } else {
-    const uint64_t nwords = ((uint64_t)N + 31) / 32;
-    const uint64_t nblocks = (nwords + 1023) / 1024;
-    unsigned char* pb = (unsigned char*)c->prefix.ensure(nwords * 8 + nblocks * 4 + 1024);
-    unsigned int* bitmap = (unsigned int*)pb;
-    unsigned int* wprefix = bitmap + nwords;
-    unsigned int* bprefix = wprefix + nwords;
-    launch_rank_bitmap(list_fst, list_slot, G, N, bitmap, wprefix, bprefix, order, st);
   }
   HIPCHECK(hipGetLastError());
   size_t obytes = 0;
@@ -1325,7 +1318,18 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       o += ((size_t)G * dtype_size(out_dt[j]) + 255) & ~size_t(255);
     }
   }
-  launch_emit(e, sa, order, G, nsum, S, st);
+  if (order) {
+    launch_emit(e, sa, order, G, nsum, S, st);
+  } else {
+    // more groups: rank by a bitmap of first rows, emit each group at its rank in one pass
+    const uint64_t nwords = ((uint64_t)N + 31) / 32;
+    const uint64_t nblocks = (nwords + 1023) / 1024;
+    unsigned char* pb = (unsigned char*)c->prefix.ensure(nwords * 8 + nblocks * 4 + 1024);
+    unsigned int* bitmap = (unsigned int*)pb;
+    unsigned int* wprefix = bitmap + nwords;
+    unsigned int* bprefix = wprefix + nwords;
+    launch_rank_emit_bitmap(e, sa, list_fst, list_slot, G, nsum, S, N, bitmap, wprefix, bprefix, st);
+  }
   HIPCHECK(hipGetLastError());
   if (c->dev_target) {
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));

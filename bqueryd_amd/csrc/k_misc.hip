@@ -190,6 +190,33 @@ __global__ void k_emit(EmitParams e, SlotArrays sa, const uint32_t* order, unsig
   }
 }
 
+// Large results: rank (first-row bitmap popcount) and emit in one pass over the compacted
+// list, which is in slot order -- the slot totals are read coalesced and each group's output
+// row is written at its rank (scatter-by-rank), instead of a rank pass writing `order` and an
+// emit pass gathering the totals of random slots (~100 bytes of line traffic per 8-byte read).
+__global__ void k_rank_emit(EmitParams e, SlotArrays sa, const uint32_t* list_fst, const uint32_t* list_slot,
+                            unsigned int n, int nsum, uint64_t nslots, const unsigned int* bitmap,
+                            const unsigned int* word_prefix, const unsigned int* block_prefix) {
+  const int nsum2 = e.nsum2;
+  for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t f = list_fst[i];
+    const uint32_t w = f >> 5;
+    const unsigned int r = block_prefix[w >> 10] + word_prefix[w] +
+                           (unsigned int)__popc(bitmap[w] & ((1u << (f & 31)) - 1u));
+    const uint32_t s = list_slot[i];
+    SlotTotals t;
+    t.cnt = sa.cnt[s];
+    t.fst = f;
+#pragma unroll
+    for (int v = 0; v < kMaxSums; ++v) {
+      t.acc[v] = v < nsum ? sa.acc[(size_t)v * nslots + s] : 0ull;
+      t.acc2[v] = (sa.acc2 && v < nsum2) ? sa.acc2[(size_t)v * nslots + s] : 0ull;
+    }
+    const uint64_t code = e.hash ? (uint64_t)sa.keys[s] : (uint64_t)s;
+    emit_slot(e, s, code, r, t);
+  }
+}
+
 // Small slot spaces (<= kSmallEmitSlots): compaction, first-appearance ordering and emit in
 // one workgroup, with the group count and passing rows written to hdr[0], hdr[1] -- no host
 // round trip between the compaction and the emit.  Up to 1024 groups are ranked by counting
@@ -523,6 +550,20 @@ void launch_rank_bitmap(const uint32_t* list_fst, const uint32_t* list_slot, uns
   hipLaunchKernelGGL(k_block_scan, dim3(1), dim3(1024), 0, st, block_prefix, nblocks);
   hipLaunchKernelGGL(k_rank, dim3(g ? g : 1), dim3(256), 0, st, list_fst, list_slot, n, bitmap, word_prefix,
                      block_prefix, order);
+}
+void launch_rank_emit_bitmap(const EmitParams& e, const SlotArrays& s, const uint32_t* list_fst,
+                             const uint32_t* list_slot, unsigned int n, int nsum, uint64_t nslots, int64_t nrows,
+                             unsigned int* bitmap, unsigned int* word_prefix, unsigned int* block_prefix,
+                             hipStream_t st) {
+  const uint64_t nwords = ((uint64_t)nrows + 31) / 32;
+  const uint64_t nblocks = (nwords + 1023) / 1024;
+  (void)hipMemsetAsync(bitmap, 0, nwords * 4, st);
+  const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_setbits, dim3(g ? g : 1), dim3(256), 0, st, list_fst, n, bitmap);
+  hipLaunchKernelGGL(k_word_scan, dim3((unsigned)nblocks), dim3(1024), 0, st, bitmap, nwords, word_prefix, block_prefix);
+  hipLaunchKernelGGL(k_block_scan, dim3(1), dim3(1024), 0, st, block_prefix, nblocks);
+  hipLaunchKernelGGL(k_rank_emit, dim3(g ? g : 1), dim3(256), 0, st, e, s, list_fst, list_slot, n, nsum, nslots,
+                     bitmap, word_prefix, block_prefix);
 }
 void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order, unsigned int n, int nsum,
                  uint64_t nslots, hipStream_t st) {

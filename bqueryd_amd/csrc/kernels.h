@@ -123,6 +123,11 @@ void launch_sort_small(uint32_t* list_fst, uint32_t* list_slot, unsigned int n,
 void launch_rank_bitmap(const uint32_t* list_fst, const uint32_t* list_slot, unsigned int n,
                         int64_t nrows, unsigned int* bitmap, unsigned int* word_prefix,
                         unsigned int* block_prefix, uint32_t* order, hipStream_t st);
+// rank by the first-row bitmap and emit each group at its rank, in one pass (> 8192 groups)
+void launch_rank_emit_bitmap(const EmitParams& e, const SlotArrays& s, const uint32_t* list_fst,
+                             const uint32_t* list_slot, unsigned int n, int nsum, uint64_t nslots, int64_t nrows,
+                             unsigned int* bitmap, unsigned int* word_prefix, unsigned int* block_prefix,
+                             hipStream_t st);
 void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order,
                  unsigned int n, int nsum, uint64_t nslots, hipStream_t st);
 // slot spaces up to kSmallEmitSlots: compaction + ordering + emit in one workgroup (output
