@@ -147,8 +147,6 @@ def main(argv=None):
                                   shard=rank * per_rank + i, variant=args.variant,
                                   columns=synth.query_columns(cfg))
             tables.append(ShardTable(sc, device=dev))
-        probe, _ = tables[0].groupby(cfg['groupby'], cfg['aggs'])
-        dtypes = {n: np.asarray(v).dtype for n, v in probe.items()}
         if ws > 1:
             import torch
             exchange = bdist.DeviceExchange(comm.dist, device=torch.device('cuda', local), group=comm.nccl_group)
@@ -159,6 +157,12 @@ def main(argv=None):
         fused = not args.c5_per_shard and bdist.decomposable(cfg['aggs'])
         if fused:
             colo.union(synth.query_columns(cfg))  # the rank's shard set, resident once (untimed, like the load)
+        # result dtypes from a probe of the same shape as a step (every launch the same size, so
+        # PMC per-launch averages describe the timed kernel)
+        probe, _ = colo.groupby_tables(cfg['groupby'], cfg['aggs'])
+        dtypes = {n: np.dtype(probe[0].dtypes[n]) for n in probe[0].names}
+        for p_ in probe:
+            p_.close()
 
         def step():
             # results stay in HBM; the merge (hash partition, RCCL all-to-all, reduce, gather
