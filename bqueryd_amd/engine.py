@@ -336,8 +336,18 @@ class ShardTable:
                                                       self.slot(out_mask)))
         return out_mask
 
-    def groupby(self, groupby_cols, agg_list, where_terms=None, mask=None):
-        """bquery ``ctable.groupby`` semantics; returns (OrderedDict of columns, filtered)."""
+    def _plan(self, groupby_cols, agg_list, where_terms, mask):
+        """(output names, parsed aggregations, C query struct) of a groupby, built once per
+        distinct query text and table (the struct points into arrays the plan keeps alive):
+        repeated queries on a resident shard skip the Python-side parsing."""
+        # numpy arrays print abbreviated: queries with array-valued terms are not cached
+        cacheable = all(not any(isinstance(x, np.ndarray) for x in t)
+                        for t in (where_terms or []) if isinstance(t, (list, tuple)))
+        key = (repr(groupby_cols), repr(agg_list), repr(where_terms), mask) if cacheable else None
+        plans = self.__dict__.setdefault('_plans', OrderedDict())
+        hit = plans.get(key) if cacheable else None
+        if hit is not None:
+            return hit[:3]
         groupby_cols = list(groupby_cols)
         for c in groupby_cols:
             self.slot(c)
@@ -347,6 +357,17 @@ class ShardTable:
             raise ValueError('duplicate output column names: %s' % names)
         keep = []
         q = self._query(groupby_cols, [(o[0], o[2]) for o in ops], where_terms, mask, keep)
+        if cacheable:
+            if len(plans) >= 64:
+                plans.popitem(last=False)
+            plans[key] = (names, ops, q, keep)
+        else:
+            self.__dict__['_last_plan_keep'] = keep  # the struct's arrays live until the next query
+        return names, ops, q
+
+    def groupby(self, groupby_cols, agg_list, where_terms=None, mask=None):
+        """bquery ``ctable.groupby`` semantics; returns (OrderedDict of columns, filtered)."""
+        names, ops, q = self._plan(groupby_cols, agg_list, where_terms, mask)
         res = ctypes.c_void_p()
         self.dev.check(self._lib.bqg_groupby(self.dev.handle, self.handle, ctypes.byref(q),
                                              ctypes.byref(res)))

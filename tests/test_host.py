@@ -153,3 +153,31 @@ def test_library_fails_loudly_without_gpu():
     from bqueryd_amd.engine import Device
     with pytest.raises(_lib.BqgError):
         Device(0)
+
+
+def test_groupby_plan_cache_key_is_exact():
+    """ShardTable caches the parsed query per query text; numpy-array term values (whose repr
+    is abbreviated) are never cached, and a different value list is a different plan."""
+    import numpy as np
+    from bqueryd_amd.engine import ShardTable
+
+    class Fake(ShardTable):
+        def __init__(self):  # no device: only the host-side planning is exercised
+            self.dtypes = {'a': np.dtype(np.int32), 'b': np.dtype(np.float64)}
+            self._slot = {'a': 0, 'b': 1}
+
+    t = Fake()
+    p1 = t._plan(['a'], [['b', 'sum', 's']], [('a', 'in', [1, 2])], None)
+    p2 = t._plan(['a'], [['b', 'sum', 's']], [('a', 'in', [1, 2])], None)
+    p3 = t._plan(['a'], [['b', 'sum', 's']], [('a', 'in', [1, 3])], None)
+    assert p1[2] is p2[2] and p3[2] is not p1[2]
+    big = list(range(5000))
+    big2 = list(big)
+    big2[2500] = -1
+    q1 = t._plan(['a'], [['b', 'sum', 's']], [('a', 'in', big)], None)
+    q2 = t._plan(['a'], [['b', 'sum', 's']], [('a', 'in', big2)], None)
+    assert q1[2] is not q2[2]
+    assert len(t._plans) == 4
+    with pytest.raises(ValueError):  # bquery: `in` takes lists, sets or tuples
+        t._plan(['a'], [['b', 'sum', 's']], [('a', 'in', np.arange(3))], None)
+    assert len(t._plans) == 4
