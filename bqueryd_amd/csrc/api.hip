@@ -934,8 +934,25 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       while (L.threads > 256 && part_scatter_lds(L.nparts, L.threads, nsum) > 150 * 1024) L.threads >>= 1;
       int per_cu = 2;  // count / scatter workgroups per CU (two 58 KiB scatter workgroups share a CU)
       if (const char* ev = getenv("BQGPU_PART_PER_CU")) per_cu = std::max(1, std::min(8, atoi(ev)));
+      // the count pass needs only the key columns that reach the partition bits: trailing keys
+      // whose range product R is a power of two <= 2^wbits only add `lo < R` to `hi * R`, and R
+      // divides 2^wbits, so (hi * R + lo) >> wbits does not depend on them (C3: vendor_id, range
+      // 2, is not read).  An unread column re-reads its block's first chunk, whose values are
+      // in range like any other.
       L.load_mask = 0;
-      for (int k = 0; k < pl.p.nkeys; ++k) L.load_mask |= 1u << pl.p.keys[k].col;
+      {
+        int low = pl.p.nkeys;  // keys [low, nkeys) are not needed for the partition
+        uint64_t prod = 1;
+        for (int k = pl.p.nkeys - 1; k >= 0; --k) {
+          const uint64_t r = pl.p.keys[k].range;
+          if (r == 0 || prod > (1ull << pl.wbits) / r || pl.p.keys[k].stride != prod) break;
+          const uint64_t np = prod * r;
+          if ((np & (np - 1)) != 0) break;
+          prod = np;
+          low = k;
+        }
+        for (int k = 0; k < low; ++k) L.load_mask |= 1u << pl.p.keys[k].col;
+      }
       for (int i = 0; i < pl.p.nterms; ++i) L.load_mask |= 1u << pl.p.terms[i].col;
       if (pl.p.mask_col >= 0) L.load_mask |= 1u << pl.p.mask_col;
       // contiguous row ranges, whole 4096-row tiles (a multiple of every scatter tile), at

@@ -323,3 +323,25 @@ def test_specialised_partitioned(case, oracle_c, monkeypatch):
     assert not t.dev.last_timing()['specialized']
     t.close()
     assert_tables_equal(got, ref, exact_float_sums=True)
+
+
+@pytest.mark.parametrize('jit', [False, True])
+@pytest.mark.parametrize('low_ranges', [(2, 4), (3,), (4, 3), (8192,), (16384,)])
+def test_partition_count_skips_low_keys(jit, low_ranges, oracle_c, monkeypatch):
+    """The partition count pass does not read trailing key columns whose range product is a
+    power of two <= 2^wbits (they cannot change a row's partition); other layouts read every
+    key.  Terms on a skipped key column still filter."""
+    if jit:
+        monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
+    rng = np.random.default_rng(sum(low_ranges) + jit)
+    n = 300_007
+    kr = 40_000 if int(np.prod(low_ranges)) <= 8 else 500  # keep the slot space dense
+    cols = OrderedDict(k=rng.integers(-kr, kr, n).astype(np.int32),
+                       v=np.round(rng.normal(size=n) * 64) / 64)
+    names = []
+    for i, r in enumerate(low_ranges):
+        cols['l%d' % i] = (rng.integers(0, r, n) + 7).astype(np.int16 if r > 100 else np.int8 if i else np.int32)
+        names.append('l%d' % i)
+    keys = ['k'] + names
+    run_both(cols, keys, [['v', 'sum', 's'], ['v', 'count', 'c']], [], oracle_c, exact=True)
+    run_both(cols, keys, [['v', 'sum', 's']], [(names[-1], '!=', 7)], oracle_c, exact=True)
