@@ -250,6 +250,7 @@ class ShardTable:
                                                       ctypes.byref(s)))
         self._slot[name] = s.value
         self.dtypes[name] = np.dtype(dtype)
+        self.__dict__.pop('_plans', None)  # a re-added name maps to a new slot / dtype
         return s.value
 
     def scratch_mask(self):
