@@ -1,6 +1,8 @@
 """Deterministic synthetic NYC-taxi-shaped shards.
 
-Seeds: ``numpy.random.Generator(PCG64(SeedSequence(0xB0C0 + config_id).spawn(n_shards)[i]))``.
+Seeds: ``SeedSequence(0xB0C0 + config_id).spawn(n_shards)[i]``, spawned once more into one
+PCG64 stream per column (COLUMNS order), so any subset of the columns is drawn alone and is
+the same data as in the full shard.
 Float value columns come in two variants:
 * ``exact`` -- quantised to multiples of 2**-6, so every partial sum is exact in float64 and
   GPU/CPU sums agree bit for bit in any order;
@@ -31,33 +33,60 @@ def shard_rng(config_id, n_shards, i):
     return np.random.Generator(np.random.PCG64(ss))
 
 
+def _column_rngs(config_id, n_shards, i):
+    """One child stream per column (fixed COLUMNS order): a subset of the columns is the same
+    data as the full shard, and only the requested columns are drawn."""
+    ss = np.random.SeedSequence(0xB0C0 + int(config_id)).spawn(int(n_shards))[int(i)]
+    return {c: np.random.Generator(np.random.PCG64(s)) for c, s in zip(COLUMNS, ss.spawn(len(COLUMNS)))}
+
+
+def _draw(name, rng, n, variant):
+    if name == 'payment_type':
+        return _choice(rng, PAYMENT_W, n)
+    if name == 'vendor_id':
+        return np.where(rng.random(n) < 0.47, 1, 2).astype(np.int32)
+    if name == 'pu_location_id':
+        return _choice(rng, 1.0 / np.arange(1, 266, dtype=np.float64) ** 1.1, n, offset=1)
+    if name == 'pickup_location':
+        return rng.integers(0, 500000, n, dtype=np.int32)
+    if name == 'passenger_count':
+        return _choice(rng, PASSENGER_W, n)
+    if name == 'fare_amount':
+        v = np.clip(rng.lognormal(2.3, 0.6, n), 2.5, 500.0)
+    else:  # trip_distance
+        v = np.clip(rng.lognormal(0.6, 0.8, n), 0.0, 100.0)
+    if variant == 'exact':
+        return np.round(v * 64.0) / 64.0
+    return np.round(v, 2)
+
+
+def _stable_order(keys):
+    """Row order sorting by ``keys`` (first key most significant), stable.  Small-range
+    integer keys combine into one narrow code (numpy's stable sort is a radix sort there)."""
+    code = np.zeros(len(keys[0]), np.int64)
+    span = 1
+    for k in reversed(keys):
+        lo, hi = int(k.min()), int(k.max())
+        code += (k.astype(np.int64) - lo) * span
+        span *= hi - lo + 1
+    if span <= 1 << 16:
+        code = code.astype(np.uint16)
+    elif span <= 1 << 32:
+        code = code.astype(np.uint32)
+    return np.argsort(code, kind='stable')
+
+
 def taxi_shard(nrows, config_id=0, n_shards=1, shard=0, variant='exact', columns=COLUMNS,
                sort_by=None):
     """One shard as an OrderedDict of numpy columns."""
-    rng = shard_rng(config_id, n_shards, shard)
+    rngs = _column_rngs(config_id, n_shards, shard)
     n = int(nrows)
-    out = OrderedDict()
-    # draw every column (fixed order) so a subset is the same data as the full shard
-    payment = _choice(rng, PAYMENT_W, n)
-    vendor = np.where(rng.random(n) < 0.47, 1, 2).astype(np.int32)
-    zipf_w = 1.0 / np.arange(1, 266, dtype=np.float64) ** 1.1
-    pu = _choice(rng, zipf_w, n, offset=1)
-    pickup = rng.integers(0, 500000, n, dtype=np.int32)
-    pcount = _choice(rng, PASSENGER_W, n)
-    fare = np.clip(rng.lognormal(2.3, 0.6, n), 2.5, 500.0)
-    dist = np.clip(rng.lognormal(0.6, 0.8, n), 0.0, 100.0)
-    if variant == 'exact':
-        fare = np.round(fare * 64.0) / 64.0
-        dist = np.round(dist * 64.0) / 64.0
-    else:
-        fare = np.round(fare, 2)
-        dist = np.round(dist, 2)
-    full = {'payment_type': payment, 'vendor_id': vendor, 'pu_location_id': pu,
-            'pickup_location': pickup, 'passenger_count': pcount, 'fare_amount': fare,
-            'trip_distance': dist}
+    need = list(dict.fromkeys(list(columns) + list(sort_by or [])))
+    full = {c: _draw(c, rngs[c], n, variant) for c in need}
     if sort_by:
-        order = np.lexsort(tuple(full[c] for c in reversed(sort_by)))
+        order = _stable_order([full[c] for c in sort_by])
         full = {k: v[order] for k, v in full.items()}
+    out = OrderedDict()
     for c in columns:
         out[c] = full[c]
     return out

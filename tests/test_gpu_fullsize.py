@@ -1,0 +1,79 @@
+"""Full-size (BASELINE.json configs) parity on non-dyadic data: libbqgpu vs the C restatement
+of bquery's per-shard groupby (oracle/cbquery.c).
+
+* C2: 100 M rows, cent-rounded ("raw") fares -- float64 sum and bquery's row-order Knuth mean
+  at 1e-12 relative (north_star), counts bit-exact.
+* C3: 100 M rows, ~1 M groups (partitioned path), raw and dyadic data; keys, first-appearance
+  group order and counts bit-exact, sums 1e-12 (bit-exact on dyadic data).
+* C4: 200 M rows, random and (pu_location_id, passenger_count)-sorted row order;
+  count_distinct and sorted_count_distinct bit-exact.
+
+The oracle sums every group strictly in row order (bquery's ``out[g] += v``,
+bqueryd/worker.py:313 -> ctable.groupby); the GPU sums in a different order, so the float64
+comparisons measure the reference's own rounding noise (~sqrt(n) ulp) as much as ours.
+"""
+import numpy as np
+import pytest
+
+from bqueryd_amd import synth
+from bqueryd_amd.engine import ShardTable
+from tests.helpers import assert_tables_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel_err(got, ref):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    return float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-300))) if len(ref) else 0.0
+
+
+def _gpu_groupby(cols, cfg):
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(cfg['groupby'], cfg['aggs'], where_terms=cfg['where'])
+        mode = t.dev.last_timing()['mode']
+    finally:
+        t.close()
+    return got, mode
+
+
+def _float_cols(cfg, got):
+    return [a[2] for a in cfg['aggs'] if got[a[2]].dtype.kind == 'f']
+
+
+def test_c2_full_size_raw(oracle_c):
+    cfg = synth.CONFIGS['c2']
+    cols = synth.taxi_shard(cfg['rows'], config_id=2, variant='raw', columns=synth.query_columns(cfg))
+    got, mode = _gpu_groupby(cols, cfg)
+    ref = oracle_c.handle_work(cols, cfg['groupby'], cfg['aggs'], cfg['where'])
+    errs = {c: _rel_err(got[c], ref[c]) for c in _float_cols(cfg, got)}
+    print('C2 raw: mode %d, max relative error %s' % (mode, errs))
+    for c, e in errs.items():
+        assert e <= 1e-12, (c, e)
+    assert_tables_equal(got, ref, rtol=1e-12)
+
+
+@pytest.mark.parametrize('variant', ['raw', 'exact'])
+def test_c3_full_size(variant, oracle_c):
+    cfg = synth.CONFIGS['c3']
+    cols = synth.taxi_shard(cfg['rows'], config_id=3, variant=variant, columns=synth.query_columns(cfg))
+    got, mode = _gpu_groupby(cols, cfg)
+    ref = oracle_c.handle_work(cols, cfg['groupby'], cfg['aggs'], cfg['where'])
+    errs = {c: _rel_err(got[c], ref[c]) for c in _float_cols(cfg, got)}
+    print('C3 %s: mode %d, %d groups, max relative error %s' % (variant, mode, len(ref['n']), errs))
+    assert mode == 4  # the partitioned path
+    assert len(ref['n']) > 900_000
+    exact = {'fare_sum'} if variant == 'exact' else set()
+    assert_tables_equal(got, ref, rtol=1e-12, exact_cols=exact)
+
+
+@pytest.mark.parametrize('order', ['random', 'sorted'])
+def test_c4_full_size(order, oracle_c):
+    cfg = synth.CONFIGS['c4']
+    sort_by = ['pu_location_id', 'passenger_count'] if order == 'sorted' else None
+    cols = synth.taxi_shard(cfg['rows'], config_id=4, columns=synth.query_columns(cfg), sort_by=sort_by)
+    got, mode = _gpu_groupby(cols, cfg)
+    ref = oracle_c.handle_work(cols, cfg['groupby'], cfg['aggs'], cfg['where'])
+    print('C4 %s: mode %d, %d groups, scd total %d' % (order, mode, len(ref['pc_scd']), int(ref['pc_scd'].sum())))
+    assert mode == 5  # the fused distinct pass
+    assert_tables_equal(got, ref)
