@@ -44,19 +44,22 @@ def _dist_env():
 class _Comm:
     """Barrier / max-reduce across ranks (gloo, CPU only).  Single process: no-ops."""
 
-    def __init__(self, ws, local=0, nccl=False):
+    def __init__(self, ws):
         self.ws = ws
         self.dist = None
-        self.nccl_group = None
         if ws > 1:
-            import torch
-            import torch.distributed as dist  # imported before libbqgpu: one HIP runtime
+            import torch.distributed as dist
             os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
             dist.init_process_group('gloo')
             self.dist = dist
-            if nccl:  # the data-path exchange of the aggregate=True merge: RCCL over xGMI
-                torch.cuda.set_device(local)
-                self.nccl_group = dist.new_group(backend='nccl')
+
+    def broadcast_bytes(self, b):
+        """Rank 0's bytes on every rank (the RCCL unique id of the C5 merge)."""
+        if not self.dist:
+            return b
+        box = [b]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
 
     def barrier(self):
         if self.dist:
@@ -124,7 +127,7 @@ def main(argv=None):
     args = ap.parse_args(argv)
 
     ws, rank, local = _dist_env()
-    comm = _Comm(ws, local, nccl=(args.config == 'c5'))
+    comm = _Comm(ws)
 
     from bqueryd_amd import synth
     from bqueryd_amd.engine import Device, ShardTable
@@ -147,12 +150,10 @@ def main(argv=None):
                                   shard=rank * per_rank + i, variant=args.variant,
                                   columns=synth.query_columns(cfg))
             tables.append(ShardTable(sc, device=dev))
-        if ws > 1:
-            import torch
-            exchange = bdist.DeviceExchange(comm.dist, device=torch.device('cuda', local), group=comm.nccl_group)
-        else:
-            exchange = bdist.LocalExchange()
-        backend = bdist.GpuBackend(dev)
+        # RCCL communicator inside libbqgpu (the exchange runs on device buffers); gloo only
+        # hands rank 0's unique id to the other ranks
+        uid = comm.broadcast_bytes(bdist.new_unique_id() if rank == 0 else None)
+        rccl = bdist.RcclComm(dev, rank, ws, uid)
         colo = bdist.ColocatedShards(tables)
         fused = not args.c5_per_shard and bdist.decomposable(cfg['aggs'])
         if fused:
@@ -178,8 +179,7 @@ def main(argv=None):
                     per.append(t.groupby_table(cfg['groupby'], cfg['aggs']))
                     timings.append(dev.last_timing())
             t1 = time.perf_counter()
-            merged = bdist.merge_partials_device(per, cfg['groupby'], cfg['aggs'], dtypes, backend, exchange,
-                                                 reduced=reduced)
+            merged = bdist.merge_partials_device(per, cfg['groupby'], cfg['aggs'], dtypes, rccl, reduced=reduced)
             for p in per:
                 p.close()
             phase.append((t1 - t0, time.perf_counter() - t1))
@@ -244,7 +244,7 @@ def main(argv=None):
     if phase:
         cfg_extra = {'shard_queries_ms_per_step': 1e3 * float(np.mean([p[0] for p in phase])),
                      'merge_ms_per_step': 1e3 * float(np.mean([p[1] for p in phase])),
-                     'merge': 'device-resident: results in HBM, merged without host copies',
+                     'merge': 'libbqgpu bqg_merge: results in HBM, hash-partitioned, exchanged over RCCL (world %d), reduced, gathered to rank 0' % ws,
                      'shard_pass': ('fused: the rank\'s shards aggregated in one pass (sum / count are '
                                     'decomposable; dist.ColocatedShards)' if fused else
                                     'per-shard groupby + local re-group')}

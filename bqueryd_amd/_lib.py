@@ -28,6 +28,7 @@ AGG_CODE = {'sum': 0, 'count': 1, 'count_distinct': 2, 'sorted_count_distinct': 
 T_FALSE, T_TRUE, T_EQ, T_NE, T_IN, T_NIN, T_GT, T_GE, T_LT, T_LE = -1, 0, 1, 2, 3, 4, 5, 6, 7, 8
 
 E_INVALID, E_UNSUPPORTED, E_HIP, E_OOM, E_STATE = -1, -2, -3, -4, -5
+UNIQUE_ID_BYTES = 128
 
 
 class Term(ctypes.Structure):
@@ -101,6 +102,16 @@ _PROTOS = {
     'bqg_select_rows_table': ([_P, _P, ctypes.POINTER(Query), _I32, _P, ctypes.POINTER(_P)],
                               ctypes.c_int),
     'bqg_table_nrows': ([_P, ctypes.POINTER(_I64)], ctypes.c_int),
+    'bqg_table_ncols': ([_P, ctypes.POINTER(_I32)], ctypes.c_int),
+    'bqg_table_dtype': ([_P, _I32, ctypes.POINTER(_I32)], ctypes.c_int),
+    'bqg_comm_unique_id': ([_P], ctypes.c_int),
+    'bqg_comm_init': ([_P, _I32, _I32, _P], ctypes.c_int),
+    'bqg_comm_init_all': ([_I32, _P], ctypes.c_int),
+    'bqg_comm_init_local': ([_I32, _P], ctypes.c_int),
+    'bqg_comm_destroy': ([_P], ctypes.c_int),
+    'bqg_comm_info': ([_P, ctypes.POINTER(_I32), ctypes.POINTER(_I32)], ctypes.c_int),
+    'bqg_merge': ([_P, _I32, _P, _I32, _I32, _P, _I32, ctypes.POINTER(_P)], ctypes.c_int),
+    'bqg_merge_group': ([_I32, _P, _P, _P, _I32, _I32, _P, _I32, _P], ctypes.c_int),
     'bqg_result_view_get': ([_P, ctypes.POINTER(ResultView)], ctypes.c_int),
     'bqg_hash_partition': ([_P, _P, _I32, _P, _I32, _I32, _P], ctypes.c_int),
     'bqg_result_free': ([_P], ctypes.c_int),

@@ -26,6 +26,7 @@
 #include "kernels.h"
 #include "jit.h"
 #include "ingest.h"
+#include "ctx_internal.h"
 
 using namespace bqg;
 
@@ -208,6 +209,29 @@ struct PinnedPool {
       (void)hipHostFree(free[lg].p);
       free.erase(free.begin() + lg);
     }
+  }
+};
+
+// Owns a pool block until a result takes it over (release()); an exception that unwinds the
+// call first (a JIT or launch failure, a HIP error) returns the block to the pool.
+struct BlockGuard {
+  std::shared_ptr<PinnedPool> pool;
+  PinnedBlock b{};
+  BlockGuard() = default;
+  BlockGuard(const BlockGuard&) = delete;
+  BlockGuard& operator=(const BlockGuard&) = delete;
+  void reset(const std::shared_ptr<PinnedPool>& p, PinnedBlock blk) {
+    if (b.p && pool) pool->put(b);
+    pool = p;
+    b = blk;
+  }
+  PinnedBlock release() {
+    PinnedBlock r = b;
+    b = PinnedBlock{};
+    return r;
+  }
+  ~BlockGuard() {
+    if (b.p && pool) pool->put(b);
   }
 };
 
@@ -842,13 +866,13 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     F.emit_inline = need_generic ? 0 : 1;
     // host result: the finish step writes [64-byte header | columns of S rows] straight into
     // a pooled pinned block (device-mapped host memory: no copy); device result: into HBM
-    PinnedBlock hblk{};
+    BlockGuard hblk;
     const size_t colbytes = (size_t)e.ncols * S * 8;
     if (F.emit_inline) {
       unsigned char* ob;
       if (!c->dev_target) {
-        hblk = c->pool_get(colbytes + 64);
-        ob = (unsigned char*)hblk.dev;
+        hblk.reset(c->pool, c->pool_get(colbytes + 64));
+        ob = (unsigned char*)hblk.b.dev;
       } else {
         ob = (unsigned char*)c->outcols.ensure(64 + colbytes + 256);
       }
@@ -895,14 +919,13 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       return;
     }
     if (!need_generic) {
-      PinnedBlock blk = hblk;
-      unsigned char* h = (unsigned char*)blk.p;
+      unsigned char* h = (unsigned char*)hblk.b.p;
       if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
       HIPCHECK(hipStreamSynchronize(st));
       const unsigned long long G = ((unsigned long long*)h)[0], total = ((unsigned long long*)h)[1];
       std::vector<size_t> offs;
       for (int j = 0; j < e.ncols; ++j) offs.push_back(64 + (size_t)j * S * 8);
-      bqg_result* r = block_result(c, blk, (int64_t)G, pl.has_filter && (int64_t)total < N, out_dt, offs);
+      bqg_result* r = block_result(c, hblk.release(), (int64_t)G, pl.has_filter && (int64_t)total < N, out_dt, offs);
       if (c->timing) {
         float ms = 0;
         HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
@@ -1260,9 +1283,9 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       obytes += ((size_t)S * dtype_size(out_dt[j]) + 255) & ~size_t(255);
     }
     // host result: written straight into a pooled pinned block (device-mapped, no copy)
-    PinnedBlock blk{};
-    if (!c->dev_target) blk = c->pool_get(obytes + 64);
-    unsigned char* ob = c->dev_target ? (unsigned char*)c->outcols.ensure(obytes + 256) : (unsigned char*)blk.dev;
+    BlockGuard blk;
+    if (!c->dev_target) blk.reset(c->pool, c->pool_get(obytes + 64));
+    unsigned char* ob = c->dev_target ? (unsigned char*)c->outcols.ensure(obytes + 256) : (unsigned char*)blk.b.dev;
     for (int j = 0; j < e.ncols; ++j) e.cols[j].out = ob + offs[j];
     launch_emit_small(e, sa, (uint32_t)S, nsum, (unsigned long long*)ob, st);
     HIPCHECK(hipGetLastError());
@@ -1271,7 +1294,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       hh = (const unsigned long long*)c->hhdr.ensure(64);
       HIPCHECK(hipMemcpyAsync((void*)hh, ob, 16, hipMemcpyDeviceToHost, st));
     } else {
-      hh = (const unsigned long long*)blk.p;
+      hh = (const unsigned long long*)blk.b.p;
     }
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -1286,14 +1309,13 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     }
     c->last.bytes = pl.alg_bytes + G * (int64_t)e.ncols * 8;
     if (G == 0) {
-      if (blk.p) c->pool->put(blk);
-      *out = empty_result(out_dt, filtered);
+      *out = empty_result(out_dt, filtered);  // the guard returns the block
     } else if (c->dev_target) {
       std::vector<const void*> src;
       for (int j = 0; j < e.ncols; ++j) src.push_back(e.cols[j].out);
       table_from_device(c, out_dt, src, G);
     } else {
-      *out = block_result(c, blk, G, filtered, out_dt, offs);
+      *out = block_result(c, blk.release(), G, filtered, out_dt, offs);
     }
     return;
   }
@@ -1363,8 +1385,9 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
     return;
   }
-  PinnedBlock blk = c->pool_get(obytes + 64);
-  HIPCHECK(hipMemcpyAsync(blk.p, ob, obytes, hipMemcpyDeviceToHost, st));
+  BlockGuard blk;
+  blk.reset(c->pool, c->pool_get(obytes + 64));
+  HIPCHECK(hipMemcpyAsync(blk.b.p, ob, obytes, hipMemcpyDeviceToHost, st));
   if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
   HIPCHECK(hipStreamSynchronize(st));
   std::vector<size_t> offs;
@@ -1375,7 +1398,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       o += ((size_t)G * dtype_size(out_dt[j]) + 255) & ~size_t(255);
     }
   }
-  bqg_result* r = block_result(c, blk, G, pl.has_filter && (int64_t)total < N, out_dt, offs);
+  bqg_result* r = block_result(c, blk.release(), G, pl.has_filter && (int64_t)total < N, out_dt, offs);
   if (c->timing) {
     float ms = 0;
     HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
@@ -1388,6 +1411,13 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
 }
 
 }  // namespace
+
+int bqg_internal_device(bqg_ctx* c) { return c->device; }
+hipStream_t bqg_internal_stream(bqg_ctx* c) { return c->stream; }
+void bqg_internal_set_error(bqg_ctx* c, const std::string& msg) {
+  if (c) c->err = msg;
+  g_err = msg;
+}
 
 // ======================================================================================
 // C ABI
@@ -1436,6 +1466,7 @@ int bqg_create(int device_ordinal, bqg_ctx** out) {
 
 int bqg_destroy(bqg_ctx* c) {
   if (!c) return BQG_OK;
+  bqg_internal_comm_release(c);
   int rc = guard(c, [&] {
     HIPCHECK(hipStreamSynchronize(c->stream));
     for (DevBuf* b : {&c->partials, &c->counter, &c->hdr, &c->slots, &c->terms, &c->outcols, &c->lists,
@@ -1613,6 +1644,17 @@ int bqg_table_sync(bqg_table* t) {
 
 int bqg_table_nrows(bqg_table* t, int64_t* nrows) {
   return guard(t->ctx, [&] { *nrows = t->nrows; });
+}
+
+int bqg_table_ncols(bqg_table* t, int32_t* ncols) {
+  return guard(t->ctx, [&] { *ncols = (int32_t)t->cols.size(); });
+}
+
+int bqg_table_dtype(bqg_table* t, int32_t col, int32_t* dtype) {
+  return guard(t->ctx, [&] {
+    if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
+    *dtype = t->cols[col].dtype;
+  });
 }
 
 int bqg_table_column_ptr(bqg_table* t, int32_t col, void** dev_ptr) {
@@ -1811,14 +1853,15 @@ int bqg_select_rows(bqg_ctx* c, bqg_table* t, const bqg_query* q, int32_t n_cols
       table_from_device(c, dts, src, total);
       return;
     }
-    PinnedBlock blk = c->pool_get(obytes + 64);
-    if (obytes) HIPCHECK(hipMemcpyAsync(blk.p, ob, obytes, hipMemcpyDeviceToHost, c->stream));
+    BlockGuard blk;
+    blk.reset(c->pool, c->pool_get(obytes + 64));
+    if (obytes) HIPCHECK(hipMemcpyAsync(blk.b.p, ob, obytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
     r->pool = c->pool;
-    r->block = blk;
+    r->block = blk.release();
     for (int i = 0; i < n_cols; ++i) {
       r->dtypes.push_back(t->cols[cols[i]].dtype);
-      r->ptrs.push_back((const unsigned char*)blk.p + offs[i]);
+      r->ptrs.push_back((const unsigned char*)r->block.p + offs[i]);
     }
     *out = guard_r.release();
   });

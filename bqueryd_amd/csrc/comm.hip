@@ -1,0 +1,708 @@
+// comm.hip -- multi-GPU merge of co-located shard results over RCCL (xGMI), C ABI
+// bqg_comm_* / bqg_merge* of include/bqgpu.h.
+//
+// bqueryd merges shard results on the client: every shard's finalized table is appended and
+// re-grouped with `sum` of every column ("we can only sum now", bqueryd/rpc.py:164-173).  For
+// shards that live on one node's GPUs the same merge runs here, on device buffers:
+//   1. local:     this rank's shard tables are concatenated (device to device) and summed by
+//                 key (bqg_groupby_table) -- skipped when the caller's one table is already
+//                 reduced (a co-located one-pass groupby over the rank's shards);
+//   2. partition: every row goes to rank hash(key values) mod nranks (bqg_hash_partition: a
+//                 pure function of the values, identical on every rank) -- packed per
+//                 destination, column by column, into one send buffer;
+//   3. exchange:  the [nranks x nranks] row-count matrix (ncclAllGather), then the payload
+//                 (grouped ncclSend / ncclRecv, one message per peer, self included);
+//   4. reduce:    the received rows are summed by key again (keys are disjoint across ranks);
+//   5. gather:    the reduced partitions travel to rank 0 (grouped send / recv) and are
+//                 concatenated there in rank order.
+// Only the row counts cross to the host (to size buffers).  librccl is loaded with dlopen on
+// first use, so libbqgpu itself loads where RCCL is absent; every entry here then fails with
+// a message instead.
+//
+// The merge is built from the library's own public entry points (groupby, partition,
+// select, push); this file adds the communicator and the exchange.  It runs any number of
+// local ranks from ONE host thread: bqg_merge drives one rank of a multi-process job (one
+// process per GPU), bqg_merge_group every rank of a process that owns several GPUs, with the
+// collective calls of all of them inside one ncclGroupStart / ncclGroupEnd.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "ctx_internal.h"
+
+namespace {
+
+struct CommError {
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void comm_fail(int code, const std::string& msg) { throw CommError{code, msg}; }
+
+// ------------------------------------------------------------------------------------
+// librccl, resolved at first use
+// ------------------------------------------------------------------------------------
+struct Rccl {
+  bool loaded = false;
+  std::string err;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+    if (!h) {
+      r.err = std::string("librccl could not be loaded: ") + dlerror();
+      return;
+    }
+    bool ok = true;
+    auto sym = [&](const char* name) {
+      void* p = dlsym(h, name);
+      if (!p) ok = false;
+      return p;
+    };
+    r.GetUniqueId = (decltype(r.GetUniqueId))sym("ncclGetUniqueId");
+    r.CommInitRank = (decltype(r.CommInitRank))sym("ncclCommInitRank");
+    r.CommInitAll = (decltype(r.CommInitAll))sym("ncclCommInitAll");
+    r.CommDestroy = (decltype(r.CommDestroy))sym("ncclCommDestroy");
+    r.Send = (decltype(r.Send))sym("ncclSend");
+    r.Recv = (decltype(r.Recv))sym("ncclRecv");
+    r.AllGather = (decltype(r.AllGather))sym("ncclAllGather");
+    r.GroupStart = (decltype(r.GroupStart))sym("ncclGroupStart");
+    r.GroupEnd = (decltype(r.GroupEnd))sym("ncclGroupEnd");
+    r.GetErrorString = (decltype(r.GetErrorString))sym("ncclGetErrorString");
+    if (!ok) r.err = "librccl lacks a required symbol";
+    r.loaded = ok;
+  });
+  if (!r.loaded) comm_fail(BQG_E_UNSUPPORTED, r.err);
+  return r;
+}
+
+#define NCCLCHECK(x)                                                                         \
+  do {                                                                                       \
+    ncclResult_t _r = (x);                                                                   \
+    if (_r != ncclSuccess)                                                                   \
+      comm_fail(BQG_E_HIP, std::string("RCCL error in " #x ": ") + rccl().GetErrorString(_r)); \
+  } while (0)
+
+#define HIPCK(x)                                                                              \
+  do {                                                                                        \
+    hipError_t _e = (x);                                                                      \
+    if (_e != hipSuccess) comm_fail(BQG_E_HIP, std::string("HIP error in " #x ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+// growable device buffer (stream-ordered use; freed only at communicator teardown)
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+  void* ensure(size_t bytes) {
+    bytes = std::max<size_t>(bytes, 256);
+    if (bytes > cap) {
+      const size_t c = std::max(bytes, cap + cap / 2);
+      if (p) HIPCK(hipFree(p));
+      p = nullptr;
+      cap = 0;
+      if (hipMalloc(&p, c) != hipSuccess) comm_fail(BQG_E_OOM, "device allocation for the merge exchange failed");
+      cap = c;
+    }
+    return p;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct CommState {
+  ncclComm_t comm = nullptr;  // RCCL transport; nullptr = in-process transport (see below)
+  int rank = 0, nranks = 1;
+  Buf send, recv, counts;
+};
+
+std::mutex g_mu;
+std::map<bqg_ctx*, CommState*> g_comms;
+
+CommState* state_of(bqg_ctx* c) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_comms.find(c);
+  if (it == g_comms.end()) comm_fail(BQG_E_STATE, "no communicator on this context (bqg_comm_init first)");
+  return it->second;
+}
+
+void destroy_state(CommState* s) {
+  if (!s) return;
+  if (s->comm) (void)rccl().CommDestroy(s->comm);
+  if (s->comm == nullptr) (void)hipDeviceSynchronize();  // in-process copies may target its buffers
+  s->send.release();
+  s->recv.release();
+  s->counts.release();
+  delete s;
+}
+
+template <typename F>
+int comm_guard(bqg_ctx* ctx, F&& f) {
+  try {
+    f();
+    return BQG_OK;
+  } catch (const CommError& e) {
+    bqg_internal_set_error(ctx, e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    bqg_internal_set_error(ctx, "host out of memory");
+    return BQG_E_OOM;
+  }
+}
+
+// a public entry point of this library, failing with its message
+void ck(bqg_ctx* c, int rc) {
+  if (rc != BQG_OK) comm_fail(rc, bqg_last_error(c));
+}
+
+size_t dt_size(int dt) {
+  switch (dt) {
+    case BQG_BOOL: case BQG_I8: case BQG_U8: return 1;
+    case BQG_I16: case BQG_U16: return 2;
+    case BQG_I32: case BQG_U32: case BQG_F32: return 4;
+    default: return 8;
+  }
+}
+
+size_t align16(size_t n) { return (n + 15) & ~size_t(15); }
+
+int64_t nrows_of(bqg_ctx* c, bqg_table* t) {
+  int64_t n = 0;
+  ck(c, bqg_table_nrows(t, &n));
+  return n;
+}
+
+void* col_ptr(bqg_ctx* c, bqg_table* t, int col) {
+  void* p = nullptr;
+  ck(c, bqg_table_column_ptr(t, col, &p));
+  return p;
+}
+
+struct TableOwner {  // destroys a library table on scope exit
+  bqg_table* t = nullptr;
+  TableOwner() = default;
+  TableOwner(const TableOwner&) = delete;
+  TableOwner& operator=(const TableOwner&) = delete;
+  ~TableOwner() { reset(); }
+  void reset() {
+    if (t) (void)bqg_table_destroy(t);
+    t = nullptr;
+  }
+  bqg_table* release() {
+    bqg_table* r = t;
+    t = nullptr;
+    return r;
+  }
+};
+
+// Row-concatenation of device tables (device-to-device copies) with statistics computed.
+bqg_table* concat_tables(bqg_ctx* c, const std::vector<bqg_table*>& parts, const std::vector<int32_t>& dts) {
+  int64_t total = 0;
+  for (bqg_table* p : parts) total += nrows_of(c, p);
+  TableOwner out;
+  ck(c, bqg_table_create(c, total, (int32_t)dts.size(), dts.data(), &out.t));
+  int64_t off = 0;
+  for (bqg_table* p : parts) {
+    const int64_t n = nrows_of(c, p);
+    if (n)
+      for (int j = 0; j < (int)dts.size(); ++j) ck(c, bqg_push_chunk(out.t, j, col_ptr(c, p, j), n, off));
+    off += n;
+  }
+  ck(c, bqg_table_sync(out.t));
+  return out.release();
+}
+
+// The client's re-group: sum of every non-key column by the first n_keys columns.
+bqg_table* regroup(bqg_ctx* c, bqg_table* t, int n_keys, int ncols) {
+  std::vector<int32_t> keys(std::max(1, n_keys));
+  for (int k = 0; k < n_keys; ++k) keys[k] = k;
+  std::vector<bqg_agg> aggs(std::max(1, ncols - n_keys));
+  for (int j = n_keys; j < ncols; ++j) aggs[j - n_keys] = bqg_agg{j, BQG_SUM};
+  bqg_query q{};
+  q.n_keys = n_keys;
+  q.key_cols = keys.data();
+  q.n_terms = 0;
+  q.terms = nullptr;
+  q.mask_col = -1;
+  q.n_aggs = ncols - n_keys;
+  q.aggs = aggs.data();
+  bqg_table* out = nullptr;
+  ck(c, bqg_groupby_table(c, t, &q, &out));
+  return out;
+}
+
+struct Local {
+  bqg_ctx* ctx = nullptr;
+  std::vector<bqg_table*> tables;
+  CommState* st = nullptr;
+  hipStream_t stream = nullptr;
+  TableOwner L;                   // this rank's reduced rows (+ partition column)
+  std::vector<int64_t> to_peer;   // rows for each destination rank
+  std::vector<size_t> send_off;   // byte offset of each destination's block
+  TableOwner R;                   // rows received from every rank, then reduced
+  int64_t n_recv = 0;
+  bqg_table** out = nullptr;
+};
+
+// bytes of a packed block of `rows` rows: columns one after another, 16-byte aligned
+size_t block_bytes(const std::vector<int32_t>& dts, int64_t rows) {
+  size_t b = 0;
+  for (int32_t dt : dts) b += align16((size_t)rows * dt_size(dt));
+  return b;
+}
+
+// copy the first `rows` rows of every column of `t` into a packed block at `dst`
+void pack_block(bqg_ctx* c, hipStream_t st, bqg_table* t, const std::vector<int32_t>& dts, int64_t rows,
+                unsigned char* dst) {
+  for (int j = 0; j < (int)dts.size(); ++j) {
+    const size_t nb = (size_t)rows * dt_size(dts[j]);
+    if (nb) HIPCK(hipMemcpyAsync(dst, col_ptr(c, t, j), nb, hipMemcpyDeviceToDevice, st));
+    dst += align16(nb);
+  }
+}
+
+// append a packed block of `rows` rows to table `t` at row `off`
+void unpack_block(bqg_ctx* c, bqg_table* t, const std::vector<int32_t>& dts, int64_t rows, int64_t off,
+                  const unsigned char* src) {
+  for (int j = 0; j < (int)dts.size(); ++j) {
+    const size_t nb = (size_t)rows * dt_size(dts[j]);
+    if (nb) ck(c, bqg_push_chunk(t, j, src, rows, off));
+    src += align16(nb);
+  }
+}
+
+
+// ------------------------------------------------------------------------------------
+// transport: RCCL, or in-process copies when every rank of the communicator is a local rank
+// of this call (bqg_comm_init_local: one process driving several contexts, possibly on one
+// GPU -- the test harness for the exchange logic on a one-GPU machine)
+// ------------------------------------------------------------------------------------
+struct P2P {
+  int peer;
+  void* ptr;
+  size_t bytes;
+};
+
+void sync_all(std::vector<Local>& ranks) {
+  for (Local& l : ranks) {
+    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+    HIPCK(hipStreamSynchronize(l.stream));
+  }
+}
+
+Local& by_rank(std::vector<Local>& ranks, int r) {
+  for (Local& l : ranks)
+    if (l.st->rank == r) return l;
+  comm_fail(BQG_E_STATE, "in-process transport: a rank of the communicator is not part of this merge call");
+}
+
+// every rank: `count` int64 at counts.p -> [nranks][count] at counts.p + nranks
+void xfer_allgather_i64(std::vector<Local>& ranks, size_t count) {
+  const int W = ranks[0].st->nranks;
+  if (ranks[0].st->comm) {
+    Rccl& R = rccl();
+    NCCLCHECK(R.GroupStart());
+    for (Local& l : ranks) {
+      int64_t* cnt = (int64_t*)l.st->counts.p;
+      NCCLCHECK(R.AllGather(cnt, cnt + W, count, ncclInt64, l.st->comm, l.stream));
+    }
+    NCCLCHECK(R.GroupEnd());
+    return;
+  }
+  if ((int)ranks.size() != W) comm_fail(BQG_E_STATE, "in-process transport needs every rank in one merge call");
+  sync_all(ranks);
+  for (Local& d : ranks) {
+    HIPCK(hipSetDevice(bqg_internal_device(d.ctx)));
+    for (int s = 0; s < W; ++s) {
+      Local& src = by_rank(ranks, s);
+      HIPCK(hipMemcpyAsync((int64_t*)d.st->counts.p + W + (size_t)s * count, src.st->counts.p, count * sizeof(int64_t),
+                           hipMemcpyDefault, d.stream));
+    }
+  }
+  sync_all(ranks);
+}
+
+// grouped point-to-point: sends[i] / recvs[i] of local rank i (matching pairs on both sides)
+void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& sends,
+              const std::vector<std::vector<P2P>>& recvs) {
+  if (ranks[0].st->comm) {
+    Rccl& R = rccl();
+    NCCLCHECK(R.GroupStart());
+    for (size_t i = 0; i < ranks.size(); ++i) {
+      Local& l = ranks[i];
+      for (const P2P& x : sends[i]) NCCLCHECK(R.Send(x.ptr, x.bytes, ncclUint8, x.peer, l.st->comm, l.stream));
+      for (const P2P& x : recvs[i]) NCCLCHECK(R.Recv(x.ptr, x.bytes, ncclUint8, x.peer, l.st->comm, l.stream));
+    }
+    NCCLCHECK(R.GroupEnd());
+    return;
+  }
+  sync_all(ranks);
+  for (size_t i = 0; i < ranks.size(); ++i) {
+    Local& d = ranks[i];
+    HIPCK(hipSetDevice(bqg_internal_device(d.ctx)));
+    for (const P2P& x : recvs[i]) {
+      size_t j = 0;
+      while (j < ranks.size() && ranks[j].st->rank != x.peer) ++j;
+      if (j == ranks.size()) comm_fail(BQG_E_STATE, "in-process transport: peer rank not in this merge call");
+      const P2P* m = nullptr;
+      for (const P2P& y : sends[j])
+        if (y.peer == d.st->rank) m = &y;
+      if (!m || m->bytes != x.bytes) comm_fail(BQG_E_STATE, "in-process transport: unmatched send / receive");
+      HIPCK(hipMemcpyAsync(x.ptr, m->ptr, x.bytes, hipMemcpyDefault, d.stream));
+    }
+  }
+  sync_all(ranks);
+}
+
+void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t>& dts, int reduced) {
+  const int ncols = (int)dts.size();
+  if (n_keys < 1 || n_keys > ncols) comm_fail(BQG_E_INVALID, "merge needs 1..ncols key columns");
+  const int W = ranks[0].st->nranks;
+  for (Local& l : ranks) {
+    if (l.st->nranks != W) comm_fail(BQG_E_INVALID, "local ranks of one merge must share a communicator size");
+    for (bqg_table* t : l.tables) {
+      int32_t nc = 0;
+      ck(l.ctx, bqg_table_ncols(t, &nc));
+      if (nc < ncols) comm_fail(BQG_E_INVALID, "merge input table has fewer columns than the merge schema");
+      for (int j = 0; j < ncols; ++j) {
+        int32_t dt = 0;
+        ck(l.ctx, bqg_table_dtype(t, j, &dt));
+        if (dt != dts[j]) comm_fail(BQG_E_INVALID, "merge input column dtype differs from the merge schema");
+      }
+    }
+  }
+  // 1-2. local reduce and partition by destination
+  std::vector<int32_t> key_idx(n_keys);
+  for (int k = 0; k < n_keys; ++k) key_idx[k] = k;
+  std::vector<int32_t> sel(ncols);
+  for (int j = 0; j < ncols; ++j) sel[j] = j;
+  for (Local& l : ranks) {
+    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+    l.to_peer.assign(W, 0);
+    std::vector<bqg_table*> parts;
+    for (bqg_table* t : l.tables)
+      if (nrows_of(l.ctx, t) > 0) parts.push_back(t);
+    if (!parts.empty()) {
+      TableOwner cat;
+      cat.t = concat_tables(l.ctx, parts, dts);
+      if (reduced && parts.size() == 1) l.L.t = cat.release();
+      else l.L.t = regroup(l.ctx, cat.t, n_keys, ncols);
+    }
+    const int64_t nl = l.L.t ? nrows_of(l.ctx, l.L.t) : 0;
+    std::vector<bqg_table*> per(W, nullptr);
+    struct PerOwner {
+      std::vector<bqg_table*>& v;
+      ~PerOwner() {
+        for (bqg_table* t : v)
+          if (t) (void)bqg_table_destroy(t);
+      }
+    } per_owner{per};
+    if (nl > 0) {
+      int32_t pcol = -1;
+      ck(l.ctx, bqg_table_add_column(l.L.t, BQG_U32, &pcol));
+      ck(l.ctx, bqg_hash_partition(l.ctx, l.L.t, n_keys, key_idx.data(), W, pcol, l.to_peer.data()));
+      for (int d = 0; d < W; ++d) {
+        if (!l.to_peer[d]) continue;
+        if (W == 1) break;  // everything goes to the one rank: send the table itself
+        const int64_t dv = d;
+        bqg_term term{pcol, BQG_T_EQ, 1, &dv, nullptr};
+        bqg_query q{};
+        q.n_terms = 1;
+        q.terms = &term;
+        q.mask_col = -1;
+        ck(l.ctx, bqg_select_rows_table(l.ctx, l.L.t, &q, ncols, sel.data(), &per[d]));
+      }
+    }
+    l.send_off.assign(W + 1, 0);
+    for (int d = 0; d < W; ++d) l.send_off[d + 1] = l.send_off[d] + block_bytes(dts, l.to_peer[d]);
+    unsigned char* sb = (unsigned char*)l.st->send.ensure(l.send_off[W]);
+    for (int d = 0; d < W; ++d)
+      if (l.to_peer[d]) pack_block(l.ctx, l.stream, W == 1 ? l.L.t : per[d], dts, l.to_peer[d], sb + l.send_off[d]);
+    // the row counts this rank sends, for the count exchange
+    int64_t* cnt = (int64_t*)l.st->counts.ensure(sizeof(int64_t) * (size_t)W * (W + 2));
+    HIPCK(hipMemcpyAsync(cnt, l.to_peer.data(), sizeof(int64_t) * W, hipMemcpyHostToDevice, l.stream));
+    HIPCK(hipStreamSynchronize(l.stream));  // to_peer (host) is read by the copy; per[] is freed next
+  }
+  // 3a. count matrix: every rank's row counts per destination
+  xfer_allgather_i64(ranks, (size_t)W);
+  std::vector<std::vector<int64_t>> from_peer(ranks.size(), std::vector<int64_t>(W, 0));
+  for (size_t i = 0; i < ranks.size(); ++i) {
+    Local& l = ranks[i];
+    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+    std::vector<int64_t> m((size_t)W * W);
+    HIPCK(hipMemcpyAsync(m.data(), (int64_t*)l.st->counts.p + W, sizeof(int64_t) * W * W, hipMemcpyDeviceToHost,
+                         l.stream));
+    HIPCK(hipStreamSynchronize(l.stream));
+    for (int s = 0; s < W; ++s) from_peer[i][s] = m[(size_t)s * W + l.st->rank];
+  }
+  // 3b. payload: one packed block per (source, destination) pair
+  std::vector<std::vector<size_t>> recv_off(ranks.size());
+  for (size_t i = 0; i < ranks.size(); ++i) {
+    Local& l = ranks[i];
+    recv_off[i].assign(W + 1, 0);
+    for (int s = 0; s < W; ++s) recv_off[i][s + 1] = recv_off[i][s] + block_bytes(dts, from_peer[i][s]);
+    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+    l.st->recv.ensure(recv_off[i][W]);
+  }
+  {
+    std::vector<std::vector<P2P>> sends(ranks.size()), recvs(ranks.size());
+    for (size_t i = 0; i < ranks.size(); ++i) {
+      Local& l = ranks[i];
+      unsigned char* sb = (unsigned char*)l.st->send.p;
+      unsigned char* rb = (unsigned char*)l.st->recv.p;
+      for (int p = 0; p < W; ++p) {
+        const size_t sbytes = l.send_off[p + 1] - l.send_off[p];
+        const size_t rbytes = recv_off[i][p + 1] - recv_off[i][p];
+        if (sbytes) sends[i].push_back(P2P{p, sb + l.send_off[p], sbytes});
+        if (rbytes) recvs[i].push_back(P2P{p, rb + recv_off[i][p], rbytes});
+      }
+    }
+    xfer_p2p(ranks, sends, recvs);
+  }
+  // 4. reduce the received rows
+  std::vector<int64_t> reduced_rows(ranks.size(), 0);
+  for (size_t i = 0; i < ranks.size(); ++i) {
+    Local& l = ranks[i];
+    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+    l.L.reset();  // the local rows have been sent
+    int64_t total = 0;
+    for (int s = 0; s < W; ++s) total += from_peer[i][s];
+    l.n_recv = total;
+    if (!total) continue;
+    TableOwner got;
+    ck(l.ctx, bqg_table_create(l.ctx, total, ncols, dts.data(), &got.t));
+    int64_t off = 0;
+    for (int s = 0; s < W; ++s) {
+      unpack_block(l.ctx, got.t, dts, from_peer[i][s], off, (const unsigned char*)l.st->recv.p + recv_off[i][s]);
+      off += from_peer[i][s];
+    }
+    ck(l.ctx, bqg_table_sync(got.t));
+    // one source's rows are already unique by key: only rows from two or more sources
+    // need the re-group
+    int sources = 0;
+    for (int s = 0; s < W; ++s) sources += from_peer[i][s] > 0;
+    l.R.t = sources > 1 ? regroup(l.ctx, got.t, n_keys, ncols) : got.release();
+    reduced_rows[i] = nrows_of(l.ctx, l.R.t);
+  }
+  // 5. gather to rank 0: counts, then the packed partitions
+  for (Local& l : ranks) {
+    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+    int64_t* cnt = (int64_t*)l.st->counts.p;
+    const int64_t mine = l.R.t ? nrows_of(l.ctx, l.R.t) : 0;
+    HIPCK(hipMemcpyAsync(cnt, &mine, sizeof(int64_t), hipMemcpyHostToDevice, l.stream));
+    HIPCK(hipStreamSynchronize(l.stream));
+  }
+  xfer_allgather_i64(ranks, 1);
+  std::vector<int64_t> part_rows(W, 0);
+  std::vector<size_t> goff(W + 1, 0);
+  for (Local& l : ranks) {
+    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+    HIPCK(hipMemcpyAsync(part_rows.data(), (int64_t*)l.st->counts.p + W, sizeof(int64_t) * W, hipMemcpyDeviceToHost,
+                         l.stream));
+    HIPCK(hipStreamSynchronize(l.stream));
+    // pack this rank's reduced partition into the send buffer (sent to rank 0, or kept there)
+    if (l.R.t) pack_block(l.ctx, l.stream, l.R.t, dts, nrows_of(l.ctx, l.R.t), (unsigned char*)l.st->send.ensure(block_bytes(dts, nrows_of(l.ctx, l.R.t))));
+  }
+  for (int s = 0; s < W; ++s) goff[s + 1] = goff[s] + block_bytes(dts, part_rows[s]);
+  for (Local& l : ranks)
+    if (l.st->rank == 0) {
+      HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+      l.st->recv.ensure(goff[W]);
+    }
+  {
+    std::vector<std::vector<P2P>> sends(ranks.size()), recvs(ranks.size());
+    for (size_t i = 0; i < ranks.size(); ++i) {
+      Local& l = ranks[i];
+      const size_t mine = block_bytes(dts, part_rows[l.st->rank]);
+      if (l.st->rank == 0) {
+        unsigned char* rb = (unsigned char*)l.st->recv.p;
+        for (int s = 1; s < W; ++s)
+          if (part_rows[s]) recvs[i].push_back(P2P{s, rb + goff[s], goff[s + 1] - goff[s]});
+      } else if (mine) {
+        sends[i].push_back(P2P{0, l.st->send.p, mine});
+      }
+    }
+    xfer_p2p(ranks, sends, recvs);
+  }
+  for (Local& l : ranks) {
+    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+    if (l.st->rank != 0) {
+      HIPCK(hipStreamSynchronize(l.stream));  // the send buffer is reused by the next merge
+      *l.out = nullptr;
+      continue;
+    }
+    int64_t total = 0;
+    for (int s = 0; s < W; ++s) total += part_rows[s];
+    TableOwner res;
+    ck(l.ctx, bqg_table_create(l.ctx, total, ncols, dts.data(), &res.t));
+    int64_t off = 0;
+    for (int s = 0; s < W; ++s) {
+      if (part_rows[s]) {
+        const unsigned char* src =
+            s == 0 ? (const unsigned char*)l.st->send.p : (const unsigned char*)l.st->recv.p + goff[s];
+        unpack_block(l.ctx, res.t, dts, part_rows[s], off, src);
+      }
+      off += part_rows[s];
+    }
+    ck(l.ctx, bqg_table_sync(res.t));
+    *l.out = res.release();
+  }
+  for (Local& l : ranks) l.R.reset();
+}
+
+}  // namespace
+
+void bqg_internal_comm_release(bqg_ctx* c) {
+  CommState* s = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_comms.find(c);
+    if (it == g_comms.end()) return;
+    s = it->second;
+    g_comms.erase(it);
+  }
+  try {
+    destroy_state(s);
+  } catch (...) {
+  }
+}
+
+extern "C" {
+
+int bqg_comm_unique_id(void* out) {
+  return comm_guard(nullptr, [&] {
+    if (!out) comm_fail(BQG_E_INVALID, "null output");
+    ncclUniqueId id;
+    NCCLCHECK(rccl().GetUniqueId(&id));
+    memcpy(out, &id, sizeof(id));
+  });
+}
+
+int bqg_comm_init(bqg_ctx* ctx, int32_t rank, int32_t nranks, const void* unique_id) {
+  return comm_guard(ctx, [&] {
+    if (!ctx || !unique_id) comm_fail(BQG_E_INVALID, "null context or unique id");
+    if (nranks < 1 || rank < 0 || rank >= nranks) comm_fail(BQG_E_INVALID, "rank out of range");
+    bqg_internal_comm_release(ctx);
+    HIPCK(hipSetDevice(bqg_internal_device(ctx)));
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof(id));
+    CommState* s = new CommState();
+    s->rank = rank;
+    s->nranks = nranks;
+    const ncclResult_t r = rccl().CommInitRank(&s->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+      delete s;
+      comm_fail(BQG_E_HIP, std::string("ncclCommInitRank: ") + rccl().GetErrorString(r));
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_comms[ctx] = s;
+  });
+}
+
+int bqg_comm_init_all(int32_t n, bqg_ctx* const* ctxs) {
+  return comm_guard(n > 0 && ctxs ? ctxs[0] : nullptr, [&] {
+    if (n < 1 || !ctxs) comm_fail(BQG_E_INVALID, "need at least one context");
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) {
+      devs[i] = bqg_internal_device(ctxs[i]);
+      for (int j = 0; j < i; ++j)
+        if (devs[j] == devs[i]) comm_fail(BQG_E_INVALID, "one context per GPU");
+    }
+    for (int i = 0; i < n; ++i) bqg_internal_comm_release(ctxs[i]);
+    std::vector<ncclComm_t> comms(n, nullptr);
+    NCCLCHECK(rccl().CommInitAll(comms.data(), n, devs.data()));
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (int i = 0; i < n; ++i) {
+      CommState* s = new CommState();
+      s->comm = comms[i];
+      s->rank = i;
+      s->nranks = n;
+      g_comms[ctxs[i]] = s;
+    }
+  });
+}
+
+int bqg_comm_init_local(int32_t n, bqg_ctx* const* ctxs) {
+  return comm_guard(n > 0 && ctxs ? ctxs[0] : nullptr, [&] {
+    if (n < 1 || !ctxs) comm_fail(BQG_E_INVALID, "need at least one context");
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < i; ++j)
+        if (ctxs[i] == ctxs[j]) comm_fail(BQG_E_INVALID, "one context per rank");
+    for (int i = 0; i < n; ++i) bqg_internal_comm_release(ctxs[i]);
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (int i = 0; i < n; ++i) {
+      CommState* s = new CommState();
+      s->rank = i;
+      s->nranks = n;
+      g_comms[ctxs[i]] = s;
+    }
+  });
+}
+
+int bqg_comm_destroy(bqg_ctx* ctx) {
+  return comm_guard(ctx, [&] { bqg_internal_comm_release(ctx); });
+}
+
+int bqg_comm_info(bqg_ctx* ctx, int32_t* rank, int32_t* nranks) {
+  return comm_guard(ctx, [&] {
+    CommState* s = state_of(ctx);
+    if (rank) *rank = s->rank;
+    if (nranks) *nranks = s->nranks;
+  });
+}
+
+int bqg_merge(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int32_t n_keys, int32_t n_cols,
+              const int32_t* dtypes, int32_t reduced, bqg_table** out) {
+  return bqg_merge_group(1, &ctx, &n_tables, tables, n_keys, n_cols, dtypes, reduced, out);
+}
+
+int bqg_merge_group(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,
+                    int32_t n_keys, int32_t n_cols, const int32_t* dtypes, int32_t reduced, bqg_table** out) {
+  bqg_ctx* c0 = n_local > 0 && ctxs ? ctxs[0] : nullptr;
+  return comm_guard(c0, [&] {
+    if (n_local < 1 || !ctxs || !n_tables || !out || !dtypes || n_cols < 1)
+      comm_fail(BQG_E_INVALID, "bad merge arguments");
+    std::vector<int32_t> dts(dtypes, dtypes + n_cols);
+    for (int32_t dt : dts)
+      if (dt < BQG_BOOL || dt > BQG_F64) comm_fail(BQG_E_INVALID, "unknown dtype in the merge schema");
+    std::vector<Local> ranks(n_local);
+    size_t k = 0;
+    for (int i = 0; i < n_local; ++i) {
+      ranks[i].ctx = ctxs[i];
+      ranks[i].st = state_of(ctxs[i]);
+      ranks[i].stream = bqg_internal_stream(ctxs[i]);
+      ranks[i].out = &out[i];
+      out[i] = nullptr;
+      if (n_tables[i] < 0) comm_fail(BQG_E_INVALID, "negative table count");
+      for (int j = 0; j < n_tables[i]; ++j) ranks[i].tables.push_back(tables[k++]);
+    }
+    merge_impl(ranks, n_keys, dts, reduced);
+  });
+}
+
+}  // extern "C"

@@ -37,13 +37,24 @@ class WhereMask:
     def __init__(self, ct, terms=None, device_col=None, npass=None):
         self.ct = ct
         self.terms = list(terms) if terms is not None else None
-        self.device_col = device_col
+        self.device_col = device_col  # a scratch mask column this object owns
+        self._table = ct._table if device_col is not None else None
         self._npass = npass
 
     def materialize(self):
         if self.device_col is None:
-            self.device_col, self._npass = self.ct._table_for_terms(self.terms).where(self.terms)
+            self._table = self.ct._table_for_terms(self.terms)
+            self.device_col, self._npass = self._table.where(self.terms)
         return self.device_col
+
+    def __del__(self):
+        # the mask column goes back to the shard's free list (the shard stays resident in
+        # HBM between queries: worker.ShardCache)
+        try:
+            if self.device_col is not None and self._table is not None:
+                self._table.release_mask(self.device_col)
+        except Exception:
+            pass
 
     def sum(self):
         self.materialize()
@@ -197,20 +208,27 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
         if bool_arr is None:
             return None
         table = self._ensure_device([basket_col])
-        mcol = self._mask_column(bool_arr)
-        return WhereMask(self, device_col=table.expand_subgroups(basket_col, mcol))
+        mcol, temp = self._mask_column(bool_arr)
+        try:
+            out = table.expand_subgroups(basket_col, mcol)
+        finally:
+            if temp:
+                table.release_mask(mcol)
+        return WhereMask(self, device_col=out)
 
     def _mask_column(self, bool_arr):
-        """A device BOOL column holding ``bool_arr`` (lazy masks are materialised)."""
+        """(device BOOL column holding ``bool_arr``, temporary): lazy masks are materialised
+        and stay owned by their WhereMask; a host array goes to a scratch column the caller
+        releases after the query."""
         if isinstance(bool_arr, WhereMask):
-            return bool_arr.materialize()
+            return bool_arr.materialize(), False
         arr = np.ascontiguousarray(np.asarray(bool_arr, dtype=bool))
         if len(arr) != self._len:
             raise ValueError('bool_arr length %d != table length %d' % (len(arr), self._len))
         table = self._ensure_device([])
         name = table.scratch_mask()
         table.push(name, arr)
-        return name
+        return name, True
 
     # ---- calc
     def groupby(self, groupby_cols, agg_list, bool_arr=None, rootdir=None):
@@ -223,9 +241,14 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
             terms = bool_arr.terms  # fuse the predicate into the groupby scan
             needed += [t[0] for t in parse_terms(self._dtypes, terms)]
         table = self._ensure_device(needed)
+        temp = False
         if bool_arr is not None and terms is None:
-            mask = self._mask_column(bool_arr)
-        out, _ = table.groupby(groupby_cols, agg_list, where_terms=terms, mask=mask)
+            mask, temp = self._mask_column(bool_arr)
+        try:
+            out, _ = table.groupby(groupby_cols, agg_list, where_terms=terms, mask=mask)
+        finally:
+            if temp:
+                table.release_mask(mask)
         res = ResultTable(out, rootdir=rootdir)
         if rootdir:
             res.flush()
@@ -240,9 +263,14 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
             terms = bool_arr.terms
             needed += [t[0] for t in parse_terms(self._dtypes, terms)]
         table = self._ensure_device(needed)
+        temp = False
         if bool_arr is not None and terms is None:
-            mask = self._mask_column(bool_arr)
-        out = table.select_rows(column_list, where_terms=terms, mask=mask)
+            mask, temp = self._mask_column(bool_arr)
+        try:
+            out = table.select_rows(column_list, where_terms=terms, mask=mask)
+        finally:
+            if temp:
+                table.release_mask(mask)
         res = ResultTable(out, rootdir=rootdir)
         if rootdir:
             res.flush()

@@ -2,23 +2,26 @@
 
 The reference merges on the client: every shard's finalized table is appended and re-grouped
 with ``sum`` of every column ("we can only sum now", ``bqueryd/rpc.py:164-173``).  For shards
-co-located on one node this module does the same merge across GPU ranks:
+co-located on one node the same merge runs across GPU ranks:
 
-  1. local:    each rank sums its own shards' tables by key (GPU groupby-sum);
-  2. partition: rows are assigned to rank ``hash(key values) mod world`` (GPU kernel
-               ``bqg_hash_partition``: a pure function of the key values, identical on every
-               rank, so all partials of one key meet on one rank);
-  3. exchange: one ``all_to_all_single`` per column, raw bytes with per-rank split sizes
-               (``torch.distributed``: RCCL over xGMI on GPUs, gloo on CPU);
-  4. reduce:   each rank sums the rows it received by key (GPU groupby-sum);
-  5. gather:   the reduced partitions travel to rank 0 with the same byte all-to-all.
+  1. local:     each rank sums its own shards' tables by key (GPU groupby-sum);
+  2. partition: rows are assigned to rank ``hash(key values) mod world`` (``bqg_hash_partition``:
+                a pure function of the key values, identical on every rank, so all partials of
+                one key meet on one rank);
+  3. exchange:  row counts, then the rows, between every pair of ranks;
+  4. reduce:    each rank sums the rows it received by key;
+  5. gather:    the reduced partitions travel to rank 0.
 
-The protocol is written against a small backend interface (``partition`` / ``reduce``) so the
-CPU test suite can run it under gloo with the oracle as the backend; the product backend is
-``GpuBackend`` (libbqgpu), which has no CPU fallback.
+The product path is ``merge_partials_device`` / ``merge_group_device``: libbqgpu's ``bqg_merge``
+runs all five steps on device buffers with RCCL over xGMI (``RcclComm``: one process per GPU;
+``CommGroup``: a process owning several GPUs).  ``merge_partials`` restates the same protocol
+on host tables against a small backend interface (``partition`` / ``reduce``) and a byte
+exchange (``Exchange``: torch.distributed), so the CPU test suite can run it under gloo with the
+oracle as the backend; its GPU backend is ``GpuBackend`` (libbqgpu, no CPU fallback).
 """
 from __future__ import annotations
 
+import ctypes
 from collections import OrderedDict
 
 import numpy as np
@@ -60,38 +63,7 @@ class GpuBackend:
         finally:
             t.close()
 
-    def partition_device(self, table, groupby_cols, nparts):
-        """Device ShardTable -> ``nparts`` device ShardTables, rows split by the hash of their
-        key values (the same function on every rank)."""
-        import ctypes
-        from . import _lib as L
-        names = list(table.names)
-        col = table.add_column('__part__', np.uint32)
-        keys = np.array([table.slot(c) for c in groupby_cols], np.int32)
-        counts = np.zeros(nparts, np.int64)
-        self.device.check(L.lib().bqg_hash_partition(self.device.handle, table.handle, len(keys),
-                                                     keys.ctypes.data, nparts, col, counts.ctypes.data))
-        return [table.select_rows_table(names, where_terms=[('__part__', '==', p)]) for p in range(nparts)]
-
-    def empty_table(self, names, dtypes):
-        from .engine import ShardTable
-        return ShardTable(OrderedDict((n, np.zeros(0, dtypes[n])) for n in names), device=self.device)
-
-    def table_from_buffers(self, names, dtypes, bufs, nrows):
-        """A device ShardTable whose columns are copied (device to device) from ``bufs``
-        (name -> device address)."""
-        from .engine import ShardTable
-        t = ShardTable(OrderedDict(), device=self.device, nrows=nrows)
-        for n in names:
-            t.add_column(n, dtypes[n])
-            t.names.append(n)
-            if nrows:
-                t.push_device(n, bufs[n], nrows)
-        t.sync()
-        return t
-
     def partition(self, table, groupby_cols, nparts):
-        import ctypes
         from . import _lib as L
         from .engine import ShardTable
         t = ShardTable(table, device=self.device)
@@ -164,90 +136,117 @@ class Exchange:
         return out.cpu().numpy().view(dtype)
 
 
-class DeviceExchange(Exchange):
-    """Byte all-to-all of device-resident columns: RCCL over xGMI (``torch.distributed`` with
-    the nccl backend), no host copies.  Columns of ShardTables are packed into one torch
-    device buffer per column with device-to-device copies."""
-
-    def column_device(self, parts, name, dtype, recv_counts):
-        """parts[dst]: ShardTables on this GPU -> (device address, torch buffer) of this rank's
-        rows of column ``name`` from every source, concatenated in rank order."""
-        import torch
-        dtype = np.dtype(dtype)
-        in_split = [int(p.nrows) * dtype.itemsize for p in parts]
-        out_split = [int(c) * dtype.itemsize for c in recv_counts]
-        stream = torch.cuda.current_stream(self.device)
-        send = torch.empty(max(1, sum(in_split)), dtype=torch.uint8, device=self.device)
-        out = torch.empty(max(1, sum(out_split)), dtype=torch.uint8, device=self.device)
-        stream.synchronize()  # the fresh buffers are idle before another stream writes them
-        off = 0
-        for p, nb in zip(parts, in_split):
-            if nb:
-                p.read_device(name, send.data_ptr() + off)  # synchronous on libbqgpu's stream
-            off += nb
-        self.dist.all_to_all_single(out[:sum(out_split)], send[:sum(in_split)], out_split, in_split,
-                                    group=self.group)
-        stream.synchronize()  # received bytes are complete before libbqgpu reads them
-        return out.data_ptr(), out
-
-    def host_bytes(self, buf, nbytes):
-        """The first ``nbytes`` of a buffer returned by ``column_device``, in host memory."""
-        return buf[:nbytes].cpu().numpy()
+def new_unique_id():
+    """An RCCL unique id (``bqg_comm_unique_id``): created once, on rank 0, and handed to every
+    rank by the host layer over any side channel (bytes)."""
+    from . import _lib as L
+    buf = ctypes.create_string_buffer(L.UNIQUE_ID_BYTES)
+    L.check(L.lib().bqg_comm_unique_id(buf), None)
+    return buf.raw
 
 
-def merge_partials_device(local_tables, groupby_cols, agg_list, dtypes, backend, exchange, reduced=False):
-    """``merge_partials`` with every step in HBM: ``local_tables`` are this rank's finalized
-    shard tables as device ShardTables (``ShardTable.groupby_table``), the reduce, partition,
-    all-to-all and gather run on device buffers, and only the merged table comes back to host
-    memory (rank 0; None elsewhere).  ``reduced``: ``local_tables`` is ONE table whose keys are
-    already unique (a co-located groupby, ``ColocatedShards``), so the local re-group is skipped."""
+class RcclComm:
+    """This process's rank of an RCCL communicator over the node's GPUs (``bqg_comm_init``
+    on a libbqgpu context: one process per GPU).  The merge's exchange runs inside libbqgpu on
+    device buffers; torch is not involved."""
+
+    def __init__(self, device, rank=0, nranks=1, unique_id=None):
+        from . import _lib as L
+        if unique_id is None:
+            if nranks != 1:
+                raise ValueError('every rank needs the same unique id (new_unique_id on rank 0)')
+            unique_id = new_unique_id()
+        self.device = device
+        self.rank, self.world = int(rank), int(nranks)
+        buf = ctypes.create_string_buffer(bytes(unique_id), L.UNIQUE_ID_BYTES)
+        device.check(L.lib().bqg_comm_init(device.handle, self.rank, self.world, buf))
+
+    def close(self):
+        from . import _lib as L
+        if self.device is not None and self.device.handle:
+            L.lib().bqg_comm_destroy(self.device.handle)
+        self.device = None
+
+
+class CommGroup:
+    """Every rank of a communicator in THIS process, one libbqgpu context (Device) per rank:
+    ``transport='rccl'`` -- RCCL over xGMI, one GPU per rank (``bqg_comm_init_all``, a process
+    owning the node's GPUs); ``'local'`` -- device-to-device copies (``bqg_comm_init_local``;
+    contexts may share one GPU)."""
+
+    def __init__(self, devices, transport='rccl'):
+        from . import _lib as L
+        self.devices = list(devices)
+        self.world = len(self.devices)
+        arr = (ctypes.c_void_p * self.world)(*[d.handle.value for d in self.devices])
+        fn = L.lib().bqg_comm_init_all if transport == 'rccl' else L.lib().bqg_comm_init_local
+        self.devices[0].check(fn(self.world, arr))
+        self.transport = transport
+
+    def close(self):
+        from . import _lib as L
+        for d in self.devices:
+            if d.handle:
+                L.lib().bqg_comm_destroy(d.handle)
+        self.devices = []
+
+
+def _schema(groupby_cols, agg_list, dtypes):
+    from . import _lib as L
     names = list(groupby_cols) + [x[2] for x in agg_list]
-    local_tables = [t for t in local_tables if t is not None and t.nrows]
-    reduced = reduced and len(local_tables) == 1
-    if exchange.world == 1:
-        if not local_tables:
-            return OrderedDict((n, np.zeros(0, dtypes[n])) for n in names)
-        if reduced:
-            return OrderedDict((n, local_tables[0].read(n)) for n in names)
-        return backend.reduce(local_tables, groupby_cols, agg_list)
-    if local_tables:
-        local = local_tables[0] if reduced else backend.reduce(local_tables, groupby_cols, agg_list, on_device=True)
-        try:
-            parts = backend.partition_device(local, groupby_cols, exchange.world)
-        finally:
-            if not reduced:
-                local.close()
-    else:
-        parts = [backend.empty_table(names, dtypes) for _ in range(exchange.world)]
-    recv_counts = exchange.counts([p.nrows for p in parts])
-    n_recv = int(np.sum(recv_counts))
-    keep = []
-    bufs = OrderedDict()
-    for n in names:
-        ptr, buf = exchange.column_device(parts, n, dtypes[n], recv_counts)
-        bufs[n] = ptr
-        keep.append(buf)
-    for p in parts:
-        p.close()
-    mine = backend.table_from_buffers(names, dtypes, bufs, n_recv)
-    del keep[:]
-    if n_recv:
-        reduced = backend.reduce([mine], groupby_cols, agg_list, on_device=True)
-        mine.close()
-        mine = reduced
-    # gather the disjoint reduced partitions to rank 0
-    empty = backend.empty_table(names, dtypes)
-    to_root = [mine.nrows if dst == 0 else 0 for dst in range(exchange.world)]
-    recv = exchange.counts(to_root)
-    gathered = OrderedDict()
-    for n in names:
-        ptr, buf = exchange.column_device([mine if dst == 0 else empty for dst in range(exchange.world)], n,
-                                          dtypes[n], recv)
-        nbytes = int(np.sum(recv)) * np.dtype(dtypes[n]).itemsize
-        gathered[n] = exchange.host_bytes(buf, nbytes).view(np.dtype(dtypes[n])) if exchange.rank == 0 else None
-    mine.close()
-    empty.close()
-    return gathered if exchange.rank == 0 else None
+    codes = (ctypes.c_int32 * len(names))(*[L.DTYPE_CODE[np.dtype(dtypes[n])] for n in names])
+    return names, codes
+
+
+def _merged_to_host(handle, names, dtypes, device):
+    from .engine import ShardTable
+    t = ShardTable._wrap(handle, names, [dtypes[n] for n in names], device)
+    try:
+        return t.to_host(names)
+    finally:
+        t.close()
+
+
+def merge_partials_device(local_tables, groupby_cols, agg_list, dtypes, comm, reduced=False):
+    """The client's ``aggregate=True`` merge (rpc.py:164-173) of every rank's shard results,
+    in HBM over RCCL (``bqg_merge``): ``local_tables`` are this rank's finalized shard tables
+    as device ShardTables (``ShardTable.groupby_table``), keys first.  Returns the merged table
+    (host columns) on rank 0, None elsewhere.  ``reduced``: ``local_tables`` is ONE table with
+    unique keys (``ColocatedShards`` one-pass groupby): the local re-group is skipped.  Rows
+    come grouped by key hash; the reference's order is the client's file-system glob order
+    (rpc.py:151), so compare after sorting by the keys."""
+    from . import _lib as L
+    names, codes = _schema(groupby_cols, agg_list, dtypes)
+    tabs = [t for t in local_tables if t is not None]
+    arr = (ctypes.c_void_p * max(1, len(tabs)))(*[t.handle.value for t in tabs])
+    out = ctypes.c_void_p()
+    dev = comm.device
+    dev.check(L.lib().bqg_merge(dev.handle, len(tabs), arr, len(groupby_cols), len(names), codes,
+                                1 if reduced else 0, ctypes.byref(out)))
+    if comm.rank != 0:
+        return None
+    return _merged_to_host(out, names, dtypes, dev)
+
+
+def merge_group_device(tables_per_rank, groupby_cols, agg_list, dtypes, group, reduced=False):
+    """``merge_partials_device`` for every rank of a ``CommGroup`` from one host thread
+    (``bqg_merge_group``): ``tables_per_rank[i]`` are rank i's device tables (on
+    ``group.devices[i]``).  Returns the merged table (host columns)."""
+    from . import _lib as L
+    names, codes = _schema(groupby_cols, agg_list, dtypes)
+    flat, counts = [], []
+    for tabs in tables_per_rank:
+        tabs = [t for t in tabs if t is not None]
+        counts.append(len(tabs))
+        flat += [t.handle.value for t in tabs]
+    w = group.world
+    ctxs = (ctypes.c_void_p * w)(*[d.handle.value for d in group.devices])
+    ntab = (ctypes.c_int32 * w)(*counts)
+    arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
+    outs = (ctypes.c_void_p * w)()
+    group.devices[0].check(L.lib().bqg_merge_group(w, ctxs, ntab, arr, len(groupby_cols), len(names), codes,
+                                                   1 if reduced else 0, outs))
+    return _merged_to_host(ctypes.c_void_p(outs[0]), names, dtypes, group.devices[0])
 
 
 def merge_partials(local_tables, groupby_cols, agg_list, dtypes, backend, exchange):
@@ -310,15 +309,25 @@ class ColocatedShards:
         self.tables = [t for t in tables if t is not None]
         self._union = None
         self._union_cols = ()
+        self._union_key = None
 
     def union(self, cols):
+        """The member shards' columns ``cols`` row-concatenated in HBM, kept while the members
+        are unchanged (their identity and write versions) and extended, never narrowed: a query
+        over new columns rebuilds the union with the old and new columns together."""
         from .engine import ShardTable
-        cols = tuple(cols)
-        if self._union is None or not set(cols) <= set(self._union_cols):
-            if self._union is not None:
-                self._union.close()
-            self._union = ShardTable.from_parts(self.tables, list(cols), device=self.tables[0].dev)
-            self._union_cols = cols
+        key = tuple((id(t), t.version) for t in self.tables)
+        if self._union is not None and key == self._union_key and set(cols) <= set(self._union_cols):
+            return self._union
+        if key == self._union_key:
+            cols = tuple(dict.fromkeys(tuple(self._union_cols) + tuple(cols)))
+        else:
+            cols = tuple(cols)
+        if self._union is not None:
+            self._union.close()
+        self._union = ShardTable.from_parts(self.tables, list(cols), device=self.tables[0].dev)
+        self._union_cols = cols
+        self._union_key = key
         return self._union
 
     def close(self):
@@ -338,11 +347,11 @@ class ColocatedShards:
             return [u.groupby_table(groupby_cols, agg_list, where_terms=where_terms)], True
         return [t.groupby_table(groupby_cols, agg_list, where_terms=where_terms) for t in self.tables], False
 
-    def groupby_merged(self, groupby_cols, agg_list, dtypes, backend, exchange, where_terms=None):
+    def groupby_merged(self, groupby_cols, agg_list, dtypes, comm, where_terms=None):
         """The ``aggregate=True`` answer over every rank's shards (rank 0; None elsewhere)."""
         per, reduced = self.groupby_tables(groupby_cols, agg_list, where_terms)
         try:
-            return merge_partials_device(per, groupby_cols, agg_list, dtypes, backend, exchange, reduced=reduced)
+            return merge_partials_device(per, groupby_cols, agg_list, dtypes, comm, reduced=reduced)
         finally:
             for p in per:
                 p.close()

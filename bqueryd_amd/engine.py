@@ -60,6 +60,21 @@ class Device:
 _devices = {}
 
 
+class _Unfreezable(Exception):
+    pass
+
+
+def _freeze(x):
+    """Hashable, type-exact image of a query argument (plan-cache key)."""
+    if isinstance(x, (list, tuple)):
+        return (type(x).__name__,) + tuple(_freeze(v) for v in x)
+    if isinstance(x, (set, frozenset)):
+        return ('set', frozenset(_freeze(v) for v in x))
+    if isinstance(x, (str, bytes, bool, int, float, type(None), np.generic)):
+        return (type(x), x)
+    raise _Unfreezable()
+
+
 def device_count():
     n = ctypes.c_int()
     L.check(L.lib().bqg_device_count(ctypes.byref(n)), None)
@@ -212,13 +227,23 @@ class ShardTable:
             raise KeyError(str(name))
         return self._slot[name]
 
+    @property
+    def version(self):
+        """Bumped by every write into the table's columns (caches over its data key on it)."""
+        return self.__dict__.get('_version', 0)
+
+    def _touch(self):
+        self.__dict__['_version'] = self.version + 1
+
     def push(self, col, array, row_offset=0):
+        self._touch()
         a = np.ascontiguousarray(array)
         self.dev.check(self._lib.bqg_push_chunk(self.handle, self.slot(col), a.ctypes.data,
                                                 len(a), int(row_offset)))
 
     def push_device(self, col, dev_ptr, nrows, row_offset=0):
         """Device-to-device copy of ``nrows`` elements at ``dev_ptr`` into column ``col``."""
+        self._touch()
         self.dev.check(self._lib.bqg_push_chunk(self.handle, self.slot(col), ctypes.c_void_p(int(dev_ptr)),
                                                 int(nrows), int(row_offset)))
 
@@ -236,6 +261,7 @@ class ShardTable:
     def load_carray(self, col, carray_dir, chunklen, nthreads=None):
         """Decode a bcolz carray directory straight into device column ``col`` (host decode
         threads, pinned double-buffered DMA; statistics follow at the next ``sync``)."""
+        self._touch()
         if not nthreads:
             nthreads = int(os.environ.get('BQGPU_INGEST_THREADS', '0')) or min(16, len(os.sched_getaffinity(0)))
         self.dev.check(self._lib.bqg_table_load_carray(self.handle, self.slot(col), os.fsencode(carray_dir),
@@ -254,11 +280,23 @@ class ShardTable:
         return s.value
 
     def scratch_mask(self):
-        """A fresh device BOOL column for masks (reused across calls)."""
+        """A device BOOL column for a mask, taken from the table's free list when one was
+        released (``release_mask``), else added: a resident shard queried in a loop keeps a
+        constant number of mask columns."""
+        free = self.__dict__.setdefault('_free_masks', [])
+        if free:
+            return free.pop()
         name = '__mask_%d__' % len(self._scratch)
-        s = self.add_column(name, np.bool_)
+        self.add_column(name, np.bool_)
         self._scratch.append(name)
         return name
+
+    def release_mask(self, name):
+        """Return a ``scratch_mask`` column to the free list (its contents are dead)."""
+        if name in self._scratch and getattr(self, 'handle', None):
+            free = self.__dict__.setdefault('_free_masks', [])
+            if name not in free:
+                free.append(name)
 
     def read(self, col):
         s = self.slot(col)
@@ -341,10 +379,14 @@ class ShardTable:
         """(output names, parsed aggregations, C query struct) of a groupby, built once per
         distinct query text and table (the struct points into arrays the plan keeps alive):
         repeated queries on a resident shard skip the Python-side parsing."""
-        # numpy arrays print abbreviated: queries with array-valued terms are not cached
-        cacheable = all(not any(isinstance(x, np.ndarray) for x in t)
-                        for t in (where_terms or []) if isinstance(t, (list, tuple)))
-        key = (repr(groupby_cols), repr(agg_list), repr(where_terms), mask) if cacheable else None
+        # the key is the query's values with their types (np.float32(0.1) and 0.1 normalise to
+        # different bounds); anything but plain lists / tuples / sets of scalars and strings
+        # (arrays, generators, other iterables) is not cached
+        try:
+            key = (_freeze(groupby_cols), _freeze(agg_list), _freeze(where_terms or []), mask)
+            cacheable = True
+        except _Unfreezable:
+            key, cacheable = None, False
         plans = self.__dict__.setdefault('_plans', OrderedDict())
         hit = plans.get(key) if cacheable else None
         if hit is not None:

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BQG_ABI_VERSION 2
+#define BQG_ABI_VERSION 3
 
 /* error codes */
 #define BQG_OK 0
@@ -168,6 +168,8 @@ int bqg_table_stats(bqg_table* t, int32_t col, int64_t* imin, int64_t* imax, dou
 /* Copy rows of a device column back to host memory (or into device memory). */
 int bqg_table_read(bqg_table* t, int32_t col, void* host, int64_t nrows, int64_t row_offset);
 int bqg_table_nrows(bqg_table* t, int64_t* nrows);
+int bqg_table_ncols(bqg_table* t, int32_t* ncols);
+int bqg_table_dtype(bqg_table* t, int32_t col, int32_t* dtype);
 
 /* ---------------- calc path ---------------- */
 /* where_terms: AND of the terms -> BOOL column `out_mask_col` (device); *n_pass receives the
@@ -198,6 +200,40 @@ int bqg_result_view_get(bqg_result* r, bqg_result_view* out);
 int bqg_hash_partition(bqg_ctx* ctx, bqg_table* t, int32_t n_keys, const int32_t* key_cols,
                        int32_t nparts, int32_t out_col, int64_t* counts);
 int bqg_result_free(bqg_result* r);
+
+/* ---------------- multi-GPU: RCCL over xGMI ----------------
+ * The aggregate=True merge of co-located shards: the client's re-group of every shard's
+ * finalized table with `sum` of every column (rpc.py:164-173), run across the node's GPUs on
+ * device buffers.  One communicator per context; librccl is loaded on first use.
+ *   bqg_comm_unique_id   ncclGetUniqueId: called once (rank 0); the host layer hands the
+ *                        BQG_UNIQUE_ID_BYTES bytes to every rank (any side channel)
+ *   bqg_comm_init        one rank per process (ncclCommInitRank on the context's GPU)
+ *   bqg_comm_init_all    every rank in this process: one context per GPU (ncclCommInitAll)
+ *   bqg_comm_init_local  every rank in this process, exchanging by device copies instead of
+ *                        RCCL (contexts may share a GPU: the exchange logic on one GPU)
+ *   bqg_merge            collective: every rank calls it with its partial tables (columns:
+ *                        n_keys key columns, then the finalized aggregations, dtypes as
+ *                        given); the merged table (sum of every non-key column by key) is
+ *                        returned on rank 0 as a new device table, NULL elsewhere.
+ *                        `reduced`: this rank's one table already has unique keys (a
+ *                        co-located one-pass groupby), so the local re-group is skipped.
+ *                        Rows of the merged table come grouped by key hash, not in the
+ *                        client's first-appearance order (which is file-system order in the
+ *                        reference, rpc.py:151); compare after sorting by the keys.
+ *   bqg_merge_group      the same for n_local ranks driven from one host thread (a process
+ *                        owning several GPUs, after bqg_comm_init_all); n_tables[i] tables
+ *                        of rank i follow each other in `tables`; out[i] per rank. */
+#define BQG_UNIQUE_ID_BYTES 128
+int bqg_comm_unique_id(void* out);
+int bqg_comm_init(bqg_ctx* ctx, int32_t rank, int32_t nranks, const void* unique_id);
+int bqg_comm_init_all(int32_t n, bqg_ctx* const* ctxs);
+int bqg_comm_init_local(int32_t n, bqg_ctx* const* ctxs);
+int bqg_comm_destroy(bqg_ctx* ctx);
+int bqg_comm_info(bqg_ctx* ctx, int32_t* rank, int32_t* nranks);
+int bqg_merge(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int32_t n_keys, int32_t n_cols,
+              const int32_t* dtypes, int32_t reduced, bqg_table** out);
+int bqg_merge_group(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,
+                    int32_t n_keys, int32_t n_cols, const int32_t* dtypes, int32_t reduced, bqg_table** out);
 
 #ifdef __cplusplus
 }

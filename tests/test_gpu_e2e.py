@@ -108,6 +108,27 @@ def test_worker_factorization_check_and_errors(tmp_path):
         calc.handle_work(_calc_msg('s.bcolzs', ['nope'], [['fare_amount', 'sum', 'f']], []))
 
 
+def test_worker_mask_columns_stay_flat(tmp_path):
+    """Repeated filtered + basket-expanded queries on one resident shard reuse the shard's
+    scratch mask columns (no HBM growth per query, plan cache kept)."""
+    n = 20_000
+    cols = synth.taxi_shard(n, config_id=2, columns=('payment_type', 'passenger_count', 'fare_amount'))
+    cols['basket'] = (np.arange(n) // 7).astype(np.int32)
+    root = os.path.join(str(tmp_path), 's.bcolzs')
+    bcolz_io.write_ctable(root, cols)
+    calc = CalcPath(str(tmp_path))
+    where = [('passenger_count', '>=', 2)]
+    ref = bo.handle_work(cols, ['payment_type'], [['fare_amount', 'sum', 'f']], where, expand_filter_column='basket')
+    scratch = []
+    for _ in range(6):
+        msg = calc.handle_work(_calc_msg('s.bcolzs', ['payment_type'], [['fare_amount', 'sum', 'f']], where,
+                                         expand_filter_column='basket'))
+        got = rpc.read_shard_results(rpc.tar_of_tars({'s.bcolzs': msg['data']}))[0]
+        assert_tables_equal(got, ref, exact_float_sums=True)
+        scratch.append(len(calc.cache.open(root)._table._scratch))
+    assert scratch[-1] == scratch[0] <= 2, scratch
+
+
 def test_c2_full_size_parity(oracle_c):
     """BASELINE configs[1] at full size (100 M rows) against the C restatement."""
     cfg = synth.CONFIGS['c2']

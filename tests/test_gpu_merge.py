@@ -1,6 +1,7 @@
-"""aggregate=True merge of co-located shard results on one GPU (bqueryd_amd/dist.py): the
-device reduce of the row-concatenated finalized tables must equal the reference client merge
-(rpc.py:164-173), including its first-appearance group order."""
+"""aggregate=True merge of co-located shard results (bqueryd_amd/dist.py, libbqgpu bqg_merge):
+the reduce of the row-concatenated finalized tables must equal the reference client merge
+(rpc.py:164-173) -- in its first-appearance group order on one rank, after sorting by the keys
+across ranks (the client's own order is file-system glob order, rpc.py:151)."""
 from collections import OrderedDict
 
 import numpy as np
@@ -62,21 +63,110 @@ def _shards(n_shards, rows, mod):
 AGGS_SC = [['fare_amount', 'sum', 'fare_sum'], ['fare_amount', 'count', 'n']]
 
 
-def test_device_resident_single_rank_merge():
-    """Per-shard results kept in HBM (groupby_table), concatenated device to device, summed:
-    the reference client merge, in its group order."""
-    shards = _shards(5, 120_000, 30_000)
+def _device_results(shards, dev=None, aggs=AGGS_SC):
     per = []
     for s in shards:
-        t = ShardTable(s)
-        per.append(t.groupby_table(KEYS, AGGS_SC))
+        t = ShardTable(s, device=dev)
+        per.append(t.groupby_table(KEYS, aggs))
         t.close()
-    dtypes = OrderedDict((k, per[0].dtypes[k]) for k in per[0].names)
-    merged = bdist.merge_partials_device(per, KEYS, AGGS_SC, dtypes, bdist.GpuBackend(), bdist.LocalExchange())
-    for p in per:
-        p.close()
+    return per
+
+
+def _dtypes(aggs=AGGS_SC):
+    d = OrderedDict([('pickup_location', np.dtype(np.int32)), ('vendor_id', np.dtype(np.int32))])
+    for a in aggs:
+        d[a[2]] = np.dtype(np.float64) if a[1] in ('sum', 'mean', 'std') else np.dtype(np.int64)
+    return d
+
+
+def test_rccl_merge_world_one():
+    """bqg_merge over a one-rank RCCL communicator (bqg_comm_init): partition, RCCL
+    all-gather of the row counts, RCCL send/recv of the rows, reduce and gather all run; with
+    one rank the result keeps the client's first-appearance group order (rpc.py:164-173)."""
+    from bqueryd_amd.engine import get_device
+    shards = _shards(5, 120_000, 30_000)
+    per = _device_results(shards)
+    comm = bdist.RcclComm(get_device())
+    try:
+        merged = bdist.merge_partials_device(per, KEYS, AGGS_SC, _dtypes(), comm)
+        again = bdist.merge_partials_device(per, KEYS, AGGS_SC, _dtypes(), comm)  # buffers reused
+        empty = bdist.merge_partials_device([], KEYS, AGGS_SC, _dtypes(), comm)
+    finally:
+        comm.close()
+        for p in per:
+            p.close()
     ref = bo.client_merge([bo.handle_work(s, KEYS, AGGS_SC, []) for s in shards], KEYS, AGGS_SC, aggregate=True)
     assert_tables_equal(merged, ref)
+    assert_tables_equal(again, ref)
+    assert all(len(v) == 0 for v in empty.values())
+
+
+def test_rccl_comm_init_all_one_gpu():
+    """bqg_comm_init_all (a process owning the node's GPUs) with the one GPU of this box."""
+    from bqueryd_amd.engine import Device
+    dev = Device(0)
+    shards = _shards(4, 60_000, 8_000)
+    per = _device_results(shards, dev)
+    group = bdist.CommGroup([dev], transport='rccl')
+    try:
+        merged = bdist.merge_group_device([per], KEYS, AGGS_SC, _dtypes(), group)
+    finally:
+        group.close()
+        for p in per:
+            p.close()
+    ref = bo.client_merge([bo.handle_work(s, KEYS, AGGS_SC, []) for s in shards], KEYS, AGGS_SC, aggregate=True)
+    assert_tables_equal(merged, ref)
+
+
+@pytest.mark.parametrize('world, nshards', [(2, 6), (3, 7), (4, 3)])
+def test_merge_in_process_ranks(world, nshards):
+    """World 2-4 on one GPU: every rank a libbqgpu context, the exchange by device copies
+    (bqg_comm_init_local) -- the same partition / pack / reduce / gather code as over RCCL,
+    including a rank that holds no shard (world 4, 3 shards)."""
+    from bqueryd_amd.engine import Device
+    devs = [Device(0) for _ in range(world)]
+    shards = _shards(nshards, 50_000, 9_000)
+    per = [_device_results([s for i, s in enumerate(shards) if i % world == r], devs[r]) for r in range(world)]
+    group = bdist.CommGroup(devs, transport='local')
+    try:
+        merged = bdist.merge_group_device(per, KEYS, AGGS_SC, _dtypes(), group)
+    finally:
+        group.close()
+        for tabs in per:
+            for p in tabs:
+                p.close()
+    ref = bo.client_merge([bo.handle_work(s, KEYS, AGGS_SC, []) for s in shards], KEYS, AGGS_SC, aggregate=True)
+    assert_tables_equal(sort_by_keys(merged, KEYS), sort_by_keys(ref, KEYS))
+
+
+def test_colocated_in_process_ranks():
+    """Co-located one-pass groupby per rank (reduced=True) merged across 3 in-process ranks."""
+    from bqueryd_amd.engine import Device
+    world = 3
+    devs = [Device(0) for _ in range(world)]
+    shards = _shards(7, 40_000, 6_000)
+    tables = [[ShardTable(s, device=devs[r]) for i, s in enumerate(shards) if i % world == r] for r in range(world)]
+    colos = [bdist.ColocatedShards(t) for t in tables]
+    per = []
+    for c in colos:
+        p, reduced = c.groupby_tables(KEYS, AGGS_SC)
+        assert reduced
+        per.append(p)
+    group = bdist.CommGroup(devs, transport='local')
+    try:
+        merged = bdist.merge_group_device(per, KEYS, AGGS_SC, _dtypes(), group, reduced=True)
+    finally:
+        group.close()
+        for tabs in per:
+            for p in tabs:
+                p.close()
+        for c in colos:
+            c.close()
+        for ts in tables:
+            for t in ts:
+                t.close()
+    ref = bo.client_merge([bo.handle_work(s, KEYS, AGGS_SC, []) for s in shards], KEYS, AGGS_SC, aggregate=True)
+    assert_tables_equal(sort_by_keys(merged, KEYS), sort_by_keys(ref, KEYS))
 
 
 def test_groupby_table_and_select_rows_table_match_host_results():
@@ -98,72 +188,6 @@ def test_groupby_table_and_select_rows_table_match_host_results():
         t.close()
 
 
-class _ThreadExchange:
-    """World of ``world`` ranks as threads of one process on one GPU: the collectives are
-    host copies between threads (test harness for the device merge protocol; the product
-    exchange is DeviceExchange over RCCL)."""
-
-    def __init__(self, rank, world, shared):
-        self.rank, self.world, self.sh = rank, world, shared
-
-    def counts(self, send_counts):
-        self.sh['counts'][self.rank] = np.asarray(send_counts, np.int64)
-        self.sh['barrier'].wait()
-        r = np.array([self.sh['counts'][src][self.rank] for src in range(self.world)], np.int64)
-        self.sh['barrier'].wait()
-        return r
-
-    def column_device(self, parts, name, dtype, recv_counts):
-        self.sh['cols'][self.rank] = [p.read(name) if p.nrows else np.zeros(0, dtype) for p in parts]
-        self.sh['barrier'].wait()
-        mine = np.concatenate([self.sh['cols'][src][self.rank] for src in range(self.world)]).astype(dtype)
-        self.sh['barrier'].wait()
-        # the receive buffer: a device column (torch is not imported in this process)
-        buf = ShardTable(OrderedDict(x=np.concatenate([mine.view(np.uint8), np.zeros(1, np.uint8)])),
-                         device=parts[0].dev)
-        return buf.column_ptr('x'), buf
-
-    def host_bytes(self, buf, nbytes):
-        return buf.read('x')[:nbytes]
-
-
-def test_device_merge_protocol_two_ranks_as_threads():
-    import threading
-    from bqueryd_amd.engine import Device
-    shards = _shards(6, 50_000, 9_000)
-    world = 2
-    shared = {'barrier': threading.Barrier(world), 'counts': [None] * world, 'cols': [None] * world}
-    results, errors = [None] * world, []
-
-    def rank_main(rank):
-        try:
-            dev = Device(0)
-            per = []
-            for i, s in enumerate(shards):
-                if i % world == rank:
-                    t = ShardTable(s, device=dev)
-                    per.append(t.groupby_table(KEYS, AGGS_SC))
-                    t.close()
-            dtypes = OrderedDict((k, per[0].dtypes[k]) for k in per[0].names)
-            results[rank] = bdist.merge_partials_device(per, KEYS, AGGS_SC, dtypes, bdist.GpuBackend(dev),
-                                                        _ThreadExchange(rank, world, shared))
-            for p in per:
-                p.close()
-        except Exception as e:  # noqa: BLE001 -- re-raised in the main thread
-            errors.append(e)
-            shared['barrier'].abort()
-
-    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
-    for th in threads:
-        th.start()
-    for th in threads:
-        th.join(timeout=120)
-    assert not errors, errors
-    assert results[1] is None
-    ref = bo.client_merge([bo.handle_work(s, KEYS, AGGS_SC, []) for s in shards], KEYS, AGGS_SC, aggregate=True)
-    assert_tables_equal(sort_by_keys(results[0], KEYS), sort_by_keys(ref, KEYS))
-
-
 @pytest.mark.parametrize('aggs, where', [
     (AGGS_SC, []),
     (AGGS_SC, [('vendor_id', '==', 2)]),
@@ -181,44 +205,11 @@ def test_colocated_shards_single_rank(aggs, where):
     dtypes = OrderedDict((k, per[0].dtypes[k]) for k in per[0].names)
     for p in per:
         p.close()
-    merged = colo.groupby_merged(KEYS, aggs, dtypes, bdist.GpuBackend(), bdist.LocalExchange(), where_terms=where)
+    comm = bdist.RcclComm(tables[0].dev)
+    merged = colo.groupby_merged(KEYS, aggs, dtypes, comm, where_terms=where)
+    comm.close()
     colo.close()
     for t in tables:
         t.close()
     ref = bo.client_merge([bo.handle_work(s, KEYS, aggs, where) for s in shards], KEYS, aggs, aggregate=True)
     assert_tables_equal(merged, ref)
-
-
-def test_colocated_shards_two_ranks_as_threads():
-    import threading
-    from bqueryd_amd.engine import Device
-    shards = _shards(6, 50_000, 9_000)
-    world = 2
-    shared = {'barrier': threading.Barrier(world), 'counts': [None] * world, 'cols': [None] * world}
-    results, errors = [None] * world, []
-    dtypes = OrderedDict([('pickup_location', np.dtype(np.int32)), ('vendor_id', np.dtype(np.int32)),
-                          ('fare_sum', np.dtype(np.float64)), ('n', np.dtype(np.int64))])
-
-    def rank_main(rank):
-        try:
-            dev = Device(0)
-            tables = [ShardTable(s, device=dev) for i, s in enumerate(shards) if i % world == rank]
-            colo = bdist.ColocatedShards(tables)
-            results[rank] = colo.groupby_merged(KEYS, AGGS_SC, dtypes, bdist.GpuBackend(dev),
-                                                _ThreadExchange(rank, world, shared))
-            colo.close()
-            for t in tables:
-                t.close()
-        except Exception as e:  # noqa: BLE001 -- re-raised in the main thread
-            errors.append(e)
-            shared['barrier'].abort()
-
-    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
-    for th in threads:
-        th.start()
-    for th in threads:
-        th.join(timeout=120)
-    assert not errors, errors
-    assert results[1] is None
-    ref = bo.client_merge([bo.handle_work(s, KEYS, AGGS_SC, []) for s in shards], KEYS, AGGS_SC, aggregate=True)
-    assert_tables_equal(sort_by_keys(results[0], KEYS), sort_by_keys(ref, KEYS))

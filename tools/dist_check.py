@@ -1,15 +1,16 @@
 #!/usr/bin/env python3
 """GPU merge check, launched under torch.distributed.run (one process per GPU).
 
-Imports torch first (so libbqgpu binds the HIP runtime torch loaded), initialises the nccl
-(RCCL) process group, runs per-shard groupbys on the GPU, merges them with
-bqueryd_amd.dist.merge_partials over RCCL, and on rank 0 checks the result against the
-oracle's client merge (rpc.py:164-173).  Exit code 0 = parity.
+torch.distributed (gloo, CPU) only hands rank 0's RCCL unique id to the other ranks and
+provides the final barrier; the merge itself is libbqgpu's bqg_merge over RCCL on device
+buffers (bqueryd_amd.dist.RcclComm / merge_partials_device).  Each rank runs per-shard
+groupbys into HBM tables and, separately, one co-located pass over its shards
+(ColocatedShards); rank 0 checks both merges against the oracle's client merge
+(rpc.py:164-173).  Exit code 0 = parity.
 """
 import os
 import sys
 
-import torch  # noqa: F401  (must precede libbqgpu: one HIP runtime per process)
 import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -22,39 +23,53 @@ from bqueryd_amd import synth  # noqa: E402
 from bqueryd_amd.engine import Device, ShardTable  # noqa: E402
 
 
+def _check(merged, ref):
+    order_g = np.lexsort((merged['vendor_id'], merged['pickup_location']))
+    order_r = np.lexsort((ref['vendor_id'], ref['pickup_location']))
+    ok = len(merged['n']) == len(ref['n'])
+    for c in ref:
+        if not ok:
+            break
+        g, r = merged[c][order_g], ref[c][order_r]
+        same = np.array_equal(g, r) if r.dtype.kind != 'f' else np.allclose(g, r, rtol=1e-12, atol=0)
+        ok &= bool(same) and g.dtype == r.dtype
+    return ok
+
+
 def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
-    dist.init_process_group('nccl')
+    dist.init_process_group('gloo')
     rank, world = dist.get_rank(), dist.get_world_size()
+    uid = [bdist.new_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
     dev = Device(local)
+    comm = bdist.RcclComm(dev, rank, world, uid[0])
     keys = ['pickup_location', 'vendor_id']
     aggs = [['fare_amount', 'sum', 'fare_sum'], ['fare_amount', 'count', 'n']]
     nshards = 4 * world
     shards = [synth.taxi_shard(200_000, config_id=5, n_shards=nshards, shard=i,
                                columns=('pickup_location', 'vendor_id', 'fare_amount')) for i in range(nshards)]
-    mine = []
-    for i in range(rank, nshards, world):
-        t = ShardTable(shards[i], device=dev)
-        out, _ = t.groupby(keys, aggs)
-        t.close()
-        mine.append(out)
+    tables = [ShardTable(shards[i], device=dev) for i in range(rank, nshards, world)]
+    per = [t.groupby_table(keys, aggs) for t in tables]
     dtypes = {'pickup_location': np.dtype(np.int32), 'vendor_id': np.dtype(np.int32),
               'fare_sum': np.dtype(np.float64), 'n': np.dtype(np.int64)}
-    merged = bdist.merge_partials(mine, keys, aggs, dtypes, bdist.GpuBackend(dev),
-                                  bdist.Exchange(dist, device=torch.device('cuda', local)))
+    merged = bdist.merge_partials_device(per, keys, aggs, dtypes, comm)
+    colo = bdist.ColocatedShards(tables)
+    merged_colo = colo.groupby_merged(keys, aggs, dtypes, comm)
     ok = True
     if rank == 0:
         from oracle import bquery_oracle as bo
-        per = [bo.handle_work(s, keys, aggs, []) for s in shards]
-        ref = bo.client_merge(per, keys, aggs, aggregate=True)
-        order_g = np.lexsort((merged['vendor_id'], merged['pickup_location']))
-        order_r = np.lexsort((ref['vendor_id'], ref['pickup_location']))
-        for c in ref:
-            g, r = merged[c][order_g], ref[c][order_r]
-            same = np.array_equal(g, r) if r.dtype.kind != 'f' else np.allclose(g, r, rtol=1e-12, atol=0)
-            ok &= bool(same) and g.dtype == r.dtype
+        ref = bo.client_merge([bo.handle_work(s, keys, aggs, []) for s in shards], keys, aggs, aggregate=True)
+        ok = _check(merged, ref) and _check(merged_colo, ref)
         print('dist_check world=%d groups=%d ok=%s' % (world, len(ref['n']), ok), flush=True)
+    else:
+        ok = merged is None and merged_colo is None
+    for p in per:
+        p.close()
+    colo.close()
+    for t in tables:
+        t.close()
+    comm.close()
     dist.barrier()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)
