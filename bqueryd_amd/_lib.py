@@ -115,6 +115,7 @@ _PROTOS = {
     'bqg_result_view_get': ([_P, ctypes.POINTER(ResultView)], ctypes.c_int),
     'bqg_hash_partition': ([_P, _P, _I32, _P, _I32, _I32, _P], ctypes.c_int),
     'bqg_result_free': ([_P], ctypes.c_int),
+    'bqg_factorize': ([_P, _P, _I32, _P, _P, _I64, ctypes.POINTER(_I64)], ctypes.c_int),
 }
 
 _lib = None

@@ -169,29 +169,45 @@ def read_carray(rootdir, out=None, pool=None):
     return out
 
 
-def write_carray(rootdir, arr, chunklen=None, clevel=5, shuffle=1, cname='lz4'):
+def _json_bytes(obj):
+    return json.dumps(obj, ensure_ascii=True).encode('ascii') + b'\n'
+
+
+def carray_files(arr, chunklen=None, clevel=5, shuffle=1, cname='lz4'):
+    """The files of a carray directory: [(path relative to the carray rootdir, bytes)]."""
     arr = np.ascontiguousarray(arr)
     if arr.dtype.kind not in 'biuf':
         raise NotImplementedError('bcolz writer: dtype %s' % arr.dtype)
-    os.makedirs(os.path.join(rootdir, 'meta'), exist_ok=True)
-    os.makedirs(os.path.join(rootdir, 'data'), exist_ok=True)
     n = len(arr)
     chunklen = chunklen or _chunklen_for(arr.dtype.itemsize, n)
+    files = []
     cbytes = 0
     for i, lo in enumerate(range(0, n, chunklen)):
         frame = compress_chunk(arr[lo:lo + chunklen], clevel, shuffle, cname)
-        with open(os.path.join(rootdir, 'data', '__%d.blp' % i), 'wb') as f:
-            f.write(bloscpack_header(1))
-            f.write(frame)
+        files.append(('data/__%d.blp' % i, bloscpack_header(1) + frame))
         cbytes += len(frame) + BLOSCPACK_HEADER
     dflt = False if arr.dtype.kind == 'b' else (0.0 if arr.dtype.kind == 'f' else 0)
-    _dump_json(os.path.join(rootdir, 'meta', 'storage'), {
+    files.append(('meta/storage', _json_bytes({
         'dtype': str(arr.dtype),
         'cparams': {'clevel': clevel, 'shuffle': shuffle, 'cname': cname, 'quantize': 0},
-        'chunklen': int(chunklen), 'expectedlen': int(max(n, 1)), 'dflt': dflt})
-    _dump_json(os.path.join(rootdir, 'meta', 'sizes'),
-               {'shape': [int(n)], 'nbytes': int(arr.nbytes), 'cbytes': int(cbytes)})
-    _dump_json(os.path.join(rootdir, ATTRS), {})
+        'chunklen': int(chunklen), 'expectedlen': int(max(n, 1)), 'dflt': dflt})))
+    files.append(('meta/sizes', _json_bytes({'shape': [int(n)], 'nbytes': int(arr.nbytes), 'cbytes': int(cbytes)})))
+    files.append((ATTRS, _json_bytes({})))
+    return files
+
+
+def _write_files(rootdir, files):
+    for rel, data in files:
+        path = os.path.join(rootdir, rel)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, 'wb') as f:
+            f.write(data)
+
+
+def write_carray(rootdir, arr, chunklen=None, clevel=5, shuffle=1, cname='lz4'):
+    os.makedirs(os.path.join(rootdir, 'meta'), exist_ok=True)
+    os.makedirs(os.path.join(rootdir, 'data'), exist_ok=True)
+    _write_files(rootdir, carray_files(arr, chunklen, clevel, shuffle, cname))
 
 
 # ------------------------------------------------------------------------------------------
@@ -240,12 +256,73 @@ def ctable_dtypes(rootdir):
     return OrderedDict((n, CArrayMeta(ctable_column_dir(rootdir, n)).dtype) for n in ctable_names(rootdir))
 
 
+def ctable_files(columns, chunklen=None, cname='lz4'):
+    """The files of a ctable rootdir: [(relative path, bytes)], column directories first."""
+    names = list(columns.keys())
+    files = []
+    for n in names:
+        files += [(n + '/' + rel, data) for rel, data in carray_files(columns[n], chunklen=chunklen, cname=cname)]
+    files.append((ROOTDIRS, _json_bytes({'names': names, 'dirs': {n: n for n in names}})))
+    files.append((ATTRS, _json_bytes({})))
+    return files
+
+
 def write_ctable(rootdir, columns, chunklen=None, cname='lz4'):
     """Write an OrderedDict of equal-length arrays as a bcolz ctable rootdir."""
     os.makedirs(rootdir, exist_ok=True)
-    names = list(columns.keys())
-    for n in names:
-        write_carray(ctable_column_dir(rootdir, n), columns[n], chunklen=chunklen, cname=cname)
-    _dump_json(os.path.join(rootdir, ROOTDIRS), {'names': names, 'dirs': {n: n for n in names}})
-    _dump_json(os.path.join(rootdir, ATTRS), {})
+    _write_files(rootdir, ctable_files(columns, chunklen, cname))
     return rootdir
+
+
+def ctable_tar(columns, arcname, chunklen=None, cname='lz4'):
+    """Bytes of ``tarfile.open(mode='w').add(<ctable rootdir>, arcname=arcname)``
+    (worker.py:337-345), built in memory: the same members (directories first, then their
+    files) without writing the ctable to disk and reading it back."""
+    import io
+    import tarfile
+    import time
+    files = ctable_files(columns, chunklen, cname)
+    now = int(time.time())
+    dirs = set([''])
+    for rel, _ in files:
+        parts = rel.split('/')[:-1]
+        for i in range(len(parts)):
+            dirs.add('/'.join(parts[:i + 1]))
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode='w') as tf:
+        for d in sorted(dirs):
+            info = tarfile.TarInfo(arcname + ('/' + d if d else ''))
+            info.type = tarfile.DIRTYPE
+            info.mode = 0o755
+            info.mtime = now
+            tf.addfile(info)
+        for rel, data in files:
+            info = tarfile.TarInfo(arcname + '/' + rel)
+            info.size = len(data)
+            info.mode = 0o644
+            info.mtime = now
+            tf.addfile(info, io.BytesIO(data))
+    return buf.getvalue()
+
+
+def read_ctable_files(files, columns=None):
+    """A ctable from its files in memory ({relative path: bytes}, e.g. a result tar's
+    members with the top directory stripped) -> OrderedDict name -> numpy array."""
+    names = [str(n) for n in json.loads(files[ROOTDIRS].decode('ascii'))['names']]
+    out = OrderedDict()
+    for n in (columns or names):
+        if n not in names:
+            raise KeyError(str(n))
+        sizes = json.loads(files[n + '/meta/sizes'].decode('ascii'))
+        storage = json.loads(files[n + '/meta/storage'].decode('ascii'))
+        length, chunklen = int(sizes['shape'][0]), int(storage['chunklen'])
+        arr = np.empty(length, dtype=np.dtype(storage['dtype']))
+        for i, lo in enumerate(range(0, length, chunklen)):
+            data = files[n + '/data/__%d.blp' % i]
+            if data[:4] != BLOSCPACK_MAGIC:
+                raise ValueError('%s chunk %d: not a bloscpack chunk' % (n, i))
+            tmp = arr[lo:lo + chunklen]
+            if decompress_into(data[BLOSCPACK_HEADER:], tmp) != tmp.nbytes:
+                raise ValueError('%s chunk %d: short chunk' % (n, i))
+        out[n] = arr
+    return out

@@ -1891,6 +1891,58 @@ int bqg_hash_partition(bqg_ctx* c, bqg_table* t, int32_t n_keys, const int32_t* 
   });
 }
 
+int bqg_factorize(bqg_ctx* c, bqg_table* t, int32_t col, int64_t* labels, void* values, int64_t values_cap,
+                  int64_t* n_values) {
+  return guard(c, [&] {
+    if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
+    if (!n_values) fail(BQG_E_INVALID, "null n_values");
+    Column& k = t->cols[col];
+    if (dtype_is_float(k.dtype) || k.dtype == BQG_BOOL) fail(BQG_E_UNSUPPORTED, "factor cache of a float / bool column");
+    compute_stats(t, col);
+    const uint64_t range = k.stats.empty ? 1 : (uint64_t)k.stats.imax - (uint64_t)k.stats.imin + 1;
+    if (range == 0 || range > (1ull << 27)) fail(BQG_E_UNSUPPORTED, "factor cache of a column spanning more than 2^27 values");
+    // distinct values in first-appearance order: a groupby over the column with no aggregation
+    bqg_table* vt = nullptr;
+    {
+      const int32_t key = col;
+      bqg_query q{};
+      q.n_keys = 1;
+      q.key_cols = &key;
+      q.mask_col = -1;
+      struct Reset {
+        bqg_ctx* c;
+        ~Reset() { c->dev_target = nullptr; }
+      } reset{c};
+      c->dev_target = &vt;
+      bqg_result* r = nullptr;
+      run_groupby(c, t, &q, &r);
+      if (r) table_from_host_result(c, r);
+    }
+    std::unique_ptr<bqg_table, int (*)(bqg_table*)> vown(vt, bqg_table_destroy);
+    const int64_t G = vt->nrows;
+    *n_values = G;
+    if (values && G > values_cap) fail(BQG_E_INVALID, "values buffer holds %lld, column has %lld distinct values",
+                                       (long long)values_cap, (long long)G);
+    const int64_t vmin = k.stats.empty ? 0 : k.stats.imin;
+    int32_t* lut = (int32_t*)c->misc.ensure(range * 4 + 256);
+    const bool dev_out = labels && mem_kind(labels) == 2;
+    long long* out = nullptr;
+    if (labels) out = dev_out ? (long long*)labels : (long long*)c->outcols.ensure((size_t)t->nrows * 8 + 256);
+    const Column& vc = vt->cols[0];
+    if (labels) {
+      launch_factor_labels(DevCol{vc.dev, vc.dtype, dtype_lg(vc.dtype)}, G, DevCol{k.dev, k.dtype, dtype_lg(k.dtype)},
+                           t->nrows, vmin, lut, out, c->stream);
+      HIPCHECK(hipGetLastError());
+      if (!dev_out && t->nrows)
+        HIPCHECK(hipMemcpyAsync(labels, out, (size_t)t->nrows * 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    if (values && G)
+      HIPCHECK(hipMemcpyAsync(values, vc.dev, (size_t)G * dtype_size(vc.dtype),
+                              mem_kind(values) == 2 ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+  });
+}
+
 int bqg_result_view_get(bqg_result* r, bqg_result_view* out) {
   if (!r || !out) return BQG_E_INVALID;
   out->n_rows = r->n_rows;

@@ -657,6 +657,42 @@ void launch_expand_subgroups(const DevCol& basket, const unsigned char* mask, un
                      mask, out, run_any);
 }
 
+// ------------------------------------------------------------------------------------
+// bquery's factor cache (auto_cache, worker.py:291): label of every row = first-appearance
+// rank of its value.  `vals` holds the distinct values in label order (a groupby over the
+// column); lut[v - vmin] = label, then one gather per row.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_factor_lut(DevCol vals, int64_t n, int64_t vmin, int32_t* lut) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    Chunk c;
+    row_word_to_chunk(c, vals, i, load_row_word(vals, i));
+    uint64_t v[1];
+    decode<1>(c, vals.dtype, v);
+    lut[v[0] - (uint64_t)vmin] = (int32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_factor_labels(DevCol col, int64_t n, int64_t vmin, const int32_t* lut,
+                                                          long long* out) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    Chunk c;
+    row_word_to_chunk(c, col, i, load_row_word(col, i));
+    uint64_t v[1];
+    decode<1>(c, col.dtype, v);
+    out[i] = (long long)lut[v[0] - (uint64_t)vmin];
+  }
+}
+
+void launch_factor_labels(const DevCol& vals, int64_t nvals, const DevCol& col, int64_t nrows, int64_t vmin,
+                          int32_t* lut, long long* out, hipStream_t st) {
+  auto grid = [](int64_t n) {
+    int64_t b = (n + kBlock - 1) / kBlock;
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(b, 8192));
+  };
+  if (nvals > 0) hipLaunchKernelGGL(k_factor_lut, dim3(grid(nvals)), dim3(kBlock), 0, st, vals, nvals, vmin, lut);
+  if (nrows > 0) hipLaunchKernelGGL(k_factor_labels, dim3(grid(nrows)), dim3(kBlock), 0, st, col, nrows, vmin, lut, out);
+}
+
 int device_cu_count() {
   int dev = 0, n = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;

@@ -191,6 +191,10 @@ struct PartitionCols {
 void launch_hash_partition(const PartitionCols& k, int64_t nrows, uint32_t nparts, uint32_t* out,
                            unsigned long long* counts, hipStream_t st);
 
+// factor cache labels (bquery auto_cache): lut [range] scratch, out [nrows] int64 labels
+void launch_factor_labels(const DevCol& vals, int64_t nvals, const DevCol& col, int64_t nrows, int64_t vmin,
+                          int32_t* lut, long long* out, hipStream_t st);
+
 int device_cu_count();
 
 }  // namespace bqg

@@ -28,7 +28,7 @@ import numpy as np
 
 from . import bcolz_io
 from .engine import ShardTable, get_device
-from .terms import parse_terms
+from .terms import any_value_satisfies, parse_terms
 
 
 class WhereMask:
@@ -186,21 +186,64 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
 
     def where_terms_factorization_check(self, term_list):
         """False iff a term's column has a factor cache (``<col>.values``) in the rootdir and
-        none of the cached values can satisfy the term [ext-bquery, unverified]."""
+        none of the cached values can satisfy the term; the first term without a cache ends
+        the check [ext-bquery, unverified].  The cached values (a few per column) are read
+        once per cache directory and tested on the host."""
         terms = parse_terms(self._dtypes, term_list)
         for col, code, value in terms:
-            values_dir = os.path.join(self.rootdir, col + '.values') if self.rootdir else None
-            if not values_dir or not os.path.isdir(values_dir):
+            vals = self._cached_values(col)
+            if vals is None:
                 break
-            vals = bcolz_io.read_carray(values_dir)
-            t = ShardTable(OrderedDict([(col, vals.astype(self._dtypes[col]))]), device=self.device)
-            try:
-                _, npass = t.where([(col, _op_name(code), value)])
-            finally:
-                t.close()
-            if npass == 0:
+            if not any_value_satisfies(vals.astype(self._dtypes[col]), code, value):
                 return False
         return True
+
+    # ---- factor caches (bquery auto_cache: <col>.factor / <col>.values next to the columns)
+    def cache_valid(self, col):
+        """bquery's test: the column and its ``.values`` cache both exist."""
+        if not self.rootdir:
+            return False
+        coldir = bcolz_io.ctable_column_dir(self.rootdir, col)
+        return os.path.exists(os.path.join(coldir, '__attrs__')) and os.path.exists(
+            os.path.join(coldir + '.values', '__attrs__'))
+
+    def _cached_values(self, col):
+        if not self.rootdir:
+            return None
+        values_dir = bcolz_io.ctable_column_dir(self.rootdir, col) + '.values'
+        try:
+            key = os.stat(os.path.join(values_dir, '__attrs__')).st_mtime_ns
+        except OSError:
+            return None
+        memo = self.__dict__.setdefault('_values_memo', {})
+        hit = memo.get(col)
+        if hit is None or hit[0] != key:
+            hit = memo[col] = (key, bcolz_io.read_carray(values_dir))
+        return hit[1]
+
+    def _auto_cache(self, cols):
+        """bquery's ``auto_cache=True`` side effect of a groupby (worker.py:291): the factor
+        caches of every groupby column that has none -- labels and values from the GPU
+        (``bqg_factorize``), compressed and written by a background thread into temporary
+        directories next to the columns and renamed into place (.factor before .values, so a
+        valid cache always has both).  Columns the kernel cannot factorize (floats, value
+        ranges above 2^27) get no cache, which only disables the early-out for them."""
+        if not (self.auto_cache and self.rootdir and os.access(self.rootdir, os.W_OK)):
+            return
+        pending = self.__dict__.setdefault('_caching', set())
+        for col in cols:
+            if col in pending or self.cache_valid(col):
+                continue
+            try:
+                labels, values = self._ensure_device([col]).factorize(col)
+            except NotImplementedError:
+                continue
+            pending.add(col)
+            _cache_writer().submit(_write_factor_cache, self.rootdir, col, labels, values)
+
+    def flush_caches(self):
+        """Wait until the factor caches this process scheduled are on disk."""
+        _cache_writer().submit(lambda: None).result()
 
     def is_in_ordered_subgroups(self, basket_col=None, bool_arr=None, _max_len_subgroup=1000):
         if basket_col is None:
@@ -241,6 +284,7 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
             terms = bool_arr.terms  # fuse the predicate into the groupby scan
             needed += [t[0] for t in parse_terms(self._dtypes, terms)]
         table = self._ensure_device(needed)
+        self._auto_cache(groupby_cols)
         temp = False
         if bool_arr is not None and terms is None:
             mask, temp = self._mask_column(bool_arr)
@@ -253,6 +297,28 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
         if rootdir:
             res.flush()
         return res
+
+    def groupby_device(self, groupby_cols, agg_list, bool_arr=None):
+        """``groupby`` whose result stays in HBM (a ShardTable: keys, then aggregations) -- the
+        input of the node-level merge (worker.CalcPath, dist.merge_group_device)."""
+        from .terms import parse_agg_list
+        groupby_cols = list(groupby_cols)
+        ops = parse_agg_list(self._dtypes, agg_list)
+        needed = groupby_cols + [o[0] for o in ops]
+        terms, mask = None, None
+        if isinstance(bool_arr, WhereMask) and bool_arr.device_col is None:
+            terms = bool_arr.terms
+            needed += [t[0] for t in parse_terms(self._dtypes, terms)]
+        table = self._ensure_device(needed)
+        self._auto_cache(groupby_cols)
+        temp = False
+        if bool_arr is not None and terms is None:
+            mask, temp = self._mask_column(bool_arr)
+        try:
+            return table.groupby_table(groupby_cols, agg_list, where_terms=terms, mask=mask)
+        finally:
+            if temp:
+                table.release_mask(mask)
 
     def select(self, column_list, bool_arr=None, rootdir=None):
         """``bcolz.fromiter(ct[column_list].where(bool_arr), ...)`` (worker.py:316-323)."""
@@ -293,8 +359,30 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
         return pd.DataFrame(OrderedDict((n, self._host_column(n)) for n in self.names))
 
 
-_OP_NAMES = {1: '==', 2: '!=', 3: 'in', 4: 'nin', 5: '>', 6: '>=', 7: '<', 8: '<='}
+_writer = None
 
 
-def _op_name(code):
-    return _OP_NAMES[code]
+def _cache_writer():
+    """One background thread writes factor caches (the worker stays single-threaded)."""
+    global _writer
+    if _writer is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _writer = ThreadPoolExecutor(max_workers=1, thread_name_prefix='bqgpu-cache')
+    return _writer
+
+
+def _write_factor_cache(rootdir, col, labels, values):
+    import shutil
+    import tempfile
+    coldir = bcolz_io.ctable_column_dir(rootdir, col)
+    for suffix, arr in (('.factor', labels), ('.values', values)):
+        tmp = tempfile.mkdtemp(prefix='.bqgpu-cache-', dir=rootdir)
+        try:
+            bcolz_io.write_carray(tmp, arr)
+            final = coldir + suffix
+            if os.path.exists(final):
+                shutil.rmtree(final, ignore_errors=True)
+            os.rename(tmp, final)
+        except OSError:
+            shutil.rmtree(tmp, ignore_errors=True)
+            return

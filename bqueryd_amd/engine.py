@@ -451,6 +451,27 @@ class ShardTable:
         """The table's columns as numpy arrays."""
         return OrderedDict((c, self.read(c)) for c in (cols or self.names))
 
+    def factorize(self, col, labels=True):
+        """bquery's factor cache of column ``col`` (``bqg_factorize``): (int64 first-appearance
+        label of every row, or None; distinct values in label order).  Integer columns spanning
+        at most 2^27 values (else NotImplementedError)."""
+        s = self.slot(col)
+        dt = np.dtype(self.dtypes[col])
+        if dt.kind not in 'iu':
+            raise NotImplementedError('factor cache of a %s column' % dt)
+        st = self.stats(col)
+        span = 1 if st['empty'] else int(st['max']) - int(st['min']) + 1
+        if span > 1 << 27:
+            raise NotImplementedError('factor cache of a column spanning more than 2^27 values')
+        cap = min(self.nrows, span)
+        values = np.empty(max(cap, 1), dtype=dt)
+        lab = np.empty(self.nrows, np.int64) if labels else None
+        n_values = ctypes.c_int64()
+        self.dev.check(self._lib.bqg_factorize(self.dev.handle, self.handle, s,
+                                               lab.ctypes.data if labels else None, values.ctypes.data,
+                                               len(values), ctypes.byref(n_values)))
+        return lab, values[:n_values.value]
+
     def select_rows(self, cols, where_terms=None, mask=None):
         """aggregate=False: the passing rows of ``cols`` in row order."""
         cols = list(cols)

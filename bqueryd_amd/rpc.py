@@ -14,16 +14,13 @@
 from __future__ import annotations
 
 import io
-import os
 import tarfile
-import tempfile
 from collections import OrderedDict
 
 import numpy as np
 
 from . import bcolz_io
 from .ctable import ctable
-from .worker import rm_file_or_dir
 
 
 def tar_of_tars(results):
@@ -40,21 +37,24 @@ def tar_of_tars(results):
 
 
 def read_shard_results(result_tar):
-    """-> list of OrderedDict tables, one per non-empty shard reply, in member-name order."""
+    """-> list of OrderedDict tables, one per non-empty shard reply, in member-name order.
+
+    The reference untars every inner tar into a temporary directory and opens it as a
+    ctable (rpc.py:137-162); here the inner tars are read in memory (same files, no disk
+    round trip): the ctable directory is the first top-level entry of each inner tar."""
     tables = []
-    tmp_dir = tempfile.mkdtemp(prefix='tar_dir_')
-    try:
-        with tarfile.open(fileobj=io.BytesIO(result_tar), mode='r') as outer:
-            members = sorted(outer.getmembers(), key=lambda m: m.name)
-            for i, m in enumerate(members):
-                inner = outer.extractfile(m).read()
-                new_dir = os.path.join(tmp_dir, 'bcolz_' + str(i))
-                with tarfile.open(fileobj=io.BytesIO(inner), mode='r') as t:
-                    t.extractall(new_dir)
-                ctable_dir = sorted(os.path.join(new_dir, d) for d in os.listdir(new_dir))[0]
-                tables.append(bcolz_io.read_ctable(ctable_dir))
-    finally:
-        rm_file_or_dir(tmp_dir)
+    with tarfile.open(fileobj=io.BytesIO(result_tar), mode='r') as outer:
+        members = sorted(outer.getmembers(), key=lambda m: m.name)
+        for m in members:
+            inner = outer.extractfile(m).read()
+            with tarfile.open(fileobj=io.BytesIO(inner), mode='r') as t:
+                files = [x for x in t.getmembers() if x.isfile()]
+                if not files:
+                    continue
+                top = sorted(set(x.name.split('/', 1)[0] for x in files))[0]
+                data = {x.name.split('/', 1)[1]: t.extractfile(x).read() for x in files
+                        if x.name.startswith(top + '/')}
+            tables.append(bcolz_io.read_ctable_files(data))
     return tables
 
 

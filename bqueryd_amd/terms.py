@@ -143,3 +143,30 @@ def parse_agg_list(dtypes, agg_list):
             dt = np.dtype(dtypes[in_col])
         ops.append((in_col, out_col, op, dt))
     return ops
+
+
+def any_value_satisfies(values, code, value):
+    """True iff some element of ``values`` (a factor cache: the distinct values of a column)
+    satisfies the parsed term -- the test ``ctable.where_terms_factorization_check`` applies
+    to each term whose column has a ``<col>.values`` cache (worker.py:298) [ext-bquery,
+    unverified].  Same exact int / float rules as the row predicate (``normalize``); host
+    logic over a handful of cached values, not a row scan."""
+    values = np.asarray(values)
+    op, ivals, fvals = normalize(values.dtype, code, value)
+    if op == L.T_TRUE:
+        return len(values) > 0
+    if op == L.T_FALSE or len(values) == 0:
+        return False
+    if values.dtype.kind == 'f':
+        x = values.astype(np.float64)
+        ref = np.asarray(fvals, np.float64)
+    else:
+        x = values.astype(np.uint64 if values.dtype == np.uint64 else np.int64)
+        ref = np.asarray(ivals, x.dtype) if values.dtype != np.uint64 else np.asarray(
+            [v & 0xFFFFFFFFFFFFFFFF for v in ivals], np.uint64)
+    if op in (L.T_IN, L.T_NIN):
+        hit = np.isin(x, ref)
+        return bool(np.any(hit if op == L.T_IN else ~hit))
+    v = ref[0]
+    hit = {L.T_EQ: x == v, L.T_NE: x != v, L.T_GT: x > v, L.T_GE: x >= v, L.T_LT: x < v, L.T_LE: x <= v}[op]
+    return bool(np.any(hit))

@@ -201,6 +201,16 @@ int bqg_hash_partition(bqg_ctx* ctx, bqg_table* t, int32_t n_keys, const int32_t
                        int32_t nparts, int32_t out_col, int64_t* counts);
 int bqg_result_free(bqg_result* r);
 
+/* ---------------- factor caches (bquery auto_cache, worker.py:291) ----------------
+ * The <col>.factor / <col>.values carrays bquery writes next to a shard's columns the first
+ * time it groups by `col` (read back by where_terms_factorization_check, worker.py:298):
+ * labels[nrows] (int64, host or device memory; NULL to skip) = first-appearance rank of each
+ * row's value over ALL rows; values[*n_values] (column dtype; NULL to skip; at most
+ * values_cap) = the distinct values in label order.  Integer columns spanning at most 2^27
+ * values; otherwise BQG_E_UNSUPPORTED (no cache is written). */
+int bqg_factorize(bqg_ctx* ctx, bqg_table* t, int32_t col, int64_t* labels, void* values, int64_t values_cap,
+                  int64_t* n_values);
+
 /* ---------------- multi-GPU: RCCL over xGMI ----------------
  * The aggregate=True merge of co-located shards: the client's re-group of every shard's
  * finalized table with `sum` of every column (rpc.py:164-173), run across the node's GPUs on

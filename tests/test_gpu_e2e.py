@@ -108,6 +108,89 @@ def test_worker_factorization_check_and_errors(tmp_path):
         calc.handle_work(_calc_msg('s.bcolzs', ['nope'], [['fare_amount', 'sum', 'f']], []))
 
 
+def _write_shards(tmp_path, n_shards, rows, extra=None):
+    files, shards = [], []
+    for i in range(n_shards):
+        s = synth.taxi_shard(rows, config_id=5, n_shards=n_shards, shard=i,
+                             columns=('pickup_location', 'vendor_id', 'passenger_count', 'fare_amount'))
+        s['pickup_location'] = (s['pickup_location'] % 5_000).astype(np.int32)
+        if extra:
+            extra(s)
+        fn = 'tripdata-%d.bcolzs' % i
+        bcolz_io.write_ctable(os.path.join(str(tmp_path), fn), s)
+        files.append(fn)
+        shards.append(s)
+    return files, shards
+
+
+@pytest.mark.parametrize('aggs, where, expand', [
+    ([['fare_amount', 'sum', 'fare_sum'], ['fare_amount', 'count', 'n']], [], None),
+    ([['fare_amount', 'sum', 'fare_sum'], ['fare_amount', 'count', 'n']], [('passenger_count', '>=', 2)], None),
+    ([['fare_amount', 'mean', 'fm'], ['passenger_count', 'count_distinct', 'pcd']], [('vendor_id', '==', 2)], None),
+    ([['fare_amount', 'sum', 'fare_sum']], [('passenger_count', '==', 3)], 'basket'),
+])
+def test_node_level_calc_matches_per_shard_replies(tmp_path, aggs, where, expand):
+    """One message with the node's files (args[0] a list, aggregate=True) -> ONE result tar
+    holding the GPU-merged table (bqg_merge over RCCL); the unchanged client merge of that tar
+    equals the client merge of the per-file replies (controller.py:471-508, rpc.py:164-173)."""
+    def add_basket(s):
+        s['basket'] = (np.arange(len(s['vendor_id'])) // 5).astype(np.int32)
+    files, shards = _write_shards(tmp_path, 5, 30_000, extra=add_basket)
+    keys = ['pickup_location', 'vendor_id']
+    calc = CalcPath(str(tmp_path))
+    kwargs = {'aggregate': True}
+    if expand:
+        kwargs['expand_filter_column'] = expand
+    msg = calc.handle_work(_calc_msg(files, keys, aggs, where, **kwargs))
+    assert msg['filenames'] == files and msg['data']
+    got = rpc.uncompress_groupby_to_df(rpc.tar_of_tars({'node': msg['data']}), keys, aggs, where, aggregate=True)
+    got = OrderedDict((c, got[c].values) for c in got.columns)
+    per = [bo.handle_work(s, keys, aggs, where, expand_filter_column=expand) for s in shards]
+    ref = bo.client_merge(per, keys, aggs, aggregate=True)
+    assert_tables_equal(sort_by_keys(got, keys), sort_by_keys(ref, keys))
+    # the same answer through the per-file path (the default)
+    replies = OrderedDict((fn, calc.handle_work(_calc_msg(fn, keys, aggs, where, **kwargs))['data']) for fn in files)
+    per_file = rpc.uncompress_groupby_to_df(rpc.tar_of_tars(replies), keys, aggs, where, aggregate=True)
+    per_file = OrderedDict((c, per_file[c].values) for c in per_file.columns)
+    assert_tables_equal(sort_by_keys(per_file, keys), sort_by_keys(ref, keys))
+
+
+def test_node_level_calc_needs_explicit_aggregate(tmp_path):
+    files, _ = _write_shards(tmp_path, 2, 1000)
+    calc = CalcPath(str(tmp_path))
+    with pytest.raises(ValueError, match='aggregate=True'):
+        calc.handle_work(_calc_msg(files, ['vendor_id'], [['fare_amount', 'sum', 'f']], []))
+
+
+def test_auto_cache_factor_files_and_check(tmp_path):
+    """A groupby with auto_cache=True writes bquery's <col>.factor / <col>.values caches
+    (labels = first-appearance rank over all rows, values in label order); the factorization
+    check over them agrees with the oracle's on every term shape (worker.py:291, 298-301)."""
+    files, shards = _write_shards(tmp_path, 1, 40_000)
+    root = os.path.join(str(tmp_path), files[0])
+    calc = CalcPath(str(tmp_path))
+    calc.handle_work(_calc_msg(files[0], ['passenger_count', 'vendor_id'], [['fare_amount', 'sum', 'f']], []))
+    ct = calc.cache.open(root)
+    ct.flush_caches()
+    for col in ('passenger_count', 'vendor_id'):
+        labels, uniq = bo.factorize(shards[0][col])
+        np.testing.assert_array_equal(bcolz_io.read_carray(os.path.join(root, col + '.factor')), labels)
+        np.testing.assert_array_equal(bcolz_io.read_carray(os.path.join(root, col + '.values')), uniq)
+        assert ct.cache_valid(col)
+    assert not ct.cache_valid('fare_amount')  # float columns get no cache
+    values = {c: bcolz_io.read_carray(os.path.join(root, c + '.values')) for c in ('passenger_count', 'vendor_id')}
+    for terms in ([('passenger_count', '==', 42)], [('passenger_count', '==', 3)], [('passenger_count', '>', 9)],
+                  [('passenger_count', '>=', 9)], [('passenger_count', '<', 0)], [('passenger_count', '<=', 0.5)],
+                  [('passenger_count', 'in', [11, 12])], [('passenger_count', 'in', [11, 2])],
+                  [('passenger_count', 'nin', list(range(10)))], [('vendor_id', '!=', 1)],
+                  [('vendor_id', '==', 1.5)], [('fare_amount', '>', 1e9), ('vendor_id', '==', 7)],
+                  [('vendor_id', '==', 7), ('fare_amount', '>', 1e9)]):
+        assert ct.where_terms_factorization_check(terms) == bo.factorization_check(values, shards[0], terms), terms
+    msg = calc.handle_work(_calc_msg(files[0], ['vendor_id'], [['fare_amount', 'sum', 'f']],
+                                     [('passenger_count', 'in', [11, 12])]))
+    assert msg['data'] == ''
+
+
 def test_worker_mask_columns_stay_flat(tmp_path):
     """Repeated filtered + basket-expanded queries on one resident shard reuse the shard's
     scratch mask columns (no HBM growth per query, plan cache kept)."""
