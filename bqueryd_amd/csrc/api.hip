@@ -981,20 +981,28 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       // contiguous row ranges, whole 4096-row tiles (a multiple of every scatter tile), at
       // most 2^(32 - wbits) rows each so that (row - begin) << wbits | slot_low fits 32 bits
       const int64_t ptile = 4096;
-      const int64_t ptiles = (N + ptile - 1) / ptile;
-      const int64_t max_tiles_per_block = std::max<int64_t>(1, (int64_t(1) << (32 - pl.wbits)) / ptile);
-      L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, ptiles));
-      L.blocks = (int)std::max<int64_t>(L.blocks, (ptiles + max_tiles_per_block - 1) / max_tiles_per_block);
-      L.rows_per_block = ((ptiles + L.blocks - 1) / L.blocks) * ptile;
-      // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
-      // slot table allows one per CU; C3 on MI355X: 2 splits 0.34 ms vs 4 splits 0.36 ms)
-      {
-        const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)nsum) + ((size_t)L.blocks + 1) * 4;
+      // row batches (BQGPU_PART_BATCH rows, a multiple of the tile): each batch's entries
+      // round-trip through the Infinity Cache instead of HBM when they fit in it
+      int64_t batch = N;
+      if (const char* ev = getenv("BQGPU_PART_BATCH"))
+        batch = std::max<int64_t>(ptile, (atoll(ev) + ptile - 1) / ptile * ptile);
+      if (batch > N) batch = N;
+      auto shape = [&](PartLaunch& P, int64_t nrows) {
+        const int64_t ptiles = (nrows + ptile - 1) / ptile;
+        const int64_t max_tiles_per_block = std::max<int64_t>(1, (int64_t(1) << (32 - pl.wbits)) / ptile);
+        P.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, ptiles));
+        P.blocks = (int)std::max<int64_t>(P.blocks, (ptiles + max_tiles_per_block - 1) / max_tiles_per_block);
+        P.rows_per_block = ((ptiles + P.blocks - 1) / P.blocks) * ptile;
+        // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
+        // slot table allows one per CU; C3 on MI355X: 2 splits 0.34 ms vs 4 splits 0.36 ms)
+        const size_t agg_lds = ((size_t)1 << P.wbits) * (8 + 8 * (size_t)nsum) + ((size_t)P.blocks + 1) * 4;
         const int fit = std::max(1, (int)((160 * 1024) / agg_lds));
-        L.splits = std::max(1, std::min(L.blocks, (c->cu * fit + L.nparts / 2) / L.nparts));
-      }
-      if (const char* ev = getenv("BQGPU_PART_SPLITS")) L.splits = std::max(1, std::min(L.blocks, atoi(ev)));
-      L.capacity = ((uint64_t)N + 3) & ~3ull;  // 16-byte aligned value arrays
+        P.splits = std::max(1, std::min(P.blocks, (c->cu * fit + P.nparts / 2) / P.nparts));
+        if (const char* ev = getenv("BQGPU_PART_SPLITS")) P.splits = std::max(1, std::min(P.blocks, atoi(ev)));
+      };
+      shape(L, batch);
+      L.row_base = 0;
+      L.capacity = ((uint64_t)batch + 3) & ~3ull;  // 16-byte aligned value arrays
       const size_t ncounts = (size_t)L.nparts * L.blocks + 1;
       unsigned char* pb = (unsigned char*)c->prefix.ensure(ncounts * 4 + (2 * (ncounts / 1024 + 2) + 4096) * 4 + 1024);
       L.counts = (uint32_t*)pb;
@@ -1018,7 +1026,17 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         L.chunks = fs ? chunks : 1;
         c->last.specialized = fc ? 1 : 0;
       }
-      launch_partitioned(pl.p, sa, L, scan_scratch, st, fc, fs);
+      for (int64_t b0 = 0; b0 < N; b0 += batch) {
+        const int64_t nb = std::min(batch, N - b0);
+        ScanParams pb = pl.p;
+        pb.nrows = nb;
+        for (int i = 0; i < pb.ncols; ++i) pb.cols[i].ptr += (size_t)b0 << pb.cols[i].lg;
+        PartLaunch Lb = L;
+        if (nb != batch) shape(Lb, nb);
+        Lb.row_base = b0;
+        if (b0 > 0) HIPCHECK(hipMemsetAsync(Lb.counts + (size_t)Lb.nparts * Lb.blocks, 0, 4, st));
+        launch_partitioned(pb, sa, Lb, scan_scratch, st, fc, fs);
+      }
     } else {
       launch_scan_global(pl.p, sa, scan_blocks(c, N, 8), st);
     }

@@ -113,7 +113,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       if (i < lo || i >= hi) continue;
       while (i >= rs[b + 1]) ++b;
       const uint32_t s = mm[k] & lowmask;
-      const uint32_t row = (uint32_t)((int64_t)b * L.rows_per_block) + (mm[k] >> L.wbits);
+      const uint32_t row = (uint32_t)(L.row_base + (int64_t)b * L.rows_per_block) + (mm[k] >> L.wbits);
       atomicAdd(&cnt[s], 1u);
       if (fst[s] > row) atomicMin(&fst[s], row);
     }

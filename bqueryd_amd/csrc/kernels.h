@@ -167,6 +167,7 @@ struct PartLaunch {
   int64_t rows_per_block;    // contiguous rows per count/scatter workgroup: a multiple of the
                              // scatter tile and <= 2^(32 - wbits) (row-in-block | slot_low
                              // packs into one 32-bit word)
+  int64_t row_base;          // table row of the launch's row 0 (batched launches)
   uint64_t capacity;         // entry capacity (>= passing rows)
   uint32_t* counts;          // [nparts * blocks + 1] -> exclusive offsets in place
   uint32_t* meta;            // [capacity]: (row - block begin) << wbits | slot_low

@@ -123,3 +123,159 @@ def test_first_appearance_and_skip_slot():
     out = bo.groupby(cols, ['k'], [['v', 'sum', 's']], bool_arr=np.array([0, 1, 1, 1, 0, 1], bool))
     np.testing.assert_array_equal(out['k'], [3, 5, 9, 7])  # first appearance among passing rows
     np.testing.assert_array_equal(out['s'], [1, 2, 3, 5])
+
+
+# ---------------------------------------------------------------------------------------------
+# More of the oracle pinned against pandas, the reference's own test oracle
+# (tests/test_simple_rpc.py:151-172): pandas expresses bquery's semantics directly for
+#   * first-appearance group order            -> groupby(sort=False)
+#   * filters (the skip slot's rows dropped)  -> df[mask]
+#   * count_distinct                          -> nunique
+#   * std (population)                        -> std(ddof=0)
+#   * raw rows (aggregate=False)              -> df[mask][cols]
+#   * basket expansion                        -> transform('any') over runs of equal baskets
+#   * the client merge (rpc.py:164-173)       -> concat + groupby(sort=False).sum()
+# Still bquery-only (no pandas counterpart): sorted_count_distinct's zero-initialised `last`
+# rule (pinned below only up to that rule), Knuth's incremental mean rounding (pinned at
+# 1e-12, not bitwise), the float32 row-order sum.
+# ---------------------------------------------------------------------------------------------
+def _pd_groupby(df, keys, spec):
+    """spec: [(in_col, pandas method, out_col)] -> OrderedDict in first-appearance order."""
+    g = df.groupby(keys, sort=False)
+    out = OrderedDict()
+    first = g.size()
+    idx = first.index
+    if len(keys) == 1:
+        out[keys[0]] = np.asarray(idx)
+    else:
+        for i, k in enumerate(keys):
+            out[k] = np.asarray(idx.get_level_values(i))
+    for in_col, method, out_col in spec:
+        s = g[in_col]
+        if method == 'std0':
+            r = s.std(ddof=0)
+        elif method == 'count':
+            r = s.size()
+        else:
+            r = getattr(s, method)()
+        out[out_col] = np.asarray(r.reindex(idx))
+    return out
+
+
+def _cmp(got, ref, exact=(), rtol=1e-12):
+    assert list(got) == list(ref), (list(got), list(ref))
+    for c in ref:
+        g, r = np.asarray(got[c]), np.asarray(ref[c])
+        assert len(g) == len(r), c
+        if c in exact or r.dtype.kind in 'iub':
+            np.testing.assert_array_equal(g, r.astype(g.dtype), err_msg=c)
+        else:
+            np.testing.assert_allclose(g, r, rtol=rtol, atol=0, err_msg=c)
+
+
+def _cols(n=30_000, seed=0):
+    c = synth.taxi_shard(n, config_id=3, n_shards=8, shard=seed,
+                         columns=('pickup_location', 'vendor_id', 'passenger_count', 'payment_type', 'fare_amount'))
+    c['pickup_location'] = (c['pickup_location'] % 700).astype(np.int32)
+    return c
+
+
+def test_pandas_multikey_first_appearance_order():
+    cols = _cols()
+    keys = ['pickup_location', 'vendor_id']
+    got = bo.groupby(cols, keys, [['fare_amount', 'sum', 's'], ['fare_amount', 'count', 'n'],
+                                  ['fare_amount', 'mean', 'm']])
+    ref = _pd_groupby(pd.DataFrame(cols), keys, [('fare_amount', 'sum', 's'), ('fare_amount', 'count', 'n'),
+                                                 ('fare_amount', 'mean', 'm')])
+    _cmp(got, ref, exact=('s',))  # dyadic data: sums exact in any order
+
+
+@pytest.mark.parametrize('terms', [
+    [('passenger_count', '>=', 2)],
+    [('passenger_count', 'in', [1, 3, 5]), ('vendor_id', '==', 2)],
+    [('payment_type', 'nin', [0, 1]), ('fare_amount', '<', 12.5)],
+    [('passenger_count', '==', 2.5)],  # nothing passes
+])
+def test_pandas_filtered_groupby_and_raw_rows(terms):
+    cols = _cols()
+    df = pd.DataFrame(cols)
+    mask = np.ones(len(df), bool)
+    for col, op, val in terms:
+        s = df[col]
+        mask &= {'>=': s >= val, '==': s == val, '<': s < val}.get(op) if op not in ('in', 'nin') else \
+            (s.isin(val) if op == 'in' else ~s.isin(val))
+    np.testing.assert_array_equal(bo.where_terms(cols, terms), mask)
+    keys = ['payment_type', 'vendor_id']
+    got = bo.handle_work(cols, keys, [['fare_amount', 'sum', 's'], ['passenger_count', 'count', 'n']], terms)
+    ref = _pd_groupby(df[mask], keys, [('fare_amount', 'sum', 's'), ('passenger_count', 'count', 'n')])
+    _cmp(got, ref, exact=('s',))
+    raw = bo.handle_work(cols, keys, [['fare_amount', 'sum', 's']], terms, aggregate=False)
+    for c in keys + ['fare_amount']:
+        np.testing.assert_array_equal(raw[c], df[mask][c].values)
+
+
+def test_pandas_count_distinct_and_population_std():
+    cols = _cols()
+    got = bo.groupby(cols, ['pickup_location'], [['passenger_count', 'count_distinct', 'cd'],
+                                                 ['fare_amount', 'std', 'sd'], ['payment_type', 'count_distinct', 'pd']])
+    ref = _pd_groupby(pd.DataFrame(cols), ['pickup_location'], [('passenger_count', 'nunique', 'cd'),
+                                                                ('fare_amount', 'std0', 'sd'),
+                                                                ('payment_type', 'nunique', 'pd')])
+    _cmp(got, ref, rtol=1e-10)  # Welford vs pandas' two-pass std: rounding only
+
+
+def test_pandas_sorted_count_distinct_up_to_the_zero_init_rule():
+    """pandas counts value runs per group; bquery's zero-initialised last[] makes a group's
+    first row count only when its value is non-zero, except the very first row (label 0)."""
+    cols = _cols(8_000)
+    cols['passenger_count'][::7] = 0
+    k, v = 'pickup_location', 'passenger_count'
+    got = bo.groupby(cols, [k], [[v, 'sorted_count_distinct', 'scd']])
+    df = pd.DataFrame(cols)
+    runs = df.groupby(k, sort=False)[v].apply(lambda s: int((s != s.shift()).sum()))
+    first_val = df.groupby(k, sort=False)[v].first()
+    expect = runs - (first_val == 0).astype(int)
+    expect.iloc[0] = runs.iloc[0]  # the first processed row always counts (out[0] = 1)
+    np.testing.assert_array_equal(got[k], runs.index.values)
+    np.testing.assert_array_equal(got['scd'], expect.values)
+
+
+def test_pandas_basket_expansion():
+    cols = _cols(5_000)
+    cols['basket'] = (np.arange(5_000) // 6).astype(np.int32)
+    mask = bo.where_terms(cols, [('passenger_count', '==', 3)])
+    got = bo.is_in_ordered_subgroups(cols['basket'], mask)
+    s = pd.Series(mask)
+    run = (pd.Series(cols['basket']) != pd.Series(cols['basket']).shift()).cumsum()
+    np.testing.assert_array_equal(got, s.groupby(run).transform('any').values)
+
+
+def test_pandas_client_merge():
+    shards = [_cols(4_000, seed=i) for i in range(4)]
+    for i, s in enumerate(shards):
+        s['vendor_id'] = ((s['vendor_id'] + i) % 3).astype(np.int32)
+    keys = ['vendor_id', 'payment_type']
+    aggs = [['fare_amount', 'sum', 'fs'], ['fare_amount', 'count', 'n'], ['passenger_count', 'mean', 'pm']]
+    per = [bo.handle_work(s, keys, aggs, []) for s in shards]
+    got = bo.client_merge(per, keys, aggs, aggregate=True)
+    cat = pd.concat([pd.DataFrame(p) for p in per], ignore_index=True)
+    ref = _pd_groupby(cat, keys, [('fs', 'sum', 'fs'), ('n', 'sum', 'n'), ('pm', 'sum', 'pm')])
+    _cmp(got, ref, exact=('fs',))
+
+
+@pytest.mark.parametrize('name', [n for n in SINGLE if n.startswith('where_') or n in ('c2_filtered', 'c3_multikey')])
+def test_golden_fixtures_against_pandas(name):
+    """The committed golden outputs (sum / count / mean aggregations) equal pandas over the
+    same inputs and filters."""
+    q, cols, out = load_case(name)
+    terms = _terms(q)
+    mask = bo.where_terms(cols, terms) if terms else np.ones(len(next(iter(cols.values()))), bool)
+    spec = []
+    for a in q['aggs']:
+        method = {'sum': 'sum', 'count': 'count', 'mean': 'mean', 'std': 'std0',
+                  'count_distinct': 'nunique'}.get(a[1])
+        if method is None:
+            pytest.skip('no pandas counterpart for %s' % a[1])
+        spec.append((a[0], method, a[2]))
+    ref = _pd_groupby(pd.DataFrame(cols)[mask], q['groupby'], spec)
+    _cmp(out, ref, rtol=1e-12)
