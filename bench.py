@@ -18,7 +18,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import platform
 import sys
 import time
 
@@ -98,6 +97,35 @@ def _cpu_baseline(cols, cfg, reps=2):
         best = dt if best is None else min(best, dt)
     n = len(next(iter(cols.values())))
     return n / best, best
+
+
+def _cpu_cluster_baseline(cfg, args, rows, single):
+    """The reference's deployment shape on this host's cores (oracle/cpu_cluster.py): one
+    controller + N single-threaded workers running the C port of bquery's per-shard groupby
+    over 8 shards of the workload, client sum-merge (rpc.py:164-173); N = 2 and N = all
+    cores.  ``value`` is the all-cores cluster."""
+    from oracle import cpu_cluster
+    cores = cpu_cluster.host_cores()
+    n_shards = 8
+    per = max(1, rows // n_shards)
+    counts = sorted(set([2, cores]))
+    res, _ = cpu_cluster.run(cfg, n_shards, per, counts, config_id=synth_config_id(args.config),
+                             variant=args.variant)
+    rate, secs = res[cores]
+    return {'value': rate, 'unit': 'rows/s', 'cores': cores, 'kind': 'port',
+            'sample': ('%s as %d shards x %d rows: 1 controller + %d single-threaded worker processes '
+                       '(oracle/cbquery.c, the C port of bquery\'s multi-pass per-shard groupby: where mask, '
+                       'khash factorize, filter re-factorize, one pass per aggregation; misc/supervisor.conf:21, '
+                       'worker.py:40) + client sum-merge (rpc.py:164-173), best of 2 (%.3f s); shards in shared '
+                       'memory, blosc decode not included' % (args.config.upper(), n_shards, per, cores, secs)),
+            'cpu_model': cpu_cluster.cpu_model(),
+            'workers_2': {'value': res[2][0], 'unit': 'rows/s', 'cores': 2, 'seconds': res[2][1]},
+            'single_worker_one_shard': single}
+
+
+def synth_config_id(config):
+    from bqueryd_amd import synth
+    return synth.CONFIG_ID[config]
 
 
 def _load_traffic(config, rows):
@@ -231,12 +259,10 @@ def main(argv=None):
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.config != 'c5':
         rate, secs = _cpu_baseline(cols, cfg)
-        cpu = {'value': rate, 'unit': 'rows/s', 'cores': 1, 'kind': 'port',
-               'sample': 'full %s shard (%d rows), oracle/cbquery.c single-threaded C port of '
-                         'bquery\'s multi-pass per-shard groupby (where mask, khash factorize, '
-                         'filter re-factorize, one pass per aggregation), best of 2 (%.2f s), '
-                         'host %s' % (args.config.upper(), rows, secs, platform.processor() or
-                                      platform.machine())}
+        single = {'value': rate, 'unit': 'rows/s', 'cores': 1,
+                  'sample': 'one %d-row %s shard, one worker (best of 2: %.2f s)' % (rows, args.config.upper(), secs)}
+        del cols
+        cpu = _cpu_cluster_baseline(cfg, args, rows, single)
     traffic = _load_traffic(args.config, rows)
     comm.close()
     if rank != 0:

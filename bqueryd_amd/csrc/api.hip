@@ -1275,9 +1275,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       hipFunction_t sfn = nullptr;
       if (fused && N >= jit_min_rows()) {
         const int cd_mode = d.cd.bitmap == nullptr ? 0 : (d.cd.lds_bitmap_words > 0 ? 1 : 2);
-        std::string spec = jit_spec(pc.p) + "#define BQ_SLOT_BITS " + std::to_string(d.slot_bits) +
-                           "\n#define BQ_SCD_CD " + std::to_string(cd_mode) + "\n";
-        if (const char* ev = getenv("BQGPU_SCD_EXPERIMENT")) spec += std::string("#define ") + ev + "\n";  // profiling only
+        std::string spec = jit_spec(pc.p) + "#define BQ_SCD_CD " + std::to_string(cd_mode) + "\n";
         sfn = jit_function(d.compact ? "bq_jit_scd_fused32" : "bq_jit_scd_fused", spec);
         c->last.specialized = sfn ? 1 : 0;
       }

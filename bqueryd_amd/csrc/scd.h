@@ -7,7 +7,7 @@
 // consumes it 64 rows per step in row order, one row per lane (coalesced 4- or 8-byte loads,
 // kScdAhead steps in flight).  Inside a step the lanes of one slot find each other through a
 // per-slot 64-bit lane mask in wave-private LDS (every lane ORs its bit, then reads the word
-// back; BQ_SCD_BALLOT_MATCH selects one ballot per slot-id bit instead); the previous row of a slot inside the step is the
+// back); the previous row of a slot inside the step is the
 // highest lower lane of its match mask (one bpermute); the slot's first lane in the step
 // folds the whole step into the per-slot state {last, first, rows, changes, first row} in LDS
 // with one read and one write.  Per-slot row counts and first rows come out of the same pass
@@ -130,28 +130,13 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         if (cc == c) vcd = v[c][0];
       }
       if (COMPACT) vb = (uint32_t)(vb - (uint64_t)d.vmin);
-      // lanes of this lane's slot: one ballot per slot-id bit
       uint64_t match = __ballot(act);
       if (match == 0) continue;
-#ifdef BQ_SCD_BALLOT_MATCH
-      // (alternative) one ballot per slot-id bit
-#ifdef BQ_SLOT_BITS
-#pragma unroll
-      for (int bit = 0; bit < BQ_SLOT_BITS; ++bit) {
-#else
-      for (int bit = 0; bit < d.slot_bits; ++bit) {
-#endif
-        const bool on = (s >> bit) & 1u;
-        const uint64_t bb = __ballot(act && on);
-        match &= on ? bb : ~bb;
-      }
-#else
       // lanes of this lane's slot: every lane ORs its bit into the slot's LDS mask word, then
       // reads the word back (a wave's LDS instructions execute in program order; OR does not
       // depend on the order of the lanes); the slot's first lane clears it below
       if (act) atomicOr(&tbl[s], 1ull << lane);
       match = act ? tbl[s] : 0ull;
-#endif
       const uint64_t below = match & lanes_below;
       const int pl = below ? 63 - __clzll((long long)below) : lane;
       const int hl = (act && match) ? 63 - __clzll((long long)match) : lane;
@@ -166,14 +151,8 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       const bool diff = act && below != 0 && !scd_equal(vb, pv, isf);
       const uint64_t dm = __ballot(diff);
       bool run_start = diff;  // first row of a value run of its slot (set below for first lanes)
-#ifdef BQ_SCD_SKIP_STATE
-      if (act && below == 0 && dm == 0x1234567ull) {
-#else
       if (act && below == 0) {
-#endif
-#ifndef BQ_SCD_BALLOT_MATCH
         tbl[s] = 0ull;  // after every lane's read of the mask (program order)
-#endif
         const uint32_t add_rows = (uint32_t)__popcll(match), add_ch = (uint32_t)__popcll(dm & match);
         if (COMPACT) {
           ScdSlot32 cur = st32[s];
@@ -207,7 +186,6 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
           st[s] = cur;
         }
       }
-#ifndef BQ_SCD_SKIP_CD
       // count_distinct of the same column: only the first row of a value run of its slot can
       // add a (slot, value) pair (every later row of the run repeats one already added), so
       // the pair check runs at run starts only (most rows of a sorted column skip it)
@@ -225,7 +203,6 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
           atomicAdd(&d.cd.out[s], 1ull);
         }
       }
-#endif
     }
   }
   // count_distinct: merge the workgroup's pair bitmap into the device bitmap; every pair bit
