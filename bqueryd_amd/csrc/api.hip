@@ -533,8 +533,9 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
       dk.range = r + 1;                                                       // 0 means 2^64
     }
     const unsigned __int128 rr = dk.range ? (unsigned __int128)dk.range : ((unsigned __int128)1 << 64);
-    space *= rr;
-    if (space > ((unsigned __int128)1 << 100)) space = ((unsigned __int128)1 << 100);
+    // saturate at 2^100 before the product can wrap (two full-range 64-bit keys: 2^128)
+    const unsigned __int128 cap100 = (unsigned __int128)1 << 100;
+    space = space > cap100 / rr ? cap100 : space * rr;
     bits += dk.range ? bits_for(dk.range) : 64;
   }
   pl.p.ncols = (int)pl.tcol.size();
@@ -558,12 +559,13 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
   const uint64_t kDenseMax = std::max<uint64_t>(1ull << 24, std::min<uint64_t>(2ull * (uint64_t)t->nrows, 1ull << 27));
   bool hash = any_float || space > kDenseMax;
   if (hash) {
-    if (any_float && q->n_keys > 1)
-      fail(BQG_E_UNSUPPORTED, "float groupby columns are supported only as the single key");
-    if (!any_float && bits > 63) fail(BQG_E_UNSUPPORTED, "groupby key space wider than 63 bits");
+    // wide keys (hash mode 2): float columns in a multi-column key, or packed codes over 63
+    // bits (e.g. a full-range int64 / uint64 key): the table holds a hash half and a
+    // representative row whose key values are compared in full
+    const bool wide = (any_float && q->n_keys > 1) || (!any_float && bits > 63);
     // packed power-of-two strides: last key in the low bits
     uint64_t shift = 0;
-    for (int k = q->n_keys - 1; k >= 0; --k) {
+    for (int k = wide ? -1 : q->n_keys - 1; k >= 0; --k) {
       DevKey& dk = pl.p.keys[k];
       if (dk.is_float) {
         dk.stride = 1;
@@ -581,7 +583,12 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     while (cap < 2 * est) cap <<= 1;
     pl.nslots = cap;
     pl.mode = kGlobalHash;
-    pl.p.hash = 1;
+    pl.p.hash = wide ? 2 : 1;
+    if (wide)
+      for (int k = 0; k < q->n_keys; ++k) {
+        pl.p.keys[k].stride = 1;
+        pl.p.keys[k].range = 0;
+      }
   } else {
     uint64_t stride = 1;
     for (int k = q->n_keys - 1; k >= 0; --k) {
@@ -636,6 +643,8 @@ void build_emit(bqg_table* t, const bqg_query* q, const Plan& pl, EmitParams& e,
   for (int k = 0; k < q->n_keys; ++k) {
     e.keys[k] = pl.p.keys[k];
     e.key_dtype[k] = t->cols[q->key_cols[k]].dtype;
+    const Column& kc = t->cols[q->key_cols[k]];
+    e.key_cols[k] = DevCol{kc.dev, kc.dtype, dtype_lg(kc.dtype)};
     EmitCol& ec = e.cols[k];
     ec.kind = 0;
     ec.key = k;

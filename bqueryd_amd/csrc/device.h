@@ -248,11 +248,34 @@ __device__ __forceinline__ uint32_t vals_pass(const ScanParams& p, int64_t row0,
   return pass;
 }
 
-// dense mixed-radix (or packed, hash mode) group code of each row
+// canonical 64-bit identity of a key value (float keys: NaN == NaN, -0.0 == +0.0)
+__device__ __forceinline__ uint64_t key_identity(uint64_t v, bool is_float) {
+  return is_float ? canon_f64_bits(v) : v;
+}
+
+// dense mixed-radix (or packed, hash mode 1) group code of each row; hash mode 2 (wide
+// keys: key spaces over 63 bits, float columns in a multi-column key): a 64-bit hash of the
+// keys' canonical values, resolved against the stored representative row (slot_lookup)
 template <int NC, int R>
 __device__ __forceinline__ void vals_code(const ScanParams& p, const uint64_t (&v)[NC][R], uint64_t (&code)[R]) {
 #pragma unroll
   for (int r = 0; r < R; ++r) code[r] = 0;
+  if (p.hash == 2) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) code[r] = 0x243F6A8885A308D3ull;
+#pragma unroll
+    for (int k = 0; k < BQ_LOOP_BOUND(p.nkeys, kMaxKeys); ++k) {
+      if (k >= p.nkeys) break;
+      const DevKey& key = p.keys[k];
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (key.col == c) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) code[r] = mix64(code[r] ^ (key_identity(v[c][r], key.is_float) + (uint64_t)k));
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < BQ_LOOP_BOUND(p.nkeys, kMaxKeys); ++k) {
     if (k >= p.nkeys) break;
@@ -293,6 +316,59 @@ __device__ __forceinline__ uint64_t hash_slot(const SlotArrays& sa, uint64_t mas
   return kEmpty;
 }
 
+// key value of column `kc` at `row` (a slot's representative row), canonical
+__device__ __forceinline__ uint64_t key_at_row(const DevCol& kc, bool is_float, uint32_t row) {
+  Chunk c;
+  row_word_to_chunk(c, kc, row, load_row_word(kc, row));
+  uint64_t v[1];
+  decode<1>(c, kc.dtype, v);
+  return key_identity(v[0], is_float);
+}
+
+// Slot of row r's key: hash modes 1 (packed code stored in the table) and 2 (wide keys: the
+// table word is hash_hi32 << 32 | representative row; a candidate with the same hash half
+// matches only when every key value at its representative row equals this row's).  The
+// representative is the inserting row, written with the claim itself (one 64-bit CAS), so a
+// reader never sees a half-built entry.  kEmpty: absent (lookup) or table full.
+template <int NC, int R>
+__device__ __forceinline__ uint64_t slot_lookup(const ScanParams& p, const SlotArrays& sa, uint64_t mask,
+                                                const uint64_t (&v)[NC][R], const uint64_t (&code)[R], int r,
+                                                uint32_t row, bool insert) {
+  if (p.hash != 2) return hash_slot(sa, mask, code[r], insert);
+  const uint32_t hi = (uint32_t)(code[r] >> 32);
+  uint64_t pos = code[r] & mask;
+  for (uint64_t i = 0; i <= mask; ++i) {
+    unsigned long long w = sa.keys[pos];
+    if (w == kEmpty) {
+      if (!insert) return kEmpty;
+      const unsigned long long mine = ((unsigned long long)hi << 32) | row;
+      const unsigned long long prev = atomicCAS(&sa.keys[pos], kEmpty, mine);
+      if (prev == kEmpty) {
+        const unsigned int f = atomicAdd(sa.hash_fill, 1u);
+        if ((uint64_t)(f + 1) * 2 > mask + 1) atomicOr(sa.overflow, 1u);
+        return pos;
+      }
+      w = prev;
+    }
+    if ((uint32_t)(w >> 32) == hi) {
+      const uint32_t rep = (uint32_t)w;
+      bool same = true;
+#pragma unroll
+      for (int k = 0; k < BQ_LOOP_BOUND(p.nkeys, kMaxKeys); ++k) {
+        if (k >= p.nkeys) break;
+        const DevKey& key = p.keys[k];
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+          if (key.col == c) same &= key_at_row(p.cols[c], key.is_float, rep) == key_identity(v[c][r], key.is_float);
+      }
+      if (same) return pos;
+    }
+    pos = (pos + 1) & mask;
+  }
+  atomicOr(sa.overflow, 1u);
+  return kEmpty;
+}
+
 // ------------------------------------------------------------------------------------
 // Emit helpers (shared by the private finish kernel and the generic emit kernel)
 // ------------------------------------------------------------------------------------
@@ -319,7 +395,10 @@ __device__ __forceinline__ void emit_slot(const EmitParams& e, uint64_t slot, ui
     uint64_t bits = 0;
     if (c.kind == 0) {
       const DevKey& k = e.keys[c.key];
-      if (k.is_float) {
+      if (e.hash == 2) {  // wide keys: the value at the slot's representative row
+        bits = key_at_row(e.key_cols[c.key], k.is_float, (uint32_t)code);
+        if (c.out_dtype == BQG_F32) bits = __float_as_uint((float)as_f64(bits));
+      } else if (k.is_float) {
         bits = code;
         if (c.out_dtype == BQG_F32) bits = __float_as_uint((float)as_f64(code));
       } else {

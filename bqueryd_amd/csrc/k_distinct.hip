@@ -34,7 +34,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_count_distinct(ScanParams p, Slot
       if (!(pass & (1u << r))) continue;
       uint64_t s = code[r];
       if (HASH) {
-        s = hash_slot(sa, hmask, code[r], false);
+        s = slot_lookup<NC, 4>(p, sa, hmask, v, code, r, (uint32_t)(row0 + r), false);
         if (s == kEmpty) continue;
       }
       uint64_t vcode = 0;
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_scd(ScanParams p, SlotArrays sa, 
         vals_code<NC, 1>(p, v, code);
         slot = code[0];
         if (HASH && act) {
-          slot = hash_slot(sa, hmask, code[0], false);
+          slot = slot_lookup<NC, 1>(p, sa, hmask, v, code, 0, (uint32_t)row, false);
           if (slot == kEmpty) act = false;
         }
 #pragma unroll

@@ -102,11 +102,11 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_global(ScanParams p, SlotArr
     for (int r = 0; r < 4; ++r) {
       if (pass & (1u << r)) {
         uint64_t s = code[r];
+        const uint32_t row = (uint32_t)(row0 + r);
         if (HASH) {
-          s = hash_slot(sa, hmask, code[r], true);
+          s = slot_lookup<NC, 4>(p, sa, hmask, v, code, r, row, true);
           if (s == kEmpty) continue;
         }
-        const uint32_t row = (uint32_t)(row0 + r);
         atomicAdd(&sa.cnt[s], 1ull);
         if (sa.fst[s] > row) atomicMin(&sa.fst[s], row);
 #pragma unroll

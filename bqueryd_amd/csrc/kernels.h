@@ -25,6 +25,7 @@ struct EmitParams {
   int32_t nsum2;  // std second-moment states in SlotArrays::acc2
   DevKey keys[kMaxKeys];
   int32_t key_dtype[kMaxKeys];
+  DevCol key_cols[kMaxKeys];  // hash mode 2: key columns, read at each slot's representative row
   EmitCol cols[kMaxKeys + kMaxAggs];
   const unsigned long long* cd[kMaxAggs];        // count_distinct per slot
   const unsigned long long* scd_changes[kMaxAggs];

@@ -97,6 +97,48 @@ def test_hash_mode_multi_key(oracle_c):
     run_both(cols, ['b', 'a'], [['v', 'mean', 'm']], [('b', '>', 7)], oracle_c)
 
 
+def _wide_key_cols(n, seed):
+    rng = np.random.default_rng(seed)
+    i64 = rng.integers(-2**63, 2**63 - 1, 400, dtype=np.int64)
+    i64[:2] = [-2**63, 2**63 - 1]  # both ends of the range
+    u64 = rng.integers(0, 2**64 - 1, 300, dtype=np.uint64)
+    u64[:2] = [0, 2**64 - 1]
+    f = np.array([0.5, -0.0, 0.0, np.nan, 3.25, -7.0, 1e300, -1e-300])
+    return OrderedDict(a=i64[rng.integers(0, len(i64), n)], u=u64[rng.integers(0, len(u64), n)],
+                       f=f[rng.integers(0, len(f), n)], g=rng.integers(0, 5, n).astype(np.int16),
+                       v=rng.integers(-1000, 1000, n).astype(np.int64), w=np.round(rng.normal(size=n) * 64) / 64)
+
+
+def _assert_float_key_tables(got, ref, float_keys):
+    """keys compare by value (-0.0 == +0.0, NaN == NaN: bquery's khash identity); the rest exactly
+    or within the float tolerance"""
+    for k in float_keys:
+        np.testing.assert_array_equal(got[k], ref[k])
+    assert_tables_equal(OrderedDict((c, v) for c, v in got.items() if c not in float_keys),
+                        OrderedDict((c, v) for c, v in ref.items() if c not in float_keys))
+
+
+@pytest.mark.parametrize('keys', [['a'], ['u'], ['a', 'u'], ['f', 'g'], ['g', 'f', 'a'], ['u', 'f']])
+def test_wide_key_spaces(keys, oracle_c):
+    """Key spaces the packed 64-bit code cannot hold (hash mode 2): a full-range int64 or
+    uint64 key, composite keys wider than 63 bits, float columns inside a multi-column key."""
+    cols = _wide_key_cols(120_000, 21)
+    aggs = [['v', 'sum', 'vs'], ['w', 'mean', 'wm'], ['v', 'count', 'n'], ['g', 'count_distinct', 'gcd'],
+            ['w', 'std', 'wsd']]
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(keys, aggs)
+        assert t.dev.last_timing()['mode'] == 3  # global hash
+        got_f, _ = t.groupby(keys, aggs[:3], where_terms=[('v', '>', 100)])
+    finally:
+        t.close()
+    ref = oracle_c.groupby(cols, keys, aggs)
+    ref_f = oracle_c.groupby(cols, keys, aggs[:3], oracle_c.where_terms(cols, [('v', '>', 100)]))
+    fk = [k for k in keys if k == 'f']
+    _assert_float_key_tables(got, ref, fk)
+    _assert_float_key_tables(got_f, ref_f, fk)
+
+
 def test_float_key(oracle_c):
     rng = np.random.default_rng(8)
     n = 20_000
