@@ -40,6 +40,20 @@ def _dist_env():
     return ws, rank, local
 
 
+class _stdout_to_stderr:
+    """Route file descriptor 1 to stderr for a block (native libraries printing to stdout)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 class _Comm:
     """Barrier / max-reduce across ranks (gloo, CPU only).  Single process: no-ops."""
 
@@ -180,8 +194,10 @@ def main(argv=None):
             tables.append(ShardTable(sc, device=dev))
         # RCCL communicator inside libbqgpu (the exchange runs on device buffers); gloo only
         # hands rank 0's unique id to the other ranks
-        uid = comm.broadcast_bytes(bdist.new_unique_id() if rank == 0 else None)
-        rccl = bdist.RcclComm(dev, rank, ws, uid)
+        # (librccl prints a version banner on stdout at init: kept off the one-JSON-line stdout)
+        with _stdout_to_stderr():
+            uid = comm.broadcast_bytes(bdist.new_unique_id() if rank == 0 else None)
+            rccl = bdist.RcclComm(dev, rank, ws, uid)
         colo = bdist.ColocatedShards(tables)
         fused = not args.c5_per_shard and bdist.decomposable(cfg['aggs'])
         if fused:

@@ -233,7 +233,8 @@ bqg_table* concat_tables(bqg_ctx* c, const std::vector<bqg_table*>& parts, const
       for (int j = 0; j < (int)dts.size(); ++j) ck(c, bqg_push_chunk(out.t, j, col_ptr(c, p, j), n, off));
     off += n;
   }
-  ck(c, bqg_table_sync(out.t));
+  // no bqg_table_sync: the copies are ordered on the context's stream before anything that
+  // reads the table, and the regroup's planner computes the key statistics it needs
   return out.release();
 }
 
@@ -262,6 +263,7 @@ struct Local {
   CommState* st = nullptr;
   hipStream_t stream = nullptr;
   TableOwner L;                   // this rank's reduced rows (+ partition column)
+  bqg_table* Lv = nullptr;        // the table whose rows this rank sends (L, or the caller's)
   std::vector<int64_t> to_peer;   // rows for each destination rank
   std::vector<size_t> send_off;   // byte offset of each destination's block
   TableOwner R;                   // rows received from every rank, then reduced
@@ -408,12 +410,17 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     for (bqg_table* t : l.tables)
       if (nrows_of(l.ctx, t) > 0) parts.push_back(t);
     if (!parts.empty()) {
-      TableOwner cat;
-      cat.t = concat_tables(l.ctx, parts, dts);
-      if (reduced && parts.size() == 1) l.L.t = cat.release();
-      else l.L.t = regroup(l.ctx, cat.t, n_keys, ncols);
+      if (reduced && parts.size() == 1 && W == 1) {
+        l.Lv = parts[0];  // one rank, keys already unique: the caller's table is sent as it is
+      } else {
+        TableOwner cat;
+        cat.t = concat_tables(l.ctx, parts, dts);
+        if (reduced && parts.size() == 1) l.L.t = cat.release();
+        else l.L.t = regroup(l.ctx, cat.t, n_keys, ncols);
+        l.Lv = l.L.t;
+      }
     }
-    const int64_t nl = l.L.t ? nrows_of(l.ctx, l.L.t) : 0;
+    const int64_t nl = l.Lv ? nrows_of(l.ctx, l.Lv) : 0;
     std::vector<bqg_table*> per(W, nullptr);
     struct PerOwner {
       std::vector<bqg_table*>& v;
@@ -422,13 +429,14 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
           if (t) (void)bqg_table_destroy(t);
       }
     } per_owner{per};
-    if (nl > 0) {
+    if (nl > 0 && W == 1) {
+      l.to_peer[0] = nl;  // one rank: every row goes to itself, no partition pass
+    } else if (nl > 0) {
       int32_t pcol = -1;
       ck(l.ctx, bqg_table_add_column(l.L.t, BQG_U32, &pcol));
       ck(l.ctx, bqg_hash_partition(l.ctx, l.L.t, n_keys, key_idx.data(), W, pcol, l.to_peer.data()));
       for (int d = 0; d < W; ++d) {
         if (!l.to_peer[d]) continue;
-        if (W == 1) break;  // everything goes to the one rank: send the table itself
         const int64_t dv = d;
         bqg_term term{pcol, BQG_T_EQ, 1, &dv, nullptr};
         bqg_query q{};
@@ -442,7 +450,7 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     for (int d = 0; d < W; ++d) l.send_off[d + 1] = l.send_off[d] + block_bytes(dts, l.to_peer[d]);
     unsigned char* sb = (unsigned char*)l.st->send.ensure(l.send_off[W]);
     for (int d = 0; d < W; ++d)
-      if (l.to_peer[d]) pack_block(l.ctx, l.stream, W == 1 ? l.L.t : per[d], dts, l.to_peer[d], sb + l.send_off[d]);
+      if (l.to_peer[d]) pack_block(l.ctx, l.stream, W == 1 ? l.Lv : per[d], dts, l.to_peer[d], sb + l.send_off[d]);
     // the row counts this rank sends, for the count exchange
     int64_t* cnt = (int64_t*)l.st->counts.ensure(sizeof(int64_t) * (size_t)W * (W + 2));
     HIPCK(hipMemcpyAsync(cnt, l.to_peer.data(), sizeof(int64_t) * W, hipMemcpyHostToDevice, l.stream));
@@ -490,6 +498,7 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     Local& l = ranks[i];
     HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
     l.L.reset();  // the local rows have been sent
+    l.Lv = nullptr;
     int64_t total = 0;
     for (int s = 0; s < W; ++s) total += from_peer[i][s];
     l.n_recv = total;
@@ -501,7 +510,6 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       unpack_block(l.ctx, got.t, dts, from_peer[i][s], off, (const unsigned char*)l.st->recv.p + recv_off[i][s]);
       off += from_peer[i][s];
     }
-    ck(l.ctx, bqg_table_sync(got.t));
     // one source's rows are already unique by key: only rows from two or more sources
     // need the re-group
     int sources = 0;
@@ -525,8 +533,10 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     HIPCK(hipMemcpyAsync(part_rows.data(), (int64_t*)l.st->counts.p + W, sizeof(int64_t) * W, hipMemcpyDeviceToHost,
                          l.stream));
     HIPCK(hipStreamSynchronize(l.stream));
-    // pack this rank's reduced partition into the send buffer (sent to rank 0, or kept there)
-    if (l.R.t) pack_block(l.ctx, l.stream, l.R.t, dts, nrows_of(l.ctx, l.R.t), (unsigned char*)l.st->send.ensure(block_bytes(dts, nrows_of(l.ctx, l.R.t))));
+    // pack this rank's reduced partition into the send buffer (rank 0 keeps its own table)
+    if (l.R.t && l.st->rank != 0)
+      pack_block(l.ctx, l.stream, l.R.t, dts, nrows_of(l.ctx, l.R.t),
+                 (unsigned char*)l.st->send.ensure(block_bytes(dts, nrows_of(l.ctx, l.R.t))));
   }
   for (int s = 0; s < W; ++s) goff[s + 1] = goff[s] + block_bytes(dts, part_rows[s]);
   for (Local& l : ranks)
@@ -556,20 +566,26 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       *l.out = nullptr;
       continue;
     }
-    int64_t total = 0;
+    int64_t total = 0, others = 0;
     for (int s = 0; s < W; ++s) total += part_rows[s];
+    others = total - part_rows[0];
+    if (others == 0 && l.R.t) {  // every merged row is in rank 0's own partition
+      HIPCK(hipStreamSynchronize(l.stream));
+      *l.out = l.R.release();
+      continue;
+    }
     TableOwner res;
     ck(l.ctx, bqg_table_create(l.ctx, total, ncols, dts.data(), &res.t));
     int64_t off = 0;
     for (int s = 0; s < W; ++s) {
-      if (part_rows[s]) {
-        const unsigned char* src =
-            s == 0 ? (const unsigned char*)l.st->send.p : (const unsigned char*)l.st->recv.p + goff[s];
-        unpack_block(l.ctx, res.t, dts, part_rows[s], off, src);
+      if (part_rows[s] && s == 0) {
+        for (int j = 0; j < ncols; ++j) ck(l.ctx, bqg_push_chunk(res.t, j, col_ptr(l.ctx, l.R.t, j), part_rows[0], 0));
+      } else if (part_rows[s]) {
+        unpack_block(l.ctx, res.t, dts, part_rows[s], off, (const unsigned char*)l.st->recv.p + goff[s]);
       }
       off += part_rows[s];
     }
-    ck(l.ctx, bqg_table_sync(res.t));
+    HIPCK(hipStreamSynchronize(l.stream));
     *l.out = res.release();
   }
   for (Local& l : ranks) l.R.reset();
