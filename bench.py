@@ -118,22 +118,33 @@ def _cpu_cluster_baseline(cfg, args, rows, single):
     controller + N single-threaded workers running the C port of bquery's per-shard groupby
     over 8 shards of the workload, client sum-merge (rpc.py:164-173); N = 2 and N = all
     cores.  ``value`` is the all-cores cluster."""
+    import shutil
+    import tempfile
     from oracle import cpu_cluster
     cores = cpu_cluster.host_cores()
     n_shards = 8
     per = max(1, rows // n_shards)
     counts = sorted(set([2, cores]))
-    res, _ = cpu_cluster.run(cfg, n_shards, per, counts, config_id=synth_config_id(args.config),
-                             variant=args.variant)
-    rate, secs = res[cores]
+    tmp = tempfile.mkdtemp(prefix='bqgpu-cpu-cluster-')
+    try:
+        res, _ = cpu_cluster.run(cfg, n_shards, per, counts, config_id=synth_config_id(args.config),
+                                 variant=args.variant, bcolz_dir=tmp)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    rate, secs = res[cores]['bcolz']
     return {'value': rate, 'unit': 'rows/s', 'cores': cores, 'kind': 'port',
-            'sample': ('%s as %d shards x %d rows: 1 controller + %d single-threaded worker processes '
-                       '(oracle/cbquery.c, the C port of bquery\'s multi-pass per-shard groupby: where mask, '
-                       'khash factorize, filter re-factorize, one pass per aggregation; misc/supervisor.conf:21, '
-                       'worker.py:40) + client sum-merge (rpc.py:164-173), best of 2 (%.3f s); shards in shared '
-                       'memory, blosc decode not included' % (args.config.upper(), n_shards, per, cores, secs)),
+            'sample': ('%s as %d bcolz shards x %d rows (lz4): 1 controller + %d single-threaded worker processes, '
+                       'each reading + blosc-decoding its shard on one thread and running oracle/cbquery.c (the C '
+                       'port of bquery\'s multi-pass per-shard groupby: where mask, khash factorize, filter '
+                       're-factorize, one pass per aggregation; misc/supervisor.conf:21, worker.py:40) + the client '
+                       'sum-merge (rpc.py:164-173); best of 2: %.3f s' % (args.config.upper(), n_shards, per, cores,
+                                                                           secs)),
             'cpu_model': cpu_cluster.cpu_model(),
-            'workers_2': {'value': res[2][0], 'unit': 'rows/s', 'cores': 2, 'seconds': res[2][1]},
+            'decoded_columns': {'value': res[cores]['decoded'][0], 'unit': 'rows/s', 'cores': cores,
+                                'seconds': res[cores]['decoded'][1],
+                                'sample': 'the same, columns handed over decoded (shared memory): compute only'},
+            'workers_2': {'value': res[2]['bcolz'][0], 'unit': 'rows/s', 'cores': 2, 'seconds': res[2]['bcolz'][1],
+                          'decoded_value': res[2]['decoded'][0]},
             'single_worker_one_shard': single}
 
 

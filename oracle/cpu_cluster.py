@@ -13,11 +13,11 @@ controller sends one calc message per shard file to a free worker (``controller.
 * the parent is the controller (a shared queue hands out one shard index per message, so a
   free worker takes the next shard) and the client (``bquery_oracle.client_merge`` with
   ``aggregate=True`` over the replies);
-* shards are the bench's synthetic taxi shards, generated once before the timed region into
-  shared memory that every worker maps (a node's data dir: any free worker can take any
-  shard); the reference reads them from bcolz files, and their blosc decode is NOT included,
-  so this baseline is the compute of the reference's calc path only -- an upper bound on its
-  throughput.
+* shards are the bench's synthetic taxi shards, written before the timed region as bcolz
+  ctables (a node's data dir: any free worker can take any shard); the worker that takes a
+  message reads and blosc-decodes the shard's columns on its one thread, as the reference's
+  worker does, then runs the C port.  A second timing hands the workers the decoded columns
+  through shared memory: the compute of the calc path alone.
 
 Timed: from the first dispatched message to the merged table on the client.
 """
@@ -29,25 +29,35 @@ import platform
 import time
 
 
-def _worker(wid, layout, cfg, tasks, results, ready):
+def _worker(wid, layout, files, cfg, tasks, results, ready):
     import numpy as np
     from multiprocessing import shared_memory
     from oracle import cbquery
     cbquery.lib()
-    # the node's shard files, shared read-only by every worker (the reference's data dir)
     blocks, data = [], {}
-    for i, cols in layout.items():
-        data[i] = {}
-        for name, (shm_name, dtype, n) in cols.items():
-            shm = shared_memory.SharedMemory(name=shm_name)
-            blocks.append(shm)
-            data[i][name] = np.ndarray((n,), dtype=np.dtype(dtype), buffer=shm.buf)
+    if files is None:
+        # decoded shards, shared read-only by every worker
+        for i, cols in layout.items():
+            data[i] = {}
+            for name, (shm_name, dtype, n) in cols.items():
+                shm = shared_memory.SharedMemory(name=shm_name)
+                blocks.append(shm)
+                data[i][name] = np.ndarray((n,), dtype=np.dtype(dtype), buffer=shm.buf)
+    else:
+        from bqueryd_amd import bcolz_io
+        bcolz_io.blosc()
     ready.put(wid)
     while True:
         i = tasks.get()
         if i is None:
             break
-        out = cbquery.handle_work(data[i], cfg['groupby'], cfg['aggs'], cfg['where'])
+        if files is None:
+            cols = data[i]
+        else:
+            # the shard's bcolz columns, blosc-decoded on this worker's one thread
+            # (bcolz.set_nthreads(1), worker.py:40) -- what bquery iterates over
+            cols = bcolz_io.read_ctable(files[i], columns=list(layout[i]), nthreads=1)
+        out = cbquery.handle_work(cols, cfg['groupby'], cfg['aggs'], cfg['where'])
         results.put((i, {k: np.array(v) for k, v in out.items()}))
     data.clear()
     for shm in blocks:
@@ -75,9 +85,13 @@ def cpu_model():
     return platform.processor() or platform.machine()
 
 
-def run(cfg, n_shards, rows_per_shard, worker_counts, config_id=2, variant='exact', reps=2):
+def run(cfg, n_shards, rows_per_shard, worker_counts, config_id=2, variant='exact', reps=2, bcolz_dir=None):
     """Time one aggregate=True query over ``n_shards`` shards with each worker count in
-    ``worker_counts``; returns {n_workers: (rows/s, best seconds)} and the last merged table."""
+    ``worker_counts``; returns {n_workers: {'decoded': (rows/s, s), 'bcolz': (rows/s, s)}} and
+    the last merged table.  'decoded': the shards' columns already in (shared) memory -- the
+    compute of the calc path alone; 'bcolz' (when ``bcolz_dir`` is given): the shards are
+    bcolz ctables (lz4, the writer of bqueryd_amd.bcolz_io) under ``bcolz_dir``, read and
+    blosc-decoded by the worker that takes the message, as the reference's worker does."""
     from multiprocessing import shared_memory
 
     import numpy as np
@@ -85,11 +99,17 @@ def run(cfg, n_shards, rows_per_shard, worker_counts, config_id=2, variant='exac
     from bqueryd_amd import synth
     from oracle import bquery_oracle as bo
     columns = synth.query_columns(cfg)
-    shms, layout, out, merged = [], {}, {}, None
+    shms, layout, out, merged, files = [], {}, {}, None, None
+    if bcolz_dir is not None:
+        import os as _os
+        from bqueryd_amd import bcolz_io
+        files = {i: _os.path.join(bcolz_dir, 'shard-%d.bcolzs' % i) for i in range(n_shards)}
     try:
         for i in range(n_shards):
             cols = synth.taxi_shard(rows_per_shard, config_id=config_id, n_shards=n_shards, shard=i,
                                     variant=variant, columns=columns)
+            if files is not None:
+                bcolz_io.write_ctable(files[i], cols)
             layout[i] = {}
             for name, arr in cols.items():
                 shm = shared_memory.SharedMemory(create=True, size=max(1, arr.nbytes))
@@ -98,9 +118,11 @@ def run(cfg, n_shards, rows_per_shard, worker_counts, config_id=2, variant='exac
                 layout[i][name] = (shm.name, arr.dtype.str, len(arr))
             del cols
         ctx = mp.get_context('spawn')
-        for n_workers in worker_counts:
+        for n_workers, source in [(n, src) for n in worker_counts for src in
+                                  (['decoded'] + (['bcolz'] if files is not None else []))]:
             tasks, results, ready = ctx.Queue(), ctx.Queue(), ctx.Queue()
-            procs = [ctx.Process(target=_worker, args=(w, layout, cfg, tasks, results, ready), daemon=True)
+            procs = [ctx.Process(target=_worker, args=(w, layout, files if source == 'bcolz' else None, cfg,
+                                                       tasks, results, ready), daemon=True)
                      for w in range(n_workers)]
             for p in procs:
                 p.start()
@@ -126,7 +148,7 @@ def run(cfg, n_shards, rows_per_shard, worker_counts, config_id=2, variant='exac
                 for p in procs:
                     if p.is_alive():
                         p.terminate()
-            out[n_workers] = (n_shards * rows_per_shard / best, best)
+            out.setdefault(n_workers, {})[source] = (n_shards * rows_per_shard / best, best)
     finally:
         for shm in shms:
             shm.close()

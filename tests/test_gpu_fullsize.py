@@ -77,3 +77,40 @@ def test_c4_full_size(order, oracle_c):
     print('C4 %s: mode %d, %d groups, scd total %d' % (order, mode, len(ref['pc_scd']), int(ref['pc_scd'].sum())))
     assert mode == 5  # the fused distinct pass
     assert_tables_equal(got, ref)
+
+
+def test_float32_sum_realistic_groups(oracle_c):
+    """float32 sums on cent-rounded data with 10^5 - 10^6 rows per group.
+
+    bquery accumulates a float32 sum in float32 in row order (the oracle's restatement); at
+    these group sizes that running sum drifts from the true sum by 2e-6 - 2e-4 relative
+    (stagnation: an addend below half an ulp of the running sum is lost), and no parallel
+    reduction can reproduce the drift.  libbqgpu defines a float32 sum as the float64 sum of
+    the values rounded once to float32.  Checked here: bit-exact against that
+    definition (float64 sums of cent values are exact to well below a float32 ulp), within the
+    oracle's own drift of its row-order value, and the count / mean columns against the
+    oracle at the usual tolerances."""
+    rng = np.random.default_rng(31)
+    n = 4_000_000
+    cols = {'g': rng.integers(0, 8, n).astype(np.int32),
+            'f': np.round(np.clip(rng.lognormal(2.3, 0.6, n), 2.5, 500.0), 2).astype(np.float32)}
+    aggs = [['f', 'sum', 'fs'], ['f', 'mean', 'fm'], ['f', 'count', 'n']]
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(['g'], aggs)
+    finally:
+        t.close()
+    ref = oracle_c.groupby(cols, ['g'], aggs)
+    np.testing.assert_array_equal(got['g'], ref['g'])
+    np.testing.assert_array_equal(got['n'], ref['n'])
+    np.testing.assert_allclose(got['fm'], ref['fm'], rtol=1e-12, atol=0)
+    # float32 values of magnitude < 512 are multiples of 2^-20 or coarser, so float64 sums of
+    # up to ~10^6 of them are exact in any order: one rounding to float32 is the definition
+    label = np.empty(int(ref['g'].max()) + 1, np.int64)
+    label[ref['g']] = np.arange(len(ref['g']))
+    exact = np.bincount(label[cols['g']], weights=cols['f'].astype(np.float64), minlength=len(ref['g']))
+    np.testing.assert_array_equal(got['fs'], exact.astype(np.float32))
+    drift = np.abs(ref['fs'].astype(np.float64) - exact) / exact
+    print('float32 row-order drift of the reference restatement: max %.2e' % drift.max())
+    assert got['fs'].dtype == np.float32
+    np.testing.assert_allclose(got['fs'], ref['fs'], rtol=max(1e-6, 2 * float(drift.max())), atol=0)
