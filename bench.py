@@ -186,7 +186,8 @@ def main(argv=None):
     from bqueryd_amd.engine import Device, ShardTable
 
     cfg = synth.CONFIGS[args.config]
-    dev = Device(local)
+    # BQGPU_BENCH_DEVICE pins every rank to one GPU (rehearsing the multi-rank path on a one-GPU box)
+    dev = Device(int(os.environ.get('BQGPU_BENCH_DEVICE', local)))
     npass_expected = None
     timings = []
     phase = []  # C5: (shard queries s, merge s) per step
