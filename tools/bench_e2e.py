@@ -129,8 +129,28 @@ def main():
                                 'rows_per_s': total_rows / cold[0],
                                 'note': 'includes bcolz decode on the host and the H2D copy'}
 
+            # node-level message: the node's files in one message, one merged reply
+            def node_query(calc):
+                m = messages.CalcMessage({'payload': 'groupby', 'token': 'ab' * 8, 'filename': files[0]})
+                m.set_args_kwargs([list(files), GROUPBY, AGGS, []], {'aggregate': True})
+                t0 = time.perf_counter()
+                data = calc.handle_work(m)['data']
+                t1 = time.perf_counter()
+                df = rpc.uncompress_groupby_to_df(rpc.tar_of_tars({files[0]: data}), GROUPBY, AGGS, [],
+                                                  aggregate=True, device=dev)
+                t2 = time.perf_counter()
+                check(df)
+                return t2 - t0, t1 - t0, t2 - t1
+
+            node_query(calc)
+            node = min((node_query(calc) for _ in range(args.reps)), key=lambda x: x[0])
+            line['gpu_node_warm'] = {'s_per_query': node[0], 'worker_s': node[1], 'client_merge_s': node[2],
+                                     'rows_per_s': total_rows / node[0],
+                                     'note': 'one node-level message (args[0] = the files, aggregate=True): one '
+                                             'pass over the resident shard union + RCCL merge, one reply'}
+
         # CPU: the reference's architecture (one calc per shard on a pool of worker processes)
-        ctx = mp.get_context('fork')
+        ctx = mp.get_context('spawn')  # no fork of a process that initialised the GPU
         with ctx.Pool(args.cpu_workers) as pool:
             pool.map(_cpu_task, [(os.path.join(data_dir, files[0]),)])
             best = None
