@@ -59,6 +59,16 @@ class Timing(ctypes.Structure):
                 ('bytes', ctypes.c_int64), ('mode', ctypes.c_int32), ('specialized', ctypes.c_int32)]
 
 
+# enum bqg_decode
+DECODE_AUTO, DECODE_HOST, DECODE_DEVICE = 0, 1, 2
+DECODE_CODE = {'auto': DECODE_AUTO, 'host': DECODE_HOST, 'device': DECODE_DEVICE}
+
+
+class IngestStats(ctypes.Structure):
+    _fields_ = [('chunks', ctypes.c_int64), ('compressed_bytes', ctypes.c_int64), ('bytes', ctypes.c_int64),
+                ('device_splits', ctypes.c_int64), ('host_chunks', ctypes.c_int64), ('decoder', ctypes.c_int32)]
+
+
 class BqgError(RuntimeError):
     pass
 
@@ -87,6 +97,7 @@ _PROTOS = {
     'bqg_table_add_column': ([_P, _I32, ctypes.POINTER(_I32)], ctypes.c_int),
     'bqg_push_chunk': ([_P, _I32, _P, _I64, _I64], ctypes.c_int),
     'bqg_table_load_carray': ([_P, _I32, ctypes.c_char_p, _I64, _I32], ctypes.c_int),
+    'bqg_table_load_carray_ex': ([_P, _I32, ctypes.c_char_p, _I64, _I32, _I32, _P], ctypes.c_int),
     'bqg_table_sync': ([_P], ctypes.c_int),
     'bqg_table_column_ptr': ([_P, _I32, ctypes.POINTER(_P)], ctypes.c_int),
     'bqg_table_stats': ([_P, _I32, ctypes.POINTER(_I64), ctypes.POINTER(_I64),

@@ -1638,12 +1638,14 @@ int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows, i
   });
 }
 
-int bqg_table_load_carray(bqg_table* t, int32_t col, const char* carray_dir, int64_t chunklen, int32_t nthreads) {
+int bqg_table_load_carray_ex(bqg_table* t, int32_t col, const char* carray_dir, int64_t chunklen, int32_t nthreads,
+                             int32_t decode, bqg_ingest_stats* stats) {
   bqg_ctx* c = t->ctx;
   return guard(c, [&] {
     if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
     if (!carray_dir) fail(BQG_E_INVALID, "null carray directory");
     if (chunklen <= 0) fail(BQG_E_INVALID, "chunklen must be positive");
+    if (decode < BQG_DECODE_AUTO || decode > BQG_DECODE_DEVICE) fail(BQG_E_INVALID, "unknown decoder %d", decode);
     Column& k = t->cols[col];
     k.stats.valid = false;
     HIPCHECK(hipStreamSynchronize(c->stream));  // the column's zero-fill has landed
@@ -1655,9 +1657,26 @@ int bqg_table_load_carray(bqg_table* t, int32_t col, const char* carray_dir, int
     job.itemsize = (int)dtype_size(k.dtype);
     job.chunklen = chunklen;
     job.nthreads = nthreads;
+    job.device_decode = decode != BQG_DECODE_HOST;
+    job.stream = c->stream;
+    IngestStats st;
     std::string err;
-    if (ingest_carray(job, c->ingest, nullptr, err) != 0) fail(BQG_E_INVALID, "%s", err.c_str());
+    const int rc = job.device_decode ? ingest_carray_device(job, c->ingest, &st, err)
+                                     : ingest_carray(job, c->ingest, &st, err);
+    if (rc != 0) fail(BQG_E_INVALID, "%s", err.c_str());
+    if (stats) {
+      stats->chunks = st.chunks;
+      stats->compressed_bytes = st.compressed_bytes;
+      stats->bytes = st.bytes;
+      stats->device_splits = st.device_splits;
+      stats->host_chunks = job.device_decode ? st.host_fallback : st.chunks;
+      stats->decoder = job.device_decode ? BQG_DECODE_DEVICE : BQG_DECODE_HOST;
+    }
   });
+}
+
+int bqg_table_load_carray(bqg_table* t, int32_t col, const char* carray_dir, int64_t chunklen, int32_t nthreads) {
+  return bqg_table_load_carray_ex(t, col, carray_dir, chunklen, nthreads, BQG_DECODE_AUTO, nullptr);
 }
 
 int bqg_table_sync(bqg_table* t) {

@@ -31,6 +31,7 @@
 #include <thread>
 #include <vector>
 
+#include "blosc_gpu.h"
 #include "ingest.h"
 
 namespace bqg {
@@ -98,6 +99,14 @@ bool read_file(const std::string& path, std::vector<unsigned char>& buf, std::st
 }  // namespace
 
 IngestPool::~IngestPool() {
+  for (DecodeSlot& d : slots) {
+    if (d.done) (void)hipEventSynchronize(d.done);
+    if (d.host) (void)hipHostFree(d.host);
+    if (d.dev) (void)hipFree(d.dev);
+    if (d.tmp) (void)hipFree(d.tmp);
+    if (d.done) (void)hipEventDestroy(d.done);
+  }
+  if (bad) (void)hipFree(bad);
   for (IngestWorker& w : workers) {
     if (w.stream) (void)hipStreamSynchronize(w.stream);
     for (int k = 0; k < 2; ++k) {
@@ -244,6 +253,373 @@ int ingest_carray(const IngestJob& job, IngestPool& pool, IngestStats* stats, st
     stats->compressed_bytes = comp_bytes.load();
     stats->bytes = (int64_t)job.nrows * job.itemsize;
     stats->threads = nthreads;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// On-GPU decode.  Per batch of chunks (about kBatchBytes decoded): host threads pread the
+// chunk files into a page-locked buffer (16-byte aligned frames), the host parses the frame
+// headers into split / block task lists, one DMA carries the compressed bytes and the tasks,
+// k_blosc_decode writes every stream to its place in the column (byte-shuffled blocks to a
+// scratch buffer first) and k_blosc_unshuffle finishes those.  Two slots alternate, so the
+// file reads of batch b+1 overlap the copy and kernels of batch b.
+
+namespace {
+
+constexpr size_t kBatchBytes = size_t(256) << 20;  // decoded bytes per batch
+constexpr size_t kRawPiece = size_t(64) << 10;      // stored-raw bytes per copy task
+
+bool grow_host(void*& p, size_t& cap, size_t want) {
+  if (cap >= want) return true;
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  cap = 0;
+  want += want / 4;
+  if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+    p = nullptr;
+    return false;
+  }
+  cap = want;
+  return true;
+}
+
+bool grow_dev(void*& p, size_t& cap, size_t want) {
+  if (cap >= want) return true;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  want += want / 4;
+  if (hipMalloc(&p, want) != hipSuccess) {
+    p = nullptr;
+    return false;
+  }
+  cap = want;
+  return true;
+}
+
+int32_t le32(const unsigned char* p) {
+  int32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+
+struct ChunkFile {
+  int64_t index;
+  size_t off;   // of the file in the slot's host buffer
+  size_t size;  // file bytes
+};
+
+enum class Plan { kTasks, kFallback, kError };
+
+// Task lists for one chunk file (bloscpack header + blosc1 frame) already in the host buffer
+// at f.off.  dst / tmp: the chunk's place in the column / in the slot's shuffle scratch.
+Plan plan_chunk(const unsigned char* file, const ChunkFile& f, uint64_t dst, uint64_t tmp, size_t want,
+                size_t chunk_bytes, const std::string& dir, std::vector<BloscSplit>& splits,
+                std::vector<BloscBlock>& blocks, std::string& err) {
+  const std::string where = "chunk " + std::to_string(f.index) + " of " + dir;
+  if (f.size < kBloscpackHeader + kBloscHeader || memcmp(file, "blpk", 4) != 0) {
+    err = where + " is not a bloscpack chunk";
+    return Plan::kError;
+  }
+  const unsigned char* frame = file + kBloscpackHeader;
+  const size_t avail = f.size - kBloscpackHeader;
+  const unsigned flags = frame[2], ts = frame[3];
+  const int64_t nbytes = le32(frame + 4), blocksize = le32(frame + 8), cbytes = le32(frame + 12);
+  if (cbytes < (int64_t)kBloscHeader || (size_t)cbytes > avail || nbytes < (int64_t)want ||
+      nbytes > (int64_t)chunk_bytes) {
+    err = where + ": frame holds " + std::to_string(nbytes) + " bytes, expected " + std::to_string(want);
+    return Plan::kError;
+  }
+  if ((size_t)nbytes != want) return Plan::kFallback;  // a padded last frame: host copies `want`
+  if (nbytes == 0) return Plan::kTasks;
+  const uint64_t frame_src = f.off + kBloscpackHeader;
+  if (flags & 0x2) {  // memcpyed: the items follow the header as they are
+    if (kBloscHeader + (size_t)nbytes > (size_t)cbytes) {
+      err = where + ": truncated memcpyed frame";
+      return Plan::kError;
+    }
+    for (size_t k = 0; k < (size_t)nbytes; k += kRawPiece) {
+      const uint32_t n = (uint32_t)std::min(kRawPiece, (size_t)nbytes - k);
+      splits.push_back({frame_src + kBloscHeader + k, dst + k, n, n, kSplitRaw, 0});
+    }
+    return Plan::kTasks;
+  }
+  const int codec = (int)(flags >> 5);
+  if ((flags & 0x4) || (codec != kSplitBloscLz && codec != kSplitLz4) || ts == 0) return Plan::kFallback;
+  if (blocksize <= 0) {
+    err = where + ": bad blocksize";
+    return Plan::kError;
+  }
+  const int64_t nblocks = (nbytes + blocksize - 1) / blocksize;
+  const int64_t leftover = nbytes % blocksize;
+  if ((int64_t)kBloscHeader + 4 * nblocks > cbytes) {
+    err = where + ": truncated block table";
+    return Plan::kError;
+  }
+  const bool shuffle = (flags & 0x1) && ts > 1;
+  const uint64_t out = shuffle ? tmp : dst;
+  const size_t splits0 = splits.size(), blocks0 = blocks.size();
+  for (int64_t b = 0; b < nblocks; ++b) {
+    const bool last_partial = b == nblocks - 1 && leftover != 0;
+    const int64_t bsize = last_partial ? leftover : blocksize;
+    const int64_t nsplits =
+        (!(flags & 0x10) && ts <= 16 && blocksize / (int64_t)ts >= 128 && !last_partial) ? (int64_t)ts : 1;
+    if (bsize % nsplits != 0) {
+      splits.resize(splits0);
+      blocks.resize(blocks0);
+      return Plan::kFallback;
+    }
+    const int64_t neblock = bsize / nsplits;
+    int64_t p = le32(frame + kBloscHeader + 4 * b);
+    const uint64_t boff = (uint64_t)(b * blocksize);
+    for (int64_t j = 0; j < nsplits; ++j) {
+      if (p < 0 || p + 4 > cbytes) {
+        err = where + ": block " + std::to_string(b) + " out of the frame";
+        return Plan::kError;
+      }
+      const int64_t csize = le32(frame + p);
+      p += 4;
+      if (csize < 0 || p + csize > cbytes) {
+        err = where + ": block " + std::to_string(b) + " out of the frame";
+        return Plan::kError;
+      }
+      splits.push_back({frame_src + (uint64_t)p, out + boff + (uint64_t)(j * neblock), (uint32_t)csize,
+                        (uint32_t)neblock, csize == neblock ? (int32_t)kSplitRaw : (int32_t)codec, 0});
+      p += csize;
+    }
+    if (shuffle) blocks.push_back({tmp + boff, dst + boff, (uint32_t)bsize, ts});
+  }
+  return Plan::kTasks;
+}
+
+// host libblosc decode of one chunk file already in memory, `want` bytes to dst (synchronous)
+bool host_decode_chunk(const BloscApi& bl, const unsigned char* file, size_t chunk_bytes, size_t want, void* dst,
+                       hipStream_t st, std::vector<unsigned char>& buf, std::string& err) {
+  buf.resize(chunk_bytes + kBloscHeader);
+  const int got = bl.decompress_ctx(file + kBloscpackHeader, buf.data(), buf.size(), 1);
+  if (got < 0 || (size_t)got < want) {
+    err = "blosc decompression failed";
+    return false;
+  }
+  if (hipMemcpyAsync(dst, buf.data(), want, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    err = "host-to-device copy failed";
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+int ingest_carray_device(const IngestJob& job, IngestPool& pool, IngestStats* stats, std::string& err) {
+  if (job.nrows < 0 || job.itemsize <= 0 || job.chunklen <= 0) {
+    err = "bad carray geometry";
+    return -1;
+  }
+  const int64_t nchunks = job.nrows ? (job.nrows + job.chunklen - 1) / job.chunklen : 0;
+  if (nchunks == 0) return 0;
+  const size_t chunk_bytes = (size_t)job.chunklen * (size_t)job.itemsize;
+  if (chunk_bytes > (size_t)INT32_MAX) {
+    err = "chunk larger than a blosc1 frame";
+    return -1;
+  }
+  hipStream_t st = job.stream;
+  if (pool.device != job.device) {
+    // resources of another device: drop them (the slots are re-created below)
+    pool.workers.clear();
+    for (DecodeSlot& d : pool.slots) {
+      if (d.done) (void)hipEventSynchronize(d.done);
+      if (d.host) (void)hipHostFree(d.host);
+      if (d.dev) (void)hipFree(d.dev);
+      if (d.tmp) (void)hipFree(d.tmp);
+      if (d.done) (void)hipEventDestroy(d.done);
+      d = DecodeSlot();
+    }
+    if (pool.bad) (void)hipFree(pool.bad);
+    pool.bad = nullptr;
+    pool.device = job.device;
+  }
+  for (DecodeSlot& d : pool.slots)
+    if (!d.done && hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess) {
+      err = "ingest: HIP event creation failed";
+      return -1;
+    }
+  if (!pool.bad && hipMalloc(&pool.bad, sizeof(unsigned int)) != hipSuccess) {
+    pool.bad = nullptr;
+    err = "ingest: device allocation failed";
+    return -1;
+  }
+  if (hipMemsetAsync(pool.bad, 0, sizeof(unsigned int), st) != hipSuccess) {
+    err = "ingest: device memset failed";
+    return -1;
+  }
+  const int64_t per_batch = std::max<int64_t>(1, (int64_t)(kBatchBytes / chunk_bytes));
+  const int nthreads = job.nthreads > 0 ? job.nthreads : 8;
+  int64_t comp_total = 0, nsplits_total = 0, nfallback = 0;
+  std::vector<BloscSplit> splits;
+  std::vector<BloscBlock> blocks;
+  std::vector<ChunkFile> files;
+  std::vector<unsigned char> hostbuf;
+  auto chunk_path = [&](int64_t i) {
+    char name[64];
+    snprintf(name, sizeof(name), "/data/__%lld.blp", (long long)i);
+    return job.carray_dir + name;
+  };
+
+  for (int64_t c0 = 0, b = 0; c0 < nchunks; c0 += per_batch, ++b) {
+    const int64_t c1 = std::min(nchunks, c0 + per_batch);
+    DecodeSlot& slot = pool.slots[b & 1];
+    if (hipEventSynchronize(slot.done) != hipSuccess) {
+      err = "ingest: HIP event wait failed";
+      return -1;
+    }
+    // file sizes -> 16-byte aligned places in the slot's host buffer
+    files.clear();
+    size_t total = 0;
+    for (int64_t i = c0; i < c1; ++i) {
+      struct stat sb;
+      const std::string path = chunk_path(i);
+      if (stat(path.c_str(), &sb) != 0) {
+        err = "ingest: cannot open " + path;
+        return -1;
+      }
+      files.push_back({i, total, (size_t)sb.st_size});
+      total += ((size_t)sb.st_size + 15) & ~(size_t)15;
+    }
+    const size_t comp_bytes = total + kBloscPad;
+    if (!grow_host(slot.host, slot.host_cap, comp_bytes) || !grow_dev(slot.dev, slot.dev_cap, comp_bytes)) {
+      err = "ingest: staging allocation failed";
+      return -1;
+    }
+    unsigned char* hbase = static_cast<unsigned char*>(slot.host);
+    memset(hbase + total, 0, kBloscPad);
+    // parallel reads (host threads do nothing else)
+    {
+      std::atomic<size_t> next{0};
+      std::atomic<bool> failed{false};
+      std::mutex mu;
+      std::string first;
+      auto reader = [&] {
+        for (;;) {
+          const size_t k = next.fetch_add(1);
+          if (k >= files.size() || failed.load(std::memory_order_relaxed)) return;
+          const ChunkFile& f = files[k];
+          const std::string path = chunk_path(f.index);
+          const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+          size_t got = 0;
+          if (fd >= 0) {
+            while (got < f.size) {
+              const ssize_t n = pread(fd, hbase + f.off + got, f.size - got, (off_t)got);
+              if (n <= 0) break;
+              got += (size_t)n;
+            }
+            close(fd);
+          }
+          if (got != f.size) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (first.empty()) first = (fd < 0 ? "ingest: cannot open " : "ingest: short read of ") + path;
+            failed = true;
+            return;
+          }
+        }
+      };
+      const int nt = (int)std::min<size_t>((size_t)nthreads, files.size());
+      std::vector<std::thread> th;
+      for (int t = 1; t < nt; ++t) th.emplace_back(reader);
+      reader();
+      for (std::thread& t : th) t.join();
+      if (failed) {
+        err = first;
+        return -1;
+      }
+    }
+    // tasks (byte-shuffled blocks decode into the slot's scratch, then un-shuffle)
+    const size_t batch_out = (size_t)(c1 - c0) * chunk_bytes;
+    if (!grow_dev(slot.tmp, slot.tmp_cap, batch_out)) {
+      err = "ingest: shuffle scratch allocation failed";
+      return -1;
+    }
+    splits.clear();
+    blocks.clear();
+    std::vector<int64_t> fallback;
+    for (const ChunkFile& f : files) {
+      const size_t want = (size_t)std::min<int64_t>(job.chunklen, job.nrows - f.index * job.chunklen) * job.itemsize;
+      const uint64_t dst = reinterpret_cast<uint64_t>(job.dev_dst) + (uint64_t)f.index * chunk_bytes;
+      const uint64_t tmp = reinterpret_cast<uint64_t>(slot.tmp) + (uint64_t)(f.index - c0) * chunk_bytes;
+      std::string e;
+      const Plan pl = plan_chunk(hbase + f.off, f, dst, tmp, want, chunk_bytes, job.carray_dir, splits, blocks, e);
+      if (pl == Plan::kError) {
+        err = "ingest: " + e;
+        return -1;
+      }
+      if (pl == Plan::kFallback) fallback.push_back((int64_t)(&f - files.data()));
+    }
+    // task lists after the compressed bytes (8-byte aligned), one DMA for both
+    const size_t split_off = (comp_bytes + 15) & ~(size_t)15;
+    const size_t block_off = split_off + splits.size() * sizeof(BloscSplit);
+    const size_t all = block_off + blocks.size() * sizeof(BloscBlock);
+    if (all > slot.host_cap || all > slot.dev_cap) {
+      // tasks did not fit the padding: grow both, keeping the compressed bytes
+      std::vector<unsigned char> keep(hbase, hbase + comp_bytes);
+      if (!grow_host(slot.host, slot.host_cap, all) || !grow_dev(slot.dev, slot.dev_cap, all)) {
+        err = "ingest: staging allocation failed";
+        return -1;
+      }
+      hbase = static_cast<unsigned char*>(slot.host);
+      memcpy(hbase, keep.data(), comp_bytes);
+    }
+    if (!splits.empty()) memcpy(hbase + split_off, splits.data(), splits.size() * sizeof(BloscSplit));
+    if (!blocks.empty()) memcpy(hbase + block_off, blocks.data(), blocks.size() * sizeof(BloscBlock));
+    unsigned char* dbase = static_cast<unsigned char*>(slot.dev);
+    if (hipMemcpyAsync(dbase, hbase, all, hipMemcpyHostToDevice, st) != hipSuccess) {
+      err = "ingest: host-to-device copy failed";
+      return -1;
+    }
+    launch_blosc_decode(dbase, reinterpret_cast<const BloscSplit*>(dbase + split_off), (int)splits.size(), pool.bad,
+                        st);
+    launch_blosc_unshuffle(reinterpret_cast<const BloscBlock*>(dbase + block_off), (int)blocks.size(), st);
+    if (hipGetLastError() != hipSuccess || hipEventRecord(slot.done, st) != hipSuccess) {
+      err = "ingest: blosc decode launch failed";
+      return -1;
+    }
+    for (int64_t k : fallback) {
+      const ChunkFile& f = files[k];
+      const BloscApi& bl = blosc_api();
+      if (!bl.err.empty()) {
+        err = bl.err;
+        return -1;
+      }
+      const size_t want = (size_t)std::min<int64_t>(job.chunklen, job.nrows - f.index * job.chunklen) * job.itemsize;
+      std::string e;
+      if (!host_decode_chunk(bl, hbase + f.off, chunk_bytes, want,
+                             static_cast<unsigned char*>(job.dev_dst) + (size_t)f.index * chunk_bytes, st, hostbuf,
+                             e)) {
+        err = "ingest: chunk " + std::to_string(f.index) + " of " + job.carray_dir + ": " + e;
+        return -1;
+      }
+    }
+    comp_total += (int64_t)total;
+    nsplits_total += (int64_t)splits.size();
+    nfallback += (int64_t)fallback.size();
+  }
+  unsigned int bad = 0;
+  if (hipMemcpyAsync(&bad, pool.bad, sizeof(bad), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    err = "ingest: device decode failed";
+    return -1;
+  }
+  if (bad) {
+    err = "ingest: on-GPU blosc decode of " + job.carray_dir + " failed (corrupt stream)";
+    return -1;
+  }
+  if (stats) {
+    stats->chunks = nchunks;
+    stats->compressed_bytes = comp_total;
+    stats->bytes = (int64_t)job.nrows * job.itemsize;
+    stats->threads = nthreads;
+    stats->device_splits = nsplits_total;
+    stats->host_fallback = nfallback;
   }
   return 0;
 }

@@ -258,14 +258,23 @@ class ShardTable:
         self.dev.check(self._lib.bqg_table_column_ptr(self.handle, self.slot(col), ctypes.byref(p)))
         return p.value or 0
 
-    def load_carray(self, col, carray_dir, chunklen, nthreads=None):
-        """Decode a bcolz carray directory straight into device column ``col`` (host decode
-        threads, pinned double-buffered DMA; statistics follow at the next ``sync``)."""
+    def load_carray(self, col, carray_dir, chunklen, nthreads=None, decode=None):
+        """Decode a bcolz carray directory straight into device column ``col``; statistics
+        follow at the next ``sync``.  ``decode``: 'device' (host threads read the chunk files,
+        the GPU decodes the blosc frames), 'host' (host threads decode, pinned double-buffered
+        DMA) or 'auto' (default; env BQGPU_INGEST_DECODE).  Returns the ingest report as a
+        dict."""
         self._touch()
         if not nthreads:
             nthreads = int(os.environ.get('BQGPU_INGEST_THREADS', '0')) or min(16, len(os.sched_getaffinity(0)))
-        self.dev.check(self._lib.bqg_table_load_carray(self.handle, self.slot(col), os.fsencode(carray_dir),
-                                                       int(chunklen), int(nthreads)))
+        decode = decode or os.environ.get('BQGPU_INGEST_DECODE', 'auto')
+        if decode not in L.DECODE_CODE:
+            raise ValueError('decode must be one of %s' % sorted(L.DECODE_CODE))
+        st = L.IngestStats()
+        self.dev.check(self._lib.bqg_table_load_carray_ex(self.handle, self.slot(col), os.fsencode(carray_dir),
+                                                          int(chunklen), int(nthreads), L.DECODE_CODE[decode],
+                                                          ctypes.byref(st)))
+        return {f: getattr(st, f) for f, _ in st._fields_}
 
     def sync(self):
         self.dev.check(self._lib.bqg_table_sync(self.handle))

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BQG_ABI_VERSION 3
+#define BQG_ABI_VERSION 4
 
 /* error codes */
 #define BQG_OK 0
@@ -160,6 +160,23 @@ int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows,
  * by the next bqg_table_sync. */
 int bqg_table_load_carray(bqg_table* t, int32_t col, const char* carray_dir, int64_t chunklen,
                           int32_t nthreads);
+/* The same with a choice of decoder and a report.  BQG_DECODE_DEVICE: the host threads only
+ * read the chunk files into page-locked memory, the compressed bytes cross PCIe, and the
+ * blosc1 frames are decoded on the GPU (BloscLZ and LZ4 streams, byte shuffle, memcpyed
+ * frames; a chunk with another codec -- zstd, zlib, snappy -- or bit shuffle is decoded by
+ * host libblosc as in the host path).  BQG_DECODE_AUTO picks the device decoder.  A corrupt
+ * stream fails the call (BQG_E_INVALID) on either path. */
+enum bqg_decode { BQG_DECODE_AUTO = 0, BQG_DECODE_HOST = 1, BQG_DECODE_DEVICE = 2 };
+typedef struct {
+  int64_t chunks;
+  int64_t compressed_bytes;  /* chunk file bytes read */
+  int64_t bytes;             /* decoded bytes written to the column */
+  int64_t device_splits;     /* compressed streams decoded on the GPU */
+  int64_t host_chunks;       /* chunks decoded by host libblosc */
+  int32_t decoder;           /* BQG_DECODE_HOST / BQG_DECODE_DEVICE: the one that ran */
+} bqg_ingest_stats;
+int bqg_table_load_carray_ex(bqg_table* t, int32_t col, const char* carray_dir, int64_t chunklen,
+                             int32_t nthreads, int32_t decode, bqg_ingest_stats* stats);
 /* Wait for pushes and compute per-column statistics (min / max / has_nan). */
 int bqg_table_sync(bqg_table* t);
 int bqg_table_column_ptr(bqg_table* t, int32_t col, void** dev_ptr);

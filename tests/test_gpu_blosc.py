@@ -1,0 +1,182 @@
+"""GPU: on-GPU blosc1 decode of bcolz carrays (bqg_table_load_carray_ex, decode='device').
+
+The frames are written by the system c-blosc 1.x (bcolz_io.compress_chunk -> libblosc, the
+library bcolz itself links); the device decoder's column must equal, byte for byte, the numpy
+array the frames were made from -- the same check as the host path's (test_gpu_ingest.py) --
+and the report must say which chunks ran where.  Codecs the kernels do not decode (zstd,
+zlib) must come back through host libblosc, and corrupt streams must fail the call.
+"""
+import os
+import struct
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+
+from bqueryd_amd import _lib, bcolz_io
+from bqueryd_amd.engine import ShardTable
+
+pytestmark = pytest.mark.gpu
+
+
+def _array(dtype, n, seed, kind='random'):
+    rng = np.random.default_rng(seed)
+    dt = np.dtype(dtype)
+    if kind == 'runs':  # sorted, long runs: long LZ matches
+        return np.sort(rng.integers(0, 50, n)).astype(dt)
+    if kind == 'cents':  # taxi-like fares: shuffled high bytes compress, low bytes do not
+        return np.round(np.clip(rng.lognormal(2.3, 0.6, n), 2.5, 500.0), 2).astype(dt)
+    if dt.kind == 'b':
+        return rng.random(n) < 0.3
+    if dt.kind == 'f':
+        return rng.normal(size=n).astype(dt)
+    info = np.iinfo(dt)
+    lo, hi = (0, 1000) if kind == 'small' else (info.min, info.max)
+    return rng.integers(lo, hi, n, dtype=dt, endpoint=True)
+
+
+def _load(d, a, decode='device', nthreads=3):
+    t = ShardTable(OrderedDict(), nrows=len(a))
+    try:
+        t.add_column('x', a.dtype)
+        rep = t.load_carray('x', d, bcolz_io.CArrayMeta(d).chunklen, nthreads=nthreads, decode=decode)
+        t.sync()
+        got = t.read('x')
+    finally:
+        t.close()
+    return got, rep
+
+
+CASES = [('int32', 100_003, 4096, 'small'), ('float64', 77_777, 1000, 'random'), ('int8', 5, 2, 'random'),
+         ('uint64', 65_536, 65_536, 'random'), ('bool', 12_345, 777, 'random'), ('int16', 1, 1024, 'random'),
+         ('int64', 300_001, 131_072, 'runs'), ('float64', 250_000, 131_072, 'cents'),
+         ('float32', 200_000, 50_000, 'cents'), ('uint16', 99_999, 33_333, 'small')]
+
+
+@pytest.mark.parametrize('cname', ['lz4', 'blosclz', 'lz4hc'])
+@pytest.mark.parametrize('shuffle', [1, 0])
+@pytest.mark.parametrize('dtype,n,chunklen,kind', CASES)
+def test_device_decode_matches(tmp_path, cname, shuffle, dtype, n, chunklen, kind):
+    a = _array(dtype, n, n + shuffle, kind)
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=chunklen, cname=cname, shuffle=shuffle)
+    got, rep = _load(d, a)
+    np.testing.assert_array_equal(got, a)
+    assert rep['decoder'] == _lib.DECODE_DEVICE
+    assert rep['host_chunks'] == 0
+    assert rep['chunks'] == -(-n // chunklen)
+    assert rep['bytes'] == a.nbytes
+
+
+@pytest.mark.parametrize('clevel', [1, 9])
+def test_device_decode_clevels(tmp_path, clevel):
+    a = _array('int64', 500_000, clevel, 'runs')
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=200_000, clevel=clevel, cname='blosclz')
+    got, _ = _load(d, a)
+    np.testing.assert_array_equal(got, a)
+
+
+def test_memcpyed_frames(tmp_path):
+    """Incompressible bytes: blosc stores the frame as it is (flags bit 1)."""
+    a = np.random.default_rng(5).integers(0, 256, 300_000, dtype=np.uint8)
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=70_000, cname='lz4', shuffle=0, clevel=9)
+    with open(os.path.join(d, 'data', '__0.blp'), 'rb') as f:
+        flags = f.read()[16 + 2]
+    assert flags & 0x2, 'expected a memcpyed frame (flags %#x)' % flags
+    got, rep = _load(d, a)
+    np.testing.assert_array_equal(got, a)
+    assert rep['host_chunks'] == 0
+
+
+@pytest.mark.parametrize('cname', ['zstd', 'zlib'])
+def test_other_codecs_fall_back_to_host(tmp_path, cname):
+    a = _array('int32', 50_000, 3, 'small')
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=8192, cname=cname)
+    got, rep = _load(d, a)
+    np.testing.assert_array_equal(got, a)
+    assert rep['decoder'] == _lib.DECODE_DEVICE
+    assert rep['host_chunks'] == rep['chunks'] == 7
+
+
+def test_mixed_codecs_in_one_carray(tmp_path):
+    """Chunk files written with different codecs (a carray appended to under other cparams)."""
+    a = _array('float64', 40_000, 4, 'cents')
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=10_000, cname='lz4')
+    other = bcolz_io.carray_files(a, chunklen=10_000, cname='zstd')
+    for rel, data in other:
+        if rel in ('data/__1.blp', 'data/__3.blp'):
+            with open(os.path.join(d, rel), 'wb') as f:
+                f.write(data)
+    got, rep = _load(d, a)
+    np.testing.assert_array_equal(got, a)
+    assert rep['host_chunks'] == 2
+
+
+def test_device_and_host_decoders_agree_multibatch(tmp_path):
+    """More chunks than one 256 MiB batch: both staging slots and the batch loop run."""
+    n = 40_000_000
+    a = _array('int64', n, 9, 'small')
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=1 << 20, cname='lz4')
+    got, rep = _load(d, a, nthreads=8)
+    np.testing.assert_array_equal(got, a)
+    assert rep['chunks'] == -(-n // (1 << 20)) and rep['host_chunks'] == 0
+    got_h, rep_h = _load(d, a, decode='host', nthreads=8)
+    assert rep_h['decoder'] == _lib.DECODE_HOST
+    np.testing.assert_array_equal(got_h, got)
+
+
+def _first_split(frame):
+    """(offset of the first split's int32 size in the frame, its size) of a non-memcpyed frame."""
+    bstart = struct.unpack_from('<i', frame, 16)[0]
+    return bstart, struct.unpack_from('<i', frame, bstart)[0]
+
+
+@pytest.mark.parametrize('cname', ['lz4', 'blosclz'])
+def test_corrupt_stream_fails(tmp_path, cname):
+    a = _array('int64', 100_000, 1, 'runs')
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=50_000, cname=cname)
+    path = os.path.join(d, 'data', '__1.blp')
+    with open(path, 'rb') as f:
+        data = bytearray(f.read())
+    off, csize = _first_split(bytes(data[16:]))
+    assert 0 < csize < 100_000
+    # a stream of 0xFF bytes: LZ4 literal lengths / BloscLZ matches that overrun the output
+    data[16 + off + 4:16 + off + 4 + csize] = b'\xff' * csize
+    with open(path, 'wb') as f:
+        f.write(bytes(data))
+    with pytest.raises(_lib.BqgError, match='corrupt'):
+        _load(d, a)
+
+
+def test_bad_split_size_fails(tmp_path):
+    a = _array('int32', 30_000, 2, 'small')
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=10_000, cname='lz4')
+    path = os.path.join(d, 'data', '__2.blp')
+    with open(path, 'rb') as f:
+        data = bytearray(f.read())
+    off, _ = _first_split(bytes(data[16:]))
+    struct.pack_into('<i', data, 16 + off, 1 << 30)
+    with open(path, 'wb') as f:
+        f.write(bytes(data))
+    with pytest.raises(_lib.BqgError, match='out of the frame'):
+        _load(d, a)
+
+
+def test_missing_chunk_and_magic(tmp_path):
+    a = np.arange(10_000, dtype=np.int32)
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=1000)
+    with open(os.path.join(d, 'data', '__3.blp'), 'r+b') as f:
+        f.write(b'nope')
+    with pytest.raises(_lib.BqgError, match='bloscpack'):
+        _load(d, a)
+    os.remove(os.path.join(d, 'data', '__3.blp'))
+    with pytest.raises(_lib.BqgError, match='cannot open'):
+        _load(d, a)

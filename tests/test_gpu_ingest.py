@@ -1,5 +1,5 @@
-"""GPU: cold-path ingest (bqg_table_load_carray) -- bcolz carrays decoded on host threads
-straight into HBM, compared byte for byte with the numpy columns they were written from."""
+"""GPU: cold-path ingest (bqg_table_load_carray) -- bcolz carrays decoded on host threads or
+on the GPU straight into HBM, compared byte for byte with the numpy columns they were written from."""
 import os
 from collections import OrderedDict
 
@@ -15,11 +15,12 @@ from tests.helpers import assert_tables_equal
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize('decode', ['host', 'device'])
 @pytest.mark.parametrize('cname', ['lz4', 'blosclz', 'zstd', 'zlib'])
 @pytest.mark.parametrize('dtype,n,chunklen', [('int32', 100_003, 4096), ('float64', 77_777, 1000),
                                               ('int8', 5, 2), ('uint64', 65_536, 65_536),
                                               ('bool', 12_345, 777), ('int16', 1, 1024)])
-def test_load_carray_roundtrip(tmp_path, cname, dtype, n, chunklen):
+def test_load_carray_roundtrip(tmp_path, cname, dtype, n, chunklen, decode):
     rng = np.random.default_rng(n)
     if dtype == 'bool':
         a = rng.random(n) < 0.3
@@ -33,7 +34,7 @@ def test_load_carray_roundtrip(tmp_path, cname, dtype, n, chunklen):
     t = ShardTable(OrderedDict(), nrows=n)
     try:
         t.add_column('x', a.dtype)
-        t.load_carray('x', d, bcolz_io.CArrayMeta(d).chunklen, nthreads=3)
+        t.load_carray('x', d, bcolz_io.CArrayMeta(d).chunklen, nthreads=3, decode=decode)
         t.sync()
         got = t.read('x')
     finally:
@@ -41,7 +42,8 @@ def test_load_carray_roundtrip(tmp_path, cname, dtype, n, chunklen):
     np.testing.assert_array_equal(got, a)
 
 
-def test_load_carray_errors(tmp_path):
+@pytest.mark.parametrize('decode', ['host', 'device'])
+def test_load_carray_errors(tmp_path, decode):
     a = np.arange(10_000, dtype=np.int32)
     d = str(tmp_path / 'col')
     bcolz_io.write_carray(d, a, chunklen=1000)
@@ -51,10 +53,10 @@ def test_load_carray_errors(tmp_path):
         with open(os.path.join(d, 'data', '__3.blp'), 'r+b') as f:
             f.write(b'nope')  # bad bloscpack magic
         with pytest.raises(_lib.BqgError, match='bloscpack'):
-            t.load_carray('x', d, 1000)
+            t.load_carray('x', d, 1000, decode=decode)
         os.remove(os.path.join(d, 'data', '__3.blp'))
         with pytest.raises(_lib.BqgError, match='cannot open'):
-            t.load_carray('x', d, 1000)
+            t.load_carray('x', d, 1000, decode=decode)
     finally:
         t.close()
 

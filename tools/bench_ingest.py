@@ -3,7 +3,8 @@
 ctable -> host blosc decode threads -> pinned double buffers -> H2D -> HBM, then the query.
 
 Legs (best of --reps, page cache warm -- the disk itself is not measured):
-  ingest     bqg_table_load_carray of the query's three columns (decoded bytes / s)
+  ingest_host    bqg_table_load_carray of the query's three columns, host blosc decode threads
+  ingest_device  the same with the frames decoded on the GPU (decoded bytes / s)
   cold_query ctable(rootdir) + where_terms + groupby with nothing resident (ingest + query)
   warm_query the same query again (columns resident in HBM)
   host_decode_1t  the reference's own cold path shape: one thread decoding every chunk
@@ -49,13 +50,13 @@ def main():
         on_disk = sum(os.path.getsize(os.path.join(dp, f)) for dp, _, fs in os.walk(root) for f in fs)
         dev = Device(0)
 
-        def ingest():
+        def ingest(decode):
             t = ShardTable({}, device=dev, nrows=args.rows)
             t0 = time.perf_counter()
             for name in cols:
                 meta = bcolz_io.CArrayMeta(bcolz_io.ctable_column_dir(root, name))
                 t.add_column(name, meta.dtype)
-                t.load_carray(name, meta.rootdir, meta.chunklen, nthreads=args.threads)
+                t.load_carray(name, meta.rootdir, meta.chunklen, nthreads=args.threads, decode=decode)
             dev.synchronize()
             dt = time.perf_counter() - t0
             t.close()
@@ -67,8 +68,13 @@ def main():
             ct.groupby(cfg['groupby'], cfg['aggs'], bool_arr=bool_arr)
             return time.perf_counter() - t0
 
-        ingest()  # first touch: page cache, pinned staging
-        ingest_s = min(ingest() for _ in range(args.reps))
+        legs = {}
+        for decode in ('host', 'device'):
+            ingest(decode)  # first touch: page cache, pinned staging
+            s = min(ingest(decode) for _ in range(args.reps))
+            legs['ingest_' + decode] = {'s': s, 'decoded_GBps': nbytes / s / 1e9, 'rows_per_s': args.rows / s,
+                                        'threads': args.threads}
+            print('ingest %s: %.1f ms' % (decode, s * 1e3), file=sys.stderr, flush=True)
         cold, warm = [], []
         for _ in range(args.reps):
             ct = ctable(rootdir=root, mode='r', auto_cache=True, device=dev)
@@ -83,8 +89,7 @@ def main():
             'workload': 'C2 shard cold path: %d rows, columns %s, bcolz/%s on local disk (page cache warm)'
                         % (args.rows, list(cols), args.cname),
             'decoded_bytes': nbytes, 'on_disk_bytes': on_disk, 'write_s': write_s,
-            'ingest': {'s': ingest_s, 'decoded_GBps': nbytes / ingest_s / 1e9, 'rows_per_s': args.rows / ingest_s,
-                       'threads': args.threads},
+            **legs,
             'cold_query': {'s': min(cold), 'rows_per_s': args.rows / min(cold)},
             'warm_query': {'s': min(warm), 'rows_per_s': args.rows / min(warm)},
             'host_decode_1t': {'s': host_1t, 'decoded_GBps': nbytes / host_1t / 1e9,
