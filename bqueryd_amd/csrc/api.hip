@@ -1657,7 +1657,7 @@ int bqg_table_load_carray_ex(bqg_table* t, int32_t col, const char* carray_dir, 
     job.itemsize = (int)dtype_size(k.dtype);
     job.chunklen = chunklen;
     job.nthreads = nthreads;
-    job.device_decode = decode != BQG_DECODE_HOST;
+    job.device_decode = decode == BQG_DECODE_DEVICE;  // AUTO: the host decoder
     job.stream = c->stream;
     IngestStats st;
     std::string err;

@@ -24,8 +24,15 @@ namespace bqg {
 
 namespace {
 
-constexpr int kWin = 1024;       // bytes of compressed input per wave in LDS
-constexpr int kDecWaves = 4;     // waves per workgroup
+constexpr int kWin = 1024;        // bytes of compressed input per wave in LDS
+constexpr uint32_t kRing = 32768; // bytes of decoded history per wave in LDS
+// one wave per workgroup, 33 KiB of LDS each: 4 waves per CU
+
+// address-space-qualified pointers: global (not flat) loads and stores, so an LDS wait
+// (lgkmcnt) never waits for the wave's outstanding global stores as well
+typedef __attribute__((address_space(1))) unsigned char gbyte;
+typedef __attribute__((address_space(3))) unsigned char lbyte;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -33,93 +40,200 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// a 16-byte-aligned kWin-byte window of the compressed bytes in the wave's LDS, reloaded when
-// the parse leaves it; every call is wave-uniform
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// The split's compressed bytes: a 16-byte-aligned kWin-byte window of them in the wave's LDS
+// (reloaded when the parse leaves it) and a cursor `ip` that hands out header bytes from an
+// 8-byte register copy, so a token costs one LDS round trip, not one per byte.  Every call
+// is wave-uniform.
 struct Window {
-  const unsigned char* src;  // the split's first compressed byte
-  const unsigned char* base; // first byte of the window (16-byte aligned)
-  unsigned char* win;
+  const gbyte* src;  // the split's first compressed byte
+  lbyte* win;
+  int32_t lo;        // split offset of the window's first byte (may be < 0: alignment)
   int lane;
+  uint32_t ip;       // cursor: offset of the next byte in the split
+  uint64_t q;        // bytes [ip, ip + have) of the split, low byte first
+  uint32_t have;
+
   __device__ __forceinline__ void load(uint32_t at) {
-    base = reinterpret_cast<const unsigned char*>(reinterpret_cast<uintptr_t>(src + at) & ~(uintptr_t)15);
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(src + at) & 15);
+    lo = (int32_t)uniform(at - mis);
     // 16 bytes per lane; the staging buffer is padded by kBloscPad, so the window never
     // leaves the allocation
-    const uint4 v = *reinterpret_cast<const uint4*>(base + lane * 16);
-    *reinterpret_cast<uint4*>(win + lane * 16) = v;
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(src + lo + lane * 16);
+    *(__attribute__((address_space(3))) u32x4*)(win + lane * 16) = v;
     wave_lds_sync();
   }
-  __device__ __forceinline__ uint32_t byte(uint32_t ip) {
-    const unsigned char* p = src + ip;
-    if (p < base || p >= base + kWin) load(ip);
-    return win[p - base];
+  // the window covers split bytes [ip + at, ip + at + n); returns the first one's LDS offset
+  __device__ __forceinline__ uint32_t cover(uint32_t at, uint32_t n) {
+    const int32_t p = (int32_t)(ip + at);
+    if (p < lo || p + (int32_t)n > lo + kWin) load(ip + at);
+    return (uint32_t)(p - lo);
+  }
+  __device__ __forceinline__ void fill() {
+    const uint32_t off = cover(0, 16);
+    const __attribute__((address_space(3))) uint64_t* w64 = (const __attribute__((address_space(3))) uint64_t*)(win);
+    const uint64_t a = w64[off >> 3], b = w64[(off >> 3) + 1];
+    const uint32_t sh = (off & 7) * 8;
+    const uint64_t v = sh ? (a >> sh) | (b << (64 - sh)) : a;
+    q = ((uint64_t)uniform((uint32_t)(v >> 32)) << 32) | uniform((uint32_t)v);
+    have = 8;
+  }
+  __device__ __forceinline__ uint32_t next() {
+    if (!have) fill();
+    const uint32_t b = (uint32_t)q & 255u;
+    q >>= 8;
+    --have;
+    ++ip;
+    return b;
+  }
+  __device__ __forceinline__ void skip(uint32_t n) {
+    if (n < have) {
+      q >>= 8 * n;
+      have -= n;
+    } else {
+      have = 0;
+    }
+    ip += n;
   }
 };
 
-__device__ __forceinline__ void copy_literals(const unsigned char* src, unsigned char* dst, uint32_t n, int lane) {
-  for (uint32_t i = (uint32_t)lane; i < n; i += 64) dst[i] = src[i];
+// The wave's output: global bytes plus the last kRing of them in LDS.  A match whose source
+// lies in that history is copied LDS -> registers -> global without waiting for the wave's
+// global stores; only a match reaching further back waits for them (vmcnt) and reads the
+// output through L2.
+struct Out {
+  gbyte* dst;   // the split's output (global)
+  lbyte* ring;  // kRing bytes of LDS: position p lives at ring[p % kRing]
+  int lane;
+  __device__ __forceinline__ void put(uint32_t p, unsigned char v) {
+    dst[p] = v;
+    ring[p & (kRing - 1)] = v;
+  }
+};
+
+// n literal bytes at the cursor -> output position op
+__device__ __forceinline__ void copy_literals(Window& w, Out& o, uint32_t op, uint32_t n) {
+  for (uint32_t c = 0; c < n; c += 64) {
+    const uint32_t off = w.cover(c, 64);
+    const uint32_t i = c + (uint32_t)o.lane;
+    if (i < n) o.put(op + i, w.win[off + o.lane]);
+  }
+  wave_lds_sync();
+  w.skip(n);
 }
 
 // a byte of this split's output, written earlier by this wave: an agent-scope load misses
 // the (non-coherent) L1, which may hold a line fetched before the byte was stored
-__device__ __forceinline__ unsigned char out_byte(const unsigned char* p) {
+__device__ __forceinline__ unsigned char out_byte(const gbyte* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// dst[i] = dst[i - dist] for i in [0, n): every byte comes from [dst - dist, dst), written
-// before this match -- the wave's stores are drained (vmcnt counts stores on gfx9) first
-__device__ __forceinline__ void copy_match(unsigned char* dst, uint32_t dist, uint32_t n, int lane) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const unsigned char* ref = dst - dist;
-  if (dist >= n) {
-    for (uint32_t i = (uint32_t)lane; i < n; i += 64) dst[i] = out_byte(ref + i);
-    return;
+// out[op + i] = out[op + i - dist] for i in [0, n)
+__device__ __forceinline__ void copy_match(Out& o, uint32_t op, uint32_t dist, uint32_t n) {
+  const uint32_t lane = (uint32_t)o.lane;
+  if (dist <= 64) {
+    // the period [op - dist, op) in registers, then byte i = period[i mod dist] by lane
+    // permute: no reads of bytes written by this match
+    const uint32_t per = o.ring[(op - dist + lane % dist) & (kRing - 1)];
+    const uint32_t step = 64u % dist;
+    uint32_t j = lane % dist;
+    for (uint32_t c = 0; c < n; c += 64) {
+      const uint32_t v = (uint32_t)__shfl((int)per, (int)j, 64);
+      if (c + lane < n) o.put(op + c + lane, (unsigned char)v);
+      j += step;
+      if (j >= dist) j -= dist;
+    }
+  } else if (dist <= kRing) {
+    // sources at least 64 back: a 64-byte step reads only bytes of earlier steps, still in
+    // the ring (a byte is overwritten kRing positions later)
+    for (uint32_t c = 0; c < n; c += 64) {
+      const uint32_t i = c + lane;
+      if (i < n) o.put(op + i, o.ring[(op + i - dist) & (kRing - 1)]);
+      if (c + 128 > dist) wave_lds_sync();  // the next step reads this one's bytes
+    }
+  } else {
+    // far back: through global memory once the wave's stores have drained
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (uint32_t c = 0; c < n; c += 64) {
+      const uint32_t i = c + lane;
+      if (i < n) o.put(op + i, out_byte(o.dst + op + i - dist));
+      if (c + 128 > dist) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // sources of the next step
+    }
   }
-  const uint32_t step = 64u % dist;
-  uint32_t j = (uint32_t)lane % dist;
-  for (uint32_t i = (uint32_t)lane; i < n; i += 64) {
-    dst[i] = out_byte(ref + j);
-    j += step;
-    if (j >= dist) j -= dist;
-  }
+  wave_lds_sync();
 }
 
+constexpr uint32_t kBad = 0xFFFFFFFFu;
+
+#ifdef BQG_BLOSC_PROF
+// micro-benchmark instrumentation (tools/micro): cycles and counts per phase of the LZ4 loop
+__device__ unsigned long long g_blosc_prof[16];
+#define PROF_DECL uint64_t prof_t = __builtin_readcyclecounter(), prof_acc[5] = {0, 0, 0, 0, 0}, prof_n[5] = {0, 0, 0, 0, 0}
+#define PROF_MARK(k)                                      \
+  do {                                                    \
+    const uint64_t now_ = __builtin_readcyclecounter();   \
+    prof_acc[k] += now_ - prof_t;                         \
+    prof_n[k] += 1;                                       \
+    prof_t = now_;                                        \
+  } while (0)
+#define PROF_FLUSH                                                                   \
+  do {                                                                               \
+    if (o.lane == 0)                                                                 \
+      for (int k_ = 0; k_ < 5; ++k_) {                                               \
+        atomicAdd(&g_blosc_prof[k_], (unsigned long long)prof_acc[k_]);              \
+        atomicAdd(&g_blosc_prof[8 + k_], (unsigned long long)prof_n[k_]);            \
+      }                                                                              \
+  } while (0)
+#else
+#define PROF_DECL
+#define PROF_MARK(k)
+#define PROF_FLUSH
+#endif
+
 // LZ4 block format: [token][literal length ext][literals][offset u16 LE][match length ext]
-__device__ uint32_t lz4_wave(Window& w, const unsigned char* src, uint32_t clen, unsigned char* dst, uint32_t dlen,
-                             int lane) {
-  uint32_t ip = 0, op = 0;
-  while (ip < clen) {
-    const uint32_t token = w.byte(ip++);
+__device__ uint32_t lz4_wave(Window& w, uint32_t clen, Out& o, uint32_t dlen) {
+  uint32_t op = 0;
+  PROF_DECL;
+  while (w.ip < clen) {
+    const uint32_t token = w.next();
     uint32_t lit = token >> 4;
     if (lit == 15) {
       uint32_t b;
       do {
-        if (ip >= clen) return 0xFFFFFFFFu;
-        b = w.byte(ip++);
+        if (w.ip >= clen) return kBad;
+        b = w.next();
         lit += b;
       } while (b == 255);
     }
-    if (ip + lit > clen || op + lit > dlen) return 0xFFFFFFFFu;
-    copy_literals(src + ip, dst + op, lit, lane);
-    ip += lit;
+    if (w.ip + lit > clen || op + lit > dlen) return kBad;
+    PROF_MARK(0);
+    if (lit) {
+      copy_literals(w, o, op, lit);
+      PROF_MARK(1);
+    }
     op += lit;
-    if (ip >= clen) break;  // the last sequence carries literals only
-    if (ip + 2 > clen) return 0xFFFFFFFFu;
-    const uint32_t off = w.byte(ip) | (w.byte(ip + 1) << 8);
-    ip += 2;
+    if (w.ip >= clen) break;  // the last sequence carries literals only
+    if (w.ip + 2 > clen) return kBad;
+    const uint32_t lo = w.next();
+    const uint32_t off = lo | (w.next() << 8);
     uint32_t mlen = token & 15u;
     if (mlen == 15) {
       uint32_t b;
       do {
-        if (ip >= clen) return 0xFFFFFFFFu;
-        b = w.byte(ip++);
+        if (w.ip >= clen) return kBad;
+        b = w.next();
         mlen += b;
       } while (b == 255);
     }
     mlen += 4;
-    if (off == 0 || off > op || op + mlen > dlen) return 0xFFFFFFFFu;
-    copy_match(dst + op, off, mlen, lane);
+    if (off == 0 || off > op || op + mlen > dlen) return kBad;
+    PROF_MARK(0);
+    copy_match(o, op, off, mlen);
+    PROF_MARK(off <= 64 ? 2 : off <= kRing ? 3 : 4);
     op += mlen;
   }
+  PROF_FLUSH;
   return op;
 }
 
@@ -128,11 +242,10 @@ __device__ uint32_t lz4_wave(Window& w, const unsigned char* src, uint32_t clen,
 // + next byte + 1, or 8192 + a big-endian u16 when that byte is 255 and ctrl & 31 == 31
 constexpr uint32_t kBloscLzMaxDistance = 8191;
 
-__device__ uint32_t blosclz_wave(Window& w, const unsigned char* src, uint32_t clen, unsigned char* dst,
-                                 uint32_t dlen, int lane) {
+__device__ uint32_t blosclz_wave(Window& w, uint32_t clen, Out& o, uint32_t dlen) {
   if (clen == 0) return 0;
-  uint32_t ip = 0, op = 0;
-  uint32_t ctrl = w.byte(ip++) & 31u;
+  uint32_t op = 0;
+  uint32_t ctrl = w.next() & 31u;
   for (;;) {
     if (ctrl >= 32) {
       uint32_t len = (ctrl >> 5) - 1;
@@ -140,35 +253,34 @@ __device__ uint32_t blosclz_wave(Window& w, const unsigned char* src, uint32_t c
       if (len == 6) {
         uint32_t code;
         do {
-          if (ip + 1 >= clen) return 0xFFFFFFFFu;
-          code = w.byte(ip++);
+          if (w.ip + 1 >= clen) return kBad;
+          code = w.next();
           len += code;
         } while (code == 255);
-      } else if (ip + 1 >= clen) {
-        return 0xFFFFFFFFu;
+      } else if (w.ip + 1 >= clen) {
+        return kBad;
       }
-      const uint32_t code = w.byte(ip++);
+      const uint32_t code = w.next();
       len += 3;
       uint32_t dist = ofs + code + 1;
       if (code == 255 && ofs == (31u << 8)) {
-        if (ip + 1 >= clen) return 0xFFFFFFFFu;
-        ofs = (w.byte(ip) << 8) + w.byte(ip + 1);
-        ip += 2;
+        if (w.ip + 1 >= clen) return kBad;
+        const uint32_t hi = w.next();
+        ofs = (hi << 8) + w.next();
         dist = ofs + kBloscLzMaxDistance + 1;
       }
-      if (op + len > dlen || dist > op) return 0xFFFFFFFFu;
-      copy_match(dst + op, dist, len, lane);
+      if (op + len > dlen || dist > op) return kBad;
+      copy_match(o, op, dist, len);
       op += len;
-      if (ip >= clen) break;
-      ctrl = w.byte(ip++);
+      if (w.ip >= clen) break;
+      ctrl = w.next();
     } else {
       const uint32_t n = ctrl + 1;
-      if (op + n > dlen || ip + n > clen) return 0xFFFFFFFFu;
-      copy_literals(src + ip, dst + op, n, lane);
+      if (op + n > dlen || w.ip + n > clen) return kBad;
+      copy_literals(w, o, op, n);
       op += n;
-      ip += n;
-      if (ip >= clen) break;
-      ctrl = w.byte(ip++);
+      if (w.ip >= clen) break;
+      ctrl = w.next();
     }
   }
   return op;
@@ -176,27 +288,32 @@ __device__ uint32_t blosclz_wave(Window& w, const unsigned char* src, uint32_t c
 
 }  // namespace
 
-__global__ __launch_bounds__(64 * kDecWaves) void k_blosc_decode(const unsigned char* comp, const BloscSplit* tasks,
-                                                                 int ntasks, unsigned int* bad) {
-  __shared__ __align__(16) unsigned char win_all[kDecWaves][kWin];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__global__ __launch_bounds__(64) void k_blosc_decode(const unsigned char* comp, const BloscSplit* tasks, int ntasks,
+                                                     unsigned int* bad) {
+  __shared__ __align__(16) unsigned char win_s[kWin];
+  __shared__ __align__(16) unsigned char ring_s[kRing];
+  const int lane = threadIdx.x;
   Window w;
-  w.base = nullptr;
-  w.win = win_all[wave];
+  w.win = (lbyte*)(win_s);
   w.lane = lane;
-  for (int t = blockIdx.x * kDecWaves + wave; t < ntasks; t += gridDim.x * kDecWaves) {
+  Out o;
+  o.ring = (lbyte*)(ring_s);
+  o.lane = lane;
+  const gbyte* gcomp = (const gbyte*)(comp);
+  for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
     const BloscSplit s = tasks[t];
-    const unsigned char* src = comp + s.src;
-    unsigned char* dst = reinterpret_cast<unsigned char*>(s.dst);
+    const gbyte* src = gcomp + s.src;
+    o.dst = (gbyte*)(s.dst);
     uint32_t got;
     if (s.codec == kSplitRaw) {
-      copy_literals(src, dst, s.dsize, lane);
+      for (uint32_t i = (uint32_t)lane; i < s.dsize; i += 64) o.dst[i] = src[i];
       got = s.dsize;
     } else {
       w.src = src;
+      w.ip = 0;
+      w.have = 0;
       w.load(0);
-      got = s.codec == kSplitLz4 ? lz4_wave(w, src, s.csize, dst, s.dsize, lane)
-                                 : blosclz_wave(w, src, s.csize, dst, s.dsize, lane);
+      got = s.codec == kSplitLz4 ? lz4_wave(w, s.csize, o, s.dsize) : blosclz_wave(w, s.csize, o, s.dsize);
     }
     if (got != s.dsize && lane == 0) atomicOr(bad, 1u);  // a vector atomic (one lane)
   }
@@ -238,8 +355,7 @@ __global__ __launch_bounds__(256) void k_blosc_unshuffle(const BloscBlock* block
 void launch_blosc_decode(const unsigned char* comp, const BloscSplit* tasks, int ntasks, unsigned int* bad,
                          hipStream_t st) {
   if (ntasks <= 0) return;
-  const int blocks = std::min(65535, (ntasks + kDecWaves - 1) / kDecWaves);
-  hipLaunchKernelGGL(k_blosc_decode, dim3(blocks), dim3(64 * kDecWaves), 0, st, comp, tasks, ntasks, bad);
+  hipLaunchKernelGGL(k_blosc_decode, dim3(std::min(65535, ntasks)), dim3(64), 0, st, comp, tasks, ntasks, bad);
 }
 
 void launch_blosc_unshuffle(const BloscBlock* blocks, int nblocks, hipStream_t st) {
