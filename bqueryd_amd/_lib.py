@@ -98,6 +98,7 @@ _PROTOS = {
     'bqg_push_chunk': ([_P, _I32, _P, _I64, _I64], ctypes.c_int),
     'bqg_table_load_carray': ([_P, _I32, ctypes.c_char_p, _I64, _I32], ctypes.c_int),
     'bqg_table_load_carray_ex': ([_P, _I32, ctypes.c_char_p, _I64, _I32, _I32, _P], ctypes.c_int),
+    'bqg_table_load_carrays': ([_P, _I32, _P, _P, _P, _I32, _I32, _P], ctypes.c_int),
     'bqg_table_sync': ([_P], ctypes.c_int),
     'bqg_table_column_ptr': ([_P, _I32, ctypes.POINTER(_P)], ctypes.c_int),
     'bqg_table_stats': ([_P, _I32, ctypes.POINTER(_I64), ctypes.POINTER(_I64),

@@ -1638,41 +1638,58 @@ int bqg_push_chunk(bqg_table* t, int32_t col, const void* host, int64_t nrows, i
   });
 }
 
-int bqg_table_load_carray_ex(bqg_table* t, int32_t col, const char* carray_dir, int64_t chunklen, int32_t nthreads,
-                             int32_t decode, bqg_ingest_stats* stats) {
+int bqg_table_load_carrays(bqg_table* t, int32_t n, const int32_t* cols, const char* const* carray_dirs,
+                           const int64_t* chunklens, int32_t nthreads, int32_t decode, bqg_ingest_stats* stats) {
   bqg_ctx* c = t->ctx;
   return guard(c, [&] {
-    if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
-    if (!carray_dir) fail(BQG_E_INVALID, "null carray directory");
-    if (chunklen <= 0) fail(BQG_E_INVALID, "chunklen must be positive");
+    if (n < 0 || (n && (!cols || !carray_dirs || !chunklens))) fail(BQG_E_INVALID, "bad column list");
     if (decode < BQG_DECODE_AUTO || decode > BQG_DECODE_DEVICE) fail(BQG_E_INVALID, "unknown decoder %d", decode);
-    Column& k = t->cols[col];
-    k.stats.valid = false;
-    HIPCHECK(hipStreamSynchronize(c->stream));  // the column's zero-fill has landed
-    IngestJob job;
-    job.device = c->device;
-    job.dev_dst = k.dev;
-    job.carray_dir = carray_dir;
-    job.nrows = t->nrows;
-    job.itemsize = (int)dtype_size(k.dtype);
-    job.chunklen = chunklen;
-    job.nthreads = nthreads;
-    job.device_decode = decode == BQG_DECODE_DEVICE;  // AUTO: the host decoder
-    job.stream = c->stream;
-    IngestStats st;
-    std::string err;
-    const int rc = job.device_decode ? ingest_carray_device(job, c->ingest, &st, err)
-                                     : ingest_carray(job, c->ingest, &st, err);
-    if (rc != 0) fail(BQG_E_INVALID, "%s", err.c_str());
-    if (stats) {
-      stats->chunks = st.chunks;
-      stats->compressed_bytes = st.compressed_bytes;
-      stats->bytes = st.bytes;
-      stats->device_splits = st.device_splits;
-      stats->host_chunks = job.device_decode ? st.host_fallback : st.chunks;
-      stats->decoder = job.device_decode ? BQG_DECODE_DEVICE : BQG_DECODE_HOST;
+    std::vector<IngestJob> jobs(n);
+    for (int i = 0; i < n; ++i) {
+      const int32_t col = cols[i];
+      if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
+      if (!carray_dirs[i]) fail(BQG_E_INVALID, "null carray directory");
+      if (chunklens[i] <= 0) fail(BQG_E_INVALID, "chunklen must be positive");
+      for (int k = 0; k < i; ++k)
+        if (cols[k] == col) fail(BQG_E_INVALID, "column %d listed twice", col);
+      Column& k = t->cols[col];
+      k.stats.valid = false;
+      IngestJob& job = jobs[i];
+      job.device = c->device;
+      job.dev_dst = k.dev;
+      job.carray_dir = carray_dirs[i];
+      job.nrows = t->nrows;
+      job.itemsize = (int)dtype_size(k.dtype);
+      job.chunklen = chunklens[i];
+      job.nthreads = nthreads;
+      job.device_decode = decode != BQG_DECODE_HOST;  // AUTO: the device decoder
+      job.stream = c->stream;
     }
+    HIPCHECK(hipStreamSynchronize(c->stream));  // the columns' zero-fill has landed
+    std::vector<IngestStats> st(n);
+    std::string err;
+    const bool dev = decode != BQG_DECODE_HOST;
+    if (dev) {
+      if (ingest_carrays_device(jobs, c->ingest, st, err) != 0) fail(BQG_E_INVALID, "%s", err.c_str());
+    } else {
+      for (int i = 0; i < n; ++i)
+        if (ingest_carray(jobs[i], c->ingest, &st[i], err) != 0) fail(BQG_E_INVALID, "%s", err.c_str());
+    }
+    if (stats)
+      for (int i = 0; i < n; ++i) {
+        stats[i].chunks = st[i].chunks;
+        stats[i].compressed_bytes = st[i].compressed_bytes;
+        stats[i].bytes = st[i].bytes;
+        stats[i].device_splits = st[i].device_splits;
+        stats[i].host_chunks = dev ? st[i].host_fallback : st[i].chunks;
+        stats[i].decoder = dev ? BQG_DECODE_DEVICE : BQG_DECODE_HOST;
+      }
   });
+}
+
+int bqg_table_load_carray_ex(bqg_table* t, int32_t col, const char* carray_dir, int64_t chunklen, int32_t nthreads,
+                             int32_t decode, bqg_ingest_stats* stats) {
+  return bqg_table_load_carrays(t, 1, &col, &carray_dir, &chunklen, nthreads, decode, stats);
 }
 
 int bqg_table_load_carray(bqg_table* t, int32_t col, const char* carray_dir, int64_t chunklen, int32_t nthreads) {

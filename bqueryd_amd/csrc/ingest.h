@@ -68,5 +68,9 @@ int ingest_carray(const IngestJob& job, IngestPool& pool, IngestStats* stats, st
 // bcolz defaults) and byte shuffle are decoded by kernels; chunks with another codec, bit
 // shuffle or a short last frame are decoded by host libblosc as in ingest_carray.
 int ingest_carray_device(const IngestJob& job, IngestPool& pool, IngestStats* stats, std::string& err);
+// Several columns at once (one table's, one device and stream): the chunks of all of them form
+// one sequence of batches, so one column's file reads overlap the previous one's kernels.
+int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, std::vector<IngestStats>& stats,
+                          std::string& err);
 
 }  // namespace bqg

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <functional>
 #include <cstdio>
 #include <cstdlib>
@@ -267,7 +268,7 @@ int ingest_carray(const IngestJob& job, IngestPool& pool, IngestStats* stats, st
 
 namespace {
 
-constexpr size_t kBatchBytes = size_t(256) << 20;  // decoded bytes per batch
+constexpr size_t kBatchBytes = size_t(512) << 20;  // decoded bytes per batch
 constexpr size_t kRawPiece = size_t(64) << 10;      // stored-raw bytes per copy task
 
 bool grow_host(void*& p, size_t& cap, size_t want) {
@@ -305,6 +306,7 @@ int32_t le32(const unsigned char* p) {
 }
 
 struct ChunkFile {
+  int job;      // column (index into the jobs)
   int64_t index;
   size_t off;   // of the file in the slot's host buffer
   size_t size;  // file bytes
@@ -412,20 +414,39 @@ bool host_decode_chunk(const BloscApi& bl, const unsigned char* file, size_t chu
 
 }  // namespace
 
-int ingest_carray_device(const IngestJob& job, IngestPool& pool, IngestStats* stats, std::string& err) {
-  if (job.nrows < 0 || job.itemsize <= 0 || job.chunklen <= 0) {
-    err = "bad carray geometry";
-    return -1;
+int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, std::vector<IngestStats>& stats,
+                          std::string& err) {
+  stats.assign(jobs.size(), IngestStats());
+  if (jobs.empty()) return 0;
+  // every chunk of every column, in order: batches may span columns, so the file reads of
+  // one column overlap the kernels of the previous one
+  struct ChunkRef {
+    int job;
+    int64_t index;
+  };
+  std::vector<ChunkRef> chunks;
+  std::vector<size_t> chunk_bytes(jobs.size());
+  for (size_t j = 0; j < jobs.size(); ++j) {
+    const IngestJob& job = jobs[j];
+    if (job.nrows < 0 || job.itemsize <= 0 || job.chunklen <= 0) {
+      err = "bad carray geometry";
+      return -1;
+    }
+    chunk_bytes[j] = (size_t)job.chunklen * (size_t)job.itemsize;
+    if (chunk_bytes[j] > (size_t)INT32_MAX) {
+      err = "chunk larger than a blosc1 frame";
+      return -1;
+    }
+    const int64_t n = job.nrows ? (job.nrows + job.chunklen - 1) / job.chunklen : 0;
+    for (int64_t i = 0; i < n; ++i) chunks.push_back({(int)j, i});
+    stats[j].chunks = n;
+    stats[j].bytes = job.nrows * job.itemsize;
+    stats[j].threads = job.nthreads > 0 ? job.nthreads : 8;
   }
-  const int64_t nchunks = job.nrows ? (job.nrows + job.chunklen - 1) / job.chunklen : 0;
-  if (nchunks == 0) return 0;
-  const size_t chunk_bytes = (size_t)job.chunklen * (size_t)job.itemsize;
-  if (chunk_bytes > (size_t)INT32_MAX) {
-    err = "chunk larger than a blosc1 frame";
-    return -1;
-  }
-  hipStream_t st = job.stream;
-  if (pool.device != job.device) {
+  if (chunks.empty()) return 0;
+  const IngestJob& job0 = jobs[0];
+  hipStream_t st = job0.stream;
+  if (pool.device != job0.device) {
     // resources of another device: drop them (the slots are re-created below)
     pool.workers.clear();
     for (DecodeSlot& d : pool.slots) {
@@ -438,7 +459,7 @@ int ingest_carray_device(const IngestJob& job, IngestPool& pool, IngestStats* st
     }
     if (pool.bad) (void)hipFree(pool.bad);
     pool.bad = nullptr;
-    pool.device = job.device;
+    pool.device = job0.device;
   }
   for (DecodeSlot& d : pool.slots)
     if (!d.done && hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess) {
@@ -454,37 +475,45 @@ int ingest_carray_device(const IngestJob& job, IngestPool& pool, IngestStats* st
     err = "ingest: device memset failed";
     return -1;
   }
-  const int64_t per_batch = std::max<int64_t>(1, (int64_t)(kBatchBytes / chunk_bytes));
-  const int nthreads = job.nthreads > 0 ? job.nthreads : 8;
-  int64_t comp_total = 0, nsplits_total = 0, nfallback = 0;
+  const int nthreads = job0.nthreads > 0 ? job0.nthreads : 8;
+  // BQGPU_INGEST_TRACE=1: per-batch host phase times on stderr (tools/bench_ingest.py)
+  static const bool trace = getenv("BQGPU_INGEST_TRACE") != nullptr;
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t0) { return std::chrono::duration<double, std::milli>(clk::now() - t0).count(); };
   std::vector<BloscSplit> splits;
   std::vector<BloscBlock> blocks;
   std::vector<ChunkFile> files;
   std::vector<unsigned char> hostbuf;
-  auto chunk_path = [&](int64_t i) {
+  auto chunk_path = [&](int j, int64_t i) {
     char name[64];
     snprintf(name, sizeof(name), "/data/__%lld.blp", (long long)i);
-    return job.carray_dir + name;
+    return jobs[j].carray_dir + name;
   };
 
-  for (int64_t c0 = 0, b = 0; c0 < nchunks; c0 += per_batch, ++b) {
-    const int64_t c1 = std::min(nchunks, c0 + per_batch);
+  for (size_t c0 = 0, b = 0; c0 < chunks.size(); ++b) {
+    // the batch: chunks up to kBatchBytes decoded (at least one)
+    size_t c1 = c0, batch_out = 0;
+    while (c1 < chunks.size() && (c1 == c0 || batch_out + chunk_bytes[chunks[c1].job] <= kBatchBytes))
+      batch_out += chunk_bytes[chunks[c1++].job];
     DecodeSlot& slot = pool.slots[b & 1];
+    const clk::time_point t_wait = clk::now();
     if (hipEventSynchronize(slot.done) != hipSuccess) {
       err = "ingest: HIP event wait failed";
       return -1;
     }
+    const double wait_ms = ms_since(t_wait);
+    const clk::time_point t_read = clk::now();
     // file sizes -> 16-byte aligned places in the slot's host buffer
     files.clear();
     size_t total = 0;
-    for (int64_t i = c0; i < c1; ++i) {
+    for (size_t c = c0; c < c1; ++c) {
       struct stat sb;
-      const std::string path = chunk_path(i);
+      const std::string path = chunk_path(chunks[c].job, chunks[c].index);
       if (stat(path.c_str(), &sb) != 0) {
         err = "ingest: cannot open " + path;
         return -1;
       }
-      files.push_back({i, total, (size_t)sb.st_size});
+      files.push_back({chunks[c].job, chunks[c].index, total, (size_t)sb.st_size});
       total += ((size_t)sb.st_size + 15) & ~(size_t)15;
     }
     const size_t comp_bytes = total + kBloscPad;
@@ -505,7 +534,7 @@ int ingest_carray_device(const IngestJob& job, IngestPool& pool, IngestStats* st
           const size_t k = next.fetch_add(1);
           if (k >= files.size() || failed.load(std::memory_order_relaxed)) return;
           const ChunkFile& f = files[k];
-          const std::string path = chunk_path(f.index);
+          const std::string path = chunk_path(f.job, f.index);
           const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
           size_t got = 0;
           if (fd >= 0) {
@@ -534,33 +563,47 @@ int ingest_carray_device(const IngestJob& job, IngestPool& pool, IngestStats* st
         return -1;
       }
     }
+    const double read_ms = ms_since(t_read);
+    const clk::time_point t_plan = clk::now();
     // tasks (byte-shuffled blocks decode into the slot's scratch, then un-shuffle)
-    const size_t batch_out = (size_t)(c1 - c0) * chunk_bytes;
     if (!grow_dev(slot.tmp, slot.tmp_cap, batch_out)) {
       err = "ingest: shuffle scratch allocation failed";
       return -1;
     }
     splits.clear();
     blocks.clear();
-    std::vector<int64_t> fallback;
-    for (const ChunkFile& f : files) {
+    std::vector<size_t> fallback;
+    uint64_t tmp_at = reinterpret_cast<uint64_t>(slot.tmp);
+    for (size_t k = 0; k < files.size(); ++k) {
+      const ChunkFile& f = files[k];
+      const IngestJob& job = jobs[f.job];
+      const size_t cb = chunk_bytes[f.job];
       const size_t want = (size_t)std::min<int64_t>(job.chunklen, job.nrows - f.index * job.chunklen) * job.itemsize;
-      const uint64_t dst = reinterpret_cast<uint64_t>(job.dev_dst) + (uint64_t)f.index * chunk_bytes;
-      const uint64_t tmp = reinterpret_cast<uint64_t>(slot.tmp) + (uint64_t)(f.index - c0) * chunk_bytes;
+      const uint64_t dst = reinterpret_cast<uint64_t>(job.dev_dst) + (uint64_t)f.index * cb;
+      const size_t ns0 = splits.size();
       std::string e;
-      const Plan pl = plan_chunk(hbase + f.off, f, dst, tmp, want, chunk_bytes, job.carray_dir, splits, blocks, e);
+      const Plan pl = plan_chunk(hbase + f.off, f, dst, tmp_at, want, cb, job.carray_dir, splits, blocks, e);
+      tmp_at += cb;
       if (pl == Plan::kError) {
         err = "ingest: " + e;
         return -1;
       }
-      if (pl == Plan::kFallback) fallback.push_back((int64_t)(&f - files.data()));
+      if (pl == Plan::kFallback) fallback.push_back(k);
+      stats[f.job].compressed_bytes += (int64_t)f.size;
+      stats[f.job].device_splits += (int64_t)(splits.size() - ns0);
     }
-    // task lists after the compressed bytes (8-byte aligned), one DMA for both
+    // heaviest streams first (compressed size; stored-raw copies last): the long serial decodes
+    // start in the first dispatch wave, spread over the CUs, instead of doubling up on SIMDs
+    std::stable_sort(splits.begin(), splits.end(), [](const BloscSplit& x, const BloscSplit& y) {
+      const uint32_t kx = x.codec == kSplitRaw ? 0 : x.csize, ky = y.codec == kSplitRaw ? 0 : y.csize;
+      return kx > ky;
+    });
+    // task lists after the compressed bytes, one DMA for all
     const size_t split_off = (comp_bytes + 15) & ~(size_t)15;
     const size_t block_off = split_off + splits.size() * sizeof(BloscSplit);
     const size_t all = block_off + blocks.size() * sizeof(BloscBlock);
     if (all > slot.host_cap || all > slot.dev_cap) {
-      // tasks did not fit the padding: grow both, keeping the compressed bytes
+      // tasks did not fit the slack: grow both, keeping the compressed bytes
       std::vector<unsigned char> keep(hbase, hbase + comp_bytes);
       if (!grow_host(slot.host, slot.host_cap, all) || !grow_dev(slot.dev, slot.dev_cap, all)) {
         err = "ingest: staging allocation failed";
@@ -583,45 +626,51 @@ int ingest_carray_device(const IngestJob& job, IngestPool& pool, IngestStats* st
       err = "ingest: blosc decode launch failed";
       return -1;
     }
-    for (int64_t k : fallback) {
+    if (trace)
+      fprintf(stderr, "[ingest] batch %zu: %zu chunks, %.1f MB -> %.1f MB, %zu splits; wait %.2f ms, read %.2f ms, plan+launch %.2f ms\n",
+              b, c1 - c0, total / 1e6, batch_out / 1e6, splits.size(), wait_ms, read_ms, ms_since(t_plan));
+    for (size_t k : fallback) {
       const ChunkFile& f = files[k];
+      const IngestJob& job = jobs[f.job];
       const BloscApi& bl = blosc_api();
       if (!bl.err.empty()) {
         err = bl.err;
         return -1;
       }
+      const size_t cb = chunk_bytes[f.job];
       const size_t want = (size_t)std::min<int64_t>(job.chunklen, job.nrows - f.index * job.chunklen) * job.itemsize;
       std::string e;
-      if (!host_decode_chunk(bl, hbase + f.off, chunk_bytes, want,
-                             static_cast<unsigned char*>(job.dev_dst) + (size_t)f.index * chunk_bytes, st, hostbuf,
-                             e)) {
+      if (!host_decode_chunk(bl, hbase + f.off, cb, want, static_cast<unsigned char*>(job.dev_dst) + (size_t)f.index * cb,
+                             st, hostbuf, e)) {
         err = "ingest: chunk " + std::to_string(f.index) + " of " + job.carray_dir + ": " + e;
         return -1;
       }
+      stats[f.job].host_fallback += 1;
     }
-    comp_total += (int64_t)total;
-    nsplits_total += (int64_t)splits.size();
-    nfallback += (int64_t)fallback.size();
+    c0 = c1;
   }
   unsigned int bad = 0;
+  const clk::time_point t_tail = clk::now();
   if (hipMemcpyAsync(&bad, pool.bad, sizeof(bad), hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess) {
     err = "ingest: device decode failed";
     return -1;
   }
+  if (trace) fprintf(stderr, "[ingest] tail wait %.2f ms\n", ms_since(t_tail));
   if (bad) {
-    err = "ingest: on-GPU blosc decode of " + job.carray_dir + " failed (corrupt stream)";
+    std::string dirs;
+    for (const IngestJob& j : jobs) dirs += (dirs.empty() ? "" : ", ") + j.carray_dir;
+    err = "ingest: on-GPU blosc decode of " + dirs + " failed (corrupt stream)";
     return -1;
   }
-  if (stats) {
-    stats->chunks = nchunks;
-    stats->compressed_bytes = comp_total;
-    stats->bytes = (int64_t)job.nrows * job.itemsize;
-    stats->threads = nthreads;
-    stats->device_splits = nsplits_total;
-    stats->host_fallback = nfallback;
-  }
   return 0;
+}
+
+int ingest_carray_device(const IngestJob& job, IngestPool& pool, IngestStats* stats, std::string& err) {
+  std::vector<IngestStats> st;
+  const int rc = ingest_carrays_device(std::vector<IngestJob>{job}, pool, st, err);
+  if (rc == 0 && stats) *stats = st[0];
+  return rc;
 }
 
 }  // namespace bqg

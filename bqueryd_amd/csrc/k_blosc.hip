@@ -132,6 +132,25 @@ __device__ __forceinline__ unsigned char out_byte(const gbyte* p) {
 // out[op + i] = out[op + i - dist] for i in [0, n)
 __device__ __forceinline__ void copy_match(Out& o, uint32_t op, uint32_t dist, uint32_t n) {
   const uint32_t lane = (uint32_t)o.lane;
+  if (dist == 1 && n >= 2048) {
+    // a long run of one byte (the zero planes of shuffled integers): 16-byte stores, and only
+    // the last kRing bytes go to the history
+    const uint32_t v = o.ring[(op - 1) & (kRing - 1)];
+    const uint32_t v4 = v * 0x01010101u;
+    gbyte* d = o.dst + op;
+    const uint32_t head = (uint32_t)((16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15);
+    if (lane < head) d[lane] = (unsigned char)v;
+    const uint32_t body = (n - head) & ~15u;
+    typedef __attribute__((address_space(1))) u32x4 g32x4;
+    g32x4* d16 = (g32x4*)(d + head);
+    const u32x4 w = {v4, v4, v4, v4};
+    for (uint32_t i = lane; i < body / 16; i += 64) d16[i] = w;
+    for (uint32_t i = head + body + lane; i < n; i += 64) d[i] = (unsigned char)v;
+    const uint32_t r0 = n > kRing ? n - kRing : 0;  // history: positions op + r0 .. op + n
+    for (uint32_t i = r0 + lane; i < n; i += 64) o.ring[(op + i) & (kRing - 1)] = (unsigned char)v;
+    wave_lds_sync();
+    return;
+  }
   if (dist <= 64) {
     // the period [op - dist, op) in registers, then byte i = period[i mod dist] by lane
     // permute: no reads of bytes written by this match
@@ -168,8 +187,8 @@ constexpr uint32_t kBad = 0xFFFFFFFFu;
 
 #ifdef BQG_BLOSC_PROF
 // micro-benchmark instrumentation (tools/micro): cycles and counts per phase of the LZ4 loop
-__device__ unsigned long long g_blosc_prof[16];
-#define PROF_DECL uint64_t prof_t = __builtin_readcyclecounter(), prof_acc[5] = {0, 0, 0, 0, 0}, prof_n[5] = {0, 0, 0, 0, 0}
+__device__ unsigned long long g_blosc_prof[32];
+#define PROF_DECL uint64_t prof_t = __builtin_readcyclecounter(), prof_acc[8] = {}, prof_n[8] = {}
 #define PROF_MARK(k)                                      \
   do {                                                    \
     const uint64_t now_ = __builtin_readcyclecounter();   \
@@ -180,9 +199,9 @@ __device__ unsigned long long g_blosc_prof[16];
 #define PROF_FLUSH                                                                   \
   do {                                                                               \
     if (o.lane == 0)                                                                 \
-      for (int k_ = 0; k_ < 5; ++k_) {                                               \
+      for (int k_ = 0; k_ < 8; ++k_) {                                               \
         atomicAdd(&g_blosc_prof[k_], (unsigned long long)prof_acc[k_]);              \
-        atomicAdd(&g_blosc_prof[8 + k_], (unsigned long long)prof_n[k_]);            \
+        atomicAdd(&g_blosc_prof[16 + k_], (unsigned long long)prof_n[k_]);           \
       }                                                                              \
   } while (0)
 #else
@@ -191,47 +210,241 @@ __device__ unsigned long long g_blosc_prof[16];
 #define PROF_FLUSH
 #endif
 
-// LZ4 block format: [token][literal length ext][literals][offset u16 LE][match length ext]
+// ---- LZ4 ------------------------------------------------------------------------------
+// Block format: sequences [token][literal length ext][literals][offset u16 LE][match length
+// ext]; the last sequence carries literals only.
+//
+// A sequence costs the serial loop one or two LDS round trips (its header, its match source),
+// which leaves a wave at ~1000 cycles per sequence on low-entropy planes (~22 K sequences per
+// 128 KiB split).  So sequences are decoded in groups of up to 64, one per lane:
+//  1. every lane parses the sequence that would start at each of 4 candidate offsets of the
+//     next kSpan compressed bytes (speculative: most candidates are not sequence starts);
+//  2. the true chain of starts through those parses is found by pointer doubling over the
+//     candidates' next-start table (lane permutes), up to 64 sequences / kGroupOut bytes;
+//  3. each sequence's lane writes its literals into the LDS history, then the matches run in
+//     rounds -- a match whose source lies wholly before the first unfinished match's start
+//     is final and copies (lane-serially, 4 bytes per LDS round trip);
+//  4. the group's decoded bytes are stored from the history to global memory, coalesced.
+// Long literal runs / matches (> kLong) and sequences not wholly inside the window go through
+// the wave-cooperative serial path, one at a time.
+constexpr uint32_t kSpan = 256;
+constexpr uint32_t kGroupOut = 4096;
+constexpr uint32_t kLong = 64;
+constexpr uint32_t kRingSafe = kRing - kGroupOut;  // group matches reaching further read global
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kDead = 1024;  // jump-table mark of a non-sequence candidate (> any next)
+
+// one sequence at the cursor, wave-cooperative; returns the new output position or kBad
+__device__ uint32_t lz4_one(Window& w, uint32_t clen, Out& o, uint32_t op, uint32_t dlen) {
+  const uint32_t token = w.next();
+  uint32_t lit = token >> 4;
+  if (lit == 15) {
+    uint32_t b;
+    do {
+      if (w.ip >= clen) return kBad;
+      b = w.next();
+      lit += b;
+    } while (b == 255);
+  }
+  if (w.ip + lit > clen || op + lit > dlen) return kBad;
+  if (lit) copy_literals(w, o, op, lit);
+  op += lit;
+  if (w.ip >= clen) return op;  // the last sequence
+  if (w.ip + 2 > clen) return kBad;
+  const uint32_t lo = w.next();
+  const uint32_t off = lo | (w.next() << 8);
+  uint32_t mlen = token & 15u;
+  if (mlen == 15) {
+    uint32_t b;
+    do {
+      if (w.ip >= clen) return kBad;
+      b = w.next();
+      mlen += b;
+    } while (b == 255);
+  }
+  mlen += 4;
+  if (off == 0 || off > op || op + mlen > dlen) return kBad;
+  copy_match(o, op, off, mlen);
+  return op + mlen;
+}
+
+struct Seq {
+  uint32_t next;    // split offset after the sequence; kNone: not a group sequence (not wholly
+                    // inside window and split, or a literal run / match longer than kLong)
+  uint32_t lit;     // literal bytes
+  uint32_t litpos;  // split offset of the literals
+  uint32_t dist;    // match offset (0: the last sequence)
+  uint32_t mlen;    // match bytes
+};
+
+// bytes [rel, rel + 4) of the window, little-endian: two aligned dword reads (the window
+// array is padded by 16 bytes)
+__device__ __forceinline__ uint32_t peek4(const lbyte* win, uint32_t rel) {
+  const __attribute__((address_space(3))) uint32_t* w32 = (const __attribute__((address_space(3))) uint32_t*)(win);
+  const uint32_t a = w32[rel >> 2], b = w32[(rel >> 2) + 1];
+  return __builtin_amdgcn_alignbyte(b, a, rel & 3);
+}
+
+// the sequence that would start at split offset c, parsed from the window (per lane): two
+// dependent LDS round trips -- the header word, then the offset word past the literals
+__device__ __forceinline__ Seq lz4_seq_at(const Window& w, uint32_t c, uint32_t clen) {
+  Seq s = {kNone, 0, 0, 0, 0};
+  const int32_t rel = (int32_t)c - w.lo;
+  if (c >= clen || rel < 0 || rel >= kWin) return s;
+  const uint32_t end = min(clen - c, (uint32_t)(kWin - rel));  // bytes readable from c
+  const uint32_t h = peek4(w.win, (uint32_t)rel);
+  const uint32_t token = h & 255u;
+  uint32_t q = 1, lit = token >> 4;
+  if (lit == 15) {  // one extension byte at most: longer runs are not group sequences
+    if (end < 2) return s;
+    const uint32_t x = (h >> 8) & 255u;
+    lit += x;
+    q = 2;
+    if (x == 255) return s;
+  }
+  if (lit > kLong || lit > end - q) return s;
+  s.litpos = c + q;
+  s.lit = lit;
+  q += lit;
+  if (q == clen - c) {  // the last sequence
+    s.next = clen;
+    return s;
+  }
+  if (q + 2 > end) return s;
+  const uint32_t g = peek4(w.win, (uint32_t)rel + q);
+  s.dist = g & 0xFFFFu;
+  q += 2;
+  uint32_t m = token & 15u;
+  if (m == 15) {
+    if (q >= end) return s;
+    const uint32_t x = (g >> 16) & 255u;
+    m += x;
+    ++q;
+    if (x == 255) return s;
+  }
+  s.mlen = m + 4;
+  if (s.mlen > kLong) return s;
+  s.next = c + q;
+  return s;
+}
+
+// inclusive prefix sum over the wave: DPP row shifts, then row broadcasts
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
+// D(x) for a jump table held as 4 x 64 lanes (entry x at lane x % 64 of register x / 64):
+// every lane gathers its own x by lane permute; x >= kSpan (left the span, or dead) is fixed
+__device__ __forceinline__ uint32_t jump(const uint32_t (&tbl)[4], uint32_t x) {
+  const int l = (int)(x & 63);
+  const uint32_t a = (uint32_t)__shfl((int)tbl[0], l, 64), b = (uint32_t)__shfl((int)tbl[1], l, 64);
+  const uint32_t c = (uint32_t)__shfl((int)tbl[2], l, 64), d = (uint32_t)__shfl((int)tbl[3], l, 64);
+  const uint32_t k = x >> 6;
+  const uint32_t v = k == 0 ? a : k == 1 ? b : k == 2 ? c : d;
+  return x < kSpan ? v : x;
+}
+
 __device__ uint32_t lz4_wave(Window& w, uint32_t clen, Out& o, uint32_t dlen) {
+  const uint32_t lane = (uint32_t)o.lane;
+  constexpr uint32_t M = kRing - 1;
   uint32_t op = 0;
   PROF_DECL;
   while (w.ip < clen) {
-    const uint32_t token = w.next();
-    uint32_t lit = token >> 4;
-    if (lit == 15) {
-      uint32_t b;
-      do {
-        if (w.ip >= clen) return kBad;
-        b = w.next();
-        lit += b;
-      } while (b == 255);
+    const uint32_t ip = w.ip;
+    // 1. speculative parses of the candidate starts ip + 64 k + lane
+    w.cover(0, kSpan + 2 * kLong);
+    // jump table D0 over the 4 x 64 candidates: the next start relative to ip (>= kSpan: the
+    // chain leaves the span), or kDead + c for a candidate that is not a group sequence
+    uint32_t d[6][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t c = 64 * k + lane;
+      const Seq s = lz4_seq_at(w, ip + c, clen);
+      d[0][k] = s.next == kNone ? kDead + c : s.next - ip;
     }
-    if (w.ip + lit > clen || op + lit > dlen) return kBad;
     PROF_MARK(0);
-    if (lit) {
-      copy_literals(w, o, op, lit);
-      PROF_MARK(1);
+    // 2. the chain of true starts by pointer doubling: D(j+1) = D(j) o D(j), then lane i
+    //    composes the D(j) of the bits of i: e_i = D0^i(0), the i-th sequence start
+#pragma unroll
+    for (int j = 1; j < 6; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[j][k] = jump(d[j - 1], d[j - 1][k]);
+    uint32_t e = 0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const uint32_t f = jump(d[j], e);
+      if ((lane >> j) & 1) e = f;
     }
-    op += lit;
-    if (w.ip >= clen) break;  // the last sequence carries literals only
-    if (w.ip + 2 > clen) return kBad;
-    const uint32_t lo = w.next();
-    const uint32_t off = lo | (w.next() << 8);
-    uint32_t mlen = token & 15u;
-    if (mlen == 15) {
-      uint32_t b;
-      do {
-        if (w.ip >= clen) return kBad;
-        b = w.next();
-        mlen += b;
-      } while (b == 255);
+    const uint32_t en = jump(d[0], e);  // the start after e_i
+    uint32_t t = (uint32_t)__builtin_popcountll(__ballot(e < kSpan && en < kDead));
+    PROF_MARK(1);
+    if (t == 0) {
+      op = lz4_one(w, clen, o, op, dlen);
+      if (op == kBad) return kBad;
+      PROF_MARK(7);
+      continue;
     }
-    mlen += 4;
-    if (off == 0 || off > op || op + mlen > dlen) return kBad;
-    PROF_MARK(0);
-    copy_match(o, op, off, mlen);
-    PROF_MARK(off <= 64 ? 2 : off <= kRing ? 3 : 4);
-    op += mlen;
+    // 3. the group: one sequence per lane (at most kGroupOut decoded bytes)
+    Seq s = {0, 0, 0, 0, 0};
+    if (lane < t) s = lz4_seq_at(w, ip + e, clen);
+    const uint32_t sz = s.lit + s.mlen;
+    const uint32_t incl = wave_incl_scan(sz);
+    t = max(1u, min(t, (uint32_t)__builtin_popcountll(__ballot(incl <= kGroupOut))));
+    const bool act = lane < t;
+    if (!act) s = Seq{0, 0, 0, 0, 0};
+    const uint32_t out = __builtin_amdgcn_readlane(incl, t - 1);
+    const uint32_t p = ip + __builtin_amdgcn_readlane(en, t - 1);
+    const uint32_t ostart = op + incl - sz, ms = ostart + s.lit;
+    const bool bad = act && (ms + s.mlen > dlen || (s.mlen && (s.dist == 0 || s.dist > ms)));
+    if (__ballot(bad)) return kBad;
+    PROF_MARK(2);
+    if (act && s.lit) {
+      const lbyte* lsrc = w.win + (s.litpos - w.lo);
+      for (uint32_t j = 0; j < s.lit; ++j) o.ring[(ostart + j) & M] = lsrc[j];
+    }
+    if (__ballot(act && s.mlen && s.dist > kRingSafe)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_lds_sync();
+    PROF_MARK(3);
+    uint64_t pend = __ballot(act && s.mlen != 0);
+    while (pend) {
+      const uint32_t u = (uint32_t)__builtin_ctzll(pend);
+      const uint32_t F = __builtin_amdgcn_readlane(ms, u);
+      const bool ready = ((pend >> lane) & 1) && ms - s.dist + min(s.mlen, s.dist) <= F;
+      if (ready) {
+        const uint32_t src = ms - s.dist;
+        if (s.dist > kRingSafe) {
+          for (uint32_t j = 0; j < s.mlen; ++j) o.ring[(ms + j) & M] = out_byte(o.dst + src + j);
+        } else if (s.dist >= 4) {
+          for (uint32_t j = 0; j < s.mlen; j += 4) {
+            const uint32_t b0 = o.ring[(src + j) & M], b1 = o.ring[(src + j + 1) & M];
+            const uint32_t b2 = o.ring[(src + j + 2) & M], b3 = o.ring[(src + j + 3) & M];
+            o.ring[(ms + j) & M] = (unsigned char)b0;
+            if (j + 1 < s.mlen) o.ring[(ms + j + 1) & M] = (unsigned char)b1;
+            if (j + 2 < s.mlen) o.ring[(ms + j + 2) & M] = (unsigned char)b2;
+            if (j + 3 < s.mlen) o.ring[(ms + j + 3) & M] = (unsigned char)b3;
+          }
+        } else {
+          for (uint32_t j = 0; j < s.mlen; ++j) o.ring[(ms + j) & M] = o.ring[(src + j) & M];
+        }
+      }
+      wave_lds_sync();
+      pend &= ~__ballot(ready);
+      PROF_MARK(5);
+    }
+    PROF_MARK(4);
+    // 4. the group's bytes to global memory
+    for (uint32_t c = 0; c < out; c += 64)
+      if (c + lane < out) o.dst[op + c + lane] = o.ring[(op + c + lane) & M];
+    op += out;
+    w.ip = p;
+    w.have = 0;
+    PROF_MARK(6);
   }
   PROF_FLUSH;
   return op;
@@ -290,7 +503,7 @@ __device__ uint32_t blosclz_wave(Window& w, uint32_t clen, Out& o, uint32_t dlen
 
 __global__ __launch_bounds__(64) void k_blosc_decode(const unsigned char* comp, const BloscSplit* tasks, int ntasks,
                                                      unsigned int* bad) {
-  __shared__ __align__(16) unsigned char win_s[kWin];
+  __shared__ __align__(16) unsigned char win_s[kWin + 16];
   __shared__ __align__(16) unsigned char ring_s[kRing];
   const int lane = threadIdx.x;
   Window w;

@@ -161,17 +161,20 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
         if self._table is None:
             self._table = ShardTable(OrderedDict(), device=self.device, nrows=self._len)
         missing = [n for n in names if n not in self._table.dtypes]
+        cold = []
         for n in missing:
             self._table.add_column(n, self._dtypes[n])
             self._table.names.append(n)
             if n in self._host:
                 self._table.push(n, self._host[n])
             else:
-                # cold path: the bcolz chunks decode on host threads straight into HBM
                 meta = bcolz_io.CArrayMeta(bcolz_io.ctable_column_dir(self.rootdir, n))
                 if meta.length != self._len:
                     raise ValueError('column %s has %d rows, table has %d' % (n, meta.length, self._len))
-                self._table.load_carray(n, meta.rootdir, meta.chunklen)
+                cold.append((n, meta.rootdir, meta.chunklen))
+        if cold:
+            # cold path: the bcolz chunks of every missing column, straight into HBM in one call
+            self._table.load_carrays(cold)
         if missing:
             self._table.sync()
         return self._table

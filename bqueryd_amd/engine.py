@@ -264,17 +264,26 @@ class ShardTable:
         the GPU decodes the blosc frames), 'host' (host threads decode, pinned double-buffered
         DMA) or 'auto' (default; env BQGPU_INGEST_DECODE).  Returns the ingest report as a
         dict."""
+        return self.load_carrays([(col, carray_dir, chunklen)], nthreads=nthreads, decode=decode)[0]
+
+    def load_carrays(self, specs, nthreads=None, decode=None):
+        """``load_carray`` for several columns in one call: [(col, carray_dir, chunklen)].  With
+        the device decoder the columns' chunks are batched together (file reads of one column
+        overlap the kernels of the previous one).  Returns one report per column."""
         self._touch()
         if not nthreads:
             nthreads = int(os.environ.get('BQGPU_INGEST_THREADS', '0')) or min(16, len(os.sched_getaffinity(0)))
         decode = decode or os.environ.get('BQGPU_INGEST_DECODE', 'auto')
         if decode not in L.DECODE_CODE:
             raise ValueError('decode must be one of %s' % sorted(L.DECODE_CODE))
-        st = L.IngestStats()
-        self.dev.check(self._lib.bqg_table_load_carray_ex(self.handle, self.slot(col), os.fsencode(carray_dir),
-                                                          int(chunklen), int(nthreads), L.DECODE_CODE[decode],
-                                                          ctypes.byref(st)))
-        return {f: getattr(st, f) for f, _ in st._fields_}
+        n = len(specs)
+        cols = (ctypes.c_int32 * max(n, 1))(*[self.slot(c) for c, _, _ in specs])
+        dirs = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(d) for _, d, _ in specs])
+        lens = (ctypes.c_int64 * max(n, 1))(*[int(k) for _, _, k in specs])
+        st = (L.IngestStats * max(n, 1))()
+        self.dev.check(self._lib.bqg_table_load_carrays(self.handle, n, cols, dirs, lens, int(nthreads),
+                                                        L.DECODE_CODE[decode], st))
+        return [{f: getattr(st[i], f) for f, _ in L.IngestStats._fields_} for i in range(n)]
 
     def sync(self):
         self.dev.check(self._lib.bqg_table_sync(self.handle))

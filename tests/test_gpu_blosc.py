@@ -31,7 +31,7 @@ def _array(dtype, n, seed, kind='random'):
     if dt.kind == 'f':
         return rng.normal(size=n).astype(dt)
     info = np.iinfo(dt)
-    lo, hi = (0, 1000) if kind == 'small' else (info.min, info.max)
+    lo, hi = (0, min(1000, info.max // 4)) if kind == 'small' else (info.min, info.max)
     return rng.integers(lo, hi, n, dtype=dt, endpoint=True)
 
 
@@ -117,8 +117,8 @@ def test_mixed_codecs_in_one_carray(tmp_path):
 
 
 def test_device_and_host_decoders_agree_multibatch(tmp_path):
-    """More chunks than one 256 MiB batch: both staging slots and the batch loop run."""
-    n = 40_000_000
+    """More chunks than one 512 MiB batch: both staging slots and the batch loop run."""
+    n = 80_000_000
     a = _array('int64', n, 9, 'small')
     d = str(tmp_path / 'col')
     bcolz_io.write_carray(d, a, chunklen=1 << 20, cname='lz4')
@@ -180,3 +180,44 @@ def test_missing_chunk_and_magic(tmp_path):
     os.remove(os.path.join(d, 'data', '__3.blp'))
     with pytest.raises(_lib.BqgError, match='cannot open'):
         _load(d, a)
+
+
+@pytest.mark.parametrize('decode', ['device', 'host'])
+def test_load_carrays_several_columns(tmp_path, decode):
+    """One call for several columns: batches span columns on the device path; every column
+    and its report must come out as if loaded alone."""
+    n = 3_000_000
+    cols = OrderedDict([('a', _array('int32', n, 1, 'small')), ('b', _array('float64', n, 2, 'cents')),
+                        ('c', _array('int8', n, 3, 'small')), ('d', _array('uint16', n, 4, 'runs'))])
+    cnames = {'a': 'lz4', 'b': 'blosclz', 'c': 'zstd', 'd': 'lz4'}
+    chunklens = {'a': 262_144, 'b': 100_000, 'c': 1 << 20, 'd': 77_777}
+    t = ShardTable(OrderedDict(), nrows=n)
+    try:
+        specs = []
+        for k, a in cols.items():
+            d = str(tmp_path / k)
+            bcolz_io.write_carray(d, a, chunklen=chunklens[k], cname=cnames[k])
+            t.add_column(k, a.dtype)
+            specs.append((k, d, chunklens[k]))
+        reps = t.load_carrays(specs, nthreads=4, decode=decode)
+        t.sync()
+        for (k, a), rep in zip(cols.items(), reps):
+            np.testing.assert_array_equal(t.read(k), a)
+            assert rep['chunks'] == -(-n // chunklens[k]) and rep['bytes'] == a.nbytes
+            if decode == 'device':
+                assert rep['host_chunks'] == (rep['chunks'] if cnames[k] == 'zstd' else 0), (k, rep)
+    finally:
+        t.close()
+
+
+def test_load_carrays_rejects_duplicates(tmp_path):
+    a = np.arange(1000, dtype=np.int32)
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=100)
+    t = ShardTable(OrderedDict(), nrows=len(a))
+    try:
+        t.add_column('x', a.dtype)
+        with pytest.raises(_lib.BqgError, match='twice'):
+            t.load_carrays([('x', d, 100), ('x', d, 100)], decode='device')
+    finally:
+        t.close()

@@ -32,6 +32,7 @@ def main():
     ap.add_argument('--threads', type=int, default=16)
     ap.add_argument('--cname', default='lz4')
     ap.add_argument('--dir', default=None, help='scratch directory for the shard (default: a temp dir)')
+    ap.add_argument('--decode', default='auto', help='decoder of the cold_query leg (auto / host / device)')
     args = ap.parse_args()
 
     from bqueryd_amd import bcolz_io, synth
@@ -53,10 +54,12 @@ def main():
         def ingest(decode):
             t = ShardTable({}, device=dev, nrows=args.rows)
             t0 = time.perf_counter()
+            specs = []
             for name in cols:
                 meta = bcolz_io.CArrayMeta(bcolz_io.ctable_column_dir(root, name))
                 t.add_column(name, meta.dtype)
-                t.load_carray(name, meta.rootdir, meta.chunklen, nthreads=args.threads, decode=decode)
+                specs.append((name, meta.rootdir, meta.chunklen))
+            t.load_carrays(specs, nthreads=args.threads, decode=decode)
             dev.synchronize()
             dt = time.perf_counter() - t0
             t.close()
@@ -76,6 +79,7 @@ def main():
                                         'threads': args.threads}
             print('ingest %s: %.1f ms' % (decode, s * 1e3), file=sys.stderr, flush=True)
         cold, warm = [], []
+        os.environ['BQGPU_INGEST_DECODE'] = args.decode
         for _ in range(args.reps):
             ct = ctable(rootdir=root, mode='r', auto_cache=True, device=dev)
             cold.append(query(ct))
@@ -90,7 +94,7 @@ def main():
                         % (args.rows, list(cols), args.cname),
             'decoded_bytes': nbytes, 'on_disk_bytes': on_disk, 'write_s': write_s,
             **legs,
-            'cold_query': {'s': min(cold), 'rows_per_s': args.rows / min(cold)},
+            'cold_query': {'s': min(cold), 'rows_per_s': args.rows / min(cold), 'decode': args.decode},
             'warm_query': {'s': min(warm), 'rows_per_s': args.rows / min(warm)},
             'host_decode_1t': {'s': host_1t, 'decoded_GBps': nbytes / host_1t / 1e9,
                                'note': 'one thread, host memory only (the reference worker\'s decode shape)'},

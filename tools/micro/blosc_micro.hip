@@ -6,6 +6,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "k_blosc.hip"  // one translation unit: the instrumentation symbols are file-local
@@ -84,17 +85,18 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost));
 #ifdef BQG_BLOSC_PROF
     if (v.size() == 1) {
-      unsigned long long pr[16];
+      unsigned long long pr[32];
       CK(hipMemset(bad, 0, 4));
-      unsigned long long z[16] = {};
+      unsigned long long z[32] = {};
       CK(hipMemcpyToSymbol(HIP_SYMBOL(bqg::g_blosc_prof), z, sizeof z));
       bqg::launch_blosc_decode(dcomp, dt, 1, bad, 0);
       CK(hipDeviceSynchronize());
       CK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(bqg::g_blosc_prof), sizeof pr));
-      const char* nm[5] = {"parse", "literals", "match<=64", "match ring", "match far"};
-      for (int k = 0; k < 5; ++k)
-        if (pr[8 + k]) printf("    %-11s n=%8llu  cycles/op %8.1f  total %.2f Mcyc\n", nm[k], pr[8 + k],
-                              (double)pr[k] / pr[8 + k], pr[k] / 1e6);
+      const char* nm[8] = {"spec parse", "chain", "reparse+scan", "literals", "round tail", "round", "flush",
+                           "serial seq"};
+      for (int k = 0; k < 8; ++k)
+        if (pr[16 + k]) printf("    %-12s n=%8llu  cycles/op %8.1f  total %.2f Mcyc\n", nm[k], pr[16 + k],
+                               (double)pr[k] / pr[16 + k], pr[k] / 1e6);
     }
 #endif
     printf("%-28s %6zu splits  %9.3f ms  %8.2f GB/s out  (comp %llu)  bad=%u\n", what, v.size(), ms,
@@ -102,6 +104,27 @@ int main(int argc, char** argv) {
     return 0;
   };
   if (run(all, "all")) return 1;
+  {
+    // byte-exact check of every copy against <frame>.expect (the shuffled block bytes)
+    std::string ep = std::string(argv[1]) + ".expect";
+    FILE* fe = fopen(ep.c_str(), "rb");
+    if (fe) {
+      std::vector<unsigned char> ex((size_t)nbytes), got((size_t)nbytes * reps);
+      const size_t rd = fread(ex.data(), 1, ex.size(), fe);
+      fclose(fe);
+      CK(hipMemcpy(got.data(), dout, got.size(), hipMemcpyDeviceToHost));
+      size_t bad_bytes = 0, first = (size_t)-1;
+      for (int r = 0; r < reps; ++r)
+        for (size_t i = 0; i < ex.size(); ++i)
+          if (got[(size_t)r * nbytes + i] != ex[i]) {
+            if (first == (size_t)-1) first = (size_t)r * nbytes + i;
+            ++bad_bytes;
+          }
+      printf("check vs %s (%zu bytes): %zu mismatches (first at %zd)\n", ep.c_str(), rd, bad_bytes,
+             (ssize_t)first);
+      if (bad_bytes) return 3;
+    }
+  }
   for (size_t i = 0; i < std::min<size_t>(all.size(), 16); ++i) {
     if (all[i].codec == bqg::kSplitRaw) continue;
     char name[64];
