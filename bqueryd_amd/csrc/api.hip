@@ -1260,6 +1260,16 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       if (waves > needg) waves = needg;
       while (waves > 64 && waves * S * 28 > budget) waves /= 2;
       if (waves < 1) waves = 1;
+      if (fused && d.compact) {
+        // 16-bit per-slot row counts: at most kScdCompactMaxRows rows per wave chunk
+        const uint64_t need = ((uint64_t)N + kScdCompactMaxRows - 1) / kScdCompactMaxRows;
+        if (need * S * 28 > budget) {
+          d.compact = 0;  // that many chunk states do not fit: the wide pass (32-bit counts)
+          d.wave_lds = scd_fused_wave_lds(S, false);
+        } else if (waves < need) {
+          waves = need;
+        }
+      }
       d.waves = (int)waves;
       d.chunk_rows = (((int64_t)((N + waves - 1) / waves)) + grain - 1) / grain * grain;
       d.lds_state = (S * 24 * (kBlock / 64) <= 64 * 1024) ? 1 : 0;
@@ -1662,7 +1672,7 @@ int bqg_table_load_carrays(bqg_table* t, int32_t n, const int32_t* cols, const c
       job.itemsize = (int)dtype_size(k.dtype);
       job.chunklen = chunklens[i];
       job.nthreads = nthreads;
-      job.device_decode = decode != BQG_DECODE_HOST;  // AUTO: the device decoder (DESIGN.md §6)
+      job.device_decode = decode != BQG_DECODE_HOST;  // AUTO: the device decoder (DESIGN.md §3)
       job.stream = c->stream;
     }
     HIPCHECK(hipStreamSynchronize(c->stream));  // the columns' zero-fill has landed

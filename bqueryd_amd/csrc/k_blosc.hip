@@ -146,8 +146,13 @@ __device__ __forceinline__ void copy_match(Out& o, uint32_t op, uint32_t dist, u
     const u32x4 w = {v4, v4, v4, v4};
     for (uint32_t i = lane; i < body / 16; i += 64) d16[i] = w;
     for (uint32_t i = head + body + lane; i < n; i += 64) d[i] = (unsigned char)v;
-    const uint32_t r0 = n > kRing ? n - kRing : 0;  // history: positions op + r0 .. op + n
-    for (uint32_t i = r0 + lane; i < n; i += 64) o.ring[(op + i) & (kRing - 1)] = (unsigned char)v;
+    if (n >= kRing) {  // the whole history becomes this byte
+      typedef __attribute__((address_space(3))) u32x4 l32x4;
+      l32x4* r16 = (l32x4*)o.ring;
+      for (uint32_t i = lane; i < kRing / 16; i += 64) r16[i] = w;
+    } else {
+      for (uint32_t i = lane; i < n; i += 64) o.ring[(op + i) & (kRing - 1)] = (unsigned char)v;
+    }
     wave_lds_sync();
     return;
   }

@@ -106,9 +106,12 @@ struct ScdLaunch {
 // LDS bytes per wave of k_scd_fused for a slot space of nslots: a 32-byte state per slot (20
 // bytes with compact 32-bit value codes) plus an 8-byte lane mask per slot
 inline size_t scd_fused_wave_lds(uint64_t nslots, bool compact = false) {
-  const size_t state = compact ? (((size_t)nslots * 20 + 7) & ~size_t(7)) : (size_t)nslots * 32;
+  // compact: 8-byte states + first values + first rows; wide: 32-byte states; then the
+  // 8-byte lane masks
+  const size_t state = compact ? (((size_t)nslots * 16 + 7) & ~size_t(7)) : (size_t)nslots * 32;
   return (state + (size_t)nslots * 8 + 15) & ~size_t(15);
 }
+constexpr int64_t kScdCompactMaxRows = 65280;  // rows per wave chunk of the compact pass (16-bit counts)
 constexpr size_t kScdFusedMaxLds = 80 * 1024;  // per workgroup (4 waves + shared cd filter)
 // fused_fn: query-specialised (JIT) k_scd_fused, or nullptr for the precompiled kernel
 // pass_done (optional): recorded between the pass and the chunk combine (kernel timing)

@@ -31,8 +31,13 @@ struct __align__(16) ScdSlot {
   uint32_t first_row;
   uint32_t pad;
 };
-struct __align__(16) ScdSlot32 {
-  uint32_t last, first, rows, changes;
+// Compact: 8 bytes of hot state per slot -- the first lane of a slot in a step reads and
+// writes it with one ds_read_b64 / ds_write_b64 -- rows and changes as 16-bit halves of `rc`
+// (chunks of at most kScdCompactMaxRows rows); the first value and first row live apart
+// (written once per slot and chunk).
+struct __align__(8) ScdSlot32 {
+  uint32_t last;  // value code of the slot's last row so far
+  uint32_t rc;    // rows (bits 0-15) | changes (bits 16-31)
 };
 
 constexpr int kScdAhead = 4;  // 64-row steps loaded ahead of the one being folded
@@ -54,17 +59,19 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
   const int S = (int)p.nslots;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned char* wbase = smem + (size_t)wave * d.wave_lds;
-  ScdSlot* st = reinterpret_cast<ScdSlot*>(wbase);        // wide state [S]
-  ScdSlot32* st32 = reinterpret_cast<ScdSlot32*>(wbase);  // compact state [S] ...
-  uint32_t* fr32 = reinterpret_cast<uint32_t*>(st32 + S); // ... + first rows [S]
+  ScdSlot* st = reinterpret_cast<ScdSlot*>(wbase);          // wide state [S]
+  ScdSlot32* st32 = reinterpret_cast<ScdSlot32*>(wbase);    // compact state [S] ...
+  uint32_t* fv32 = reinterpret_cast<uint32_t*>(st32 + S);   // ... + first value codes [S]
+  uint32_t* fr32 = fv32 + S;                                // ... + first rows [S]
   // per-slot lane masks of the current step (after the wide or compact state, 8-aligned)
   unsigned long long* tbl = reinterpret_cast<unsigned long long*>(
-      wbase + (COMPACT ? (((size_t)S * 20 + 7) & ~size_t(7)) : (size_t)S * 32));
+      wbase + (COMPACT ? (((size_t)S * 16 + 7) & ~size_t(7)) : (size_t)S * 32));
   unsigned int* cdb = reinterpret_cast<unsigned int*>(smem + (size_t)(blockDim.x >> 6) * d.wave_lds);
   for (int i = lane; i < S; i += 64) {
     tbl[i] = 0ull;
     if (COMPACT) {
-      st32[i] = ScdSlot32{0u, 0u, 0u, 0u};
+      st32[i] = ScdSlot32{0u, 0u};
+      fv32[i] = 0u;
       fr32[i] = kNoRow;
     } else {
       st[i] = ScdSlot{0ull, 0ull, 0u, 0u, kNoRow, 0u};
@@ -155,20 +162,18 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         tbl[s] = 0ull;  // after every lane's read of the mask (program order)
         const uint32_t add_rows = (uint32_t)__popcll(match), add_ch = (uint32_t)__popcll(dm & match);
         if (COMPACT) {
-          ScdSlot32 cur = st32[s];
-          uint32_t ch = cur.changes + add_ch;
-          if (cur.rows == 0) {
-            cur.first = (uint32_t)vb;
+          const ScdSlot32 cur = st32[s];
+          const uint32_t rows = cur.rc & 0xFFFFu;
+          uint32_t ch = (cur.rc >> 16) + add_ch;
+          if (rows == 0) {
+            fv32[s] = (uint32_t)vb;
             fr32[s] = (uint32_t)row;
             run_start = true;
           } else if (cur.last != (uint32_t)vb) {
             ch += 1u;
             run_start = true;
           }
-          cur.last = (uint32_t)lastv;
-          cur.rows += add_rows;
-          cur.changes = ch;
-          st32[s] = cur;
+          st32[s] = ScdSlot32{(uint32_t)lastv, (rows + add_rows) | (ch << 16)};
         } else {
           ScdSlot cur = st[s];
           uint32_t ch = cur.changes + add_ch;
@@ -228,11 +233,12 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
     const size_t o = (size_t)w * S + i;
     if (COMPACT) {
       const ScdSlot32 c = st32[i];
-      d.st_first_row[o] = c.rows ? fr32[i] : kNoRow;
-      d.st_first[o] = (uint64_t)d.vmin + c.first;
+      const uint32_t rows = c.rc & 0xFFFFu;
+      d.st_first_row[o] = rows ? fr32[i] : kNoRow;
+      d.st_first[o] = (uint64_t)d.vmin + fv32[i];
       d.st_last[o] = (uint64_t)d.vmin + c.last;
-      d.st_changes[o] = c.changes;
-      d.st_count[o] = c.rows;
+      d.st_changes[o] = c.rc >> 16;
+      d.st_count[o] = rows;
     } else {
       const ScdSlot c = st[i];
       d.st_first_row[o] = c.rows ? c.first_row : kNoRow;

@@ -221,3 +221,36 @@ def test_load_carrays_rejects_duplicates(tmp_path):
             t.load_carrays([('x', d, 100), ('x', d, 100)], decode='device')
     finally:
         t.close()
+
+
+@pytest.mark.parametrize('cname', ['lz4', 'blosclz'])
+@pytest.mark.parametrize('period', [3_000, 20_000, 40_000, 60_000])
+def test_far_matches(tmp_path, cname, period):
+    """A random block repeated at distances past the LDS history (LZ4 / BloscLZ far offsets,
+    BloscLZ's 16-bit distance escape beyond 8191): the matches read the output back from
+    global memory."""
+    rng = np.random.default_rng(period)
+    block = rng.integers(0, 256, period, dtype=np.uint8)
+    a = np.tile(block, 1_200_000 // period + 1)[:1_200_000]
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=1_200_000, cname=cname, shuffle=0, clevel=9)
+    with open(os.path.join(d, 'data', '__0.blp'), 'rb') as f:
+        flags = f.read()[16 + 2]
+    got, rep = _load(d, a)
+    np.testing.assert_array_equal(got, a)
+    assert rep['host_chunks'] == 0, 'flags %#x' % flags
+
+
+def test_long_literal_runs_and_short_matches(tmp_path):
+    """Incompressible stretches (literal runs longer than a group sequence) between short
+    repeats, in one stream."""
+    rng = np.random.default_rng(77)
+    parts = []
+    for i in range(400):
+        parts.append(rng.integers(0, 256, int(rng.integers(1, 700)), dtype=np.uint8))
+        parts.append(np.full(int(rng.integers(4, 300)), i % 7, dtype=np.uint8))
+    a = np.concatenate(parts)
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=len(a), cname='lz4', shuffle=0)
+    got, _ = _load(d, a)
+    np.testing.assert_array_equal(got, a)
