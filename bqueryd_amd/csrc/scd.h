@@ -46,18 +46,46 @@ __device__ __forceinline__ bool scd_equal(uint64_t a, uint64_t b, bool isf) {
   return isf ? (as_f64(a) == as_f64(b)) : (a == b);
 }
 
+// Row loads of one 64-row step: rows are addressed relative to the wave's chunk (32-bit lane
+// offsets from a uniform base, so the address math is one VALU op per column), 4- and 8-byte
+// columns load their element directly, narrower ones the aligned 8-byte word holding it.
 template <int NC>
-__device__ __forceinline__ void scd_issue(const ScanParams& p, int64_t b, int64_t end, int lane, uint2 (&dst)[NC]) {
-  int64_t r = b + lane;
-  r = r < end ? r : end - 1;  // lanes past the chunk re-read its last row (end > start)
+__device__ __forceinline__ void scd_issue(const ScanParams& p, int64_t start, uint32_t rb, uint32_t nrel, int lane,
+                                          uint2 (&dst)[NC]) {
+  uint32_t r = rb + (uint32_t)lane;
+  r = r < nrel ? r : nrel - 1;  // lanes past the chunk re-read its last row (nrel > 0)
 #pragma unroll
-  for (int c = 0; c < NC; ++c) dst[c] = load_row_word(p.cols[c], r);
+  for (int c = 0; c < NC; ++c) {
+    const DevCol& col = p.cols[c];
+    // a chunk spans < 2^29 rows (nrows < 2^32, >= 64 waves), so its byte offsets fit 32 bits:
+    // the loads use a scalar base plus a 32-bit lane offset
+    const unsigned char* base = col.ptr + (start << col.lg);
+    if (col.lg == 2) {
+      dst[c] = make_uint2(*reinterpret_cast<const uint32_t*>(base + (r << 2)), 0u);
+    } else if (col.lg == 3) {
+      dst[c] = *reinterpret_cast<const uint2*>(base + (r << 3));
+    } else {
+      dst[c] = load_row_word(col, start + (int64_t)r);
+    }
+  }
+}
+
+__device__ __forceinline__ void scd_word_to_chunk(Chunk& c, const DevCol& col, int64_t row, uint2 w) {
+  if (col.lg >= 2) {
+    c.a = make_uint4(w.x, w.y, 0u, 0u);
+    c.b = make_uint4(0u, 0u, 0u, 0u);
+    c.sh = 0;
+  } else {
+    row_word_to_chunk(c, col, row, w);
+  }
 }
 
 template <int NC, bool COMPACT>
 __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLaunch& d, unsigned char* smem) {
   const int S = (int)p.nslots;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave-uniform in a register the compiler knows to be uniform: the chunk bounds and step
+  // counters below become scalar (SALU) instead of per-lane 64-bit VALU arithmetic
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   unsigned char* wbase = smem + (size_t)wave * d.wave_lds;
   ScdSlot* st = reinterpret_cast<ScdSlot*>(wbase);          // wide state [S]
   ScdSlot32* st32 = reinterpret_cast<ScdSlot32*>(wbase);    // compact state [S] ...
@@ -102,18 +130,21 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
   const bool cd_runs = cc == vc;  // count_distinct of the sorted_count_distinct column
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   uint2 ring[kScdAhead][NC];
-  if (start < end) {
+  // rows of the chunk (< 2^32: N < kNoRow); the last waves' chunks may start past the end
+  const uint32_t nrel = end > start ? (uint32_t)(end - start) : 0u;
+  if (nrel) {
 #pragma unroll
-    for (int a = 0; a < kScdAhead; ++a) scd_issue<NC>(p, start + 64 * a, end, lane, ring[a]);
+    for (int a = 0; a < kScdAhead; ++a) scd_issue<NC>(p, start, 64u * a, nrel, lane, ring[a]);
   }
-  for (int64_t gbase = start; gbase < end; gbase += 64 * kScdAhead) {
+  for (uint32_t gbase = 0; gbase < nrel; gbase += 64 * kScdAhead) {
 #pragma unroll
     for (int a = 0; a < kScdAhead; ++a) {
-      const int64_t b = gbase + 64 * a;
-      const int64_t row = b + lane;
+      const uint32_t rb = gbase + 64u * a;
+      const uint32_t rel = rb + (uint32_t)lane;
+      const int64_t row = start + (int64_t)rel;
       Chunk raw[NC];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) row_word_to_chunk(raw[c], p.cols[c], row, ring[a][c]);
+      for (int c = 0; c < NC; ++c) scd_word_to_chunk(raw[c], p.cols[c], row, ring[a][c]);
       uint64_t v[NC][1];
       decode_all<NC, 1>(p, raw, v);
       // the step's values are out of ring[a] before its refill is issued: without this
@@ -124,9 +155,9 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       // path, so the compiler waits for exactly the step it consumes (vmcnt(N), not vmcnt(0));
       // steps past the chunk end skip their work but not their loads (no `break`, whose exit
       // edge would merge a shorter load history into the loop header)
-      scd_issue<NC>(p, b + 64 * kScdAhead, end, lane, ring[a]);
-      if (b >= end) continue;
-      const bool act = row < end && (vals_pass<NC, 1>(p, row, v) & 1u);
+      scd_issue<NC>(p, start, rb + 64u * kScdAhead, nrel, lane, ring[a]);
+      if (rb >= nrel) continue;
+      const bool act = rel < nrel && (vals_pass<NC, 1>(p, row, v) & 1u);
       uint64_t code[1];
       vals_code<NC, 1>(p, v, code);
       const uint32_t s = (uint32_t)code[0];
@@ -198,7 +229,8 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         // (slot, value) pair bit (the planner fuses pair spaces < 2^30 only): an LDS
         // fire-and-forget OR (merged into the device bitmap once per workgroup at the end);
         // without an LDS bitmap, the device bitmap directly
-        const uint32_t bit = s * (uint32_t)d.cd.vrange + (uint32_t)(vcd - (uint64_t)d.cd.vmin);
+        // 32-bit arithmetic: the pair space is < 2^30
+        const uint32_t bit = s * (uint32_t)d.cd.vrange + ((uint32_t)vcd - (uint32_t)d.cd.vmin);
         const unsigned int m = 1u << (bit & 31);
         if (cd_mode == 1) {
           // read first: lanes of one word broadcast; only a new pair pays the (serialising)
