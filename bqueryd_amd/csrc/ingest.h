@@ -40,12 +40,16 @@ struct DecodeSlot {
   size_t dev_cap = 0;
   void* tmp = nullptr;   // device: decoded byte-shuffled blocks before the un-shuffle
   size_t tmp_cap = 0;
-  hipEvent_t done = nullptr;  // the slot's copy + kernels have finished
+  hipEvent_t copied = nullptr;  // the slot's host-to-device copy has finished (host reusable)
+  hipEvent_t done = nullptr;    // the slot's kernels have finished (device buffers reusable)
+  hipStream_t stream = nullptr; // the slot's decode kernels: batches decode concurrently
 };
+constexpr int kDecodeSlots = 3;
 struct IngestPool {
   int device = -1;
   std::vector<IngestWorker> workers;
-  DecodeSlot slots[2];
+  DecodeSlot slots[kDecodeSlots];
+  hipStream_t copy_stream = nullptr;  // host-to-device copies of the batches, in order
   unsigned int* bad = nullptr;  // device flag: a split failed to decode
   ~IngestPool();
 };

@@ -99,15 +99,28 @@ bool read_file(const std::string& path, std::vector<unsigned char>& buf, std::st
 
 }  // namespace
 
-IngestPool::~IngestPool() {
-  for (DecodeSlot& d : slots) {
-    if (d.done) (void)hipEventSynchronize(d.done);
+// drops the on-GPU decode's staging (its streams' work first)
+void release_decode(IngestPool& pool) {
+  if (pool.copy_stream) (void)hipStreamSynchronize(pool.copy_stream);
+  for (DecodeSlot& d : pool.slots)
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+  for (DecodeSlot& d : pool.slots) {
     if (d.host) (void)hipHostFree(d.host);
     if (d.dev) (void)hipFree(d.dev);
     if (d.tmp) (void)hipFree(d.tmp);
+    if (d.copied) (void)hipEventDestroy(d.copied);
     if (d.done) (void)hipEventDestroy(d.done);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+    d = DecodeSlot();
   }
-  if (bad) (void)hipFree(bad);
+  if (pool.bad) (void)hipFree(pool.bad);
+  pool.bad = nullptr;
+  if (pool.copy_stream) (void)hipStreamDestroy(pool.copy_stream);
+  pool.copy_stream = nullptr;
+}
+
+IngestPool::~IngestPool() {
+  release_decode(*this);
   for (IngestWorker& w : workers) {
     if (w.stream) (void)hipStreamSynchronize(w.stream);
     for (int k = 0; k < 2; ++k) {
@@ -268,7 +281,15 @@ int ingest_carray(const IngestJob& job, IngestPool& pool, IngestStats* stats, st
 
 namespace {
 
-constexpr size_t kBatchBytes = size_t(512) << 20;  // decoded bytes per batch
+// decoded bytes per batch (BQGPU_INGEST_BATCH_MB overrides; tools/bench_ingest.py)
+size_t batch_bytes() {
+  static const size_t b = [] {
+    const char* e = getenv("BQGPU_INGEST_BATCH_MB");
+    const long mb = e ? atol(e) : 256;
+    return (size_t)(mb > 0 ? mb : 256) << 20;
+  }();
+  return b;
+}
 constexpr size_t kRawPiece = size_t(64) << 10;      // stored-raw bytes per copy task
 
 bool grow_host(void*& p, size_t& cap, size_t want) {
@@ -445,33 +466,31 @@ int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, 
   }
   if (chunks.empty()) return 0;
   const IngestJob& job0 = jobs[0];
-  hipStream_t st = job0.stream;
   if (pool.device != job0.device) {
-    // resources of another device: drop them (the slots are re-created below)
+    // resources of another device: drop them (re-created below)
     pool.workers.clear();
-    for (DecodeSlot& d : pool.slots) {
-      if (d.done) (void)hipEventSynchronize(d.done);
-      if (d.host) (void)hipHostFree(d.host);
-      if (d.dev) (void)hipFree(d.dev);
-      if (d.tmp) (void)hipFree(d.tmp);
-      if (d.done) (void)hipEventDestroy(d.done);
-      d = DecodeSlot();
-    }
-    if (pool.bad) (void)hipFree(pool.bad);
-    pool.bad = nullptr;
+    release_decode(pool);
     pool.device = job0.device;
   }
+  if (!pool.copy_stream && hipStreamCreateWithFlags(&pool.copy_stream, hipStreamNonBlocking) != hipSuccess) {
+    err = "ingest: HIP stream creation failed";
+    return -1;
+  }
   for (DecodeSlot& d : pool.slots)
-    if (!d.done && hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess) {
-      err = "ingest: HIP event creation failed";
+    if ((!d.done && hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess) ||
+        (!d.copied && hipEventCreateWithFlags(&d.copied, hipEventDisableTiming) != hipSuccess) ||
+        (!d.stream && hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess)) {
+      err = "ingest: HIP event / stream creation failed";
       return -1;
     }
+  hipStream_t cs = pool.copy_stream;
   if (!pool.bad && hipMalloc(&pool.bad, sizeof(unsigned int)) != hipSuccess) {
     pool.bad = nullptr;
     err = "ingest: device allocation failed";
     return -1;
   }
-  if (hipMemsetAsync(pool.bad, 0, sizeof(unsigned int), st) != hipSuccess) {
+  // on the copy stream: every decode kernel follows its batch's copy, so this clear too
+  if (hipMemsetAsync(pool.bad, 0, sizeof(unsigned int), cs) != hipSuccess) {
     err = "ingest: device memset failed";
     return -1;
   }
@@ -493,11 +512,13 @@ int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, 
   for (size_t c0 = 0, b = 0; c0 < chunks.size(); ++b) {
     // the batch: chunks up to kBatchBytes decoded (at least one)
     size_t c1 = c0, batch_out = 0;
-    while (c1 < chunks.size() && (c1 == c0 || batch_out + chunk_bytes[chunks[c1].job] <= kBatchBytes))
+    while (c1 < chunks.size() && (c1 == c0 || batch_out + chunk_bytes[chunks[c1].job] <= batch_bytes()))
       batch_out += chunk_bytes[chunks[c1++].job];
-    DecodeSlot& slot = pool.slots[b & 1];
+    // three slots in turn: batch b's file reads overlap batch b-1's copy and b-2's kernels
+    DecodeSlot& slot = pool.slots[b % kDecodeSlots];
+    hipStream_t st = slot.stream;
     const clk::time_point t_wait = clk::now();
-    if (hipEventSynchronize(slot.done) != hipSuccess) {
+    if (hipEventSynchronize(slot.copied) != hipSuccess) {  // the slot's host buffer is free
       err = "ingest: HIP event wait failed";
       return -1;
     }
@@ -517,7 +538,15 @@ int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, 
       total += ((size_t)sb.st_size + 15) & ~(size_t)15;
     }
     const size_t comp_bytes = total + kBloscPad;
-    if (!grow_host(slot.host, slot.host_cap, comp_bytes) || !grow_dev(slot.dev, slot.dev_cap, comp_bytes)) {
+    // device buffers of the slot are reallocated only once its previous kernels are done
+    if ((slot.dev_cap < comp_bytes || slot.tmp_cap < batch_out) && hipEventSynchronize(slot.done) != hipSuccess) {
+      err = "ingest: HIP event wait failed";
+      return -1;
+    }
+    // sized once for a full batch (page-locked allocations cost ~0.1 ms per MB): compressed
+    // bytes are at most the decoded bytes plus the frame headers and the alignment
+    const size_t slot_bytes = std::max(comp_bytes, batch_bytes() + batch_bytes() / 16 + kBloscPad);
+    if (!grow_host(slot.host, slot.host_cap, slot_bytes) || !grow_dev(slot.dev, slot.dev_cap, slot_bytes)) {
       err = "ingest: staging allocation failed";
       return -1;
     }
@@ -566,7 +595,7 @@ int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, 
     const double read_ms = ms_since(t_read);
     const clk::time_point t_plan = clk::now();
     // tasks (byte-shuffled blocks decode into the slot's scratch, then un-shuffle)
-    if (!grow_dev(slot.tmp, slot.tmp_cap, batch_out)) {
+    if (!grow_dev(slot.tmp, slot.tmp_cap, std::max(batch_out, batch_bytes()))) {
       err = "ingest: shuffle scratch allocation failed";
       return -1;
     }
@@ -604,6 +633,10 @@ int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, 
     const size_t all = block_off + blocks.size() * sizeof(BloscBlock);
     if (all > slot.host_cap || all > slot.dev_cap) {
       // tasks did not fit the slack: grow both, keeping the compressed bytes
+      if (hipEventSynchronize(slot.done) != hipSuccess) {
+        err = "ingest: HIP event wait failed";
+        return -1;
+      }
       std::vector<unsigned char> keep(hbase, hbase + comp_bytes);
       if (!grow_host(slot.host, slot.host_cap, all) || !grow_dev(slot.dev, slot.dev_cap, all)) {
         err = "ingest: staging allocation failed";
@@ -615,7 +648,10 @@ int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, 
     if (!splits.empty()) memcpy(hbase + split_off, splits.data(), splits.size() * sizeof(BloscSplit));
     if (!blocks.empty()) memcpy(hbase + block_off, blocks.data(), blocks.size() * sizeof(BloscBlock));
     unsigned char* dbase = static_cast<unsigned char*>(slot.dev);
-    if (hipMemcpyAsync(dbase, hbase, all, hipMemcpyHostToDevice, st) != hipSuccess) {
+    // copy stream: after the slot's previous kernels; decode stream: after this copy
+    if (hipStreamWaitEvent(cs, slot.done, 0) != hipSuccess ||
+        hipMemcpyAsync(dbase, hbase, all, hipMemcpyHostToDevice, cs) != hipSuccess ||
+        hipEventRecord(slot.copied, cs) != hipSuccess || hipStreamWaitEvent(st, slot.copied, 0) != hipSuccess) {
       err = "ingest: host-to-device copy failed";
       return -1;
     }
@@ -651,8 +687,9 @@ int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, 
   }
   unsigned int bad = 0;
   const clk::time_point t_tail = clk::now();
-  if (hipMemcpyAsync(&bad, pool.bad, sizeof(bad), hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess) {
+  bool ok = hipStreamSynchronize(cs) == hipSuccess;
+  for (DecodeSlot& d : pool.slots) ok = ok && hipStreamSynchronize(d.stream) == hipSuccess;
+  if (!ok || hipMemcpy(&bad, pool.bad, sizeof(bad), hipMemcpyDeviceToHost) != hipSuccess) {
     err = "ingest: device decode failed";
     return -1;
   }

