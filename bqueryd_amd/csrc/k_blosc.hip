@@ -344,6 +344,92 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
+// ---- BloscLZ ---------------------------------------------------------------------------
+// FastLZ-derived tokens: ctrl < 32 -> ctrl + 1 literals; else a match of length (ctrl >> 5) + 2
+// (7: extended by bytes until one is not 255) at distance ((ctrl & 31) << 8) + next byte + 1,
+// or 8192 + a big-endian u16 when that byte is 255 and ctrl & 31 == 31.  The first token is a
+// literal run of (first byte & 31) + 1.  A match needs at least one byte after its distance
+// byte (the stream ends with literals).  The group decoder below treats a token as a sequence
+// with either literals or a match.
+constexpr uint32_t kBloscLzMaxDistance = 8191;
+
+// one token at the cursor (not the first), wave-cooperative; the new output position or kBad
+__device__ uint32_t blosclz_one(Window& w, uint32_t clen, Out& o, uint32_t op, uint32_t dlen) {
+  const uint32_t ctrl = w.next();
+  if (ctrl < 32) {
+    const uint32_t n = ctrl + 1;
+    if (op + n > dlen || w.ip + n > clen) return kBad;
+    copy_literals(w, o, op, n);
+    return op + n;
+  }
+  uint32_t len = (ctrl >> 5) - 1;
+  uint32_t ofs = (ctrl & 31u) << 8;
+  if (len == 6) {
+    uint32_t code;
+    do {
+      if (w.ip + 1 >= clen) return kBad;
+      code = w.next();
+      len += code;
+    } while (code == 255);
+  } else if (w.ip + 1 >= clen) {
+    return kBad;
+  }
+  const uint32_t code = w.next();
+  len += 3;
+  uint32_t dist = ofs + code + 1;
+  if (code == 255 && ofs == (31u << 8)) {
+    if (w.ip + 1 >= clen) return kBad;
+    const uint32_t hi = w.next();
+    ofs = (hi << 8) + w.next();
+    dist = ofs + kBloscLzMaxDistance + 1;
+  }
+  if (op + len > dlen || dist > op) return kBad;
+  copy_match(o, op, dist, len);
+  return op + len;
+}
+
+// the token that would start at split offset c (not the first), parsed from the window
+__device__ __forceinline__ Seq blosclz_seq_at(const Window& w, uint32_t c, uint32_t clen) {
+  Seq s = {kNone, 0, 0, 0, 0};
+  const int32_t rel = (int32_t)c - w.lo;
+  if (c >= clen || rel < 0 || rel >= kWin) return s;
+  const uint32_t avail = clen - c;                 // bytes to the end of the stream
+  const uint32_t wend = (uint32_t)(kWin - rel);    // bytes to the end of the window
+  const uint64_t hb = (uint64_t)peek4(w.win, (uint32_t)rel) | ((uint64_t)peek4(w.win, (uint32_t)rel + 4) << 32);
+  const uint32_t ctrl = (uint32_t)hb & 255u;
+  if (ctrl < 32) {
+    const uint32_t n = ctrl + 1;
+    if (1 + n > min(avail, wend)) return s;
+    s.lit = n;
+    s.litpos = c + 1;
+    s.next = c + 1 + n;
+    return s;
+  }
+  uint32_t len = (ctrl >> 5) - 1, ofs = (ctrl & 31u) << 8, q = 1;
+  if (len == 6) {  // one extension byte at most: longer matches are not group sequences
+    if (q + 1 >= avail) return s;
+    const uint32_t x = (uint32_t)(hb >> (8 * q)) & 255u;
+    ++q;
+    len += x;
+    if (x == 255) return s;
+  } else if (q + 1 >= avail) {
+    return s;
+  }
+  const uint32_t code = (uint32_t)(hb >> (8 * q)) & 255u;
+  ++q;
+  uint32_t dist = ofs + code + 1;
+  if (code == 255 && ofs == (31u << 8)) {
+    if (q + 1 >= avail) return s;
+    dist = ((((uint32_t)(hb >> (8 * q)) & 255u) << 8) | ((uint32_t)(hb >> (8 * q + 8)) & 255u)) + kBloscLzMaxDistance + 1;
+    q += 2;
+  }
+  if (q > wend || len + 3 > kLong) return s;
+  s.dist = dist;
+  s.mlen = len + 3;
+  s.next = c + q;
+  return s;
+}
+
 // D(x) for a jump table held as 4 x 64 lanes (entry x at lane x % 64 of register x / 64):
 // every lane gathers its own x by lane permute; x >= kSpan (left the span, or dead) is fixed
 __device__ __forceinline__ uint32_t jump(const uint32_t (&tbl)[4], uint32_t x) {
@@ -355,11 +441,20 @@ __device__ __forceinline__ uint32_t jump(const uint32_t (&tbl)[4], uint32_t x) {
   return x < kSpan ? v : x;
 }
 
-__device__ uint32_t lz4_wave(Window& w, uint32_t clen, Out& o, uint32_t dlen) {
+// LZ4 (BLZ false) or BloscLZ (BLZ true) stream, decoded in groups of sequences
+template <bool BLZ>
+__device__ uint32_t group_wave(Window& w, uint32_t clen, Out& o, uint32_t dlen) {
   const uint32_t lane = (uint32_t)o.lane;
   constexpr uint32_t M = kRing - 1;
   uint32_t op = 0;
   PROF_DECL;
+  if (BLZ) {  // the first token: a literal run of (first byte & 31) + 1
+    if (clen == 0) return 0;
+    const uint32_t n = (w.next() & 31u) + 1;
+    if (n > dlen || w.ip + n > clen) return kBad;
+    copy_literals(w, o, 0, n);
+    op = n;
+  }
   while (w.ip < clen) {
     const uint32_t ip = w.ip;
     // 1. speculative parses of the candidate starts ip + 64 k + lane
@@ -370,7 +465,7 @@ __device__ uint32_t lz4_wave(Window& w, uint32_t clen, Out& o, uint32_t dlen) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t c = 64 * k + lane;
-      const Seq s = lz4_seq_at(w, ip + c, clen);
+      const Seq s = BLZ ? blosclz_seq_at(w, ip + c, clen) : lz4_seq_at(w, ip + c, clen);
       d[0][k] = s.next == kNone ? kDead + c : s.next - ip;
     }
     PROF_MARK(0);
@@ -390,14 +485,14 @@ __device__ uint32_t lz4_wave(Window& w, uint32_t clen, Out& o, uint32_t dlen) {
     uint32_t t = (uint32_t)__builtin_popcountll(__ballot(e < kSpan && en < kDead));
     PROF_MARK(1);
     if (t == 0) {
-      op = lz4_one(w, clen, o, op, dlen);
+      op = BLZ ? blosclz_one(w, clen, o, op, dlen) : lz4_one(w, clen, o, op, dlen);
       if (op == kBad) return kBad;
       PROF_MARK(7);
       continue;
     }
     // 3. the group: one sequence per lane (at most kGroupOut decoded bytes)
     Seq s = {0, 0, 0, 0, 0};
-    if (lane < t) s = lz4_seq_at(w, ip + e, clen);
+    if (lane < t) s = BLZ ? blosclz_seq_at(w, ip + e, clen) : lz4_seq_at(w, ip + e, clen);
     const uint32_t sz = s.lit + s.mlen;
     const uint32_t incl = wave_incl_scan(sz);
     t = max(1u, min(t, (uint32_t)__builtin_popcountll(__ballot(incl <= kGroupOut))));
@@ -455,55 +550,6 @@ __device__ uint32_t lz4_wave(Window& w, uint32_t clen, Out& o, uint32_t dlen) {
   return op;
 }
 
-// BloscLZ (FastLZ-derived): ctrl < 32 -> ctrl + 1 literals; else a match of length
-// (ctrl >> 5) + 2 (7: extended by bytes until one is not 255) at distance ((ctrl & 31) << 8)
-// + next byte + 1, or 8192 + a big-endian u16 when that byte is 255 and ctrl & 31 == 31
-constexpr uint32_t kBloscLzMaxDistance = 8191;
-
-__device__ uint32_t blosclz_wave(Window& w, uint32_t clen, Out& o, uint32_t dlen) {
-  if (clen == 0) return 0;
-  uint32_t op = 0;
-  uint32_t ctrl = w.next() & 31u;
-  for (;;) {
-    if (ctrl >= 32) {
-      uint32_t len = (ctrl >> 5) - 1;
-      uint32_t ofs = (ctrl & 31u) << 8;
-      if (len == 6) {
-        uint32_t code;
-        do {
-          if (w.ip + 1 >= clen) return kBad;
-          code = w.next();
-          len += code;
-        } while (code == 255);
-      } else if (w.ip + 1 >= clen) {
-        return kBad;
-      }
-      const uint32_t code = w.next();
-      len += 3;
-      uint32_t dist = ofs + code + 1;
-      if (code == 255 && ofs == (31u << 8)) {
-        if (w.ip + 1 >= clen) return kBad;
-        const uint32_t hi = w.next();
-        ofs = (hi << 8) + w.next();
-        dist = ofs + kBloscLzMaxDistance + 1;
-      }
-      if (op + len > dlen || dist > op) return kBad;
-      copy_match(o, op, dist, len);
-      op += len;
-      if (w.ip >= clen) break;
-      ctrl = w.next();
-    } else {
-      const uint32_t n = ctrl + 1;
-      if (op + n > dlen || w.ip + n > clen) return kBad;
-      copy_literals(w, o, op, n);
-      op += n;
-      if (w.ip >= clen) break;
-      ctrl = w.next();
-    }
-  }
-  return op;
-}
-
 }  // namespace
 
 __global__ __launch_bounds__(64) void k_blosc_decode(const unsigned char* comp, const BloscSplit* tasks, int ntasks,
@@ -531,7 +577,7 @@ __global__ __launch_bounds__(64) void k_blosc_decode(const unsigned char* comp, 
       w.ip = 0;
       w.have = 0;
       w.load(0);
-      got = s.codec == kSplitLz4 ? lz4_wave(w, s.csize, o, s.dsize) : blosclz_wave(w, s.csize, o, s.dsize);
+      got = s.codec == kSplitLz4 ? group_wave<false>(w, s.csize, o, s.dsize) : group_wave<true>(w, s.csize, o, s.dsize);
     }
     if (got != s.dsize && lane == 0) atomicOr(bad, 1u);  // a vector atomic (one lane)
   }

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Blosc frames of the C2 shard's columns for tools/micro/blosc_micro.hip: <col>.lz4 (one
-chunk, raw blosc1 frame) and <col>.lz4.expect (the decoded, still byte-shuffled block bytes the
+"""Blosc frames of the C2 shard's columns for tools/micro/blosc_micro.hip: <col>.lz4 and
+<col>.blz (one chunk each, raw blosc1 frames, LZ4 / BloscLZ) and <col>.<ext>.expect (the decoded, still byte-shuffled block bytes the
 decode kernel must produce before the un-shuffle)."""
 import os
 import struct
@@ -20,19 +20,20 @@ def main():
     cols = synth.taxi_shard(1_000_000, config_id=2, columns=synth.query_columns(cfg))
     for name, a in cols.items():
         x = np.ascontiguousarray(a[:(1 << 20) // a.itemsize])
-        f = bcolz_io.compress_chunk(x, 5, 1, 'lz4')
-        ts = f[3]
-        nbytes, bs, _ = struct.unpack_from('<iii', f, 4)
-        raw = x.view(np.uint8)
-        exp = bytearray()
-        for b0 in range(0, nbytes, bs):
-            blk = raw[b0:b0 + bs]
-            n = len(blk) // ts
-            exp += blk[:n * ts].reshape(n, ts).T.tobytes() + blk[n * ts:].tobytes()
-        with open(os.path.join(out_dir, name + '.lz4'), 'wb') as fh:
-            fh.write(f)
-        with open(os.path.join(out_dir, name + '.lz4.expect'), 'wb') as fh:
-            fh.write(bytes(exp))
+        for cname, ext in (('lz4', '.lz4'), ('blosclz', '.blz')):
+            f = bcolz_io.compress_chunk(x, 5, 1, cname)
+            ts = f[3]
+            nbytes, bs, _ = struct.unpack_from('<iii', f, 4)
+            raw = x.view(np.uint8)
+            exp = bytearray()
+            for b0 in range(0, nbytes, bs):
+                blk = raw[b0:b0 + bs]
+                n = len(blk) // ts
+                exp += blk[:n * ts].reshape(n, ts).T.tobytes() + blk[n * ts:].tobytes()
+            with open(os.path.join(out_dir, name + ext), 'wb') as fh:
+                fh.write(f)
+            with open(os.path.join(out_dir, name + ext + '.expect'), 'wb') as fh:
+                fh.write(bytes(exp))
 
 
 if __name__ == '__main__':
