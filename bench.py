@@ -172,6 +172,7 @@ def main(argv=None):
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5'])
+    ap.add_argument('--sorted', action='store_true', help='C4: rows sorted by (pu_location_id, passenger_count)')
     ap.add_argument('--c5-per-shard', action='store_true',
                     help='C5: one groupby per shard + local re-group instead of one pass over the rank\'s shards')
     ap.add_argument('--rows', type=int, default=None, help='override rows per shard')
@@ -242,8 +243,12 @@ def main(argv=None):
             return merged
     else:
         rows = args.rows or cfg['rows']
+        # --sorted: C4's second variant, rows ordered by (pu_location_id, passenger_count)
+        # (SURVEY.md §8d), the row order sorted_count_distinct is meant for
+        sort_by = ['pu_location_id', 'passenger_count'] if (args.sorted and args.config == 'c4') else None
         cols = synth.taxi_shard(rows, config_id=synth.CONFIG_ID[args.config], n_shards=max(ws, 1),
-                                shard=rank, variant=args.variant, columns=synth.query_columns(cfg))
+                                shard=rank, variant=args.variant, columns=synth.query_columns(cfg),
+                                sort_by=sort_by)
         table = ShardTable(cols, device=dev)
         if cfg['where']:
             npass_expected = int(np.count_nonzero(cols['passenger_count'] >= 2))
@@ -322,7 +327,9 @@ def main(argv=None):
                 args.config.upper(), rows,
                 '%d shards x %d rows' % (rows // (args.rows or cfg['rows'] // cfg['shards']), args.rows or cfg['rows'] // cfg['shards'])
                 if args.config == 'c5' else '1 shard', cfg['groupby'], [a[1] for a in cfg['aggs']], cfg['where'],
-                ', aggregate=True merge across ranks (RCCL all-to-all)' if args.config == 'c5' else ''),
+                ', aggregate=True merge across ranks (RCCL all-to-all)' if args.config == 'c5' else
+                (', rows sorted by (pu_location_id, passenger_count)' if (args.sorted and args.config == 'c4')
+                 else '')),
             'rows_per_gpu': rows,
             'parallelism': 'shard-per-rank x%d' % ws,
             'engine_mode': MODES[mode or 0],

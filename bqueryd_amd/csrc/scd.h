@@ -168,29 +168,45 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         if (cc == c) vcd = v[c][0];
       }
       if (COMPACT) vb = (uint32_t)(vb - (uint64_t)d.vmin);
-      uint64_t match = __ballot(act);
-      if (match == 0) continue;
-      // lanes of this lane's slot: every lane ORs its bit into the slot's LDS mask word, then
-      // reads the word back (a wave's LDS instructions execute in program order; OR does not
-      // depend on the order of the lanes); the slot's first lane clears it below
-      if (act) atomicOr(&tbl[s], 1ull << lane);
-      match = act ? tbl[s] : 0ull;
-      const uint64_t below = match & lanes_below;
-      const int pl = below ? 63 - __clzll((long long)below) : lane;
-      const int hl = (act && match) ? 63 - __clzll((long long)match) : lane;
-      uint64_t pv, lastv;
-      if (COMPACT) {
-        pv = (uint32_t)__shfl((int)(uint32_t)vb, pl, 64);     // previous row of the slot in this step
-        lastv = (uint32_t)__shfl((int)(uint32_t)vb, hl, 64);  // last row of the slot in this step
+      const uint64_t actm = __ballot(act);
+      if (actm == 0) continue;
+      // one slot for the whole step (sorted or clustered keys): the active lanes are its lanes,
+      // and the LDS mask -- 64 same-address atomics, serialised -- is skipped
+      const uint32_t s0 = __builtin_amdgcn_readlane(s, (uint32_t)__builtin_ctzll(actm));
+      const bool uni = __ballot(act && s != s0) == 0;
+      uint64_t match;
+      if (uni) {
+        match = act ? actm : 0ull;
       } else {
-        pv = __shfl(vb, pl, 64);
-        lastv = __shfl(vb, hl, 64);
+        // lanes of this lane's slot: every lane ORs its bit into the slot's LDS mask word, then
+        // reads the word back (a wave's LDS instructions execute in program order; OR does not
+        // depend on the order of the lanes); the slot's first lane clears it below
+        if (act) atomicOr(&tbl[s], 1ull << lane);
+        match = act ? tbl[s] : 0ull;
+      }
+      const uint64_t below = match & lanes_below;
+      uint64_t pv, lastv;
+      if (COMPACT && uni && (actm & (actm + 1)) == 0) {
+        // one slot on lanes 0..k: the previous row is the lane below (a DPP wave shift, no
+        // LDS) and the slot's last row in the step is lane k (a scalar read)
+        pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)vb, 0x138, 0xF, 0xF, false);  // wave_shr:1
+        lastv = (uint32_t)__builtin_amdgcn_readlane((uint32_t)vb, 63 - __clzll((long long)actm));
+      } else {
+        const int pl = below ? 63 - __clzll((long long)below) : lane;
+        const int hl = (act && match) ? 63 - __clzll((long long)match) : lane;
+        if (COMPACT) {
+          pv = (uint32_t)__shfl((int)(uint32_t)vb, pl, 64);     // previous row of the slot in this step
+          lastv = (uint32_t)__shfl((int)(uint32_t)vb, hl, 64);  // last row of the slot in this step
+        } else {
+          pv = __shfl(vb, pl, 64);
+          lastv = __shfl(vb, hl, 64);
+        }
       }
       const bool diff = act && below != 0 && !scd_equal(vb, pv, isf);
       const uint64_t dm = __ballot(diff);
       bool run_start = diff;  // first row of a value run of its slot (set below for first lanes)
       if (act && below == 0) {
-        tbl[s] = 0ull;  // after every lane's read of the mask (program order)
+        if (!uni) tbl[s] = 0ull;  // after every lane's read of the mask (program order)
         const uint32_t add_rows = (uint32_t)__popcll(match), add_ch = (uint32_t)__popcll(dm & match);
         if (COMPACT) {
           const ScdSlot32 cur = st32[s];
