@@ -1672,13 +1672,17 @@ int bqg_table_load_carrays(bqg_table* t, int32_t n, const int32_t* cols, const c
       job.itemsize = (int)dtype_size(k.dtype);
       job.chunklen = chunklens[i];
       job.nthreads = nthreads;
-      job.device_decode = decode != BQG_DECODE_HOST;  // AUTO: the device decoder
       job.stream = c->stream;
     }
+    // AUTO: the device decoder for large calls; below ~128 MB decoded the host threads win (a
+    // batch costs the device path at least one long serial stream decode, ~3 ms)
+    int64_t total = 0;
+    for (const IngestJob& j : jobs) total += j.nrows * j.itemsize;
+    const bool dev = decode == BQG_DECODE_DEVICE || (decode == BQG_DECODE_AUTO && total >= (int64_t(128) << 20));
+    for (IngestJob& j : jobs) j.device_decode = dev;
     HIPCHECK(hipStreamSynchronize(c->stream));  // the columns' zero-fill has landed
     std::vector<IngestStats> st(n);
     std::string err;
-    const bool dev = decode != BQG_DECODE_HOST;
     if (dev) {
       if (ingest_carrays_device(jobs, c->ingest, st, err) != 0) fail(BQG_E_INVALID, "%s", err.c_str());
     } else {

@@ -545,7 +545,8 @@ int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, 
     }
     // sized once for a full batch (page-locked allocations cost ~0.1 ms per MB): compressed
     // bytes are at most the decoded bytes plus the frame headers and the alignment
-    const size_t slot_bytes = std::max(comp_bytes, batch_bytes() + batch_bytes() / 16 + kBloscPad);
+    // (sized for the batch's decoded bytes, so a small call does not pin a full batch)
+    const size_t slot_bytes = std::max(comp_bytes, batch_out + batch_out / 16 + kBloscPad);
     if (!grow_host(slot.host, slot.host_cap, slot_bytes) || !grow_dev(slot.dev, slot.dev_cap, slot_bytes)) {
       err = "ingest: staging allocation failed";
       return -1;
@@ -595,7 +596,7 @@ int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, 
     const double read_ms = ms_since(t_read);
     const clk::time_point t_plan = clk::now();
     // tasks (byte-shuffled blocks decode into the slot's scratch, then un-shuffle)
-    if (!grow_dev(slot.tmp, slot.tmp_cap, std::max(batch_out, batch_bytes()))) {
+    if (!grow_dev(slot.tmp, slot.tmp_cap, batch_out)) {
       err = "ingest: shuffle scratch allocation failed";
       return -1;
     }

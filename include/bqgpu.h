@@ -164,9 +164,10 @@ int bqg_table_load_carray(bqg_table* t, int32_t col, const char* carray_dir, int
  * read the chunk files into page-locked memory, the compressed bytes cross PCIe, and the
  * blosc1 frames are decoded on the GPU (BloscLZ and LZ4 streams, byte shuffle, memcpyed
  * frames; a chunk with another codec -- zstd, zlib, snappy -- or bit shuffle is decoded by
- * host libblosc as in the host path).  BQG_DECODE_AUTO picks the device decoder (C2 shard:
- * 97 GB/s decoded into HBM vs 43 GB/s for 16 host decode threads).  A corrupt
- * stream fails the call (BQG_E_INVALID) on either path. */
+ * host libblosc as in the host path).  BQG_DECODE_AUTO picks the device decoder for calls of
+ * 128 MB decoded or more (C2 shard: 97 GB/s decoded into HBM vs 43 GB/s for 16 host decode
+ * threads) and the host decoder below (a device batch costs at least one serial stream decode,
+ * ~3 ms).  A corrupt stream fails the call (BQG_E_INVALID) on either path. */
 enum bqg_decode { BQG_DECODE_AUTO = 0, BQG_DECODE_HOST = 1, BQG_DECODE_DEVICE = 2 };
 typedef struct {
   int64_t chunks;
