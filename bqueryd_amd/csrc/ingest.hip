@@ -484,6 +484,16 @@ int ingest_carrays_device(const std::vector<IngestJob>& jobs, IngestPool& pool, 
       return -1;
     }
   hipStream_t cs = pool.copy_stream;
+  // every exit waits for the call's copies and kernels: an error return must not leave a
+  // kernel running that could still raise `bad` during the next call
+  struct Drain {
+    IngestPool& p;
+    ~Drain() {
+      if (p.copy_stream) (void)hipStreamSynchronize(p.copy_stream);
+      for (DecodeSlot& d : p.slots)
+        if (d.stream) (void)hipStreamSynchronize(d.stream);
+    }
+  } drain{pool};
   if (!pool.bad && hipMalloc(&pool.bad, sizeof(unsigned int)) != hipSuccess) {
     pool.bad = nullptr;
     err = "ingest: device allocation failed";

@@ -254,3 +254,37 @@ def test_long_literal_runs_and_short_matches(tmp_path):
     bcolz_io.write_carray(d, a, chunklen=len(a), cname='lz4', shuffle=0)
     got, _ = _load(d, a)
     np.testing.assert_array_equal(got, a)
+
+
+@pytest.mark.parametrize('cname', ['lz4', 'blosclz'])
+def test_fuzzed_streams_never_fault(tmp_path, cname):
+    """Random byte flips inside the compressed streams (headers and block tables left intact):
+    every load either decodes or fails with BqgError; the kernels never read or write outside
+    their buffers (a fault would end the process)."""
+    a = _array('int32', 400_000, 11, 'small')
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=100_000, cname=cname)
+    path = os.path.join(d, 'data', '__1.blp')
+    with open(path, 'rb') as f:
+        orig = f.read()
+    frame = orig[16:]
+    first, _ = _first_split(frame)
+    rng = np.random.default_rng(5)
+    outcomes = {'ok': 0, 'error': 0}
+    for trial in range(24):
+        data = bytearray(orig)
+        for _ in range(int(rng.integers(1, 40))):
+            pos = 16 + first + 4 + int(rng.integers(0, len(frame) - first - 4))
+            data[pos] = int(rng.integers(0, 256))
+        with open(path, 'wb') as f:
+            f.write(bytes(data))
+        try:
+            _load(d, a)
+            outcomes['ok'] += 1
+        except _lib.BqgError:
+            outcomes['error'] += 1
+    assert sum(outcomes.values()) == 24
+    with open(path, 'wb') as f:
+        f.write(orig)
+    got, _ = _load(d, a)
+    np.testing.assert_array_equal(got, a)
