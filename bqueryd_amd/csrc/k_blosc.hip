@@ -11,9 +11,10 @@
 //   compressed size and the codec's stream (stored raw when the size equals the split's
 //   decoded size); a byte-shuffled block is `typesize` planes of blocksize / typesize bytes.
 // The host (ingest.hip) parses headers and split sizes into BloscSplit / BloscBlock task
-// lists; here one wavefront decodes one split -- the stream's tokens are parsed by the whole
-// wave in lock step from an LDS window of the compressed bytes, and every literal run and
-// match is copied by the 64 lanes together -- and a second kernel un-shuffles the blocks.
+// lists; here one wavefront decodes one split (LZ4 or BloscLZ) -- up to 64 sequences at a
+// time, one per lane, found by a speculative parse and pointer doubling (see the LZ4 section);
+// long runs and matches are copied by the 64 lanes together -- and a second kernel
+// un-shuffles the blocks.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
