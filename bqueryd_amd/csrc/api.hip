@@ -775,7 +775,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   c->last = bqg_timing{};
   c->last.rows = N;
   c->last.mode = pl.mode;
-  c->last.scan_launches = pl.mode == kPartitioned ? 6 : 1;
+  c->last.scan_launches = pl.mode == kPartitioned ? 2 : 1;
 
   // bquery's zero-key, unfiltered, empty-table case yields one 'Total' row of zeros
   if (N == 0) {
@@ -961,91 +961,35 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.nparts = (int)((S + (1ull << pl.wbits) - 1) >> pl.wbits);
       // scatter workgroup: the widest whose staged tile fits in LDS (BQGPU_PART_THREADS caps it)
       L.threads = 1024;
-      L.chunks = 1;
       if (const char* ev = getenv("BQGPU_PART_THREADS")) L.threads = std::max(256, std::min(1024, atoi(ev)));
       while (L.threads > 256 && part_scatter_lds(L.nparts, L.threads, nsum) > 150 * 1024) L.threads >>= 1;
-      int per_cu = 2;  // count / scatter workgroups per CU (two 58 KiB scatter workgroups share a CU)
+      L.tile_rows = L.threads * kRowsPerThread;
+      const int64_t tr = L.tile_rows;
+      L.ntiles = (N + tr - 1) / tr;
+      // contiguous whole-tile row ranges, two scatter workgroups per CU
+      int per_cu = 2;
       if (const char* ev = getenv("BQGPU_PART_PER_CU")) per_cu = std::max(1, std::min(8, atoi(ev)));
-      // the count pass needs only the key columns that reach the partition bits: trailing keys
-      // whose range product R is a power of two <= 2^wbits only add `lo < R` to `hi * R`, and R
-      // divides 2^wbits, so (hi * R + lo) >> wbits does not depend on them (C3: vendor_id, range
-      // 2, is not read).  An unread column re-reads its block's first chunk, whose values are
-      // in range like any other.
-      L.load_mask = 0;
-      {
-        int low = pl.p.nkeys;  // keys [low, nkeys) are not needed for the partition
-        uint64_t prod = 1;
-        for (int k = pl.p.nkeys - 1; k >= 0; --k) {
-          const uint64_t r = pl.p.keys[k].range;
-          if (r == 0 || prod > (1ull << pl.wbits) / r || pl.p.keys[k].stride != prod) break;
-          const uint64_t np = prod * r;
-          if ((np & (np - 1)) != 0) break;
-          prod = np;
-          low = k;
-        }
-        for (int k = 0; k < low; ++k) L.load_mask |= 1u << pl.p.keys[k].col;
-      }
-      for (int i = 0; i < pl.p.nterms; ++i) L.load_mask |= 1u << pl.p.terms[i].col;
-      if (pl.p.mask_col >= 0) L.load_mask |= 1u << pl.p.mask_col;
-      // contiguous row ranges, whole 4096-row tiles (a multiple of every scatter tile), at
-      // most 2^(32 - wbits) rows each so that (row - begin) << wbits | slot_low fits 32 bits
-      const int64_t ptile = 4096;
-      // row batches (BQGPU_PART_BATCH rows, a multiple of the tile): each batch's entries
-      // round-trip through the Infinity Cache instead of HBM when they fit in it
-      int64_t batch = N;
-      if (const char* ev = getenv("BQGPU_PART_BATCH"))
-        batch = std::max<int64_t>(ptile, (atoll(ev) + ptile - 1) / ptile * ptile);
-      if (batch > N) batch = N;
-      auto shape = [&](PartLaunch& P, int64_t nrows) {
-        const int64_t ptiles = (nrows + ptile - 1) / ptile;
-        const int64_t max_tiles_per_block = std::max<int64_t>(1, (int64_t(1) << (32 - pl.wbits)) / ptile);
-        P.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, ptiles));
-        P.blocks = (int)std::max<int64_t>(P.blocks, (ptiles + max_tiles_per_block - 1) / max_tiles_per_block);
-        P.rows_per_block = ((ptiles + P.blocks - 1) / P.blocks) * ptile;
-        // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
-        // slot table allows one per CU; C3 on MI355X: 2 splits 0.34 ms vs 4 splits 0.36 ms)
-        const size_t agg_lds = ((size_t)1 << P.wbits) * (8 + 8 * (size_t)nsum) + ((size_t)P.blocks + 1) * 4;
-        const int fit = std::max(1, (int)((160 * 1024) / agg_lds));
-        P.splits = std::max(1, std::min(P.blocks, (c->cu * fit + P.nparts / 2) / P.nparts));
-        if (const char* ev = getenv("BQGPU_PART_SPLITS")) P.splits = std::max(1, std::min(P.blocks, atoi(ev)));
-      };
-      shape(L, batch);
-      L.row_base = 0;
-      L.capacity = ((uint64_t)batch + 3) & ~3ull;  // 16-byte aligned value arrays
-      const size_t ncounts = (size_t)L.nparts * L.blocks + 1;
-      unsigned char* pb = (unsigned char*)c->prefix.ensure(ncounts * 4 + (2 * (ncounts / 1024 + 2) + 4096) * 4 + 1024);
-      L.counts = (uint32_t*)pb;
-      uint32_t* scan_scratch = L.counts + ncounts + 1;
+      L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, L.ntiles));
+      L.rows_per_block = ((L.ntiles + L.blocks - 1) / L.blocks) * tr;
+      L.blocks = (int)((N + L.rows_per_block - 1) / L.rows_per_block);
+      // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
+      // slot table allows one per CU)
+      const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)nsum);
+      const int fit = std::max(1, (int)((160 * 1024) / agg_lds));
+      L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, (c->cu * fit + L.nparts / 2) / L.nparts));
+      if (const char* ev = getenv("BQGPU_PART_SPLITS")) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, atoi(ev)));
+      L.capacity = (uint64_t)L.ntiles * (uint64_t)tr;
+      L.hdr = (uint16_t*)c->prefix.ensure((size_t)L.ntiles * (size_t)(L.nparts + 1) * 2 + 256);
       const size_t vbytes = ((size_t)L.capacity * 8 * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
       unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + (size_t)L.capacity * 4 + 512);
       L.vals = (unsigned long long*)eb;
       L.meta = (uint32_t*)(eb + vbytes);
-      HIPCHECK(hipMemsetAsync(L.counts + ncounts - 1, 0, 4, st));
-      hipFunction_t fc = nullptr, fs = nullptr;
+      hipFunction_t fs = nullptr;
       if (N >= jit_min_rows()) {
-        // JIT scatter: CH 4-row chunks per thread per tile when the staging still fits
-        int chunks = 1;
-        if (const char* ev = getenv("BQGPU_PART_CHUNKS")) chunks = std::max(1, std::min(2, atoi(ev)));
-        if (chunks > 1 && part_scatter_lds(L.nparts, L.threads, nsum, chunks) > 150 * 1024) chunks = 1;
-        std::string spec = jit_spec(pl.p);
-        const std::string sspec = chunks > 1 ? "#define BQ_PART_CHUNKS " + std::to_string(chunks) + "\n" + spec : spec;
-        fc = jit_function("bq_jit_part_count", spec);
-        fs = fc ? jit_function("bq_jit_part_scatter", sspec) : nullptr;
-        if (!fs) fc = nullptr;
-        L.chunks = fs ? chunks : 1;
-        c->last.specialized = fc ? 1 : 0;
+        fs = jit_function("bq_jit_part_scatter", jit_spec(pl.p));
+        c->last.specialized = fs ? 1 : 0;
       }
-      for (int64_t b0 = 0; b0 < N; b0 += batch) {
-        const int64_t nb = std::min(batch, N - b0);
-        ScanParams pb = pl.p;
-        pb.nrows = nb;
-        for (int i = 0; i < pb.ncols; ++i) pb.cols[i].ptr += (size_t)b0 << pb.cols[i].lg;
-        PartLaunch Lb = L;
-        if (nb != batch) shape(Lb, nb);
-        Lb.row_base = b0;
-        if (b0 > 0) HIPCHECK(hipMemsetAsync(Lb.counts + (size_t)Lb.nparts * Lb.blocks, 0, 4, st));
-        launch_partitioned(pb, sa, Lb, scan_scratch, st, fc, fs);
-      }
+      launch_partitioned(pl.p, sa, L, st, fs);
     } else {
       launch_scan_global(pl.p, sa, scan_blocks(c, N, 8), st);
     }

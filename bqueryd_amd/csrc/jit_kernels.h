@@ -22,22 +22,11 @@ extern "C" __global__ __launch_bounds__(256, 4) void bq_jit_scan_private(bqg::Sc
   bqg::scan_private_body<BQ_NC>(p, L, smem);
 }
 
-extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_count(bqg::ScanParams pin, bqg::PartLaunch L) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  bqg::ScanParams p = pin;
-  bqg::jit_specialize(p);
-  bqg::part_count_body<BQ_NC>(p, L, smem);
-}
-
 extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_scatter(bqg::ScanParams pin, bqg::PartLaunch L) {
   extern __shared__ __align__(16) unsigned char smem[];
   bqg::ScanParams p = pin;
   bqg::jit_specialize(p);
-#ifdef BQ_PART_CHUNKS
-  bqg::part_scatter_body<BQ_NC, BQ_PART_CHUNKS>(p, L, smem);
-#else
   bqg::part_scatter_body<BQ_NC>(p, L, smem);
-#endif
 }
 
 extern "C" __global__ __launch_bounds__(256) void bq_jit_scd_fused(bqg::ScanParams pin, bqg::ScdLaunch d) {

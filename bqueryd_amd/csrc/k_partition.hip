@@ -3,21 +3,15 @@
 //
 // Per-row device atomics on a 1 M-slot table are random 8-byte memory-side operations
 // (MI355X_MICROARCH.md §Global float atomics: they execute past L2).  Instead:
-//   count:     each workgroup owns a contiguous row range and histograms its passing rows by
-//              partition p = slot >> wbits (LDS atomics) -> counts[p][block]; it reads only
-//              the key / filter columns;
-//   scan:      exclusive scan of counts in [p][block] order -> the offset of every
-//              (partition, workgroup) region; partitions are contiguous in the entry arrays;
-//   scatter:   the workgroup re-reads its rows one tile at a time, counting-sorts the tile by
-//              partition in LDS and copies the sorted tile out as runs (consecutive lanes
-//              write consecutive entries of one region: whole cache lines, no write-allocate
-//              of half-written lines);
-//   aggregate: workgroups per partition walk its regions, aggregate the entries in an LDS
-//              table of 2^wbits slots and flush the occupied slots.
-// Entries are structure-of-arrays: a 32-bit meta word ((row - block begin) << wbits |
-// slot_low; the region identifies the block) and one 64-bit value per summed column.
-// Traffic per row (C3, one f64 sum): keys 8 (count) + 16 (scatter read) + 12 written + 12
-// read back = 48 bytes against the 16 algorithmic bytes.
+//   scatter:   each workgroup owns a contiguous range of whole tiles; a tile is counting-
+//              sorted by partition p = slot >> wbits in LDS and written back linearly to the
+//              tile's own entry range, with a header of P + 1 16-bit partition offsets
+//              (partition.h);
+//   aggregate: workgroups per partition walk a range of tiles, read the partition's segment
+//              of each (16-bit header -> 4-byte meta + 8-byte values), aggregate the entries
+//              in an LDS table of 2^wbits slots and flush the occupied slots.
+// Traffic per row (C3, one f64 sum): 16 read + 12 written + 12 read back (segments of ~32
+// entries: partial edge lines, shared by neighbouring partitions through the XCD's L2).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,121 +21,105 @@
 namespace bqg {
 
 template <int NC>
-__global__ __launch_bounds__(kPartBlock) void k_part_count(ScanParams p, PartLaunch L) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  part_count_body<NC>(p, L, smem);
-}
-
-template <int NC>
 __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartLaunch L) {
   extern __shared__ __align__(16) unsigned char smem[];
   part_scatter_body<NC>(p, L, smem);
 }
 
-// One workgroup per (partition, split): the split's share of the partition's entries, four
-// consecutive entries per thread (16-byte loads), the block of each entry -- hence its row --
-// from the partition's region starts in LDS.
+// Aggregate over the tile layout.  Workgroup (partition, split): the split's tile range.  A
+// wave takes groups of G consecutive tiles; lane j < G holds tile j's segment bounds (the
+// headers of the next two groups are in flight while a group is aggregated), a wave scan of
+// the segment lengths flattens the group, and each of U wave-wide iterations in flight reads
+// 64 consecutive entries of the flattened group: an entry finds its tile with G - 1 compares
+// against wave-uniform segment starts and takes that tile's first index with one lane
+// shuffle.  Workgroups are mapped XCD-aware: the workgroups of one XCD (blockIdx % 8) take
+// consecutive partitions over the same tile range, so the edge lines their segments share
+// are read once into that XCD's L2.
+template <int G, int U>
 __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunch L, SlotArrays sa) {
   extern __shared__ __align__(16) unsigned char smem[];
+  const int P = L.nparts;
+  const int per_x = (P + 7) / 8;
+  const int bx = (int)(blockIdx.x & 7u), bi = (int)(blockIdx.x >> 3);
+  const int part = bx * per_x + bi % per_x, split = bi / per_x;
+  if (part >= P || split >= L.splits) return;  // the whole workgroup
   const int W = 1 << L.wbits;
   const int nsum = p.nsum;
-  const int B = L.blocks;
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][W]
   uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)nsum * W);    // [W]
   uint32_t* fst = cnt + W;                                                 // [W]
-  uint32_t* rs = fst + W;                                                  // [B + 1] region starts
-  const int tid = threadIdx.x;
-  const int part = blockIdx.x / L.splits, split = blockIdx.x % L.splits;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = (int)(blockDim.x >> 6);
   for (int i = tid; i < W; i += blockDim.x) {
     cnt[i] = 0;
     fst[i] = kNoRow;
   }
   for (int i = tid; i < nsum * W; i += blockDim.x) acc[i] = 0;
-  for (int i = tid; i <= B; i += blockDim.x) rs[i] = L.counts[(size_t)part * B + i];
   __syncthreads();
-  const uint32_t pbeg = rs[0], pend = rs[B];
-  const uint64_t len = pend - pbeg;
-  const uint32_t lo = pbeg + (uint32_t)(len * split / L.splits);
-  const uint32_t hi = pbeg + (uint32_t)(len * (split + 1) / L.splits);
+  const int64_t nt = L.ntiles;
+  const int64_t t_lo = nt * split / L.splits, t_hi = nt * (split + 1) / L.splits;
+  if (t_lo >= t_hi) return;  // the whole workgroup: an empty tile range leaves the table empty
   const uint32_t lowmask = (uint32_t)W - 1u;
-  const uint32_t c4e = (hi + 3u) >> 2;
-  uint32_t c4 = (lo >> 2) + tid;
-  // entries are visited in increasing order: the region of a thread's next entry is found by
-  // walking forward from its last one (a few LDS reads), falling back to a binary search
-  int b = 0;
-  auto region_of = [&](uint32_t key) {  // largest b with rs[b] <= key
-    for (int k = 0; k < 8; ++k) {
-      if (rs[b + 1] > key) return;
-      ++b;
-    }
-    int e = B - 1;
-    while (b < e) {
-      const int mid = (b + e + 1) >> 1;
-      if (rs[mid] <= key) b = mid;
-      else e = mid - 1;
-    }
+  const uint32_t TR = (uint32_t)L.tile_rows;
+  auto hload = [&](int64_t tg, uint32_t& s0, uint32_t& s1) {
+    const int64_t t = tg + lane;
+    const bool valid = lane < G && t < t_hi;
+    const uint16_t* th = L.hdr + (size_t)(valid ? t : t_lo) * (size_t)(P + 1) + part;
+    const uint32_t a = th[0], b = th[1];
+    s0 = valid ? a : 0u;
+    s1 = valid ? b : 0u;
   };
-  // two iterations' meta and first summed column are in flight while one is aggregated
-  // (clamped to the last group of the range: the same loads on every path, so the compiler
-  // waits for the oldest group with vmcnt(N) instead of draining)
-  const bool pre_v = nsum > 0;
-  const unsigned char* v0 = reinterpret_cast<const unsigned char*>(L.vals);
-  struct Grp {
-    uint4 m, v01, v23;
-  };
-  auto fetch = [&](uint32_t cc) {
-    Grp g;
-    cc = cc < c4e ? cc : (c4e > 0u ? c4e - 1u : 0u);
-    g.m = load_stream16(reinterpret_cast<const unsigned char*>(L.meta + ((size_t)cc << 2)));
-    if (pre_v) {
-      g.v01 = load_stream16(v0 + ((size_t)cc << 5));
-      g.v23 = load_stream16(v0 + ((size_t)cc << 5) + 16);
-    } else {
-      g.v01 = g.m;
-      g.v23 = g.m;
-    }
-    return g;
-  };
-  auto consume = [&](const Grp& g, uint32_t cc) {
-    const uint32_t i0 = cc << 2;
-    if (i0 >= hi) return;
-    region_of(max(i0, lo));
-    const uint32_t mm[4] = {g.m.x, g.m.y, g.m.z, g.m.w};
+  const int64_t stride = (int64_t)NW * G;
+  int64_t tg = t_lo + (int64_t)wave * G;
+  uint32_t a0, a1, b0, b1;
+  hload(tg, a0, a1);
+  hload(tg + stride, b0, b1);
+  for (; tg < t_hi; tg += stride) {
+    const uint32_t s0 = a0, s1 = a1;
+    a0 = b0;
+    a1 = b1;
+    hload(tg + 2 * stride, b0, b1);
+    const uint32_t len = s1 - s0;
+    const uint32_t incl = wave_incl_scan_u32(len, lane);
+    const uint32_t excl = incl - len;
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, G - 1);
+    uint32_t ex[G];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t i = i0 + k;
-      if (i < lo || i >= hi) continue;
-      while (i >= rs[b + 1]) ++b;
-      const uint32_t s = mm[k] & lowmask;
-      const uint32_t row = (uint32_t)(L.row_base + (int64_t)b * L.rows_per_block) + (mm[k] >> L.wbits);
-      atomicAdd(&cnt[s], 1u);
-      if (fst[s] > row) atomicMin(&fst[s], row);
-    }
-    for (int q = 0; q < nsum; ++q) {
-      const unsigned char* vp = reinterpret_cast<const unsigned char*>(L.vals + (size_t)q * L.capacity + i0);
-      const uint4 x01 = q == 0 ? g.v01 : load_stream16(vp), x23 = q == 0 ? g.v23 : load_stream16(vp + 16);
-      const unsigned long long xs[4] = {((unsigned long long)x01.y << 32) | x01.x, ((unsigned long long)x01.w << 32) | x01.z,
-                                        ((unsigned long long)x23.y << 32) | x23.x, ((unsigned long long)x23.w << 32) | x23.z};
+    for (int j = 0; j < G; ++j) ex[j] = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
+    // lane j: first entry index of tile j's segment, relative to the group's first tile
+    const uint32_t stl = (uint32_t)lane * TR + s0;
+    const size_t gbase = (size_t)tg * TR;
+    for (uint32_t e0 = 0; e0 < total; e0 += 64u * U) {
+      uint32_t m[U], rowb[U];
+      unsigned long long v[U];
+      size_t idx[U];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t i = i0 + k;
-        if (i < lo || i >= hi) continue;
-        const uint32_t s = mm[k] & lowmask;
-        if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + s]), value_f64(xs[k], p.sum_conv[q]));
-        else atomicAdd(&acc[(size_t)q * W + s], xs[k]);
+      for (int u = 0; u < U; ++u) {
+        const uint32_t e = e0 + u * 64u + lane;
+        const uint32_t ec = e < total ? e : total - 1u;
+        int j0 = 0;
+#pragma unroll
+        for (int j = 1; j < G; ++j) j0 += ec >= ex[j] ? 1 : 0;
+        const uint32_t exj = (uint32_t)__shfl((int)excl, j0, 64);
+        const uint32_t stj = (uint32_t)__shfl((int)stl, j0, 64);
+        idx[u] = gbase + stj + (ec - exj);
+        rowb[u] = (uint32_t)(gbase + (size_t)j0 * TR);
+        m[u] = L.meta[idx[u]];
+        v[u] = nsum > 0 ? L.vals[idx[u]] : 0ull;
       }
-    }
-  };
-  if (c4 < c4e) {
-    const uint32_t T = blockDim.x;
-    Grp ga = fetch(c4), gb = fetch(c4 + T);
-    for (; c4 < c4e; c4 += 2u * T) {
-      const Grp a = ga;
-      ga = fetch(c4 + 2u * T);
-      consume(a, c4);
-      const Grp bb = gb;
-      gb = fetch(c4 + 3u * T);
-      consume(bb, c4 + T);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t e = e0 + u * 64u + lane;
+        if (e >= total) continue;
+        const uint32_t sl = m[u] & lowmask;
+        const uint32_t row = rowb[u] + (m[u] >> L.wbits);
+        atomicAdd(&cnt[sl], 1u);
+        if (fst[sl] > row) atomicMin(&fst[sl], row);
+        for (int q = 0; q < nsum; ++q) {
+          const unsigned long long x = q == 0 ? v[u] : L.vals[(size_t)q * L.capacity + idx[u]];
+          if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(x, p.sum_conv[q]));
+          else atomicAdd(&acc[(size_t)q * W + sl], x);
+        }
+      }
     }
   }
   __syncthreads();
@@ -190,28 +168,21 @@ void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipSt
   }
 }
 
-void launch_partitioned(const ScanParams& p, const SlotArrays& s, PartLaunch L, uint32_t* scan_scratch,
-                        hipStream_t st, hipFunction_t fcount, hipFunction_t fscatter) {
-  const size_t hist_lds = (size_t)L.nparts * 4;
-  void* args[] = {(void*)&p, (void*)&L};
-  if (fcount) {
-    (void)hipModuleLaunchKernel(fcount, (unsigned)L.blocks, 1, 1, (unsigned)L.threads, 1, 1, (unsigned)hist_lds, st,
-                                args, nullptr);
-  } else {
-    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_count<NC>), dim3(L.blocks), dim3(L.threads), hist_lds, st, p, L));
-  }
-  // counts has one extra zero word at the end: after the scan it holds the total
-  const uint64_t n = (uint64_t)L.nparts * L.blocks + 1;
-  launch_exclusive_scan_u32(L.counts, n, scan_scratch, st);
-  const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum, fscatter ? L.chunks : 1);
+void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,
+                        hipFunction_t fscatter) {
+  const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum);
   if (fscatter) {
+    PartLaunch Lc = L;
+    ScanParams pc = p;
+    void* args[] = {(void*)&pc, (void*)&Lc};
     (void)hipModuleLaunchKernel(fscatter, (unsigned)L.blocks, 1, 1, (unsigned)L.threads, 1, 1, (unsigned)scatter_lds,
                                 st, args, nullptr);
   } else {
     BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L));
   }
-  const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)p.nsum) + ((size_t)L.blocks + 1) * 4;
-  hipLaunchKernelGGL(k_part_aggregate, dim3(L.nparts * L.splits), dim3(1024), agg_lds, st, p, L, s);
+  const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)p.nsum);
+  const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
+  hipLaunchKernelGGL((k_part_aggregate<8, 4>), dim3(grid), dim3(1024), agg_lds, st, p, L, s);
 }
 
 }  // namespace bqg

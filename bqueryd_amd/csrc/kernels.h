@@ -158,34 +158,30 @@ void launch_select_gather(const unsigned char* mask, int64_t nrows,
                           const unsigned int* tile_offsets, const DevCol* cols, int ncols,
                           void* const* outs, hipStream_t st);
 
-// Partitioned aggregation (large dense slot spaces): count -> scan -> scatter -> aggregate
+// Partitioned aggregation (large dense slot spaces): tile scatter -> aggregate
 constexpr int kPartMaxParts = 4096;
 struct PartLaunch {
   int wbits;                 // slots per partition = 2^wbits
   int nparts;                // <= kPartMaxParts
-  int blocks;                // workgroups of the count / scatter passes
-  int splits;                // aggregate workgroups per partition (block ranges)
-  int threads;               // threads of a scatter workgroup (4 rows each per tile)
-  int chunks;                // 4-row chunks per scatter thread per tile (JIT scatter only)
-  uint32_t load_mask;        // scan columns the count pass reads (keys, terms, mask)
-  int64_t rows_per_block;    // contiguous rows per count/scatter workgroup: a multiple of the
-                             // scatter tile and <= 2^(32 - wbits) (row-in-block | slot_low
-                             // packs into one 32-bit word)
-  int64_t row_base;          // table row of the launch's row 0 (batched launches)
-  uint64_t capacity;         // entry capacity (>= passing rows)
-  uint32_t* counts;          // [nparts * blocks + 1] -> exclusive offsets in place
-  uint32_t* meta;            // [capacity]: (row - block begin) << wbits | slot_low
+  int blocks;                // workgroups of the scatter pass
+  int splits;                // aggregate workgroups per partition (tile ranges)
+  int threads;               // threads of a scatter workgroup: tiles of threads * 4 rows
+  int tile_rows;             // threads * 4
+  int64_t rows_per_block;    // contiguous rows per scatter workgroup, whole tiles
+  int64_t ntiles;            // ceil(nrows / tile_rows)
+  uint64_t capacity;         // entries per array = ntiles * tile_rows
+  uint16_t* hdr;             // [ntiles][nparts + 1]: partition offsets in each sorted tile
+  uint32_t* meta;            // [capacity]: row-in-tile << wbits | slot_low
   unsigned long long* vals;  // [nsum][capacity]: summed values (canonical 64-bit)
 };
-// LDS bytes of a scatter workgroup: the staged tile (meta, destination, values), tile
-// counts (two buffers) / offsets, region cursors and two sets of scan totals
-inline size_t part_scatter_lds(int nparts, int threads, int nsum, int chunks = 1) {
-  return (size_t)threads * 4 * (size_t)chunks * (8 + 8 * (size_t)nsum) + (size_t)nparts * 16 + 2 * 16 * 4;
+// LDS bytes of a scatter workgroup: the staged tile (values, meta), tile counts (two
+// buffers) / offsets and two sets of scan totals
+inline size_t part_scatter_lds(int nparts, int threads, int nsum) {
+  return (size_t)threads * 4 * (4 + 8 * (size_t)nsum) + (size_t)nparts * 12 + 2 * 16 * 4;
 }
-// fcount / fscatter: query-specialised (JIT) count / scatter kernels, or nullptr for the
-// precompiled generic ones
-void launch_partitioned(const ScanParams& p, const SlotArrays& s, PartLaunch L, uint32_t* scan_scratch,
-                        hipStream_t st, hipFunction_t fcount = nullptr, hipFunction_t fscatter = nullptr);
+// fscatter: the query-specialised (JIT) scatter kernel, or nullptr for the precompiled one
+void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,
+                        hipFunction_t fscatter = nullptr);
 void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipStream_t st);
 
 // cross-rank merge: partition id of every row from its key values

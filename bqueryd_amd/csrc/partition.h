@@ -1,7 +1,7 @@
-// partition.h -- bodies of the partitioned-aggregation count and scatter passes (config C3),
-// shared by the precompiled kernels (k_partition.hip) and the query-specialised JIT kernels
-// (jit_kernels.h): with the query shape folded into constants the per-row dtype / operator
-// dispatch of the generic bodies disappears.
+// partition.h -- body of the partitioned-aggregation scatter pass (config C3), shared by the
+// precompiled kernel (k_partition.hip) and the query-specialised JIT kernel (jit_kernels.h):
+// with the query shape folded into constants the per-row dtype / operator dispatch of the
+// generic body disappears.
 //
 // Workgroups exchange data through LDS only, so every barrier here is lds_barrier(): a
 // __syncthreads() would also drain the tile's prefetched column loads and its streaming
@@ -61,7 +61,7 @@ __device__ __forceinline__ uint32_t block_excl_scan_1b(uint32_t v, uint32_t* wsu
   return before + incl - v;
 }
 
-// count / scatter: workgroups of up to 1024 threads, each over a contiguous row range
+// scatter: workgroups of up to 1024 threads, each over a contiguous range of whole tiles
 constexpr int kPartBlock = 1024;
 
 // A thread's 4-row chunk of the columns in `mask`, loaded unconditionally: a chunk at or past
@@ -78,169 +78,105 @@ __device__ __forceinline__ void load_rows4_clamped(const ScanParams& p, int64_t 
   for (int c = 0; c < NC; ++c) load_chunk(raw[c], p.cols[c], ((mask >> c) & 1u) ? r : home);
 }
 
-// Each thread keeps kCountChunks 4-row chunks of the key columns in flight (16 rows), so a
-// workgroup has ~128 KiB of key bytes outstanding while it histograms the previous group.
-constexpr int kCountChunks = 4;
-
+// Tile-layout scatter.  A tile is T * 4 rows (TR).  The workgroup counting-sorts each of its
+// tiles by partition (slot >> wbits) in LDS and writes the sorted tile back LINEARLY to the
+// tile's own entry range [tile * TR, tile * TR + TR) with 16-byte stores of whole lines --
+// the same stores on every path (positions past the tile's passing rows carry left-over
+// staging words that no reader looks at), so the loop waits for the next tile's loads with
+// vmcnt(N) instead of draining.  The tile's header hdr[tile][0 .. P] holds the 16-bit offset of
+// each partition's run (hdr[tile][P] = passing rows).  An entry is a 32-bit meta word
+// (row-in-tile << wbits | slot_low) and one 64-bit value per summed column.
+//
+// Measured on MI355X (tools/micro/part_micro.hip, C3 shape): the region layout this replaces
+// (count pass, scan, per-(partition, block) regions) wrote each tile as ~P runs of ~32
+// entries into P far-apart regions and ran at 3.4 TB/s of moved bytes; the linear tile
+// writes run at copy speed (2.8 GB in 0.57 ms), with no count pass and no scan.
 template <int NC>
-__device__ __forceinline__ void part_count_body(const ScanParams& p, const PartLaunch& L, unsigned char* smem) {
-  uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
-  const int tid = threadIdx.x, T = blockDim.x;
-  const int step = T * kRowsPerThread;  // rows of one chunk slice of the workgroup
-  const int tile = step * kCountChunks;
-  for (int i = tid; i < L.nparts; i += T) hist[i] = 0;
-  lds_barrier();
-  const int64_t begin = (int64_t)blockIdx.x * L.rows_per_block;
-  const int64_t end = (p.nrows < begin + L.rows_per_block ? p.nrows : begin + L.rows_per_block);
-  if (begin >= end) {
-    for (int i = tid; i < L.nparts; i += T) L.counts[(size_t)i * gridDim.x + blockIdx.x] = 0u;
-    return;
-  }
-  const int64_t home = begin;
-  Chunk raw[kCountChunks][NC];
-#pragma unroll
-  for (int u = 0; u < kCountChunks; ++u)
-    load_rows4_clamped<NC>(p, begin + (int64_t)u * step + (int64_t)tid * kRowsPerThread, end, raw[u], L.load_mask, home);
-  for (int64_t base = begin; base < end; base += tile) {
-    uint32_t part[kCountChunks][4], pass[kCountChunks];
-#pragma unroll
-    for (int u = 0; u < kCountChunks; ++u) {
-      const int64_t row0 = base + (int64_t)u * step + (int64_t)tid * kRowsPerThread;
-      uint64_t v[NC][4], code[4];
-      decode_all<NC, 4>(p, raw[u], v);
-      pass[u] = vals_pass<NC, 4>(p, row0, v);
-      const int64_t rem = end - row0;
-      pass[u] &= rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
-      vals_code<NC, 4>(p, v, code);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) part[u][r] = (uint32_t)(code[r] >> L.wbits);
-    }
-#pragma unroll
-    for (int u = 0; u < kCountChunks; ++u)
-      load_rows4_clamped<NC>(p, base + tile + (int64_t)u * step + (int64_t)tid * kRowsPerThread, end, raw[u],
-                             L.load_mask, home);
-#pragma unroll
-    for (int u = 0; u < kCountChunks; ++u)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (pass[u] & (1u << r)) atomicAdd(&hist[part[u][r]], 1u);
-  }
-  lds_barrier();
-  for (int i = tid; i < L.nparts; i += T) L.counts[(size_t)i * gridDim.x + blockIdx.x] = hist[i];
-}
-
-// Single-buffered tile staging (64 KiB for one summed column at 1024 threads and CH = 1: two
-// scatter workgroups fit on a CU, which measured faster than double buffering at one per CU);
-// the scan's wave totals alternate between two buffers so the scan needs one barrier.  CH
-// 4-row chunks per thread make a tile of CH * 4 * T rows (each chunk slice coalesced): longer
-// runs per partition and fewer barriers per row, at CH times the staging LDS.
-template <int NC, int CH = 1>
 __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const PartLaunch& L, unsigned char* smem) {
   const int T = blockDim.x, tid = threadIdx.x;
   const int P = L.nparts;
-  const int slice = T * kRowsPerThread;
-  const int tile = slice * CH;
+  const int TR = T * kRowsPerThread;
   const int nsum = p.nsum;
-  unsigned long long* sval = reinterpret_cast<unsigned long long*>(smem);             // [nsum][tile]
-  uint32_t* smeta = reinterpret_cast<uint32_t*>(sval + (size_t)nsum * tile);          // [tile]
-  uint32_t* sdst = smeta + tile;                                                       // [tile] destinations
-  uint32_t* hist2 = sdst + tile;                                                       // [2][P] tile counts
-  uint32_t* toff = hist2 + 2 * P;                                                      // [P] tile offsets
-  uint32_t* cur = toff + P;                                                            // [P] region cursors
-  uint32_t* wsum2 = cur + P;                                                           // [2][16] scan totals
-  for (int i = tid; i < P; i += T) {
-    hist2[i] = 0;
-    hist2[P + i] = 0;
-    cur[i] = L.counts[(size_t)i * gridDim.x + blockIdx.x];
-  }
+  constexpr int NS = NC < kMaxSums ? NC : kMaxSums;
+  unsigned long long* sval = reinterpret_cast<unsigned long long*>(smem);  // [nsum][TR]
+  uint32_t* smeta = reinterpret_cast<uint32_t*>(sval + (size_t)nsum * TR); // [TR]
+  uint32_t* hist2 = smeta + TR;                                            // [2][P] tile counts
+  uint32_t* toff = hist2 + 2 * P;                                          // [P] tile offsets
+  uint32_t* wsum2 = toff + P;                                              // [2][16] scan totals
+  for (int i = tid; i < 2 * P; i += T) hist2[i] = 0;
   lds_barrier();
   const int64_t begin = (int64_t)blockIdx.x * L.rows_per_block;
   const int64_t end = (p.nrows < begin + L.rows_per_block ? p.nrows : begin + L.rows_per_block);
+  if (begin >= end) return;
   const uint64_t lowmask = (1ull << L.wbits) - 1ull;
   const int per = (P + T - 1) / T;  // partitions per thread in the tile scan
   const int q0 = tid * per;
   const int q1 = min(P, q0 + per);
   const uint32_t all = (1u << NC) - 1u;
-  constexpr int NS = NC < kMaxSums ? NC : kMaxSums;
-  Chunk raw[CH][NC];
-  if (begin < end) {
-#pragma unroll
-    for (int u = 0; u < CH; ++u)
-      load_rows4_clamped<NC>(p, begin + (int64_t)u * slice + (int64_t)tid * kRowsPerThread, end, raw[u], all, begin);
-  }
+  Chunk raw[NC];
+  load_rows4_clamped<NC>(p, begin + (int64_t)tid * kRowsPerThread, end, raw, all, begin);
   int parity = 0;
-  for (int64_t base = begin; base < end; base += tile, parity ^= 1) {
+  for (int64_t base = begin; base < end; base += TR, parity ^= 1) {
     // the tile histogram alternates between two buffers: the one this tile zeroes at its end
-    // is next counted into two tiles later, past this tile's barriers, so the loop needs no
-    // trailing barrier (tile t+1's first phase touches neither the staging area nor `cur`)
+    // is next counted into two tiles later, past the next tile's barriers
     uint32_t* hist = hist2 + parity * P;
-    uint32_t pass[CH], part[CH][4], rank[CH][4], low[CH][4];
-    uint64_t sv[CH][NS][4];
-#pragma unroll
-    for (int u = 0; u < CH; ++u) {
-      const int64_t row0 = base + (int64_t)u * slice + (int64_t)tid * kRowsPerThread;
+    uint32_t pass, part[4], rank[4], low[4];
+    uint64_t sv[NS][4];
+    const int64_t row0 = base + (int64_t)tid * kRowsPerThread;
+    {
       uint64_t v[NC][4], code[4];
-      decode_all<NC, 4>(p, raw[u], v);
-      load_rows4_clamped<NC>(p, row0 + tile, end, raw[u], all, begin);
-      pass[u] = vals_pass<NC, 4>(p, row0, v);
+      decode_all<NC, 4>(p, raw, v);
+      load_rows4_clamped<NC>(p, row0 + TR, end, raw, all, begin);
+      pass = vals_pass<NC, 4>(p, row0, v);
       const int64_t rem = end - row0;
-      pass[u] &= rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
+      pass &= rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
       vals_code<NC, 4>(p, v, code);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        part[u][r] = (uint32_t)(code[r] >> L.wbits);
-        low[u][r] = (uint32_t)(code[r] & lowmask);
+        part[r] = (uint32_t)(code[r] >> L.wbits);
+        low[r] = (uint32_t)(code[r] & lowmask);
 #pragma unroll
-        for (int s = 0; s < NS; ++s) sv[u][s][r] = v[s][r];
+        for (int s = 0; s < NS; ++s) sv[s][r] = v[s][r];
       }
     }
 #pragma unroll
-    for (int u = 0; u < CH; ++u)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) rank[u][r] = (pass[u] & (1u << r)) ? atomicAdd(&hist[part[u][r]], 1u) : 0u;
+    for (int r = 0; r < 4; ++r) rank[r] = (pass & (1u << r)) ? atomicAdd(&hist[part[r]], 1u) : 0u;
     lds_barrier();
-    // tile offsets: exclusive scan of the tile histogram
+    // tile offsets: exclusive scan of the tile histogram, also the tile's header
     uint32_t local = 0;
     for (int i = q0; i < q1; ++i) local += hist[i];
     uint32_t n_tile;
     uint32_t run = block_excl_scan_1b(local, wsum2 + parity * 16, &n_tile);
+    uint16_t* th = L.hdr + (size_t)(base / TR) * (size_t)(P + 1);
     for (int i = q0; i < q1; ++i) {
       toff[i] = run;
+      th[i] = (uint16_t)run;
       run += hist[i];
     }
+    if (tid == 0) th[P] = (uint16_t)n_tile;
     lds_barrier();
-    // stage the tile sorted by partition, with each entry's destination (region cursor + rank)
+    // stage the tile sorted by partition
 #pragma unroll
-    for (int u = 0; u < CH; ++u) {
-      const int64_t row0 = base + (int64_t)u * slice + (int64_t)tid * kRowsPerThread;
+    for (int r = 0; r < 4; ++r) {
+      if (!(pass & (1u << r))) continue;
+      const uint32_t pos = toff[part[r]] + rank[r];
+      smeta[pos] = ((uint32_t)(row0 + r - base) << L.wbits) | low[r];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (!(pass[u] & (1u << r))) continue;
-        const uint32_t pos = toff[part[u][r]] + rank[u][r];
-        smeta[pos] = ((uint32_t)(row0 + r - begin) << L.wbits) | low[u][r];
-        sdst[pos] = cur[part[u][r]] + rank[u][r];
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-          if (s < nsum) sval[(size_t)s * tile + pos] = sv[u][s][r];
-      }
+      for (int s = 0; s < NS; ++s)
+        if (s < nsum) sval[(size_t)s * TR + pos] = sv[s][r];
     }
     lds_barrier();
-    // copy out: consecutive lanes -> consecutive entries of one region (whole lines)
+    // linear copy-out: one 16-byte store of meta and two per summed column, every thread
+    *reinterpret_cast<uint4*>(L.meta + base + 4 * tid) = *reinterpret_cast<const uint4*>(smeta + 4 * tid);
 #pragma unroll
-    for (int k = 0; k < kRowsPerThread * CH; ++k) {
-      const uint32_t i = (uint32_t)(tid + k * T);
-      if (i < n_tile) {
-        const uint32_t dst = sdst[i];
-        L.meta[dst] = smeta[i];
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-          if (s < nsum) L.vals[(size_t)s * L.capacity + dst] = sval[(size_t)s * tile + i];
-      }
+    for (int s = 0; s < NS; ++s) {
+      if (s >= nsum) break;
+      unsigned long long* dv = L.vals + (size_t)s * L.capacity + base;
+      const unsigned long long* lv = sval + (size_t)s * TR;
+      *reinterpret_cast<uint4*>(dv + 2 * tid) = *reinterpret_cast<const uint4*>(lv + 2 * tid);
+      *reinterpret_cast<uint4*>(dv + 2 * (tid + T)) = *reinterpret_cast<const uint4*>(lv + 2 * (tid + T));
     }
-    for (int i = q0; i < q1; ++i) {
-      cur[i] += hist[i];
-      hist[i] = 0;
-    }
+    for (int i = q0; i < q1; ++i) hist[i] = 0;
   }
 }
 

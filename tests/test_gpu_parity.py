@@ -255,7 +255,7 @@ def test_select_rows_and_expand(oracle_c):
 @pytest.mark.parametrize('krange,terms', [(9_000, []), (100_000, [('f', '>', 3)]), (1_500_000, []),
                                           (3_000_000, [('f', 'in', [1, 2, 5])])])
 def test_partitioned_mode(krange, terms, oracle_c):
-    """Dense slot spaces above the shared-LDS limit: count -> scan -> scatter -> aggregate."""
+    """Dense slot spaces above the shared-LDS limit: tile scatter -> aggregate."""
     rng = np.random.default_rng(krange)
     n = 400_000
     cols = OrderedDict(k=rng.integers(0, krange, n).astype(np.int32), k2=rng.integers(0, 2, n).astype(np.int8),
@@ -268,7 +268,7 @@ def test_partitioned_mode(krange, terms, oracle_c):
 
 
 def test_partitioned_four_sums(oracle_c):
-    """Four summed columns: the scatter stages a narrower tile (512 threads) in LDS."""
+    """Four summed columns: the scatter stages four value arrays per tile in LDS."""
     rng = np.random.default_rng(7)
     n = 300_001
     cols = OrderedDict(k=rng.integers(-700_000, 700_000, n).astype(np.int32),
@@ -340,8 +340,8 @@ def test_specialised_private_scan(case, oracle_c, monkeypatch):
 
 @pytest.mark.parametrize('case', range(3))
 def test_specialised_partitioned(case, oracle_c, monkeypatch):
-    """The run-time specialised (hiprtc) partition count / scatter kernels against the oracle,
-    forced on at small sizes; the precompiled generic kernels must give the same table."""
+    """The run-time specialised (hiprtc) partition scatter kernel against the oracle, forced on
+    at small sizes; the precompiled generic kernel must give the same table."""
     monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
     n = 500_003
     rng = np.random.default_rng(200 + case)
@@ -369,10 +369,9 @@ def test_specialised_partitioned(case, oracle_c, monkeypatch):
 
 @pytest.mark.parametrize('jit', [False, True])
 @pytest.mark.parametrize('low_ranges', [(2, 4), (3,), (4, 3), (8192,), (16384,)])
-def test_partition_count_skips_low_keys(jit, low_ranges, oracle_c, monkeypatch):
-    """The partition count pass does not read trailing key columns whose range product is a
-    power of two <= 2^wbits (they cannot change a row's partition); other layouts read every
-    key.  Terms on a skipped key column still filter."""
+def test_partition_key_layouts(jit, low_ranges, oracle_c, monkeypatch):
+    """Multi-column keys whose trailing columns stay inside one partition (range products that
+    are powers of two <= 2^wbits) and ones that do not; terms on a trailing key column."""
     if jit:
         monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
     rng = np.random.default_rng(sum(low_ranges) + jit)
@@ -387,3 +386,21 @@ def test_partition_count_skips_low_keys(jit, low_ranges, oracle_c, monkeypatch):
     keys = ['k'] + names
     run_both(cols, keys, [['v', 'sum', 's'], ['v', 'count', 'c']], [], oracle_c, exact=True)
     run_both(cols, keys, [['v', 'sum', 's']], [(names[-1], '!=', 7)], oracle_c, exact=True)
+
+
+@pytest.mark.parametrize('threads,splits,per_cu', [(256, None, None), (512, 3, 1), (1024, 64, 8), (1024, 1, 2)])
+def test_partitioned_launch_shapes(threads, splits, per_cu, oracle_c, monkeypatch):
+    """Tile sizes (256 / 512 / 1024 scatter threads: 1024- to 4096-row tiles), aggregate tile
+    splits (one, three, more splits than some partitions have tiles) and scatter workgroups per
+    CU give the same table; a partial last tile and a filter that empties whole tiles."""
+    monkeypatch.setenv('BQGPU_PART_THREADS', str(threads))
+    if splits:
+        monkeypatch.setenv('BQGPU_PART_SPLITS', str(splits))
+    if per_cu:
+        monkeypatch.setenv('BQGPU_PART_PER_CU', str(per_cu))
+    rng = np.random.default_rng(threads + (splits or 0))
+    n = 123_457
+    cols = OrderedDict(k=rng.integers(0, 200_000, n).astype(np.int32), v=np.round(rng.normal(size=n) * 64) / 64,
+                       f=np.where(np.arange(n) // 5000 % 3 == 1, 0, rng.integers(1, 5, n)).astype(np.int16))
+    run_both(cols, ['k'], [['v', 'sum', 's'], ['v', 'count', 'c']], [], oracle_c, exact=True)
+    run_both(cols, ['k'], [['v', 'sum', 's'], ['v', 'mean', 'm']], [('f', '>', 0)], oracle_c, exact=True)
