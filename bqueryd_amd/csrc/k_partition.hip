@@ -35,7 +35,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartL
 // shuffle.  Workgroups are mapped XCD-aware: the workgroups of one XCD (blockIdx % 8) take
 // consecutive partitions over the same tile range, so the edge lines their segments share
 // are read once into that XCD's L2.
-template <int G, int U>
+template <int G, int U, int NSUM>
 __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunch L, SlotArrays sa) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int P = L.nparts;
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   const int part = bx * per_x + bi % per_x, split = bi / per_x;
   if (part >= P || split >= L.splits) return;  // the whole workgroup
   const int W = 1 << L.wbits;
-  const int nsum = p.nsum;
+  constexpr int nsum = NSUM;
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][W]
   uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)nsum * W);    // [W]
   uint32_t* fst = cnt + W;                                                 // [W]
@@ -85,26 +85,28 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     uint32_t ex[G];
 #pragma unroll
     for (int j = 0; j < G; ++j) ex[j] = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
-    // lane j: first entry index of tile j's segment, relative to the group's first tile
-    const uint32_t stl = (uint32_t)lane * TR + s0;
+    // lane j: entry index of tile j's segment start minus the segment's flattened position
+    // (relative to the group's first tile): entry index = that + flattened position
+    const uint32_t dl = (uint32_t)lane * TR + s0 - excl;
     const size_t gbase = (size_t)tg * TR;
     for (uint32_t e0 = 0; e0 < total; e0 += 64u * U) {
+      constexpr int NV = NSUM > 0 ? NSUM : 1;
       uint32_t m[U], rowb[U];
-      unsigned long long v[U];
-      size_t idx[U];
+      unsigned long long v[U][NV];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t e = e0 + u * 64u + lane;
         const uint32_t ec = e < total ? e : total - 1u;
-        int j0 = 0;
+        uint32_t j0 = 0;
 #pragma unroll
-        for (int j = 1; j < G; ++j) j0 += ec >= ex[j] ? 1 : 0;
-        const uint32_t exj = (uint32_t)__shfl((int)excl, j0, 64);
-        const uint32_t stj = (uint32_t)__shfl((int)stl, j0, 64);
-        idx[u] = gbase + stj + (ec - exj);
-        rowb[u] = (uint32_t)(gbase + (size_t)j0 * TR);
-        m[u] = L.meta[idx[u]];
-        v[u] = nsum > 0 ? L.vals[idx[u]] : 0ull;
+        for (int j = 1; j < G; ++j) j0 += ec >= ex[j] ? 1u : 0u;
+        const size_t idx = gbase + (uint32_t)__shfl((int)dl, (int)j0, 64) + ec;
+        rowb[u] = (uint32_t)gbase + j0 * TR;
+        // unconditional loads (the value array exists even without a summed column): the
+        // same loads on every path, so the next group's headers stay in flight
+        m[u] = L.meta[idx];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) v[u][q] = L.vals[(size_t)q * L.capacity + idx];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -114,10 +116,10 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
         const uint32_t row = rowb[u] + (m[u] >> L.wbits);
         atomicAdd(&cnt[sl], 1u);
         if (fst[sl] > row) atomicMin(&fst[sl], row);
+#pragma unroll
         for (int q = 0; q < nsum; ++q) {
-          const unsigned long long x = q == 0 ? v[u] : L.vals[(size_t)q * L.capacity + idx[u]];
-          if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(x, p.sum_conv[q]));
-          else atomicAdd(&acc[(size_t)q * W + sl], x);
+          if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(v[u][q], p.sum_conv[q]));
+          else atomicAdd(&acc[(size_t)q * W + sl], v[u][q]);
         }
       }
     }
@@ -130,6 +132,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     const uint64_t gs = slot0 + s;
     atomicAdd(&sa.cnt[gs], (unsigned long long)c);
     atomicMin(&sa.fst[gs], fst[s]);
+#pragma unroll
     for (int q = 0; q < nsum; ++q) {
       const unsigned long long a = acc[(size_t)q * W + s];
       if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)q * p.nslots + gs]), as_f64(a));
@@ -168,6 +171,7 @@ void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipSt
   }
 }
 
+#ifndef BQG_PART_MICRO  // tools/micro/part_micro.hip includes this file for the aggregate kernel
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,
                         hipFunction_t fscatter) {
   const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum);
@@ -182,7 +186,14 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
   }
   const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)p.nsum);
   const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
-  hipLaunchKernelGGL((k_part_aggregate<8, 4>), dim3(grid), dim3(1024), agg_lds, st, p, L, s);
+  switch (p.nsum) {
+    case 0: hipLaunchKernelGGL((k_part_aggregate<8, 4, 0>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
+    case 1: hipLaunchKernelGGL((k_part_aggregate<8, 4, 1>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
+    case 2: hipLaunchKernelGGL((k_part_aggregate<8, 4, 2>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
+    case 3: hipLaunchKernelGGL((k_part_aggregate<8, 2, 3>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
+    default: hipLaunchKernelGGL((k_part_aggregate<8, 2, 4>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
+  }
 }
+#endif
 
 }  // namespace bqg
