@@ -948,7 +948,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       return;
     }
   } else {
-    launch_init_slots(sa, nsum, S, st);
+    // the partitioned aggregate writes every slot itself (no initialisation pass)
+    if (pl.mode != kPartitioned) launch_init_slots(sa, nsum, S, st);
     HIPCHECK(hipMemsetAsync(sa.hash_fill, 0, 8, st));
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
     if (pl.mode == kShared) {
@@ -980,10 +981,16 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       if (const char* ev = getenv("BQGPU_PART_SPLITS")) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, atoi(ev)));
       L.capacity = (uint64_t)L.ntiles * (uint64_t)tr;
       L.hdr = (uint16_t*)c->prefix.ensure((size_t)L.ntiles * (size_t)(L.nparts + 1) * 2 + 256);
+      // one scratch block: entry values | entry meta | split partial tables | arrival counters
       const size_t vbytes = ((size_t)L.capacity * 8 * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
-      unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + (size_t)L.capacity * 4 + 512);
+      const size_t mbytes = ((size_t)L.capacity * 4 + 255) & ~size_t(255);
+      L.partial_bytes = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)nsum);
+      const size_t pbytes = L.splits > 1 ? (size_t)L.nparts * L.splits * L.partial_bytes : 0;
+      unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + mbytes + pbytes + (size_t)L.nparts * 4 + 512);
       L.vals = (unsigned long long*)eb;
       L.meta = (uint32_t*)(eb + vbytes);
+      L.partial = eb + vbytes + mbytes;
+      L.arrive = (unsigned int*)(eb + vbytes + mbytes + pbytes);
       hipFunction_t fs = nullptr;
       if (N >= jit_min_rows()) {
         fs = jit_function("bq_jit_part_scatter", jit_spec(pl.p));

@@ -12,6 +12,9 @@
 //              in an LDS table of 2^wbits slots and flush the occupied slots.
 // Traffic per row (C3, one f64 sum): 16 read + 12 written + 12 read back (segments of ~32
 // entries: partial edge lines, shared by neighbouring partitions through the XCD's L2).
+// Measured (tools/micro/part_micro.hip): the segment reads run at ~3.4 TB/s -- a loads-only
+// probe of the aggregate takes as long as the whole kernel -- and storing each segment as one
+// run of 12-byte {meta, value} entries instead of two runs read no faster.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,14 +30,17 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartL
 }
 
 // Aggregate over the tile layout.  Workgroup (partition, split): the split's tile range.  A
-// wave takes groups of G consecutive tiles; lane j < G holds tile j's segment bounds (the
-// headers of the next two groups are in flight while a group is aggregated), a wave scan of
-// the segment lengths flattens the group, and each of U wave-wide iterations in flight reads
-// 64 consecutive entries of the flattened group: an entry finds its tile with G - 1 compares
+// wave takes groups of G consecutive tiles; lane j < G holds tile j's segment bounds, a wave
+// scan of the segment lengths flattens the group, and each of U wave-wide loads reads 64
+// consecutive entries of the flattened group: an entry finds its tile with G - 1 compares
 // against wave-uniform segment starts and takes that tile's first index with one lane
-// shuffle.  Workgroups are mapped XCD-aware: the workgroups of one XCD (blockIdx % 8) take
-// consecutive partitions over the same tile range, so the edge lines their segments share
-// are read once into that XCD's L2.
+// shuffle.  Software-pipelined: while a group's entries are aggregated, the next group's
+// entries and the header of the group after it are in flight (two register sets used in
+// turn, so no copy waits on a pending load).  Measured (tools/micro/part_micro.hip, C3
+// shape): with loads only and no LDS atomics the unpipelined loop took as long as the whole
+// aggregate -- it waited on each group's loads.  Workgroups are mapped XCD-aware: the
+// workgroups of one XCD (blockIdx % 8) take consecutive partitions over the same tile range,
+// so the edge lines their segments share are read once into that XCD's L2.
 template <int G, int U, int NSUM>
 __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunch L, SlotArrays sa) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -56,8 +62,9 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   for (int i = tid; i < nsum * W; i += blockDim.x) acc[i] = 0;
   __syncthreads();
   const int64_t nt = L.ntiles;
+  // (splits <= ntiles: every split's tile range is non-empty, and every split must reach the
+  // combine below)
   const int64_t t_lo = nt * split / L.splits, t_hi = nt * (split + 1) / L.splits;
-  if (t_lo >= t_hi) return;  // the whole workgroup: an empty tile range leaves the table empty
   const uint32_t lowmask = (uint32_t)W - 1u;
   const uint32_t TR = (uint32_t)L.tile_rows;
   auto hload = [&](int64_t tg, uint32_t& s0, uint32_t& s1) {
@@ -68,76 +75,168 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     s0 = valid ? a : 0u;
     s1 = valid ? b : 0u;
   };
-  const int64_t stride = (int64_t)NW * G;
-  int64_t tg = t_lo + (int64_t)wave * G;
-  uint32_t a0, a1, b0, b1;
-  hload(tg, a0, a1);
-  hload(tg + stride, b0, b1);
-  for (; tg < t_hi; tg += stride) {
-    const uint32_t s0 = a0, s1 = a1;
-    a0 = b0;
-    a1 = b1;
-    hload(tg + 2 * stride, b0, b1);
+  constexpr int NV = NSUM > 0 ? NSUM : 1;
+  // one group of G tiles: flattened segment starts (wave-uniform), the per-lane index base
+  // (lane j: entry index of tile j's segment start minus its flattened position) and the total
+  struct Grp {
+    uint32_t ex[G];
+    uint32_t dl, total;
+    size_t gbase;
+  };
+  // one U x 64-entry load of a group
+  struct Ent {
+    uint32_t m[U], rowb[U];
+    unsigned long long v[U][NV];
+  };
+  auto prep = [&](int64_t tg, uint32_t s0, uint32_t s1, Grp& g) {
     const uint32_t len = s1 - s0;
     const uint32_t incl = wave_incl_scan_u32(len, lane);
     const uint32_t excl = incl - len;
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, G - 1);
-    uint32_t ex[G];
+    g.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, G - 1);
 #pragma unroll
-    for (int j = 0; j < G; ++j) ex[j] = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
-    // lane j: entry index of tile j's segment start minus the segment's flattened position
-    // (relative to the group's first tile): entry index = that + flattened position
-    const uint32_t dl = (uint32_t)lane * TR + s0 - excl;
-    const size_t gbase = (size_t)tg * TR;
-    for (uint32_t e0 = 0; e0 < total; e0 += 64u * U) {
-      constexpr int NV = NSUM > 0 ? NSUM : 1;
-      uint32_t m[U], rowb[U];
-      unsigned long long v[U][NV];
+    for (int j = 0; j < G; ++j) g.ex[j] = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
+    g.dl = (uint32_t)lane * TR + s0 - excl;
+    g.gbase = (size_t)tg * TR;
+  };
+  // unconditional loads (an empty group -- past the range -- reads entry 0; the value array
+  // exists even without a summed column): the same loads on every path, so the compiler
+  // waits for exactly the set it consumes
+  auto issue = [&](const Grp& g, uint32_t e0, Ent& en) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t e = e0 + u * 64u + lane;
-        const uint32_t ec = e < total ? e : total - 1u;
-        uint32_t j0 = 0;
+    for (int u = 0; u < U; ++u) {
+      const uint32_t e = e0 + u * 64u + lane;
+      const uint32_t ec = e < g.total ? e : (g.total ? g.total - 1u : 0u);
+      uint32_t j0 = 0;
 #pragma unroll
-        for (int j = 1; j < G; ++j) j0 += ec >= ex[j] ? 1u : 0u;
-        const size_t idx = gbase + (uint32_t)__shfl((int)dl, (int)j0, 64) + ec;
-        rowb[u] = (uint32_t)gbase + j0 * TR;
-        // unconditional loads (the value array exists even without a summed column): the
-        // same loads on every path, so the next group's headers stay in flight
-        m[u] = L.meta[idx];
+      for (int j = 1; j < G; ++j) j0 += ec >= g.ex[j] ? 1u : 0u;
+      size_t idx = g.gbase + (uint32_t)__shfl((int)g.dl, (int)j0, 64) + ec;
+      idx = g.total ? idx : 0;
+      en.rowb[u] = (uint32_t)g.gbase + j0 * TR;
+      en.m[u] = L.meta[idx];
 #pragma unroll
-        for (int q = 0; q < NV; ++q) v[u][q] = L.vals[(size_t)q * L.capacity + idx];
-      }
+      for (int q = 0; q < NV; ++q) en.v[u][q] = L.vals[(size_t)q * L.capacity + idx];
+    }
+  };
+  auto consume = [&](const Grp& g, uint32_t e0, const Ent& en) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t e = e0 + u * 64u + lane;
-        if (e >= total) continue;
-        const uint32_t sl = m[u] & lowmask;
-        const uint32_t row = rowb[u] + (m[u] >> L.wbits);
-        atomicAdd(&cnt[sl], 1u);
-        if (fst[sl] > row) atomicMin(&fst[sl], row);
+    for (int u = 0; u < U; ++u) {
+      const uint32_t e = e0 + u * 64u + lane;
+      if (e >= g.total) continue;
+      const uint32_t sl = en.m[u] & lowmask;
+      const uint32_t row = en.rowb[u] + (en.m[u] >> L.wbits);
+      atomicAdd(&cnt[sl], 1u);
+      if (fst[sl] > row) atomicMin(&fst[sl], row);
 #pragma unroll
-        for (int q = 0; q < nsum; ++q) {
-          if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(v[u][q], p.sum_conv[q]));
-          else atomicAdd(&acc[(size_t)q * W + sl], v[u][q]);
-        }
+      for (int q = 0; q < nsum; ++q) {
+        if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][q], p.sum_conv[q]));
+        else atomicAdd(&acc[(size_t)q * W + sl], en.v[u][q]);
       }
     }
+  };
+  // entries of a group beyond its first U x 64 (segments longer than the typical tile share)
+  auto rest = [&](const Grp& g, Ent& en) {
+    for (uint32_t e0 = 64u * U; e0 < g.total; e0 += 64u * U) {
+      issue(g, e0, en);
+      consume(g, e0, en);
+    }
+  };
+  const int64_t stride = (int64_t)NW * G;
+  int64_t tg = t_lo + (int64_t)wave * G;
+  uint32_t ha0, ha1, hb0, hb1;  // headers of the groups two and three ahead, in turn
+  Grp ga, gb;
+  Ent ea, eb;
+  hload(tg, ha0, ha1);
+  hload(tg + stride, hb0, hb1);
+  prep(tg, ha0, ha1, ga);
+  issue(ga, 0, ea);
+  hload(tg + 2 * stride, ha0, ha1);
+  for (; tg < t_hi; tg += 2 * stride) {
+    // group tg in (ga, ea); group tg + stride's header in hb
+    prep(tg + stride, hb0, hb1, gb);
+    issue(gb, 0, eb);
+    hload(tg + 3 * stride, hb0, hb1);
+    consume(ga, 0, ea);
+    rest(ga, ea);
+    if (tg + stride >= t_hi) break;
+    // group tg + stride in (gb, eb); group tg + 2 * stride's header in ha
+    prep(tg + 2 * stride, ha0, ha1, ga);
+    issue(ga, 0, ea);
+    hload(tg + 4 * stride, ha0, ha1);
+    consume(gb, 0, eb);
+    rest(gb, eb);
   }
   __syncthreads();
+  // Combine the partition's split tables without device atomics (and without a slot-array
+  // initialisation pass): every split stores its table to its own partial record, the last
+  // split to arrive (one agent-scope counter per partition, zeroed before the launch) adds the
+  // records in split order -- the same sums whatever the arrival order -- and writes every slot
+  // of the partition, empty ones included.  Hand-off: plain stores, each wave drains, barrier,
+  // one lane's agent release, then the counter; the last arriver acquires before reading
+  // (cdna_hip_programming.md Guideline 16).  Nobody waits: no spin, no residency assumption.
   const uint64_t slot0 = (uint64_t)part << L.wbits;
-  for (int s = tid; s < W; s += blockDim.x) {
-    const uint32_t c = cnt[s];
-    if (c == 0) continue;
-    const uint64_t gs = slot0 + s;
-    atomicAdd(&sa.cnt[gs], (unsigned long long)c);
-    atomicMin(&sa.fst[gs], fst[s]);
+  const int nvalid = (int)((uint64_t)W < p.nslots - slot0 ? (uint64_t)W : p.nslots - slot0);
+  const int S = L.splits;
+  __shared__ unsigned int s_last;
+  if (S > 1) {
+    uint32_t* pc = reinterpret_cast<uint32_t*>(L.partial + ((size_t)part * S + split) * L.partial_bytes);
+    uint32_t* pf = pc + W;
+    unsigned long long* pa = reinterpret_cast<unsigned long long*>(pf + W);
+    for (int s = tid; s < W; s += blockDim.x) {
+      pc[s] = cnt[s];
+      pf[s] = fst[s];
 #pragma unroll
-    for (int q = 0; q < nsum; ++q) {
-      const unsigned long long a = acc[(size_t)q * W + s];
-      if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)q * p.nslots + gs]), as_f64(a));
-      else atomicAdd(&sa.acc[(size_t)q * p.nslots + gs], a);
+      for (int q = 0; q < nsum; ++q) pa[(size_t)q * W + s] = acc[(size_t)q * W + s];
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned int old = __hip_atomic_fetch_add(&L.arrive[part], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = old == (unsigned int)(S - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      s_last = last ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_last) return;
+  }
+  for (int s = tid; s < nvalid; s += blockDim.x) {
+    uint32_t c = 0, f = kNoRow;
+    unsigned long long a[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) a[q] = 0;
+    for (int o = 0; o < S; ++o) {
+      uint32_t oc, of;
+      unsigned long long oa[NV];
+      if (o == split) {
+        oc = cnt[s];
+        of = fst[s];
+#pragma unroll
+        for (int q = 0; q < nsum; ++q) oa[q] = acc[(size_t)q * W + s];
+      } else {
+        const uint32_t* pc = reinterpret_cast<const uint32_t*>(L.partial + ((size_t)part * S + o) * L.partial_bytes);
+        const unsigned long long* pa = reinterpret_cast<const unsigned long long*>(pc + 2 * W);
+        oc = pc[s];
+        of = pc[W + s];
+#pragma unroll
+        for (int q = 0; q < nsum; ++q) oa[q] = pa[(size_t)q * W + s];
+      }
+      c += oc;
+      f = of < f ? of : f;
+#pragma unroll
+      for (int q = 0; q < nsum; ++q) {
+        if (p.sum_is_float[q]) a[q] = as_u64(as_f64(a[q]) + as_f64(oa[q]));
+        else a[q] += oa[q];
+      }
+    }
+    const uint64_t gs = slot0 + s;
+    sa.cnt[gs] = c;
+    sa.fst[gs] = f;
+#pragma unroll
+    for (int q = 0; q < nsum; ++q) sa.acc[(size_t)q * p.nslots + gs] = a[q];
   }
 }
 
@@ -184,8 +283,7 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
   } else {
     BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L));
   }
-  const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)p.nsum);
-  const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
+  const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)p.nsum);  const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
   switch (p.nsum) {
     case 0: hipLaunchKernelGGL((k_part_aggregate<8, 4, 0>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
     case 1: hipLaunchKernelGGL((k_part_aggregate<8, 4, 1>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;

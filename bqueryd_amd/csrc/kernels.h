@@ -173,6 +173,11 @@ struct PartLaunch {
   uint16_t* hdr;             // [ntiles][nparts + 1]: partition offsets in each sorted tile
   uint32_t* meta;            // [capacity]: row-in-tile << wbits | slot_low
   unsigned long long* vals;  // [nsum][capacity]: summed values (canonical 64-bit)
+  // aggregate combine (splits > 1): per-partition arrival counters (zeroed by
+  // launch_partitioned) and [nparts][splits] partial tables of partial_bytes each
+  unsigned int* arrive;
+  unsigned char* partial;
+  size_t partial_bytes;      // 2^wbits * (8 + 8 * nsum)
 };
 // LDS bytes of a scatter workgroup: the staged tile (values, meta), tile counts (two
 // buffers) / offsets and two sets of scan totals

@@ -512,6 +512,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&L.hdr, (size_t)L.ntiles * (L.nparts + 1) * 2 + 256));
   CK(hipMalloc(&L.meta, L.capacity * 4 + 256));
   CK(hipMalloc(&L.vals, L.capacity * 8 + 256));
+  L.partial_bytes = ((size_t)1 << L.wbits) * 16;
+  CK(hipMalloc(&L.partial, (size_t)L.nparts * 8 * L.partial_bytes + 256));
+  CK(hipMalloc(&L.arrive, (size_t)L.nparts * 4 + 256));
   const size_t slds = part_scatter_lds(L.nparts, L.threads, 1);
   CK(hipFuncSetAttribute((const void*)k_scatter_lib, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   auto agg_run = [&](auto agg, const char* what, int splits) {
