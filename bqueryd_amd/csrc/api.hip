@@ -1245,7 +1245,12 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       hipFunction_t sfn = nullptr;
       if (fused && N >= jit_min_rows()) {
         const int cd_mode = d.cd.bitmap == nullptr ? 0 : (d.cd.lds_bitmap_words > 0 ? 1 : 2);
-        std::string spec = jit_spec(pc.p) + "#define BQ_SCD_CD " + std::to_string(cd_mode) + "\n";
+        // the value columns as constants (the same choice as the generic body's column loop)
+        const int nc = pc.p.ncols;
+        const int vc = d.vcol >= 0 && d.vcol < nc ? d.vcol : 0;
+        const int cc = d.cd.vcol >= 0 && d.cd.vcol < nc ? d.cd.vcol : 0;
+        std::string spec = jit_spec(pc.p) + "#define BQ_SCD_CD " + std::to_string(cd_mode) + "\n#define BQ_SCD_VC " +
+                           std::to_string(vc) + "\n#define BQ_SCD_CC " + std::to_string(cc) + "\n";
         sfn = jit_function(d.compact ? "bq_jit_scd_fused32" : "bq_jit_scd_fused", spec);
         c->last.specialized = sfn ? 1 : 0;
       }

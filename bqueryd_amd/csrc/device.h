@@ -222,11 +222,15 @@ __device__ __forceinline__ uint32_t eval_term(const DevTerm& t, const uint64_t (
   return m;
 }
 
-// R-bit pass mask of the rows starting at row0
-template <int NC, int R>
+// R-bit pass mask of the rows starting at row0 (BOUND = false: the caller has already masked
+// rows past the end, and only the where terms and the mask column are applied)
+template <int NC, int R, bool BOUND = true>
 __device__ __forceinline__ uint32_t vals_pass(const ScanParams& p, int64_t row0, const uint64_t (&v)[NC][R]) {
-  const int64_t rem = p.nrows - row0;
-  uint32_t pass = rem >= R ? ((1u << R) - 1u) : (rem > 0 ? ((1u << rem) - 1u) : 0u);
+  uint32_t pass = (1u << R) - 1u;
+  if (BOUND) {
+    const int64_t rem = p.nrows - row0;
+    pass = rem >= R ? ((1u << R) - 1u) : (rem > 0 ? ((1u << rem) - 1u) : 0u);
+  }
 #pragma unroll
   for (int t = 0; t < BQ_LOOP_BOUND(p.nterms, kMaxTerms); ++t) {
     if (t >= p.nterms) break;

@@ -120,12 +120,17 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
   const bool live = w < d.waves;  // every wave stays for the block's final count_distinct flush
   const int64_t start = live ? (int64_t)w * d.chunk_rows : 0;
   const int64_t end = live ? min(start + d.chunk_rows, p.nrows) : 0;
+#ifdef BQ_SCD_VC
+  // the JIT build fixes the value columns: no per-step select between column registers
+  constexpr int vc = BQ_SCD_VC, cc = BQ_SCD_CC;
+#else
   int vc = 0, cc = 0;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     if (d.vcol == c) vc = c;
     if (d.cd.vcol == c) cc = c;
   }
+#endif
   const bool isf = !COMPACT && dtype_is_float(p.cols[vc].dtype);
   const bool cd_runs = cc == vc;  // count_distinct of the sorted_count_distinct column
   const uint64_t lanes_below = (1ull << lane) - 1ull;
@@ -147,9 +152,29 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       for (int c = 0; c < NC; ++c) scd_word_to_chunk(raw[c], p.cols[c], row, ring[a][c]);
       uint64_t v[NC][1];
       decode_all<NC, 1>(p, raw, v);
-      // the step's values are out of ring[a] before its refill is issued: without this
-      // scheduling fence the compiler hoists the refill above the decode into fresh registers
-      // and copies them back at the loop latch, behind an s_waitcnt vmcnt(0)
+      // everything the step needs from its rows is derived before ring[a]'s refill is issued,
+      // so ring[a] is dead at the refill and the loads land in the loop-carried registers
+      // (otherwise they land in fresh ones, copied back at the loop head behind a vmcnt(0)
+      // that drains the whole prefetch); rel < nrel is the row bound (32-bit), vals_pass
+      // applies the terms only
+      const bool act = rel < nrel && (vals_pass<NC, 1, false>(p, row, v) & 1u);
+      uint64_t code[1];
+      vals_code<NC, 1>(p, v, code);
+      uint64_t vb = 0, vcd = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (vc == c) vb = v[c][0];
+        if (cc == c) vcd = v[c][0];
+      }
+      uint32_t s = (uint32_t)code[0];
+      if (COMPACT) {
+        // the derived 32-bit values are pinned here (an empty asm that redefines them): the
+        // compiler would otherwise sink their arithmetic below the refill, keeping ring[a] live
+        uint32_t vb32 = (uint32_t)(vb - (uint64_t)d.vmin), vcd32 = (uint32_t)vcd;
+        asm volatile("" : "+v"(s), "+v"(vb32), "+v"(vcd32));
+        vb = vb32;
+        vcd = vcd32;
+      }
       __builtin_amdgcn_sched_barrier(0);
       // unconditional (clamped) prefetch: the same number of loads is in flight on every
       // path, so the compiler waits for exactly the step it consumes (vmcnt(N), not vmcnt(0));
@@ -157,17 +182,6 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       // edge would merge a shorter load history into the loop header)
       scd_issue<NC>(p, start, rb + 64u * kScdAhead, nrel, lane, ring[a]);
       if (rb >= nrel) continue;
-      const bool act = rel < nrel && (vals_pass<NC, 1>(p, row, v) & 1u);
-      uint64_t code[1];
-      vals_code<NC, 1>(p, v, code);
-      const uint32_t s = (uint32_t)code[0];
-      uint64_t vb = 0, vcd = 0;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        if (vc == c) vb = v[c][0];
-        if (cc == c) vcd = v[c][0];
-      }
-      if (COMPACT) vb = (uint32_t)(vb - (uint64_t)d.vmin);
       const uint64_t actm = __ballot(act);
       if (actm == 0) continue;
       // one slot for the whole step (sorted or clustered keys): the active lanes are its lanes,
@@ -185,22 +199,27 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         match = act ? tbl[s] : 0ull;
       }
       const uint64_t below = match & lanes_below;
-      uint64_t pv, lastv;
-      if (COMPACT && uni && (actm & (actm + 1)) == 0) {
-        // one slot on lanes 0..k: the previous row is the lane below (a DPP wave shift, no
-        // LDS) and the slot's last row in the step is lane k (a scalar read)
-        pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)vb, 0x138, 0xF, 0xF, false);  // wave_shr:1
-        lastv = (uint32_t)__builtin_amdgcn_readlane((uint32_t)vb, 63 - __clzll((long long)actm));
+      uint64_t pv, lastv = 0;
+      if (COMPACT) {
+        // compact state: with several slots in the step, each slot's last lane stores `last`
+        // itself (below), so no lane needs the slot's last value -- only its previous row's;
+        // with one slot, the last value is a scalar read and the first lane stores it
+        if (uni && (actm & (actm + 1)) == 0) {
+          // one slot on lanes 0..k: the previous row is the lane below (a DPP wave shift, no LDS)
+          pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)vb, 0x138, 0xF, 0xF, false);  // wave_shr:1
+        } else {
+          // previous row of the slot in this step: lane 63 - clz(below), as the byte address
+          // (~clz) << 2 (ds_bpermute takes the lane from address bits 7..2); with below == 0 it
+          // reads an arbitrary lane, which `diff` below ignores
+          const uint32_t lz = (uint32_t)__clzll((long long)below);
+          pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(~lz << 2), (int)(uint32_t)vb);
+        }
+        if (uni) lastv = (uint32_t)__builtin_amdgcn_readlane((uint32_t)vb, 63 - __clzll((long long)actm));
       } else {
         const int pl = below ? 63 - __clzll((long long)below) : lane;
         const int hl = (act && match) ? 63 - __clzll((long long)match) : lane;
-        if (COMPACT) {
-          pv = (uint32_t)__shfl((int)(uint32_t)vb, pl, 64);     // previous row of the slot in this step
-          lastv = (uint32_t)__shfl((int)(uint32_t)vb, hl, 64);  // last row of the slot in this step
-        } else {
-          pv = __shfl(vb, pl, 64);
-          lastv = __shfl(vb, hl, 64);
-        }
+        pv = __shfl(vb, pl, 64);
+        lastv = __shfl(vb, hl, 64);  // last row of the slot in this step
       }
       const bool diff = act && below != 0 && !scd_equal(vb, pv, isf);
       const uint64_t dm = __ballot(diff);
@@ -220,7 +239,9 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
             ch += 1u;
             run_start = true;
           }
-          st32[s] = ScdSlot32{(uint32_t)lastv, (rows + add_rows) | (ch << 16)};
+          const uint32_t rc = (rows + add_rows) | (ch << 16);
+          if (uni) st32[s] = ScdSlot32{(uint32_t)lastv, rc};
+          else st32[s].rc = rc;  // `last`: the slot's last lane, below
         } else {
           ScdSlot cur = st[s];
           uint32_t ch = cur.changes + add_ch;
@@ -238,6 +259,10 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
           st[s] = cur;
         }
       }
+      // compact: the slot's last lane in the step (the highest lane of its match mask) stores
+      // its value as the slot's `last` -- after the first lane's read of the state above
+      // (program order; the same address in both lanes' expressions)
+      if (COMPACT && !uni && act && (match >> lane) == 1ull) st32[s].last = (uint32_t)vb;
       // count_distinct of the same column: only the first row of a value run of its slot can
       // add a (slot, value) pair (every later row of the run repeats one already added), so
       // the pair check runs at run starts only (most rows of a sorted column skip it)
