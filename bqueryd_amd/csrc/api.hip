@@ -964,11 +964,16 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.threads = 1024;
       if (const char* ev = getenv("BQGPU_PART_THREADS")) L.threads = std::max(256, std::min(1024, atoi(ev)));
       while (L.threads > 256 && part_scatter_lds(L.nparts, L.threads, nsum) > 150 * 1024) L.threads >>= 1;
-      L.tile_rows = L.threads * kRowsPerThread;
+      // 8192-row tiles (two 4-row chunks per thread) when the staged tile fits: the aggregate's
+      // per-tile partition segments are twice as long (BQGPU_PART_K=1|2 forces the choice)
+      L.k = (L.threads == 1024 && part_scatter_lds(L.nparts, L.threads, nsum, 2) <= 150 * 1024) ? 2 : 1;
+      if (const char* ev = getenv("BQGPU_PART_K"))
+        L.k = (atoi(ev) == 2 && part_scatter_lds(L.nparts, L.threads, nsum, 2) <= 150 * 1024) ? 2 : 1;
+      L.tile_rows = L.threads * kRowsPerThread * L.k;
       const int64_t tr = L.tile_rows;
       L.ntiles = (N + tr - 1) / tr;
-      // contiguous whole-tile row ranges, two scatter workgroups per CU
-      int per_cu = 2;
+      // contiguous whole-tile row ranges, as many scatter workgroups per CU as fit in LDS
+      int per_cu = L.k == 2 ? 1 : 2;
       if (const char* ev = getenv("BQGPU_PART_PER_CU")) per_cu = std::max(1, std::min(8, atoi(ev)));
       L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, L.ntiles));
       L.rows_per_block = ((L.ntiles + L.blocks - 1) / L.blocks) * tr;
@@ -993,7 +998,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.arrive = (unsigned int*)(eb + vbytes + mbytes + pbytes);
       hipFunction_t fs = nullptr;
       if (N >= jit_min_rows()) {
-        fs = jit_function("bq_jit_part_scatter", jit_spec(pl.p));
+        fs = jit_function("bq_jit_part_scatter", jit_spec(pl.p) + "#define BQ_PART_K " + std::to_string(L.k) + "\n");
         c->last.specialized = fs ? 1 : 0;
       }
       launch_partitioned(pl.p, sa, L, st, fs);

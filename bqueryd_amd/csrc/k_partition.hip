@@ -23,10 +23,10 @@
 
 namespace bqg {
 
-template <int NC>
+template <int NC, int K>
 __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartLaunch L) {
   extern __shared__ __align__(16) unsigned char smem[];
-  part_scatter_body<NC>(p, L, smem);
+  part_scatter_body<NC, K>(p, L, smem);
 }
 
 // Aggregate over the tile layout.  Workgroup (partition, split): the split's tile range.  A
@@ -273,24 +273,31 @@ void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipSt
 #ifndef BQG_PART_MICRO  // tools/micro/part_micro.hip includes this file for the aggregate kernel
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,
                         hipFunction_t fscatter) {
-  const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum);
+  const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum, L.k);
   if (fscatter) {
     PartLaunch Lc = L;
     ScanParams pc = p;
     void* args[] = {(void*)&pc, (void*)&Lc};
     (void)hipModuleLaunchKernel(fscatter, (unsigned)L.blocks, 1, 1, (unsigned)L.threads, 1, 1, (unsigned)scatter_lds,
                                 st, args, nullptr);
+  } else if (L.k == 2) {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC, 2>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L));
   } else {
-    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L));
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC, 1>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L));
   }
-  const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)p.nsum);  const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
+  const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)p.nsum);
+  const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
+  // G tiles per wave group: ~8 x 4096 rows of segments whichever the tile size
+#define BQG_AGG(G, U, NS) hipLaunchKernelGGL((k_part_aggregate<G, U, NS>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
+  const bool big = L.tile_rows > 4096;
   switch (p.nsum) {
-    case 0: hipLaunchKernelGGL((k_part_aggregate<8, 4, 0>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
-    case 1: hipLaunchKernelGGL((k_part_aggregate<8, 4, 1>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
-    case 2: hipLaunchKernelGGL((k_part_aggregate<8, 4, 2>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
-    case 3: hipLaunchKernelGGL((k_part_aggregate<8, 2, 3>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
-    default: hipLaunchKernelGGL((k_part_aggregate<8, 2, 4>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); break;
+    case 0: if (big) BQG_AGG(4, 4, 0); else BQG_AGG(8, 4, 0); break;
+    case 1: if (big) BQG_AGG(4, 4, 1); else BQG_AGG(8, 4, 1); break;
+    case 2: if (big) BQG_AGG(4, 4, 2); else BQG_AGG(8, 4, 2); break;
+    case 3: if (big) BQG_AGG(4, 2, 3); else BQG_AGG(8, 2, 3); break;
+    default: if (big) BQG_AGG(4, 2, 4); else BQG_AGG(8, 2, 4); break;
   }
+#undef BQG_AGG
 }
 #endif
 

@@ -166,7 +166,8 @@ struct PartLaunch {
   int blocks;                // workgroups of the scatter pass
   int splits;                // aggregate workgroups per partition (tile ranges)
   int threads;               // threads of a scatter workgroup: tiles of threads * 4 rows
-  int tile_rows;             // threads * 4
+  int tile_rows;             // threads * 4 * k
+  int k;                     // 4-row chunks per scatter thread and tile (1 or 2)
   int64_t rows_per_block;    // contiguous rows per scatter workgroup, whole tiles
   int64_t ntiles;            // ceil(nrows / tile_rows)
   uint64_t capacity;         // entries per array = ntiles * tile_rows
@@ -181,8 +182,8 @@ struct PartLaunch {
 };
 // LDS bytes of a scatter workgroup: the staged tile (values, meta), tile counts (two
 // buffers) / offsets and two sets of scan totals
-inline size_t part_scatter_lds(int nparts, int threads, int nsum) {
-  return (size_t)threads * 4 * (4 + 8 * (size_t)nsum) + (size_t)nparts * 12 + 2 * 16 * 4;
+inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1) {
+  return (size_t)threads * 4 * k * (4 + 8 * (size_t)nsum) + (size_t)nparts * 12 + 2 * 16 * 4;
 }
 // fscatter: the query-specialised (JIT) scatter kernel, or nullptr for the precompiled one
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,

@@ -78,7 +78,7 @@ __device__ __forceinline__ void load_rows4_clamped(const ScanParams& p, int64_t 
   for (int c = 0; c < NC; ++c) load_chunk(raw[c], p.cols[c], ((mask >> c) & 1u) ? r : home);
 }
 
-// Tile-layout scatter.  A tile is T * 4 rows (TR).  The workgroup counting-sorts each of its
+// Tile-layout scatter.  A tile is T * 4 * K rows (TR).  The workgroup counting-sorts each of its
 // tiles by partition (slot >> wbits) in LDS and writes the sorted tile back LINEARLY to the
 // tile's own entry range [tile * TR, tile * TR + TR) with 16-byte stores of whole lines --
 // the same stores on every path (positions past the tile's passing rows carry left-over
@@ -91,11 +91,13 @@ __device__ __forceinline__ void load_rows4_clamped(const ScanParams& p, int64_t 
 // (count pass, scan, per-(partition, block) regions) wrote each tile as ~P runs of ~32
 // entries into P far-apart regions and ran at 3.4 TB/s of moved bytes; the linear tile
 // writes run at copy speed (2.8 GB in 0.57 ms), with no count pass and no scan.
-template <int NC>
+template <int NC, int K = 1>
 __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const PartLaunch& L, unsigned char* smem) {
+  // K 4-row chunks per thread and tile (TR = T * 4 * K rows): chunk k of thread t covers rows
+  // base + k * T * 4 + t * 4 .. + 3, so every chunk load of the workgroup is one coalesced block
   const int T = blockDim.x, tid = threadIdx.x;
   const int P = L.nparts;
-  const int TR = T * kRowsPerThread;
+  const int TR = T * kRowsPerThread * K;
   const int nsum = p.nsum;
   constexpr int NS = NC < kMaxSums ? NC : kMaxSums;
   unsigned long long* sval = reinterpret_cast<unsigned long long*>(smem);  // [nsum][TR]
@@ -117,34 +119,39 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   const int q0 = tid * per;
   const int q1 = min(P, q0 + per);
   const uint32_t all = (1u << NC) - 1u;
-  Chunk raw[NC];
-  load_rows4_clamped<NC>(p, begin + (int64_t)tid * kRowsPerThread, end, raw, all, begin);
+  const int64_t CH = (int64_t)T * kRowsPerThread;  // rows of one chunk block
+  Chunk raw[K][NC];
+#pragma unroll
+  for (int k = 0; k < K; ++k) load_rows4_clamped<NC>(p, begin + k * CH + (int64_t)tid * kRowsPerThread, end, raw[k], all, begin);
   int parity = 0;
   for (int64_t base = begin; base < end; base += TR, parity ^= 1) {
     // the tile histogram alternates between two buffers: the one this tile zeroes at its end
     // is next counted into two tiles later, past the next tile's barriers
     uint32_t* hist = hist2 + parity * P;
-    uint32_t pass, part[4], rank[4], low[4];
-    uint64_t sv[NS][4];
-    const int64_t row0 = base + (int64_t)tid * kRowsPerThread;
-    {
+    uint32_t pass[K], part[K][4], rank[K][4], low[K][4];
+    uint64_t sv[NS][K][4];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t row0 = base + k * CH + (int64_t)tid * kRowsPerThread;
       uint64_t v[NC][4], code[4];
-      decode_all<NC, 4>(p, raw, v);
-      load_rows4_clamped<NC>(p, row0 + TR, end, raw, all, begin);
-      pass = vals_pass<NC, 4>(p, row0, v);
+      decode_all<NC, 4>(p, raw[k], v);
+      load_rows4_clamped<NC>(p, row0 + TR, end, raw[k], all, begin);
+      pass[k] = vals_pass<NC, 4>(p, row0, v);
       const int64_t rem = end - row0;
-      pass &= rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
+      pass[k] &= rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
       vals_code<NC, 4>(p, v, code);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        part[r] = (uint32_t)(code[r] >> L.wbits);
-        low[r] = (uint32_t)(code[r] & lowmask);
+        part[k][r] = (uint32_t)(code[r] >> L.wbits);
+        low[k][r] = (uint32_t)(code[r] & lowmask);
 #pragma unroll
-        for (int s = 0; s < NS; ++s) sv[s][r] = v[s][r];
+        for (int s = 0; s < NS; ++s) sv[s][k][r] = v[s][r];
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) rank[r] = (pass & (1u << r)) ? atomicAdd(&hist[part[r]], 1u) : 0u;
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rank[k][r] = (pass[k] & (1u << r)) ? atomicAdd(&hist[part[k][r]], 1u) : 0u;
     lds_barrier();
     // tile offsets: exclusive scan of the tile histogram, also the tile's header
     uint32_t local = 0;
@@ -161,24 +168,31 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
     lds_barrier();
     // stage the tile sorted by partition
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (!(pass & (1u << r))) continue;
-      const uint32_t pos = toff[part[r]] + rank[r];
-      smeta[pos] = ((uint32_t)(row0 + r - base) << L.wbits) | low[r];
+    for (int k = 0; k < K; ++k) {
+      const uint32_t rit0 = (uint32_t)(k * CH) + (uint32_t)tid * kRowsPerThread;  // row in tile
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
-        if (s < nsum) sval[(size_t)s * TR + pos] = sv[s][r];
+      for (int r = 0; r < 4; ++r) {
+        if (!(pass[k] & (1u << r))) continue;
+        const uint32_t pos = toff[part[k][r]] + rank[k][r];
+        smeta[pos] = ((rit0 + r) << L.wbits) | low[k][r];
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          if (s < nsum) sval[(size_t)s * TR + pos] = sv[s][k][r];
+      }
     }
     lds_barrier();
-    // linear copy-out: one 16-byte store of meta and two per summed column, every thread
-    *reinterpret_cast<uint4*>(L.meta + base + 4 * tid) = *reinterpret_cast<const uint4*>(smeta + 4 * tid);
+    // linear copy-out: K 16-byte stores of meta and 2K per summed column, every thread
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      *reinterpret_cast<uint4*>(L.meta + base + 4 * (tid + k * T)) = *reinterpret_cast<const uint4*>(smeta + 4 * (tid + k * T));
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (s >= nsum) break;
       unsigned long long* dv = L.vals + (size_t)s * L.capacity + base;
       const unsigned long long* lv = sval + (size_t)s * TR;
-      *reinterpret_cast<uint4*>(dv + 2 * tid) = *reinterpret_cast<const uint4*>(lv + 2 * tid);
-      *reinterpret_cast<uint4*>(dv + 2 * (tid + T)) = *reinterpret_cast<const uint4*>(lv + 2 * (tid + T));
+#pragma unroll
+      for (int k = 0; k < 2 * K; ++k)
+        *reinterpret_cast<uint4*>(dv + 2 * (tid + k * T)) = *reinterpret_cast<const uint4*>(lv + 2 * (tid + k * T));
     }
     for (int i = q0; i < q1; ++i) hist[i] = 0;
   }
