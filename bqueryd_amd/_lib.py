@@ -56,7 +56,8 @@ class ResultView(ctypes.Structure):
 class Timing(ctypes.Structure):
     _fields_ = [('scan_ms', ctypes.c_double), ('scan_launches', ctypes.c_int32),
                 ('total_ms', ctypes.c_double), ('rows', ctypes.c_int64),
-                ('bytes', ctypes.c_int64), ('mode', ctypes.c_int32), ('specialized', ctypes.c_int32)]
+                ('bytes', ctypes.c_int64), ('mode', ctypes.c_int32), ('specialized', ctypes.c_int32),
+                ('narrow', ctypes.c_int32)]
 
 
 # enum bqg_decode

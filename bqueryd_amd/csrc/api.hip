@@ -128,6 +128,10 @@ struct ColStats {
   int64_t imin = 0, imax = 0;
   double fmin = 0, fmax = 0;
   bool has_nan = false;
+  // float columns: an exact 32-bit integer code for every value (partitioned sums travel as
+  // codes): 1 = dyadic, code = v * 2^enc_k; 2 = cents, code = rint(v * 100); 0 = none
+  int enc = 0;
+  int enc_k = 0;
 };
 
 struct Column {
@@ -352,18 +356,18 @@ void compute_stats(bqg_table* t, int col) {
   bqg_ctx* c = t->ctx;
   Column& k = t->cols[col];
   if (k.stats.valid) return;
-  unsigned long long* d = (unsigned long long*)c->misc.ensure(4 * sizeof(unsigned long long));
-  unsigned long long init[4] = {~0ull, 0ull, 0ull, 0ull};
-  unsigned long long* h = (unsigned long long*)c->hhdr.ensure(64);
+  unsigned long long* d = (unsigned long long*)c->misc.ensure(8 * sizeof(unsigned long long));
+  unsigned long long init[8] = {~0ull, 0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
+  unsigned long long* h = (unsigned long long*)c->hhdr.ensure(128);
   memcpy(h, init, sizeof(init));
   HIPCHECK(hipMemcpyAsync(d, h, sizeof(init), hipMemcpyHostToDevice, c->stream));
   DevCol dc{k.dev, k.dtype, dtype_lg(k.dtype)};
   if (t->nrows > 0) launch_stats(dc, t->nrows, d, c->stream);
   HIPCHECK(hipGetLastError());
-  HIPCHECK(hipMemcpyAsync(h + 4, d, sizeof(init), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipMemcpyAsync(h + 8, d, sizeof(init), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
-  const unsigned long long mn = h[4], mx = h[5];
-  k.stats.has_nan = h[6] != 0;
+  const unsigned long long mn = h[8], mx = h[9], lsb = h[11], enc = h[12];
+  k.stats.has_nan = h[10] != 0;
   k.stats.empty = mn > mx;
   if (!k.stats.empty) {
     if (dtype_is_float(k.dtype)) {
@@ -375,6 +379,18 @@ void compute_stats(bqg_table* t, int col) {
       };
       k.stats.fmin = dec(mn);
       k.stats.fmax = dec(mx);
+      // exact 32-bit codes (k_stats): dyadic first (the code's sum times 2^-k is the exact sum
+      // whenever it is below 2^53), else whole hundredths; |code| < 2^31 for every value
+      const double maxabs = std::max(std::fabs(k.stats.fmin), std::fabs(k.stats.fmax));
+      if (!k.stats.has_nan) {
+        const int kk = lsb == ~0ull ? 0 : std::max(0, 4096 - (int)lsb);
+        if (!(enc & 1ull) && kk <= 62 && std::ldexp(maxabs, kk) < 2147483647.0) {
+          k.stats.enc = 1;
+          k.stats.enc_k = kk;
+        } else if (!(enc & 2ull) && maxabs * 100.0 < 2147483647.0) {
+          k.stats.enc = 2;
+        }
+      }
     } else if (k.dtype == BQG_U64) {
       k.stats.imin = (int64_t)mn;
       k.stats.imax = (int64_t)mx;
@@ -960,15 +976,31 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       PartLaunch L{};
       L.wbits = pl.wbits;
       L.nparts = (int)((S + (1ull << pl.wbits) - 1) >> pl.wbits);
+      // narrow entries: every summed column is a float column whose values all have an exact
+      // 32-bit integer code (column statistics): 8-byte instead of 12-byte C3 entries, and the
+      // sums are exact integer sums scaled back once (BQGPU_PART_NARROW=0 turns it off)
+      L.narrow = nsum > 0 && !(getenv("BQGPU_PART_NARROW") && atoi(getenv("BQGPU_PART_NARROW")) == 0);
+      for (int q = 0; q < nsum && L.narrow; ++q) {
+        compute_stats(t, pl.tcol[q]);
+        const ColStats& cs = t->cols[pl.tcol[q]].stats;
+        if (!pl.p.sum_is_float[q] || pl.p.sum_centered[q] || cs.enc == 0) {
+          L.narrow = 0;
+          break;
+        }
+        L.enc_kind[q] = cs.enc;
+        L.enc_mul[q] = cs.enc == 1 ? std::ldexp(1.0, cs.enc_k) : 100.0;
+      }
+      const bool nw = L.narrow != 0;
+      c->last.narrow = L.narrow;
       // scatter workgroup: the widest whose staged tile fits in LDS (BQGPU_PART_THREADS caps it)
       L.threads = 1024;
       if (const char* ev = getenv("BQGPU_PART_THREADS")) L.threads = std::max(256, std::min(1024, atoi(ev)));
-      while (L.threads > 256 && part_scatter_lds(L.nparts, L.threads, nsum) > 150 * 1024) L.threads >>= 1;
+      while (L.threads > 256 && part_scatter_lds(L.nparts, L.threads, nsum, 1, nw) > 150 * 1024) L.threads >>= 1;
       // 8192-row tiles (two 4-row chunks per thread) when the staged tile fits: the aggregate's
       // per-tile partition segments are twice as long (BQGPU_PART_K=1|2 forces the choice)
-      L.k = (L.threads == 1024 && part_scatter_lds(L.nparts, L.threads, nsum, 2) <= 150 * 1024) ? 2 : 1;
+      L.k = (L.threads == 1024 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw) <= 150 * 1024) ? 2 : 1;
       if (const char* ev = getenv("BQGPU_PART_K"))
-        L.k = (atoi(ev) == 2 && part_scatter_lds(L.nparts, L.threads, nsum, 2) <= 150 * 1024) ? 2 : 1;
+        L.k = (atoi(ev) == 2 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw) <= 150 * 1024) ? 2 : 1;
       L.tile_rows = L.threads * kRowsPerThread * L.k;
       const int64_t tr = L.tile_rows;
       L.ntiles = (N + tr - 1) / tr;
@@ -987,7 +1019,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.capacity = (uint64_t)L.ntiles * (uint64_t)tr;
       L.hdr = (uint16_t*)c->prefix.ensure((size_t)L.ntiles * (size_t)(L.nparts + 1) * 2 + 256);
       // one scratch block: entry values | entry meta | split partial tables | arrival counters
-      const size_t vbytes = ((size_t)L.capacity * 8 * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
+      const size_t vbytes = ((size_t)L.capacity * (nw ? 4 : 8) * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
       const size_t mbytes = ((size_t)L.capacity * 4 + 255) & ~size_t(255);
       L.partial_bytes = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)nsum);
       const size_t pbytes = L.splits > 1 ? (size_t)L.nparts * L.splits * L.partial_bytes : 0;
@@ -998,7 +1030,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.arrive = (unsigned int*)(eb + vbytes + mbytes + pbytes);
       hipFunction_t fs = nullptr;
       if (N >= jit_min_rows()) {
-        fs = jit_function("bq_jit_part_scatter", jit_spec(pl.p) + "#define BQ_PART_K " + std::to_string(L.k) + "\n");
+        fs = jit_function("bq_jit_part_scatter", jit_spec(pl.p) + "#define BQ_PART_K " + std::to_string(L.k) +
+                                                      "\n#define BQ_PART_NARROW " + std::to_string(L.narrow) + "\n");
         c->last.specialized = fs ? 1 : 0;
       }
       launch_partitioned(pl.p, sa, L, st, fs);

@@ -331,8 +331,14 @@ __device__ __forceinline__ unsigned long long ord_key_f(double d) {
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
 
+// out[0] / out[1]: min / max order key; out[2]: NaN seen; float columns also get the facts
+// that decide an exact 32-bit code for partitioned sums (api.hip, narrow entries):
+// out[3]: min over non-zero values of (exponent of the lowest set mantissa bit + 4096), so
+// every value is an integer multiple of 2^(out[3] - 4096); out[4]: bit 0 -- some value is
+// subnormal or infinite (no dyadic code), bit 1 -- some value is not a whole number of
+// hundredths (rint(v * 100) / 100 != v: no cents code).
 __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsigned long long* out) {
-  unsigned long long mn = ~0ull, mx = 0ull, nan = 0ull;
+  unsigned long long mn = ~0ull, mx = 0ull, nan = 0ull, lsb = ~0ull, enc = 0ull;
   const bool isf = dtype_is_float(c.dtype);
   const bool u64 = c.dtype == BQG_U64;
   for (int64_t row0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4; row0 < nrows;
@@ -347,6 +353,19 @@ __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsig
         const double d = chunk_f64(ch, c.dtype, r);
         if (d != d) { nan = 1; continue; }
         k = ord_key_f(d + 0.0);
+        const unsigned long long b = (unsigned long long)__double_as_longlong(d);
+        const unsigned int ex = (unsigned int)(b >> 52) & 0x7FFu;
+        // -0.0 codes as 0: bquery's sum starts at +0.0 and +0.0 + -0.0 == +0.0, so a sum never
+        // keeps the sign of a zero either way
+        const bool zero = (b << 1) == 0ull;
+        if (ex == 0x7FFu || (ex == 0u && !zero)) {
+          enc |= 1ull;
+        } else if (!zero) {
+          const unsigned long long m = (b & 0xFFFFFFFFFFFFFull) | 0x10000000000000ull;
+          lsb = min(lsb, (unsigned long long)((int)ex - 1075 + __builtin_ctzll(m) + 4096));
+        }
+        const double n = rint(d * 100.0);
+        if (n / 100.0 != d || fabs(n) > 2147483647.0) enc |= 2ull;
       } else if (u64) {
         k = (unsigned long long)chunk_i64(ch, c.dtype, r);
       } else {
@@ -361,12 +380,16 @@ __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsig
     mn = min(mn, (unsigned long long)__shfl_xor(mn, o, 64));
     mx = max(mx, (unsigned long long)__shfl_xor(mx, o, 64));
     nan |= (unsigned long long)__shfl_xor(nan, o, 64);
+    lsb = min(lsb, (unsigned long long)__shfl_xor(lsb, o, 64));
+    enc |= (unsigned long long)__shfl_xor(enc, o, 64);
   }
-  __shared__ unsigned long long smn[kBlock / 64], smx[kBlock / 64], snan[kBlock / 64];
+  __shared__ unsigned long long smn[kBlock / 64], smx[kBlock / 64], snan[kBlock / 64], slsb[kBlock / 64], senc[kBlock / 64];
   if ((threadIdx.x & 63) == 0) {
     smn[threadIdx.x >> 6] = mn;
     smx[threadIdx.x >> 6] = mx;
     snan[threadIdx.x >> 6] = nan;
+    slsb[threadIdx.x >> 6] = lsb;
+    senc[threadIdx.x >> 6] = enc;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -374,10 +397,16 @@ __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsig
       mn = min(mn, smn[q]);
       mx = max(mx, smx[q]);
       nan |= snan[q];
+      lsb = min(lsb, slsb[q]);
+      enc |= senc[q];
     }
     atomicMin(&out[0], mn);
     atomicMax(&out[1], mx);
     if (nan) atomicOr(&out[2], 1ull);
+    if (isf) {
+      atomicMin(&out[3], lsb);
+      if (enc) atomicOr(&out[4], enc);
+    }
   }
 }
 
@@ -612,7 +641,7 @@ __global__ __launch_bounds__(kBlock) void k_hash_partition(PartitionCols k, int6
   }
 }
 
-void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, hipStream_t st) {
+void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, hipStream_t st) {  // out4: 5 words
   int64_t blocks = (nrows + kTileRows - 1) / kTileRows;
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;

@@ -23,10 +23,10 @@
 
 namespace bqg {
 
-template <int NC, int K>
+template <int NC, int K, bool NARROW>
 __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartLaunch L) {
   extern __shared__ __align__(16) unsigned char smem[];
-  part_scatter_body<NC, K>(p, L, smem);
+  part_scatter_body<NC, K, NARROW>(p, L, smem);
 }
 
 // Aggregate over the tile layout.  Workgroup (partition, split): the split's tile range.  A
@@ -41,7 +41,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartL
 // aggregate -- it waited on each group's loads.  Workgroups are mapped XCD-aware: the
 // workgroups of one XCD (blockIdx % 8) take consecutive partitions over the same tile range,
 // so the edge lines their segments share are read once into that XCD's L2.
-template <int G, int U, int NSUM>
+template <int G, int U, int NSUM, bool NARROW>
 __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunch L, SlotArrays sa) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int P = L.nparts;
@@ -114,7 +114,12 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       en.rowb[u] = (uint32_t)g.gbase + j0 * TR;
       en.m[u] = L.meta[idx];
 #pragma unroll
-      for (int q = 0; q < NV; ++q) en.v[u][q] = L.vals[(size_t)q * L.capacity + idx];
+      for (int q = 0; q < NV; ++q) {
+        if (NARROW)  // the exact 32-bit code, sign-extended: summed in int64
+          en.v[u][q] = (unsigned long long)(long long)(int32_t)reinterpret_cast<const uint32_t*>(L.vals)[(size_t)q * L.capacity + idx];
+        else
+          en.v[u][q] = L.vals[(size_t)q * L.capacity + idx];
+      }
     }
   };
   auto consume = [&](const Grp& g, uint32_t e0, const Ent& en) {
@@ -128,7 +133,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       if (fst[sl] > row) atomicMin(&fst[sl], row);
 #pragma unroll
       for (int q = 0; q < nsum; ++q) {
-        if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][q], p.sum_conv[q]));
+        if (!NARROW && p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][q], p.sum_conv[q]));
         else atomicAdd(&acc[(size_t)q * W + sl], en.v[u][q]);
       }
     }
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       f = of < f ? of : f;
 #pragma unroll
       for (int q = 0; q < nsum; ++q) {
-        if (p.sum_is_float[q]) a[q] = as_u64(as_f64(a[q]) + as_f64(oa[q]));
+        if (!NARROW && p.sum_is_float[q]) a[q] = as_u64(as_f64(a[q]) + as_f64(oa[q]));
         else a[q] += oa[q];
       }
     }
@@ -236,7 +241,11 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     sa.cnt[gs] = c;
     sa.fst[gs] = f;
 #pragma unroll
-    for (int q = 0; q < nsum; ++q) sa.acc[(size_t)q * p.nslots + gs] = a[q];
+    for (int q = 0; q < nsum; ++q) {
+      // narrow: the exact sum of the codes, scaled back once (dyadic: exact below 2^53)
+      if (NARROW) a[q] = as_u64((double)(long long)a[q] / L.enc_mul[q]);
+      sa.acc[(size_t)q * p.nslots + gs] = a[q];
+    }
   }
 }
 
@@ -273,31 +282,45 @@ void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipSt
 #ifndef BQG_PART_MICRO  // tools/micro/part_micro.hip includes this file for the aggregate kernel
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,
                         hipFunction_t fscatter) {
-  const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum, L.k);
+  const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum, L.k, L.narrow != 0);
   if (fscatter) {
     PartLaunch Lc = L;
     ScanParams pc = p;
     void* args[] = {(void*)&pc, (void*)&Lc};
     (void)hipModuleLaunchKernel(fscatter, (unsigned)L.blocks, 1, 1, (unsigned)L.threads, 1, 1, (unsigned)scatter_lds,
                                 st, args, nullptr);
-  } else if (L.k == 2) {
-    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC, 2>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L));
   } else {
-    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC, 1>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L));
+#define BQG_SCATTER(K, NW) BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC, K, NW>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L))
+    if (L.k == 2) {
+      if (L.narrow) {
+        BQG_SCATTER(2, true);
+      } else {
+        BQG_SCATTER(2, false);
+      }
+    } else {
+      if (L.narrow) {
+        BQG_SCATTER(1, true);
+      } else {
+        BQG_SCATTER(1, false);
+      }
+    }
+#undef BQG_SCATTER
   }
   const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)p.nsum);
   const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
   // G tiles per wave group: ~8 x 4096 rows of segments whichever the tile size
-#define BQG_AGG(G, U, NS) hipLaunchKernelGGL((k_part_aggregate<G, U, NS>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
+#define BQG_AGG2(G, U, NS, NW) hipLaunchKernelGGL((k_part_aggregate<G, U, NS, NW>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
+#define BQG_AGG(G, U, NS) do { if (L.narrow) BQG_AGG2(G, U, NS, true); else BQG_AGG2(G, U, NS, false); } while (0)
   const bool big = L.tile_rows > 4096;
   switch (p.nsum) {
-    case 0: if (big) BQG_AGG(4, 4, 0); else BQG_AGG(8, 4, 0); break;
+    case 0: if (big) BQG_AGG2(4, 4, 0, false); else BQG_AGG2(8, 4, 0, false); break;
     case 1: if (big) BQG_AGG(4, 4, 1); else BQG_AGG(8, 4, 1); break;
     case 2: if (big) BQG_AGG(4, 4, 2); else BQG_AGG(8, 4, 2); break;
     case 3: if (big) BQG_AGG(4, 2, 3); else BQG_AGG(8, 2, 3); break;
     default: if (big) BQG_AGG(4, 2, 4); else BQG_AGG(8, 2, 4); break;
   }
 #undef BQG_AGG
+#undef BQG_AGG2
 }
 #endif
 

@@ -173,7 +173,14 @@ struct PartLaunch {
   uint64_t capacity;         // entries per array = ntiles * tile_rows
   uint16_t* hdr;             // [ntiles][nparts + 1]: partition offsets in each sorted tile
   uint32_t* meta;            // [capacity]: row-in-tile << wbits | slot_low
-  unsigned long long* vals;  // [nsum][capacity]: summed values (canonical 64-bit)
+  unsigned long long* vals;  // [nsum][capacity]: summed values (canonical 64-bit), or with
+                             // narrow: uint32_t [nsum][capacity] exact integer codes
+  // narrow entries: every summed column is a float column with an exact 32-bit code
+  // (ColStats::enc): code = v * enc_mul (dyadic: 2^k) or rint(v * enc_mul) (cents: 100); the
+  // aggregate sums codes in int64 and the total is sum * 2^-k (dyadic) or sum / 100 (cents)
+  int narrow;
+  int32_t enc_kind[kMaxSums];  // 1 dyadic, 2 cents
+  double enc_mul[kMaxSums];
   // aggregate combine (splits > 1): per-partition arrival counters (zeroed by
   // launch_partitioned) and [nparts][splits] partial tables of partial_bytes each
   unsigned int* arrive;
@@ -182,8 +189,8 @@ struct PartLaunch {
 };
 // LDS bytes of a scatter workgroup: the staged tile (values, meta), tile counts (two
 // buffers) / offsets and two sets of scan totals
-inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1) {
-  return (size_t)threads * 4 * k * (4 + 8 * (size_t)nsum) + (size_t)nparts * 12 + 2 * 16 * 4;
+inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1, bool narrow = false) {
+  return (size_t)threads * 4 * k * (4 + (narrow ? 4 : 8) * (size_t)nsum) + (size_t)nparts * 12 + 2 * 16 * 4;
 }
 // fscatter: the query-specialised (JIT) scatter kernel, or nullptr for the precompiled one
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,

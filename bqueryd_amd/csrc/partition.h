@@ -85,13 +85,20 @@ __device__ __forceinline__ void load_rows4_clamped(const ScanParams& p, int64_t 
 // staging words that no reader looks at), so the loop waits for the next tile's loads with
 // vmcnt(N) instead of draining.  The tile's header hdr[tile][0 .. P] holds the 16-bit offset of
 // each partition's run (hdr[tile][P] = passing rows).  An entry is a 32-bit meta word
-// (row-in-tile << wbits | slot_low) and one 64-bit value per summed column.
+// (row-in-tile << wbits | slot_low) and one 64-bit value per summed column -- or, NARROW, one
+// exact 32-bit integer code per summed column (PartLaunch::enc_kind: 8-byte entries for C3).
 //
 // Measured on MI355X (tools/micro/part_micro.hip, C3 shape): the region layout this replaces
 // (count pass, scan, per-(partition, block) regions) wrote each tile as ~P runs of ~32
 // entries into P far-apart regions and ran at 3.4 TB/s of moved bytes; the linear tile
 // writes run at copy speed (2.8 GB in 0.57 ms), with no count pass and no scan.
-template <int NC, int K = 1>
+// The exact 32-bit code of a summed float value (narrow entries, PartLaunch::enc_kind)
+__device__ __forceinline__ uint32_t part_enc(const ScanParams& p, const PartLaunch& L, int q, uint64_t v) {
+  const double d = value_f64(v, p.sum_conv[q]) * L.enc_mul[q];
+  return (uint32_t)(int32_t)(L.enc_kind[q] == 1 ? d : rint(d));
+}
+
+template <int NC, int K = 1, bool NARROW = false>
 __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const PartLaunch& L, unsigned char* smem) {
   // K 4-row chunks per thread and tile (TR = T * 4 * K rows): chunk k of thread t covers rows
   // base + k * T * 4 + t * 4 .. + 3, so every chunk load of the workgroup is one coalesced block
@@ -100,8 +107,9 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   const int TR = T * kRowsPerThread * K;
   const int nsum = p.nsum;
   constexpr int NS = NC < kMaxSums ? NC : kMaxSums;
-  unsigned long long* sval = reinterpret_cast<unsigned long long*>(smem);  // [nsum][TR]
-  uint32_t* smeta = reinterpret_cast<uint32_t*>(sval + (size_t)nsum * TR); // [TR]
+  unsigned long long* sval = reinterpret_cast<unsigned long long*>(smem);  // [nsum][TR] (wide)
+  uint32_t* sval32 = reinterpret_cast<uint32_t*>(smem);                    // [nsum][TR] (narrow)
+  uint32_t* smeta = reinterpret_cast<uint32_t*>(smem) + (size_t)nsum * TR * (NARROW ? 1 : 2);  // [TR]
   uint32_t* hist2 = smeta + TR;                                            // [2][P] tile counts
   uint32_t* toff = hist2 + 2 * P;                                          // [P] tile offsets
   uint32_t* wsum2 = toff + P;                                              // [2][16] scan totals
@@ -177,7 +185,10 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
         smeta[pos] = ((rit0 + r) << L.wbits) | low[k][r];
 #pragma unroll
         for (int s = 0; s < NS; ++s)
-          if (s < nsum) sval[(size_t)s * TR + pos] = sv[s][k][r];
+          if (s < nsum) {
+            if (NARROW) sval32[(size_t)s * TR + pos] = part_enc(p, L, s, sv[s][k][r]);
+            else sval[(size_t)s * TR + pos] = sv[s][k][r];
+          }
       }
     }
     lds_barrier();
@@ -188,11 +199,19 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (s >= nsum) break;
-      unsigned long long* dv = L.vals + (size_t)s * L.capacity + base;
-      const unsigned long long* lv = sval + (size_t)s * TR;
+      if (NARROW) {
+        uint32_t* dv = reinterpret_cast<uint32_t*>(L.vals) + (size_t)s * L.capacity + base;
+        const uint32_t* lv = sval32 + (size_t)s * TR;
 #pragma unroll
-      for (int k = 0; k < 2 * K; ++k)
-        *reinterpret_cast<uint4*>(dv + 2 * (tid + k * T)) = *reinterpret_cast<const uint4*>(lv + 2 * (tid + k * T));
+        for (int k = 0; k < K; ++k)
+          *reinterpret_cast<uint4*>(dv + 4 * (tid + k * T)) = *reinterpret_cast<const uint4*>(lv + 4 * (tid + k * T));
+      } else {
+        unsigned long long* dv = L.vals + (size_t)s * L.capacity + base;
+        const unsigned long long* lv = sval + (size_t)s * TR;
+#pragma unroll
+        for (int k = 0; k < 2 * K; ++k)
+          *reinterpret_cast<uint4*>(dv + 2 * (tid + k * T)) = *reinterpret_cast<const uint4*>(lv + 2 * (tid + k * T));
+      }
     }
     for (int i = q0; i < q1; ++i) hist[i] = 0;
   }

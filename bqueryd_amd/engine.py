@@ -54,7 +54,8 @@ class Device:
         t = L.Timing()
         self.check(self._lib.bqg_last_timing(self.handle, ctypes.byref(t)))
         return {'scan_ms': t.scan_ms, 'scan_launches': t.scan_launches, 'total_ms': t.total_ms,
-                'rows': t.rows, 'bytes': t.bytes, 'mode': t.mode, 'specialized': bool(t.specialized)}
+                'rows': t.rows, 'bytes': t.bytes, 'mode': t.mode, 'specialized': bool(t.specialized),
+                'narrow': bool(t.narrow)}
 
 
 _devices = {}

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BQG_ABI_VERSION 4
+#define BQG_ABI_VERSION 5
 
 /* error codes */
 #define BQG_OK 0
@@ -121,6 +121,8 @@ typedef struct {
   int32_t mode;          /* 0 private-LDS, 1 shared-LDS, 2 global dense, 3 global hash,
                             4 partitioned, 5 fused distinct pass (sorted_count_distinct) */
   int32_t specialized;   /* 1: the scan ran a query-specialised (run-time compiled) kernel */
+  int32_t narrow;        /* partitioned mode: 1 when the summed values travelled as exact 32-bit
+                            integer codes (ABI 5) */
 } bqg_timing;
 
 /* ---------------- lifecycle ---------------- */

@@ -404,3 +404,75 @@ def test_partitioned_launch_shapes(threads, splits, per_cu, oracle_c, monkeypatc
                        f=np.where(np.arange(n) // 5000 % 3 == 1, 0, rng.integers(1, 5, n)).astype(np.int16))
     run_both(cols, ['k'], [['v', 'sum', 's'], ['v', 'count', 'c']], [], oracle_c, exact=True)
     run_both(cols, ['k'], [['v', 'sum', 's'], ['v', 'mean', 'm']], [('f', '>', 0)], oracle_c, exact=True)
+
+
+def _groupby_info(cols, keys, aggs, env=None, monkeypatch=None):
+    if env:
+        for k_, v_ in env.items():
+            monkeypatch.setenv(k_, v_)
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(keys, aggs)
+        info = t.dev.last_timing()
+    finally:
+        t.close()
+        if env:
+            for k_ in env:
+                monkeypatch.delenv(k_)
+    return got, info
+
+
+@pytest.mark.parametrize('kind', ['dyadic', 'cents', 'f32_dyadic', 'two_sums', 'neg_zero', 'nan', 'huge', 'int_sum'])
+def test_partitioned_narrow_codes(kind, oracle_c, monkeypatch):
+    """Partitioned sums over float columns whose values all have an exact 32-bit integer code
+    (dyadic: v * 2^k; cents: rint(v * 100)) travel as 8-byte entries and are summed as
+    integers: dyadic sums bit-exact (and bit-identical to the 64-bit entry path), cents within
+    1e-12 of bquery's row-order sum; columns without such a code (NaN, out of int32 range,
+    integer sums) keep the 64-bit entries."""
+    rng = np.random.default_rng(11)
+    n = 300_000
+    cols = OrderedDict(k=rng.integers(0, 700_000, n).astype(np.int32))
+    aggs = [['v', 'sum', 'vs'], ['v', 'count', 'n']]
+    narrow = True
+    if kind == 'dyadic':
+        cols['v'] = np.round(rng.normal(size=n) * 4000) / 64
+    elif kind == 'cents':
+        cols['v'] = np.round(rng.lognormal(2.3, 0.6, n) * np.where(rng.random(n) < 0.2, -1, 1), 2)
+    elif kind == 'f32_dyadic':
+        cols['v'] = (np.round(rng.normal(size=n) * 256) / 16).astype(np.float32)
+    elif kind == 'two_sums':
+        cols['v'] = np.round(rng.normal(size=n) * 640) / 64
+        cols['w'] = np.round(rng.random(n) * 100, 2)
+        aggs.append(['w', 'sum', 'ws'])
+    elif kind == 'neg_zero':  # -0.0 codes as 0: bquery's sums start at +0.0 (+0.0 + -0.0 == +0.0)
+        v = np.round(rng.normal(size=n) * 64) / 64
+        v[::7] = -0.0
+        v[cols['k'] < 1000] = -0.0  # whole groups of -0.0
+        cols['v'] = v
+    elif kind == 'nan':
+        v = np.round(rng.normal(size=n) * 64) / 64
+        v[5] = np.nan
+        cols['v'] = v
+        narrow = False
+    elif kind == 'huge':
+        cols['v'] = np.round(rng.normal(size=n) * 1e9, 2)
+        narrow = False
+    else:  # int_sum: an integer summed column beside the float one
+        cols['v'] = np.round(rng.normal(size=n) * 64) / 64
+        cols['w'] = rng.integers(-9, 9, n).astype(np.int64)
+        aggs.append(['w', 'sum', 'ws'])
+        narrow = False
+    got, info = _groupby_info(cols, ['k'], aggs)
+    assert info['mode'] == 4 and info['narrow'] == narrow
+    ref = oracle_c.groupby(cols, ['k'], aggs, None)
+    exact = {'vs'} if kind in ('dyadic', 'f32_dyadic', 'neg_zero', 'nan', 'int_sum') else set()
+    if kind == 'int_sum':
+        exact.add('ws')
+    assert_tables_equal(got, ref, exact_cols=exact)
+    if narrow:
+        wide, winfo = _groupby_info(cols, ['k'], aggs, {'BQGPU_PART_NARROW': '0'}, monkeypatch)
+        assert not winfo['narrow']
+        if kind in ('dyadic', 'f32_dyadic', 'neg_zero'):
+            np.testing.assert_array_equal(got['vs'], wide['vs'])
+        else:
+            np.testing.assert_allclose(got['vs'], wide['vs'], rtol=1e-12, atol=0)
