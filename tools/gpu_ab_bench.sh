@@ -1,6 +1,8 @@
 # usage: bash tools/gpu_ab_bench.sh TAG CONFIG [bench args...] -- the same bench line from the
 # committed tree (abtest/, a git worktree built in-tree) and the working tree, alternated on
-# one box: A/B of a kernel change without box-to-box spread
+# one box: A/B of a kernel change without box-to-box spread.  Set up on the CPU side first:
+#   git worktree add abtest <baseline rev> && make -C abtest/bqueryd_amd/csrc
+# (abtest/ is git-ignored; remove it with `git worktree remove --force abtest` afterwards)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-ab}; shift

@@ -534,7 +534,7 @@ int main(int argc, char** argv) {
     }
     same(ref, fetch(b), what);
   };
-  agg_run(k_part_aggregate<8, 4, 1>, "agg G8 U4 (library)", 2);
+  agg_run(k_part_aggregate<8, 4, 1, false>, "agg G8 U4 (library)", 2);
 
   agg_run(k_agg_probe<8, 4, 1, 1>, "probe: loads only (no LDS atomics)", 2);
   agg_run(k_agg_probe<8, 4, 1, 2>, "probe: LDS atomics only (no entry loads)", 2);
