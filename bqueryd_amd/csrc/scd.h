@@ -195,7 +195,9 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         // lanes of this lane's slot: every lane ORs its bit into the slot's LDS mask word, then
         // reads the word back (a wave's LDS instructions execute in program order; OR does not
         // depend on the order of the lanes); the slot's first lane clears it below
-        if (act) atomicOr(&tbl[s], 1ull << lane);
+        // (32-bit ORs into the word's half of this lane's half-wave: the lanes of a hot slot
+        // -- same-address atomics, serialised -- split over two addresses)
+        if (act) atomicOr(reinterpret_cast<unsigned int*>(&tbl[s]) + (lane >> 5), 1u << (lane & 31));
         match = act ? tbl[s] : 0ull;
       }
       const uint64_t below = match & lanes_below;
