@@ -7,6 +7,8 @@ of bquery's per-shard groupby (oracle/cbquery.c).
   group order and counts bit-exact, sums 1e-12 (bit-exact on dyadic data).
 * C4: 200 M rows, random and (pu_location_id, passenger_count)-sorted row order;
   count_distinct and sorted_count_distinct bit-exact.
+* C5: one rank's 10 shards x 12.5 M rows in one pass + the RCCL merge (world 1) against the
+  reference client's merge of bquery's per-shard results.
 
 The oracle sums every group strictly in row order (bquery's ``out[g] += v``,
 bqueryd/worker.py:313 -> ctable.groupby); the GPU sums in a different order, so the float64
@@ -114,3 +116,44 @@ def test_float32_sum_realistic_groups(oracle_c):
     print('float32 row-order drift of the reference restatement: max %.2e' % drift.max())
     assert got['fs'].dtype == np.float32
     np.testing.assert_allclose(got['fs'], ref['fs'], rtol=max(1e-6, 2 * float(drift.max())), atol=0)
+
+
+@pytest.mark.parametrize('variant', ['raw', 'exact'])
+def test_c5_full_size(variant, oracle_c):
+    """C5 at one rank's full share: 10 shards x 12.5 M rows (the C5 generator's shards 0-9),
+    aggregated in one pass over their union (sum / count: ColocatedShards) and merged over a
+    one-rank RCCL communicator (bqg_merge) -- against bquery's per-shard results merged by the
+    reference client (rpc.py:164-173, aggregate=True): ~1 M groups in first-appearance order,
+    counts bit-exact, sums 1e-12 (bit-exact on dyadic data)."""
+    from collections import OrderedDict
+
+    from bqueryd_amd import dist as bdist
+    from oracle import bquery_oracle as bo
+    cfg = synth.CONFIGS['c5']
+    shard_rows = cfg['rows'] // cfg['shards']
+    shards = [synth.taxi_shard(shard_rows, config_id=5, n_shards=cfg['shards'], shard=i, variant=variant,
+                               columns=synth.query_columns(cfg)) for i in range(10)]
+    tables = [ShardTable(s) for s in shards]
+    colo = bdist.ColocatedShards(tables)
+    try:
+        per, reduced = colo.groupby_tables(cfg['groupby'], cfg['aggs'])
+        assert reduced
+        dtypes = OrderedDict((k, per[0].dtypes[k]) for k in per[0].names)
+        for p in per:
+            p.close()
+        comm = bdist.RcclComm(tables[0].dev)
+        try:
+            got = colo.groupby_merged(cfg['groupby'], cfg['aggs'], dtypes, comm)
+        finally:
+            comm.close()
+    finally:
+        colo.close()
+        for t in tables:
+            t.close()
+    ref = bo.client_merge([oracle_c.handle_work(s, cfg['groupby'], cfg['aggs'], cfg['where']) for s in shards],
+                          cfg['groupby'], cfg['aggs'], aggregate=True)
+    errs = {c: _rel_err(got[c], ref[c]) for c in _float_cols(cfg, got)}
+    print('C5 %s: %d groups, max relative error %s' % (variant, len(ref['n']), errs))
+    assert len(ref['n']) > 900_000
+    exact = {'fare_sum'} if variant == 'exact' else set()
+    assert_tables_equal(got, ref, rtol=1e-12, exact_cols=exact)
