@@ -982,13 +982,21 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.narrow = nsum > 0 && !(getenv("BQGPU_PART_NARROW") && atoi(getenv("BQGPU_PART_NARROW")) == 0);
       for (int q = 0; q < nsum && L.narrow; ++q) {
         compute_stats(t, pl.tcol[q]);
-        const ColStats& cs = t->cols[pl.tcol[q]].stats;
-        if (!pl.p.sum_is_float[q] || pl.p.sum_centered[q] || cs.enc == 0) {
+        const Column& col = t->cols[pl.tcol[q]];
+        const ColStats& cs = col.stats;
+        if (pl.p.sum_centered[q]) {
           L.narrow = 0;
-          break;
+        } else if (pl.p.sum_is_float[q]) {
+          L.narrow = cs.enc != 0;
+          L.enc_kind[q] = cs.enc;
+          L.enc_mul[q] = cs.enc == 1 ? std::ldexp(1.0, cs.enc_k) : 100.0;
+        } else {
+          // integers (not uint64) whose values span fewer than 2^32: code = v - min
+          L.narrow = col.dtype != BQG_U64 && pl.p.sum_conv[q] == 1 &&
+                     (cs.empty || (uint64_t)cs.imax - (uint64_t)cs.imin <= 0xFFFFFFFFull);
+          L.enc_kind[q] = 3;
+          L.enc_off[q] = cs.empty ? 0 : cs.imin;
         }
-        L.enc_kind[q] = cs.enc;
-        L.enc_mul[q] = cs.enc == 1 ? std::ldexp(1.0, cs.enc_k) : 100.0;
       }
       const bool nw = L.narrow != 0;
       c->last.narrow = L.narrow;

@@ -115,8 +115,10 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       en.m[u] = L.meta[idx];
 #pragma unroll
       for (int q = 0; q < NV; ++q) {
-        if (NARROW)  // the exact 32-bit code, sign-extended: summed in int64
-          en.v[u][q] = (unsigned long long)(long long)(int32_t)reinterpret_cast<const uint32_t*>(L.vals)[(size_t)q * L.capacity + idx];
+        if (NARROW) {  // the exact 32-bit code: float codes signed, integer offsets unsigned
+          const uint32_t code = reinterpret_cast<const uint32_t*>(L.vals)[(size_t)q * L.capacity + idx];
+          en.v[u][q] = L.enc_kind[q] == 3 ? (unsigned long long)code : (unsigned long long)(long long)(int32_t)code;
+        }
         else
           en.v[u][q] = L.vals[(size_t)q * L.capacity + idx];
       }
@@ -242,8 +244,12 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     sa.fst[gs] = f;
 #pragma unroll
     for (int q = 0; q < nsum; ++q) {
-      // narrow: the exact sum of the codes, scaled back once (dyadic: exact below 2^53)
-      if (NARROW) a[q] = as_u64((double)(long long)a[q] / L.enc_mul[q]);
+      // narrow: the exact sum of the codes, scaled back once (dyadic: exact below 2^53), or
+      // shifted back by count x offset (integers, modulo 2^64 like the 64-bit accumulator)
+      if (NARROW) {
+        if (L.enc_kind[q] == 3) a[q] += (unsigned long long)c * (unsigned long long)L.enc_off[q];
+        else a[q] = as_u64((double)(long long)a[q] / L.enc_mul[q]);
+      }
       sa.acc[(size_t)q * p.nslots + gs] = a[q];
     }
   }

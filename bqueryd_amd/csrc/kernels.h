@@ -175,12 +175,14 @@ struct PartLaunch {
   uint32_t* meta;            // [capacity]: row-in-tile << wbits | slot_low
   unsigned long long* vals;  // [nsum][capacity]: summed values (canonical 64-bit), or with
                              // narrow: uint32_t [nsum][capacity] exact integer codes
-  // narrow entries: every summed column is a float column with an exact 32-bit code
-  // (ColStats::enc): code = v * enc_mul (dyadic: 2^k) or rint(v * enc_mul) (cents: 100); the
-  // aggregate sums codes in int64 and the total is sum * 2^-k (dyadic) or sum / 100 (cents)
+  // narrow entries: every summed column has an exact 32-bit code -- floats (ColStats::enc):
+  // code = v * enc_mul (dyadic: 2^k) or rint(v * enc_mul) (cents: 100), summed in int64, total
+  // = sum * 2^-k or sum / 100; integers with max - min < 2^32: code = v - enc_off (unsigned),
+  // summed in uint64, total = sum + count * enc_off (mod 2^64, as the 64-bit path)
   int narrow;
-  int32_t enc_kind[kMaxSums];  // 1 dyadic, 2 cents
+  int32_t enc_kind[kMaxSums];  // 1 dyadic, 2 cents, 3 integer offset
   double enc_mul[kMaxSums];
+  int64_t enc_off[kMaxSums];
   // aggregate combine (splits > 1): per-partition arrival counters (zeroed by
   // launch_partitioned) and [nparts][splits] partial tables of partial_bytes each
   unsigned int* arrive;

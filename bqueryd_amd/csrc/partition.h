@@ -94,6 +94,7 @@ __device__ __forceinline__ void load_rows4_clamped(const ScanParams& p, int64_t 
 // writes run at copy speed (2.8 GB in 0.57 ms), with no count pass and no scan.
 // The exact 32-bit code of a summed float value (narrow entries, PartLaunch::enc_kind)
 __device__ __forceinline__ uint32_t part_enc(const ScanParams& p, const PartLaunch& L, int q, uint64_t v) {
+  if (L.enc_kind[q] == 3) return (uint32_t)(v - (uint64_t)L.enc_off[q]);  // canonical int64 value
   const double d = value_f64(v, p.sum_conv[q]) * L.enc_mul[q];
   return (uint32_t)(int32_t)(L.enc_kind[q] == 1 ? d : rint(d));
 }

@@ -422,13 +422,16 @@ def _groupby_info(cols, keys, aggs, env=None, monkeypatch=None):
     return got, info
 
 
-@pytest.mark.parametrize('kind', ['dyadic', 'cents', 'f32_dyadic', 'two_sums', 'neg_zero', 'nan', 'huge', 'int_sum'])
+@pytest.mark.parametrize('kind', ['dyadic', 'cents', 'f32_dyadic', 'two_sums', 'neg_zero', 'nan', 'huge', 'int_sum',
+                                  'int8_only', 'uint32_full', 'int64_wide', 'uint64'])
 def test_partitioned_narrow_codes(kind, oracle_c, monkeypatch):
     """Partitioned sums over float columns whose values all have an exact 32-bit integer code
     (dyadic: v * 2^k; cents: rint(v * 100)) travel as 8-byte entries and are summed as
     integers: dyadic sums bit-exact (and bit-identical to the 64-bit entry path), cents within
-    1e-12 of bquery's row-order sum; columns without such a code (NaN, out of int32 range,
-    integer sums) keep the 64-bit entries."""
+    1e-12 of bquery's row-order sum; integer columns spanning fewer than 2^32 values travel
+    as v - min (sums bit-exact, wrapping like the 64-bit path); columns without such a code
+    (NaN, floats out of int32 range, integers spanning 2^32 or more, uint64) keep the 64-bit
+    entries."""
     rng = np.random.default_rng(11)
     n = 300_000
     cols = OrderedDict(k=rng.integers(0, 700_000, n).astype(np.int32))
@@ -457,22 +460,32 @@ def test_partitioned_narrow_codes(kind, oracle_c, monkeypatch):
     elif kind == 'huge':
         cols['v'] = np.round(rng.normal(size=n) * 1e9, 2)
         narrow = False
-    else:  # int_sum: an integer summed column beside the float one
+    elif kind == 'int_sum':  # an integer summed column beside the float one
         cols['v'] = np.round(rng.normal(size=n) * 64) / 64
-        cols['w'] = rng.integers(-9, 9, n).astype(np.int64)
+        cols['w'] = rng.integers(-9, 9, n).astype(np.int64) + (1 << 40)
         aggs.append(['w', 'sum', 'ws'])
+    elif kind == 'int8_only':
+        cols['v'] = rng.integers(-128, 128, n).astype(np.int8)
+    elif kind == 'uint32_full':  # the whole uint32 range: codes up to 2^32 - 1
+        cols['v'] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+        cols['v'][:2] = [0, 0xFFFFFFFF]
+    elif kind == 'int64_wide':  # spans more than 2^32 values
+        cols['v'] = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)
+        narrow = False
+    else:  # uint64
+        cols['v'] = rng.integers(0, 1 << 40, n, dtype=np.uint64)
         narrow = False
     got, info = _groupby_info(cols, ['k'], aggs)
     assert info['mode'] == 4 and info['narrow'] == narrow
     ref = oracle_c.groupby(cols, ['k'], aggs, None)
-    exact = {'vs'} if kind in ('dyadic', 'f32_dyadic', 'neg_zero', 'nan', 'int_sum') else set()
+    exact = {'vs'} if kind not in ('cents', 'two_sums', 'huge') else set()
     if kind == 'int_sum':
         exact.add('ws')
     assert_tables_equal(got, ref, exact_cols=exact)
     if narrow:
         wide, winfo = _groupby_info(cols, ['k'], aggs, {'BQGPU_PART_NARROW': '0'}, monkeypatch)
         assert not winfo['narrow']
-        if kind in ('dyadic', 'f32_dyadic', 'neg_zero'):
+        if kind in ('dyadic', 'f32_dyadic', 'neg_zero', 'int_sum', 'int8_only', 'uint32_full'):
             np.testing.assert_array_equal(got['vs'], wide['vs'])
         else:
             np.testing.assert_allclose(got['vs'], wide['vs'], rtol=1e-12, atol=0)
