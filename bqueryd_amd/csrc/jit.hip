@@ -152,13 +152,6 @@ bool jit_disabled() {
 
 std::string jit_spec(const ScanParams& p) {
   std::ostringstream s;
-  // experiment hook: BQGPU_JIT_DEFS=NAME or NAME=VALUE adds `#define NAME 1` / `#define NAME
-  // VALUE` to every specialised kernel (part of the cache key)
-  if (const char* e = getenv("BQGPU_JIT_DEFS")) {
-    std::string d(e);
-    const size_t eq = d.find('=');
-    s << "#define " << (eq == std::string::npos ? d + " 1" : d.substr(0, eq) + " " + d.substr(eq + 1)) << "\n";
-  }
   s << "#define BQ_NC " << p.ncols << "\n#define BQ_SPEC ";
   s << "p.ncols=" << p.ncols << ";";
   for (int c = 0; c < p.ncols; ++c)
