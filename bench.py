@@ -333,6 +333,8 @@ def main(argv=None):
             'rows_per_gpu': rows,
             'parallelism': 'shard-per-rank x%d' % ws,
             'engine_mode': MODES[mode or 0],
+            # partitioned mode: summed values carried as exact 32-bit integer codes
+            **({'narrow_entries': bool(timings[-1].get('narrow'))} if timings and mode == 4 else {}),
             **cfg_extra,
         },
         'roofline': {
