@@ -1243,9 +1243,12 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
           if (vr != 0 && vr <= 0xFFFFFFFFull) {
             d.compact = 1;
             d.vmin = col.stats.empty ? 0 : col.stats.imin;
+            // value codes below 2^16 (compact chunks are below 2^16 rows): first value and
+            // first row share one LDS word
+            d.pack16 = vr <= 0x10000ull && !getenv("BQGPU_SCD_NO_PACK16") ? 1 : 0;
           }
         }
-        d.wave_lds = scd_fused_wave_lds(S, d.compact != 0);
+        d.wave_lds = scd_fused_wave_lds(S, d.compact != 0, d.pack16 != 0);
         d.cd = fused_cd;
         const size_t blk_lds = (kBlock / 64) * d.wave_lds + (size_t)fused_cd.lds_bitmap_words * 4;
         if (blk_lds > kScdFusedMaxLds) d.cd.lds_bitmap_words = 0;  // no LDS pre-filter
@@ -1262,6 +1265,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         const uint64_t need = ((uint64_t)N + kScdCompactMaxRows - 1) / kScdCompactMaxRows;
         if (need * S * 28 > budget) {
           d.compact = 0;  // that many chunk states do not fit: the wide pass (32-bit counts)
+          d.pack16 = 0;
           d.wave_lds = scd_fused_wave_lds(S, false);
         } else if (waves < need) {
           waves = need;
@@ -1296,7 +1300,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         const int vc = d.vcol >= 0 && d.vcol < nc ? d.vcol : 0;
         const int cc = d.cd.vcol >= 0 && d.cd.vcol < nc ? d.cd.vcol : 0;
         std::string spec = jit_spec(pc.p) + "#define BQ_SCD_CD " + std::to_string(cd_mode) + "\n#define BQ_SCD_VC " +
-                           std::to_string(vc) + "\n#define BQ_SCD_CC " + std::to_string(cc) + "\n";
+                           std::to_string(vc) + "\n#define BQ_SCD_CC " + std::to_string(cc) + "\n#define BQ_SCD_P16 " +
+                           std::to_string(d.pack16) + "\n";
         sfn = jit_function(d.compact ? "bq_jit_scd_fused32" : "bq_jit_scd_fused", spec);
         c->last.specialized = sfn ? 1 : 0;
       }

@@ -101,14 +101,15 @@ struct ScdLaunch {
   uint32_t* slot_fst;                // fused + write_slots: SlotArrays::fst to fill
   DistinctLaunch cd;                 // fused: cd.bitmap != nullptr -> count_distinct too
   int compact;                       // fused: 32-bit value codes (integer values, range < 2^32)
+  int pack16;                        // compact: value codes < 2^16, first value + first row in one word
   int64_t vmin;                      // compact: value code = v - vmin
 };
 // LDS bytes per wave of k_scd_fused for a slot space of nslots: a 32-byte state per slot (20
 // bytes with compact 32-bit value codes) plus an 8-byte lane mask per slot
-inline size_t scd_fused_wave_lds(uint64_t nslots, bool compact = false) {
-  // compact: 8-byte states + first values + first rows; wide: 32-byte states; then the
-  // 8-byte lane masks
-  const size_t state = compact ? (((size_t)nslots * 16 + 7) & ~size_t(7)) : (size_t)nslots * 32;
+inline size_t scd_fused_wave_lds(uint64_t nslots, bool compact = false, bool pack16 = false) {
+  // compact: 8-byte states + first values + first rows (pack16: one word for both); wide:
+  // 32-byte states; then the 8-byte lane masks
+  const size_t state = compact ? (((size_t)nslots * (pack16 ? 12 : 16) + 7) & ~size_t(7)) : (size_t)nslots * 32;
   return (state + (size_t)nslots * 8 + 15) & ~size_t(15);
 }
 constexpr int64_t kScdCompactMaxRows = 65280;  // rows per wave chunk of the compact pass (16-bit counts)

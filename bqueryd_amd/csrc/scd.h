@@ -89,18 +89,26 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
   unsigned char* wbase = smem + (size_t)wave * d.wave_lds;
   ScdSlot* st = reinterpret_cast<ScdSlot*>(wbase);          // wide state [S]
   ScdSlot32* st32 = reinterpret_cast<ScdSlot32*>(wbase);    // compact state [S] ...
+#ifdef BQ_SCD_P16
+  constexpr bool p16 = BQ_SCD_P16 != 0;
+#else
+  const bool p16 = d.pack16 != 0;
+#endif
+  // first value code and first row of each slot in the chunk: two words, or with p16 (value
+  // codes and chunk-relative rows below 2^16) one word {code | rel << 16} -- a smaller wave
+  // footprint, so more waves fit in LDS
   uint32_t* fv32 = reinterpret_cast<uint32_t*>(st32 + S);   // ... + first value codes [S]
-  uint32_t* fr32 = fv32 + S;                                // ... + first rows [S]
+  uint32_t* fr32 = fv32 + S;                                // ... + first rows [S] (not with p16)
   // per-slot lane masks of the current step (after the wide or compact state, 8-aligned)
   unsigned long long* tbl = reinterpret_cast<unsigned long long*>(
-      wbase + (COMPACT ? (((size_t)S * 16 + 7) & ~size_t(7)) : (size_t)S * 32));
+      wbase + (COMPACT ? (((size_t)S * (p16 ? 12 : 16) + 7) & ~size_t(7)) : (size_t)S * 32));
   unsigned int* cdb = reinterpret_cast<unsigned int*>(smem + (size_t)(blockDim.x >> 6) * d.wave_lds);
   for (int i = lane; i < S; i += 64) {
     tbl[i] = 0ull;
     if (COMPACT) {
       st32[i] = ScdSlot32{0u, 0u};
       fv32[i] = 0u;
-      fr32[i] = kNoRow;
+      if (!p16) fr32[i] = kNoRow;
     } else {
       st[i] = ScdSlot{0ull, 0ull, 0u, 0u, kNoRow, 0u};
     }
@@ -234,8 +242,12 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
           const uint32_t rows = cur.rc & 0xFFFFu;
           uint32_t ch = (cur.rc >> 16) + add_ch;
           if (rows == 0) {
-            fv32[s] = (uint32_t)vb;
-            fr32[s] = (uint32_t)row;
+            if (p16) {
+              fv32[s] = ((uint32_t)vb & 0xFFFFu) | (rel << 16);
+            } else {
+              fv32[s] = (uint32_t)vb;
+              fr32[s] = (uint32_t)row;
+            }
             run_start = true;
           } else if (cur.last != (uint32_t)vb) {
             ch += 1u;
@@ -309,8 +321,13 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
     if (COMPACT) {
       const ScdSlot32 c = st32[i];
       const uint32_t rows = c.rc & 0xFFFFu;
-      d.st_first_row[o] = rows ? fr32[i] : kNoRow;
-      d.st_first[o] = (uint64_t)d.vmin + fv32[i];
+      if (p16) {
+        d.st_first_row[o] = rows ? (uint32_t)start + (fv32[i] >> 16) : kNoRow;
+        d.st_first[o] = (uint64_t)d.vmin + (fv32[i] & 0xFFFFu);
+      } else {
+        d.st_first_row[o] = rows ? fr32[i] : kNoRow;
+        d.st_first[o] = (uint64_t)d.vmin + fv32[i];
+      }
       d.st_last[o] = (uint64_t)d.vmin + c.last;
       d.st_changes[o] = c.rc >> 16;
       d.st_count[o] = rows;

@@ -489,3 +489,21 @@ def test_partitioned_narrow_codes(kind, oracle_c, monkeypatch):
             np.testing.assert_array_equal(got['vs'], wide['vs'])
         else:
             np.testing.assert_allclose(got['vs'], wide['vs'], rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize('vrange,no_pack', [(7, False), (7, True), (65_536, False), (200_000, False)])
+def test_fused_distinct_value_widths(vrange, no_pack, oracle_c, monkeypatch):
+    """The fused distinct pass with 32-bit value codes: first value and first row share one
+    LDS word when the codes fit 16 bits (value range <= 2^16), two words otherwise (or with
+    BQGPU_SCD_NO_PACK16); every width against the oracle, at a size that runs the
+    specialised kernel over several chunks."""
+    monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
+    if no_pack:
+        monkeypatch.setenv('BQGPU_SCD_NO_PACK16', '1')
+    rng = np.random.default_rng(vrange)
+    n = 600_000
+    v = rng.integers(-3, vrange - 3, n).astype(np.int32)
+    v[:2] = [-3, vrange - 4]  # the full range
+    cols = OrderedDict(k=rng.integers(0, 200, n).astype(np.int16),
+                       v=np.repeat(v[: n // 3], 3)[:n].astype(np.int32))
+    run_both(cols, ['k'], [['v', 'count', 'n'], ['v', 'sorted_count_distinct', 'vscd']], [], oracle_c)
