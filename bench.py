@@ -116,13 +116,15 @@ def _cpu_baseline(cols, cfg, reps=2):
 def _cpu_cluster_baseline(cfg, args, rows, single):
     """The reference's deployment shape on this host's cores (oracle/cpu_cluster.py): one
     controller + N single-threaded workers running the C port of bquery's per-shard groupby
-    over 8 shards of the workload, client sum-merge (rpc.py:164-173); N = 2 and N = all
-    cores.  ``value`` is the all-cores cluster."""
+    over the workload split into max(8, 2 x cores) shards (every worker gets messages, as in
+    the reference's deployment: one message per shard file to any free worker,
+    misc/supervisor.conf:21, controller.py:113-144), client sum-merge (rpc.py:164-173);
+    N = 2 and N = all cores.  ``value`` is the all-cores cluster."""
     import shutil
     import tempfile
     from oracle import cpu_cluster
     cores = cpu_cluster.host_cores()
-    n_shards = 8
+    n_shards = max(8, 2 * cores)
     per = max(1, rows // n_shards)
     counts = sorted(set([2, cores]))
     tmp = tempfile.mkdtemp(prefix='bqgpu-cpu-cluster-')
@@ -140,6 +142,7 @@ def _cpu_cluster_baseline(cfg, args, rows, single):
                        'sum-merge (rpc.py:164-173); best of 2: %.3f s' % (args.config.upper(), n_shards, per, cores,
                                                                            secs)),
             'cpu_model': cpu_cluster.cpu_model(),
+            'n_shards': n_shards,
             'decoded_columns': {'value': res[cores]['decoded'][0], 'unit': 'rows/s', 'cores': cores,
                                 'seconds': res[cores]['decoded'][1],
                                 'sample': 'the same, columns handed over decoded (shared memory): compute only'},
@@ -154,16 +157,21 @@ def synth_config_id(config):
 
 
 def _load_traffic(config, rows):
-    """HBM bytes per scan launch from the committed rocprofv3 PMC summaries, if present."""
+    """(HBM bytes per scan launch, source) from the committed rocprofv3 PMC summary of this
+    config (profiles/pmc_<cfg>.json: separate FETCH_SIZE / WRITE_SIZE passes), if present and
+    taken at this row count.  It is NOT measured by this run: counter passes need their own
+    profiler runs (MI355X_MICROARCH.md), so the line names the file it quotes."""
     path = os.path.join(HERE, 'profiles', 'pmc_%s.json' % config)
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get('rows') == rows:
-            return d.get('hbm_bytes_per_launch')
+            src = 'profiles/pmc_%s.json (committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes%s; not this run)' % (
+                config, ', ' + d['taken'] if d.get('taken') else '')
+            return d.get('hbm_bytes_per_launch'), src
     except (OSError, ValueError):
         pass
-    return None
+    return None, None
 
 
 def main(argv=None):
@@ -296,7 +304,7 @@ def main(argv=None):
                   'sample': 'one %d-row %s shard, one worker (best of 2: %.2f s)' % (rows, args.config.upper(), secs)}
         del cols
         cpu = _cpu_cluster_baseline(cfg, args, rows, single)
-    traffic = _load_traffic(args.config, rows)
+    traffic, traffic_source = _load_traffic(args.config, rows)
     comm.close()
     if rank != 0:
         return
@@ -344,6 +352,7 @@ def main(argv=None):
             'unit': 'GB/s',
             'frac': achieved / HBM_PEAK_GBS,
             'traffic': traffic,
+            'traffic_source': traffic_source,
             'kernel': KERNELS[mode or 0],
             'kernel_avg_ms': scan_avg,
             'algorithmic_bytes_per_launch': bytes_per_launch,

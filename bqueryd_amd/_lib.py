@@ -29,6 +29,10 @@ T_FALSE, T_TRUE, T_EQ, T_NE, T_IN, T_NIN, T_GT, T_GE, T_LT, T_LE = -1, 0, 1, 2, 
 
 E_INVALID, E_UNSUPPORTED, E_HIP, E_OOM, E_STATE = -1, -2, -3, -4, -5
 UNIQUE_ID_BYTES = 128
+ABI_VERSION = 6
+OPTIONS = ('jit', 'jit_min_rows', 'partition', 'part_wbits', 'part_k', 'part_threads', 'part_per_cu',
+           'part_splits', 'part_narrow', 'fused_scd', 'scd_compact', 'scd_pack16', 'priv_ahead',
+           'private_per_cu', 'small_emit', 'hash_slots', 'distinct_slots')
 
 
 class Term(ctypes.Structure):
@@ -57,7 +61,7 @@ class Timing(ctypes.Structure):
     _fields_ = [('scan_ms', ctypes.c_double), ('scan_launches', ctypes.c_int32),
                 ('total_ms', ctypes.c_double), ('rows', ctypes.c_int64),
                 ('bytes', ctypes.c_int64), ('mode', ctypes.c_int32), ('specialized', ctypes.c_int32),
-                ('narrow', ctypes.c_int32)]
+                ('narrow', ctypes.c_int32), ('regrows', ctypes.c_int32)]
 
 
 # enum bqg_decode
@@ -91,6 +95,9 @@ _PROTOS = {
     'bqg_synchronize': ([_P], ctypes.c_int),
     'bqg_enable_timing': ([_P, ctypes.c_int], ctypes.c_int),
     'bqg_last_timing': ([_P, ctypes.POINTER(Timing)], ctypes.c_int),
+    'bqg_set_option': ([_P, ctypes.c_char_p, _I64], ctypes.c_int),
+    'bqg_get_option': ([_P, ctypes.c_char_p, ctypes.POINTER(_I64)], ctypes.c_int),
+    'bqg_reset_options': ([_P], ctypes.c_int),
     'bqg_alloc_pinned': ([_P, ctypes.c_size_t, ctypes.POINTER(_P)], ctypes.c_int),
     'bqg_free_pinned': ([_P, _P], ctypes.c_int),
     'bqg_table_create': ([_P, _I64, _I32, _P, ctypes.POINTER(_P)], ctypes.c_int),
@@ -146,6 +153,9 @@ def lib():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = res
+        if L.bqg_abi_version() != ABI_VERSION:
+            raise OSError('%s has ABI %d, this binding expects %d (rebuild it)' % (LIB_PATH, L.bqg_abi_version(),
+                                                                                   ABI_VERSION))
         _lib = L
     return _lib
 

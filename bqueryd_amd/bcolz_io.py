@@ -270,6 +270,9 @@ def ctable_files(columns, chunklen=None, cname='lz4'):
 def write_ctable(rootdir, columns, chunklen=None, cname='lz4'):
     """Write an OrderedDict of equal-length arrays as a bcolz ctable rootdir."""
     os.makedirs(rootdir, exist_ok=True)
+    for n in columns:  # bcolz creates both even for a zero-row column (no chunk file)
+        os.makedirs(os.path.join(rootdir, n, 'data'), exist_ok=True)
+        os.makedirs(os.path.join(rootdir, n, 'meta'), exist_ok=True)
     _write_files(rootdir, ctable_files(columns, chunklen, cname))
     return rootdir
 
@@ -283,25 +286,38 @@ def ctable_tar(columns, arcname, chunklen=None, cname='lz4'):
     import time
     files = ctable_files(columns, chunklen, cname)
     now = int(time.time())
-    dirs = set([''])
-    for rel, _ in files:
-        parts = rel.split('/')[:-1]
-        for i in range(len(parts)):
-            dirs.add('/'.join(parts[:i + 1]))
+    # the directory tree write_ctable creates: every column has data/ and meta/ even when a
+    # zero-row column has no chunk file (the client appends to the first result it opens,
+    # rpc.py:158-162, and bcolz then writes chunks into data/)
+    tree = {}
+    for n in columns:
+        tree.setdefault(n, {}).setdefault('data', {})
+        tree[n].setdefault('meta', {})
+    for rel, data in files:
+        parts = rel.split('/')
+        node = tree
+        for p in parts[:-1]:
+            node = node.setdefault(p, {})
+        node[parts[-1]] = data
     buf = io.BytesIO()
     with tarfile.open(fileobj=buf, mode='w') as tf:
-        for d in sorted(dirs):
-            info = tarfile.TarInfo(arcname + ('/' + d if d else ''))
-            info.type = tarfile.DIRTYPE
-            info.mode = 0o755
-            info.mtime = now
-            tf.addfile(info)
-        for rel, data in files:
-            info = tarfile.TarInfo(arcname + '/' + rel)
-            info.size = len(data)
-            info.mode = 0o644
-            info.mtime = now
-            tf.addfile(info, io.BytesIO(data))
+        # tarfile.add's order: the directory, then its entries sorted by name, depth first
+        def add(name, node):
+            if isinstance(node, dict):
+                info = tarfile.TarInfo(name)
+                info.type = tarfile.DIRTYPE
+                info.mode = 0o755
+                info.mtime = now
+                tf.addfile(info)
+                for k in sorted(node):
+                    add(name + '/' + k, node[k])
+            else:
+                info = tarfile.TarInfo(name)
+                info.size = len(node)
+                info.mode = 0o644
+                info.mtime = now
+                tf.addfile(info, io.BytesIO(node))
+        add(arcname, tree)
     return buf.getvalue()
 
 

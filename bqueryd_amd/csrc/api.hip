@@ -41,6 +41,12 @@ struct ApiError {
   int code;
   std::string msg;
 };
+// A hash table (group keys) or count_distinct set of `slots` slots filled past half during a
+// query: the query is re-run with twice the slots (run_groupby_grow).
+struct TableOverflow {
+  bool distinct;
+  uint64_t slots;
+};
 
 #define HIPCHECK(x)                                 \
   do {                                              \
@@ -292,8 +298,59 @@ struct ColumnPool {
   }
 };
 
+// Engine options: launch shapes and path choices the planner otherwise makes by itself.  Set
+// per context with bqg_set_option (tests, profiling), or once at context creation from the
+// environment (BQGPU_OPTIONS="name=value,..."; BQGPU_JIT / BQGPU_JIT_MIN_ROWS as before).
+// Nothing on the query path reads the environment.  The list is documented in bqgpu.h and
+// every non-default value is exercised against the oracle by tests/test_gpu_parity.py.
+enum Opt {
+  kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
+  kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kNumOpts
+};
+struct OptDef {
+  const char* name;
+  int64_t def, lo, hi;
+};
+constexpr OptDef kOptDefs[kNumOpts] = {
+    {"jit", 1, 0, 1},                       // run-time specialised (hiprtc) scans
+    {"jit_min_rows", 4ll << 20, 0, INT64_MAX},  // ... for tables of at least this many rows
+    {"partition", 1, 0, 1},                 // partitioned aggregation for large dense slot spaces
+    {"part_wbits", 0, 0, 13},               // slots per partition 2^wbits (0: auto, else 6..13)
+    {"part_k", 0, 0, 2},                    // 4-row chunks per scatter thread (0: auto)
+    {"part_threads", 0, 0, 1024},           // scatter workgroup size (0: auto; 256, 512, 1024)
+    {"part_per_cu", 0, 0, 8},               // scatter workgroups per CU (0: auto)
+    {"part_splits", 0, 0, 1 << 20},         // aggregate workgroups per partition (0: auto)
+    {"part_narrow", 1, 0, 1},               // exact 32-bit value codes in partition entries
+    {"fused_scd", 1, 0, 1},                 // one fused pass for count / distinct queries
+    {"scd_compact", 1, 0, 1},               // ... with 32-bit value codes when they fit
+    {"scd_pack16", 1, 0, 1},                // ... first value and row in one LDS word
+    {"priv_ahead", 0, 0, 4},                // private scan: tiles in flight (0: kernel default)
+    {"private_per_cu", 0, 0, 8},            // private scan: workgroups per CU cap (0: auto)
+    {"small_emit", 1, 0, 1},                // one-workgroup emit for <= 8192 slots
+    {"hash_slots", 0, 0, 1ll << 31},        // initial hash-table slots (0: from the row count)
+    {"distinct_slots", 0, 0, 1ll << 31},    // initial count_distinct set slots (0: from rows)
+};
+
+static int opt_index(const char* name) {
+  for (int i = 0; i < kNumOpts; ++i)
+    if (name && strcmp(name, kOptDefs[i].name) == 0) return i;
+  return -1;
+}
+
+static bool opt_valid(int i, int64_t v) {
+  if (v < kOptDefs[i].lo || v > kOptDefs[i].hi) return false;
+  if (i == kOptPartWbits) return v == 0 || v >= 6;
+  if (i == kOptPartThreads) return v == 0 || v == 256 || v == 512 || v == 1024;
+  return true;
+}
+
 struct bqg_ctx {
   int device = 0;
+  int64_t opt[kNumOpts];
+  // hash / count_distinct tables grown after an overflow (the query is re-run with them)
+  uint64_t hash_grow = 0, distinct_grow = 0;
+  int32_t last_regrows = 0;  // re-runs of the last query after a table overflow
   ColumnPool colpool;
   IngestPool ingest;  // cold-path staging: streams + pinned double buffers per decode thread
   int cu = 256;
@@ -596,7 +653,10 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     }
     uint64_t est = std::min<uint64_t>((uint64_t)std::max<int64_t>(t->nrows, 1), 1ull << 26);
     uint64_t cap = 1024;
+    if (c->opt[kOptHashSlots]) est = (uint64_t)c->opt[kOptHashSlots] / 2;
     while (cap < 2 * est) cap <<= 1;
+    // a table that overflowed on this query grows (run_groupby_grow re-runs the query)
+    if (c->hash_grow > cap) cap = c->hash_grow;
     pl.nslots = cap;
     pl.mode = kGlobalHash;
     pl.p.hash = wide ? 2 : 1;
@@ -625,16 +685,16 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
       // kPartMaxParts partitions
       const size_t per_slot = 8 + 8 * (size_t)pl.nsum;
       int wbits = 12;
-      if (const char* ev = getenv("BQGPU_PART_WBITS")) wbits = std::max(6, std::min(13, atoi(ev)));
+      if (c->opt[kOptPartWbits]) wbits = (int)c->opt[kOptPartWbits];
       while (wbits > 6 && ((size_t)1 << wbits) * per_slot > 128 * 1024) --wbits;
-      if (!getenv("BQGPU_PART_WBITS") && ((size_t)2 << wbits) * per_slot <= 128 * 1024) ++wbits;  // fewer, longer runs
+      if (!c->opt[kOptPartWbits] && ((size_t)2 << wbits) * per_slot <= 128 * 1024) ++wbits;  // fewer, longer runs
       while (((pl.nslots + (1ull << wbits) - 1) >> wbits) > (uint64_t)kPartMaxParts &&
              ((size_t)2 << wbits) * per_slot <= 128 * 1024)
         ++wbits;
       pl.wbits = wbits;
       const uint64_t parts = (pl.nslots + (1ull << wbits) - 1) >> wbits;
       pl.mode = (parts <= (uint64_t)kPartMaxParts && part_scatter_lds((int)parts, 256, pl.nsum) <= 150 * 1024 &&
-                 getenv("BQGPU_NO_PARTITION") == nullptr)
+                 c->opt[kOptPartition] != 0)
                     ? kPartitioned
                     : kGlobalDense;
     }
@@ -852,7 +912,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   int ncd = 0, nscd = 0;
   for (int a = 0; a < q->n_aggs; ++a) ncd += q->aggs[a].op == BQG_COUNT_DISTINCT, nscd += q->aggs[a].op == BQG_SORTED_COUNT_DISTINCT;
   bool fused = !pl.p.hash && nsum == 0 && nsum2 == 0 && nscd == 1 && ncd <= 1 && N < (int64_t)kNoRow &&
-               (kBlock / 64) * scd_fused_wave_lds(S) <= kScdFusedMaxLds && !getenv("BQGPU_NO_FUSED_SCD");
+               (kBlock / 64) * scd_fused_wave_lds(S) <= kScdFusedMaxLds && c->opt[kOptFusedScd] != 0;
   if (fused && ncd == 1) {
     for (int a = 0; a < q->n_aggs; ++a) {
       if (q->aggs[a].op != BQG_COUNT_DISTINCT) continue;
@@ -873,7 +933,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   } else if (pl.mode == kPrivate) {
     const size_t lds = (size_t)S * kBlock * (8 + 8 * (size_t)nsum);
     int per_cu = (int)std::min<size_t>(kPrivatePerCu, (160 * 1024) / std::max<size_t>(lds, 1));
-    if (const char* ev = getenv("BQGPU_PRIVATE_PER_CU")) per_cu = std::min(per_cu, std::max(1, atoi(ev)));
+    if (c->opt[kOptPrivatePerCu]) per_cu = std::min(per_cu, (int)c->opt[kOptPrivatePerCu]);
     if (per_cu < 1) per_cu = 1;
     PrivateLaunch L{};
     L.blocks = scan_blocks(c, N, per_cu);
@@ -905,10 +965,10 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       for (int j = 0; j < e.ncols; ++j) e.cols[j].out = ob + 64 + (size_t)j * S * 8;
     }
     hipFunction_t jfn = nullptr;
-    if (N >= jit_min_rows()) {
+    if (c->opt[kOptJit] && N >= c->opt[kOptJitMinRows]) {
       std::string spec = jit_spec(pl.p);
-      // tiles in flight per workgroup (profiling knob; default in scan_private.h)
-      if (const char* ev = getenv("BQGPU_PRIV_AHEAD")) spec += std::string("#define BQ_PRIV_AHEAD ") + std::to_string(std::max(1, std::min(4, atoi(ev)))) + "\n";
+      // tiles in flight per workgroup (profiling option; default in scan_private.h)
+      if (c->opt[kOptPrivAhead]) spec += std::string("#define BQ_PRIV_AHEAD ") + std::to_string(c->opt[kOptPrivAhead]) + "\n";
       jfn = jit_function("bq_jit_scan_private", spec);
     }
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
@@ -978,8 +1038,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.nparts = (int)((S + (1ull << pl.wbits) - 1) >> pl.wbits);
       // narrow entries: every summed column is a float column whose values all have an exact
       // 32-bit integer code (column statistics): 8-byte instead of 12-byte C3 entries, and the
-      // sums are exact integer sums scaled back once (BQGPU_PART_NARROW=0 turns it off)
-      L.narrow = nsum > 0 && !(getenv("BQGPU_PART_NARROW") && atoi(getenv("BQGPU_PART_NARROW")) == 0);
+      // sums are exact integer sums scaled back once (option part_narrow=0 turns it off)
+      L.narrow = nsum > 0 && c->opt[kOptPartNarrow] != 0;
       for (int q = 0; q < nsum && L.narrow; ++q) {
         compute_stats(t, pl.tcol[q]);
         const Column& col = t->cols[pl.tcol[q]];
@@ -1000,21 +1060,20 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       }
       const bool nw = L.narrow != 0;
       c->last.narrow = L.narrow;
-      // scatter workgroup: the widest whose staged tile fits in LDS (BQGPU_PART_THREADS caps it)
-      L.threads = 1024;
-      if (const char* ev = getenv("BQGPU_PART_THREADS")) L.threads = std::max(256, std::min(1024, atoi(ev)));
+      // scatter workgroup: the widest whose staged tile fits in LDS (option part_threads caps it)
+      L.threads = c->opt[kOptPartThreads] ? (int)c->opt[kOptPartThreads] : 1024;
       while (L.threads > 256 && part_scatter_lds(L.nparts, L.threads, nsum, 1, nw) > 150 * 1024) L.threads >>= 1;
       // 8192-row tiles (two 4-row chunks per thread) when the staged tile fits: the aggregate's
-      // per-tile partition segments are twice as long (BQGPU_PART_K=1|2 forces the choice)
+      // per-tile partition segments are twice as long (option part_k=1|2 forces the choice)
       L.k = (L.threads == 1024 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw) <= 150 * 1024) ? 2 : 1;
-      if (const char* ev = getenv("BQGPU_PART_K"))
-        L.k = (atoi(ev) == 2 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw) <= 150 * 1024) ? 2 : 1;
+      if (c->opt[kOptPartK])
+        L.k = (c->opt[kOptPartK] == 2 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw) <= 150 * 1024) ? 2 : 1;
       L.tile_rows = L.threads * kRowsPerThread * L.k;
       const int64_t tr = L.tile_rows;
       L.ntiles = (N + tr - 1) / tr;
       // contiguous whole-tile row ranges, as many scatter workgroups per CU as fit in LDS
       int per_cu = L.k == 2 ? 1 : 2;
-      if (const char* ev = getenv("BQGPU_PART_PER_CU")) per_cu = std::max(1, std::min(8, atoi(ev)));
+      if (c->opt[kOptPartPerCu]) per_cu = (int)c->opt[kOptPartPerCu];
       L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, L.ntiles));
       L.rows_per_block = ((L.ntiles + L.blocks - 1) / L.blocks) * tr;
       L.blocks = (int)((N + L.rows_per_block - 1) / L.rows_per_block);
@@ -1023,7 +1082,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)nsum);
       const int fit = std::max(1, (int)((160 * 1024) / agg_lds));
       L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, (c->cu * fit + L.nparts / 2) / L.nparts));
-      if (const char* ev = getenv("BQGPU_PART_SPLITS")) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, atoi(ev)));
+      if (c->opt[kOptPartSplits]) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, c->opt[kOptPartSplits]));
       L.capacity = (uint64_t)L.ntiles * (uint64_t)tr;
       L.hdr = (uint16_t*)c->prefix.ensure((size_t)L.ntiles * (size_t)(L.nparts + 1) * 2 + 256);
       // one scratch block: entry values | entry meta | split partial tables | arrival counters
@@ -1037,7 +1096,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.partial = eb + vbytes + mbytes;
       L.arrive = (unsigned int*)(eb + vbytes + mbytes + pbytes);
       hipFunction_t fs = nullptr;
-      if (N >= jit_min_rows()) {
+      if (c->opt[kOptJit] && N >= c->opt[kOptJitMinRows]) {
         fs = jit_function("bq_jit_part_scatter", jit_spec(pl.p) + "#define BQ_PART_K " + std::to_string(L.k) +
                                                       "\n#define BQ_PART_NARROW " + std::to_string(L.narrow) + "\n");
         c->last.specialized = fs ? 1 : 0;
@@ -1052,7 +1111,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       unsigned int hc[2];
       HIPCHECK(hipMemcpyAsync(hc, sa.hash_fill, 8, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipStreamSynchronize(st));
-      if (hc[1]) fail(BQG_E_STATE, "hash table overflow");  // caller retries with a bigger table
+      if (hc[1]) throw TableOverflow{false, S};  // run_groupby_grow re-runs with a bigger table
     }
   }
 
@@ -1179,8 +1238,10 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         if (!dtype_is_float(col.dtype) && pairs >= ((unsigned __int128)1 << 63))
           fail(BQG_E_UNSUPPORTED, "count_distinct pair space wider than 63 bits");
         uint64_t cap = 1024;
-        const uint64_t est = std::min<uint64_t>((uint64_t)N, 1ull << 27);
+        uint64_t est = std::min<uint64_t>((uint64_t)N, 1ull << 27);
+        if (c->opt[kOptDistinctSlots]) est = (uint64_t)c->opt[kOptDistinctSlots] / 2;
         while (cap < 2 * est) cap <<= 1;
+        if (c->distinct_grow > cap) cap = c->distinct_grow;
         unsigned char* sb = (unsigned char*)c->bitmap.ensure(cap * 8 + 256);
         d.set = (unsigned long long*)sb;
         d.set_mask = cap - 1;
@@ -1201,7 +1262,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         unsigned int hc[2];
         HIPCHECK(hipMemcpyAsync(hc, d.set_fill, 8, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
-        if (hc[1]) fail(BQG_E_STATE, "count_distinct set overflow");
+        if (hc[1]) throw TableOverflow{true, d.set_mask + 1};
       }
       e.cd[i] = d.out;
       ++i;
@@ -1238,14 +1299,14 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         d.fused = 1;
         // compact 32-bit value codes for integer value columns spanning < 2^32
         compute_stats(t, tc);
-        if (!dtype_is_float(col.dtype) && !getenv("BQGPU_SCD_WIDE")) {
+        if (!dtype_is_float(col.dtype) && c->opt[kOptScdCompact]) {
           const uint64_t vr = col.stats.empty ? 1 : (uint64_t)col.stats.imax - (uint64_t)col.stats.imin + 1;
           if (vr != 0 && vr <= 0xFFFFFFFFull) {
             d.compact = 1;
             d.vmin = col.stats.empty ? 0 : col.stats.imin;
             // value codes below 2^16 (compact chunks are below 2^16 rows): first value and
             // first row share one LDS word
-            d.pack16 = vr <= 0x10000ull && !getenv("BQGPU_SCD_NO_PACK16") ? 1 : 0;
+            d.pack16 = vr <= 0x10000ull && c->opt[kOptScdPack16] ? 1 : 0;
           }
         }
         d.wave_lds = scd_fused_wave_lds(S, d.compact != 0, d.pack16 != 0);
@@ -1293,7 +1354,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       d.out_changes = so + (size_t)i * S * 2;
       d.out_first = d.out_changes + S;
       hipFunction_t sfn = nullptr;
-      if (fused && N >= jit_min_rows()) {
+      if (fused && c->opt[kOptJit] && N >= c->opt[kOptJitMinRows]) {
         const int cd_mode = d.cd.bitmap == nullptr ? 0 : (d.cd.lds_bitmap_words > 0 ? 1 : 2);
         // the value columns as constants (the same choice as the generic body's column loop)
         const int nc = pc.p.ncols;
@@ -1317,7 +1378,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
 
   // ---- small slot spaces: compaction + ordering + emit in one workgroup; the header and the
   // columns (capacity S) come back in one copy, with no host round trip in between
-  if (S <= kSmallEmitSlots && !getenv("BQGPU_NO_SMALL_EMIT")) {
+  if (S <= kSmallEmitSlots && c->opt[kOptSmallEmit]) {
     std::vector<size_t> offs;
     size_t obytes = 256;  // header: groups, passing rows
     for (int j = 0; j < e.ncols; ++j) {
@@ -1452,6 +1513,28 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   *out = r;
 }
 
+// run_groupby, growing an over-full hash table or count_distinct set and re-running the query
+// (bquery's khash factorize has no cardinality ceiling, worker.py:313).  Slot ids stay below
+// 2^31 (32-bit slot lists and first rows on device).
+void run_groupby_grow(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out) {
+  struct Reset {
+    bqg_ctx* c;
+    ~Reset() { c->hash_grow = c->distinct_grow = 0; }
+  } reset{c};
+  c->hash_grow = c->distinct_grow = 0;
+  for (;;) {
+    try {
+      run_groupby(c, t, q, out);
+      return;
+    } catch (const TableOverflow& o) {
+      if (o.slots >= (1ull << 31))
+        fail(BQG_E_OOM, "%s would need more than 2^31 slots", o.distinct ? "count_distinct set" : "group hash table");
+      (o.distinct ? c->distinct_grow : c->hash_grow) = o.slots * 2;
+      ++c->last_regrows;
+    }
+  }
+}
+
 }  // namespace
 
 int bqg_internal_device(bqg_ctx* c) { return c->device; }
@@ -1476,6 +1559,58 @@ int bqg_device_count(int* n) {
   });
 }
 
+// defaults, then the environment (read once per context, never on the query path)
+static void load_options(bqg_ctx* c) {
+  for (int i = 0; i < kNumOpts; ++i) c->opt[i] = kOptDefs[i].def;
+  if (const char* e = getenv("BQGPU_JIT")) c->opt[kOptJit] = strcmp(e, "0") == 0 ? 0 : 1;
+  if (const char* e = getenv("BQGPU_JIT_MIN_ROWS")) c->opt[kOptJitMinRows] = std::max<int64_t>(0, atoll(e));
+  if (const char* e = getenv("BQGPU_OPTIONS")) {
+    std::string all(e);
+    size_t pos = 0;
+    while (pos <= all.size()) {
+      size_t end = all.find(',', pos);
+      if (end == std::string::npos) end = all.size();
+      const std::string item = all.substr(pos, end - pos);
+      pos = end + 1;
+      if (item.empty()) continue;
+      const size_t eq = item.find('=');
+      const std::string name = item.substr(0, eq);
+      const int i = opt_index(name.c_str());
+      char* tail = nullptr;
+      const long long v = eq == std::string::npos ? 0 : strtoll(item.c_str() + eq + 1, &tail, 0);
+      if (i < 0 || eq == std::string::npos || !tail || *tail || !opt_valid(i, v))
+        fail(BQG_E_INVALID, "BQGPU_OPTIONS: bad item '%s'", item.c_str());
+      c->opt[i] = v;
+    }
+  }
+}
+
+int bqg_set_option(bqg_ctx* c, const char* name, int64_t value) {
+  return guard(c, [&] {
+    if (!c) fail(BQG_E_INVALID, "null context");
+    const int i = opt_index(name);
+    if (i < 0) fail(BQG_E_INVALID, "unknown option '%s'", name ? name : "(null)");
+    if (!opt_valid(i, value)) fail(BQG_E_INVALID, "option %s: value %lld out of range", name, (long long)value);
+    c->opt[i] = value;
+  });
+}
+
+int bqg_get_option(bqg_ctx* c, const char* name, int64_t* value) {
+  return guard(c, [&] {
+    if (!c || !value) fail(BQG_E_INVALID, "null argument");
+    const int i = opt_index(name);
+    if (i < 0) fail(BQG_E_INVALID, "unknown option '%s'", name ? name : "(null)");
+    *value = c->opt[i];
+  });
+}
+
+int bqg_reset_options(bqg_ctx* c) {
+  return guard(c, [&] {
+    if (!c) fail(BQG_E_INVALID, "null context");
+    load_options(c);
+  });
+}
+
 int bqg_create(int device_ordinal, bqg_ctx** out) {
   bqg_ctx* c = nullptr;
   int rc = guard(nullptr, [&] {
@@ -1486,6 +1621,7 @@ int bqg_create(int device_ordinal, bqg_ctx** out) {
     HIPCHECK(hipSetDevice(device_ordinal));
     c = new bqg_ctx();
     c->device = device_ordinal;
+    load_options(c);
     HIPCHECK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     c->stream = c->own;
     c->cu = device_cu_count();
@@ -1545,7 +1681,10 @@ int bqg_enable_timing(bqg_ctx* c, int on) {
 }
 
 int bqg_last_timing(bqg_ctx* c, bqg_timing* out) {
-  return guard(c, [&] { *out = c->last; });
+  return guard(c, [&] {
+    *out = c->last;
+    out->regrows = c->last_regrows;
+  });
 }
 
 int bqg_alloc_pinned(bqg_ctx* c, size_t bytes, void** out) {
@@ -1825,7 +1964,8 @@ int bqg_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out) 
     if (!q || !out) fail(BQG_E_INVALID, "null query/output");
     *out = nullptr;
     c->dev_target = nullptr;
-    run_groupby(c, t, q, out);
+    c->last_regrows = 0;
+    run_groupby_grow(c, t, q, out);
   });
 }
 
@@ -1839,7 +1979,8 @@ int bqg_groupby_table(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_table** 
     } reset{c};
     c->dev_target = out;
     bqg_result* r = nullptr;
-    run_groupby(c, t, q, &r);
+    c->last_regrows = 0;
+    run_groupby_grow(c, t, q, &r);
     if (r) table_from_host_result(c, r);  // empty / synthesized results: host-built
   });
 }
@@ -1997,7 +2138,7 @@ int bqg_factorize(bqg_ctx* c, bqg_table* t, int32_t col, int64_t* labels, void* 
       } reset{c};
       c->dev_target = &vt;
       bqg_result* r = nullptr;
-      run_groupby(c, t, &q, &r);
+      run_groupby_grow(c, t, &q, &r);
       if (r) table_from_host_result(c, r);
     }
     std::unique_ptr<bqg_table, int (*)(bqg_table*)> vown(vt, bqg_table_destroy);

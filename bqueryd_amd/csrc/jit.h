@@ -16,10 +16,8 @@ namespace bqg {
 std::string jit_spec(const ScanParams& p);
 
 // module function `kernel` specialised by `spec` for the current device, or nullptr when the
-// JIT is unavailable / disabled / failed (the failure is remembered, not retried)
+// JIT is unavailable or failed (the failure is remembered, not retried); whether to use it at
+// all is the caller's choice (context options "jit" / "jit_min_rows", api.hip)
 hipFunction_t jit_function(const char* kernel, const std::string& spec);
-
-// rows from which a scan is worth specialising (BQGPU_JIT_MIN_ROWS, default 4 Mi rows)
-int64_t jit_min_rows();
 
 }  // namespace bqg

@@ -143,11 +143,6 @@ JitState& state() {
   return *s;
 }
 
-bool jit_disabled() {
-  const char* e = getenv("BQGPU_JIT");
-  return e && strcmp(e, "0") == 0;
-}
-
 }  // namespace
 
 std::string jit_spec(const ScanParams& p) {
@@ -177,13 +172,7 @@ std::string jit_spec(const ScanParams& p) {
   return s.str();
 }
 
-int64_t jit_min_rows() {
-  const char* e = getenv("BQGPU_JIT_MIN_ROWS");
-  return e ? (int64_t)atoll(e) : (int64_t)(4ll << 20);
-}
-
 hipFunction_t jit_function(const char* kernel, const std::string& spec) {
-  if (jit_disabled()) return nullptr;
   JitState& js = state();
   std::lock_guard<std::mutex> lk(js.mu);
   int dev = 0;

@@ -14,10 +14,9 @@ co-located on one node the same merge runs across GPU ranks:
 
 The product path is ``merge_partials_device`` / ``merge_group_device``: libbqgpu's ``bqg_merge``
 runs all five steps on device buffers with RCCL over xGMI (``RcclComm``: one process per GPU;
-``CommGroup``: a process owning several GPUs).  ``merge_partials`` restates the same protocol
-on host tables against a small backend interface (``partition`` / ``reduce``) and a byte
-exchange (``Exchange``: torch.distributed), so the CPU test suite can run it under gloo with the
-oracle as the backend; its GPU backend is ``GpuBackend`` (libbqgpu, no CPU fallback).
+``CommGroup``: a process owning several GPUs).  The protocol's host-side specification (the
+same five steps over torch.distributed, run under gloo by the CPU test suite) lives with the
+tests, ``tests/merge_protocol.py``.
 """
 from __future__ import annotations
 
@@ -30,110 +29,6 @@ import numpy as np
 def sum_spec(agg_list):
     """The client's merge aggregation list: ``[[x[2], 'sum', x[2]] for x in agg_list]``."""
     return [[x[2], 'sum', x[2]] for x in agg_list]
-
-
-def concat_tables(tables, names=None):
-    tables = [t for t in tables if t is not None and not (isinstance(t, str) and t == '')]
-    if not tables:
-        return None
-    names = names or list(tables[0].keys())
-    return OrderedDict((n, np.concatenate([np.asarray(t[n]) for t in tables])) for n in names)
-
-
-class GpuBackend:
-    """partition / reduce on the GPU through libbqgpu."""
-
-    def __init__(self, device=None):
-        from .engine import get_device
-        self.device = device or get_device()
-
-    def reduce(self, table, groupby_cols, agg_list, on_device=False):
-        """``table``: one table or a list of tables -- host mappings or device ShardTables --
-        row-concatenated on the device and summed by key.  ``on_device``: the result stays in
-        HBM (a ShardTable) instead of coming back as numpy arrays."""
-        from .engine import ShardTable
-        parts = table if isinstance(table, (list, tuple)) else [table]
-        names = list(groupby_cols) + [x[2] for x in agg_list]
-        t = ShardTable.from_parts(parts, names, device=self.device)
-        try:
-            if on_device:
-                return t.groupby_table(groupby_cols, sum_spec(agg_list))
-            out, _ = t.groupby(groupby_cols, sum_spec(agg_list))
-            return out
-        finally:
-            t.close()
-
-    def partition(self, table, groupby_cols, nparts):
-        from . import _lib as L
-        from .engine import ShardTable
-        t = ShardTable(table, device=self.device)
-        try:
-            col = t.add_column('__part__', np.uint32)
-            keys = np.array([t.slot(c) for c in groupby_cols], np.int32)
-            counts = np.zeros(nparts, np.int64)
-            self.device.check(L.lib().bqg_hash_partition(self.device.handle, t.handle, len(keys),
-                                                         keys.ctypes.data, nparts, col,
-                                                         counts.ctypes.data))
-            names = list(table.keys())
-            parts = []
-            for p in range(nparts):
-                if counts[p] == 0:
-                    parts.append(OrderedDict((n, np.asarray(table[n])[:0]) for n in names))
-                else:
-                    parts.append(t.select_rows(names, where_terms=[('__part__', '==', p)]))
-            return parts
-        finally:
-            t.close()
-
-
-class LocalExchange:
-    """World of one (no torch): the exchange is the identity."""
-    world = 1
-    rank = 0
-
-    def counts(self, send_counts):
-        return np.asarray(send_counts, np.int64)
-
-    def column(self, parts, dtype, recv_counts):
-        return np.ascontiguousarray(parts[0], dtype=np.dtype(dtype))
-
-
-class Exchange:
-    """Byte all-to-all over torch.distributed (nccl = RCCL on ROCm, or gloo)."""
-
-    def __init__(self, dist, device=None, group=None):
-        self.dist = dist
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
-        self.device = device
-
-    def _tensor(self, arr):
-        import torch
-        t = torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).copy())
-        return t.to(self.device) if self.device is not None else t
-
-    def counts(self, send_counts):
-        import torch
-        s = torch.tensor(np.asarray(send_counts, np.int64))
-        r = torch.empty(self.world, dtype=torch.int64)
-        if self.device is not None:
-            s, r = s.to(self.device), r.to(self.device)
-        self.dist.all_to_all_single(r, s, group=self.group)
-        return r.cpu().numpy()
-
-    def column(self, parts, dtype, recv_counts):
-        """parts[dst] -> this rank's rows from every source, concatenated in rank order."""
-        import torch
-        dtype = np.dtype(dtype)
-        send = np.concatenate([np.ascontiguousarray(p, dtype=dtype) for p in parts]) if parts else np.zeros(0, dtype)
-        in_split = [int(len(p)) * dtype.itemsize for p in parts]
-        out_split = [int(c) * dtype.itemsize for c in recv_counts]
-        out = torch.empty(sum(out_split), dtype=torch.uint8)
-        if self.device is not None:
-            out = out.to(self.device)
-        self.dist.all_to_all_single(out, self._tensor(send), out_split, in_split, group=self.group)
-        return out.cpu().numpy().view(dtype)
 
 
 def new_unique_id():
@@ -247,38 +142,6 @@ def merge_group_device(tables_per_rank, groupby_cols, agg_list, dtypes, group, r
     group.devices[0].check(L.lib().bqg_merge_group(w, ctxs, ntab, arr, len(groupby_cols), len(names), codes,
                                                    1 if reduced else 0, outs))
     return _merged_to_host(ctypes.c_void_p(outs[0]), names, dtypes, group.devices[0])
-
-
-def merge_partials(local_tables, groupby_cols, agg_list, dtypes, backend, exchange):
-    """Merge this rank's finalized shard tables with every other rank's; returns the merged
-    table on rank 0 (None elsewhere).  ``dtypes``: name -> dtype of the finalized columns
-    (needed by ranks that hold no shard)."""
-    names = list(groupby_cols) + [x[2] for x in agg_list]
-    local_tables = [t for t in local_tables
-                    if t is not None and not (isinstance(t, str) and t == '') and len(t[names[0]])]
-    if exchange.world == 1:
-        # partition / exchange / gather are the identity: one reduce of everything
-        if not local_tables:
-            return OrderedDict((n, np.zeros(0, dtypes[n])) for n in names)
-        return backend.reduce(local_tables, groupby_cols, agg_list)
-    if local_tables:
-        local = backend.reduce(local_tables, groupby_cols, agg_list)
-        parts = backend.partition(local, groupby_cols, exchange.world)
-    else:
-        parts = [OrderedDict((n, np.zeros(0, dtypes[n])) for n in names) for _ in range(exchange.world)]
-    recv_counts = exchange.counts([len(p[names[0]]) for p in parts])
-    mine = OrderedDict((n, exchange.column([p[n] for p in parts], dtypes[n], recv_counts)) for n in names)
-    if len(mine[names[0]]):
-        mine = backend.reduce(mine, groupby_cols, agg_list)
-    # gather to rank 0
-    n_mine = len(mine[names[0]])
-    to_root = [n_mine if dst == 0 else 0 for dst in range(exchange.world)]
-    recv = exchange.counts(to_root)
-    gathered = OrderedDict()
-    for n in names:
-        parts_n = [mine[n] if dst == 0 else np.zeros(0, dtypes[n]) for dst in range(exchange.world)]
-        gathered[n] = exchange.column(parts_n, dtypes[n], recv)
-    return gathered if exchange.rank == 0 else None
 
 
 # aggregations whose client-side merge (a sum of the per-shard finalized values, rpc.py:170-172)

@@ -55,7 +55,37 @@ class Device:
         self.check(self._lib.bqg_last_timing(self.handle, ctypes.byref(t)))
         return {'scan_ms': t.scan_ms, 'scan_launches': t.scan_launches, 'total_ms': t.total_ms,
                 'rows': t.rows, 'bytes': t.bytes, 'mode': t.mode, 'specialized': bool(t.specialized),
-                'narrow': bool(t.narrow)}
+                'narrow': bool(t.narrow), 'regrows': t.regrows}
+
+    def set_option(self, name, value):
+        """One engine option of this context (include/bqgpu.h: launch shapes and path choices,
+        for tests and profiling; every value gives the same results)."""
+        self.check(self._lib.bqg_set_option(self.handle, name.encode('ascii'), int(value)))
+
+    def get_option(self, name):
+        v = ctypes.c_int64()
+        self.check(self._lib.bqg_get_option(self.handle, name.encode('ascii'), ctypes.byref(v)))
+        return v.value
+
+    def reset_options(self):
+        self.check(self._lib.bqg_reset_options(self.handle))
+
+    def options(self, **values):
+        """Context manager: the given options set for the block, the previous values restored
+        after it."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def _cm():
+            old = {k: self.get_option(k) for k in values}
+            try:
+                for k, v in values.items():
+                    self.set_option(k, v)
+                yield self
+            finally:
+                for k, v in old.items():
+                    self.set_option(k, v)
+        return _cm()
 
 
 _devices = {}

@@ -3,6 +3,9 @@
 * ``tar_of_tars`` restates ``ControllerNode.process_sink_results`` (bqueryd/controller.py:
   146-221): once every shard replied, the per-shard result tars are packed into one tar with
   ``arcname=filename``; empty ``''`` replies are skipped (controller.py:175-179,196).
+* ``fan_out`` / ``CalcSegment`` restate the controller's scatter (controller.py:471-508) and
+  its gather accounting (controller.py:146-221), with the node-level patch of
+  INTEGRATION.md §4 (one message and one reply covering a GPU node's files).
 * ``uncompress_groupby_to_df`` restates ``RPC.uncompress_groupby_to_df`` (bqueryd/rpc.py:
   134-179): each inner tar is opened as a ctable and appended; with ``aggregate=True`` the
   appended table is re-grouped with ``sum`` of every finalized column ("we can only sum now",
@@ -34,6 +37,69 @@ def tar_of_tars(results):
             info.size = len(data)
             archive.addfile(info, io.BytesIO(data))
     return buf.getvalue()
+
+
+def fan_out(args, kwargs, gpu_node_files=None):
+    """The controller's scatter of one groupby RPC (``handle_calc_message``,
+    controller.py:471-508) with the node-level patch of INTEGRATION.md §4: the argument lists of
+    the worker messages, in send order.  ``gpu_node_files``: {node: [its files]} for GPU nodes
+    that take all of their files in one message; used only when the client merges by sum
+    (``kwargs['aggregate'] is True``), else every file gets its own message as in the
+    reference."""
+    args = list(args)
+    if len(args) != 4:
+        raise ValueError('expecting: path_list, groupby_col_list, measure_col_list, where_terms_list')
+    filenames = list(args[0])
+    if not filenames:
+        raise ValueError('no filenames given')
+    out = []
+    covered = set()
+    if kwargs.get('aggregate') is True and gpu_node_files:
+        for node, files in gpu_node_files.items():
+            files = [f for f in files if f in filenames and f not in covered]
+            if files:
+                out.append([files] + args[1:])
+                covered.update(files)
+    out += [[f] + args[1:] for f in filenames if f not in covered]
+    return out
+
+
+class CalcSegment:
+    """The gather state of one scattered RPC (``rpc_segment``, controller.py:489-491) and the
+    accounting of ``process_sink_results`` (controller.py:146-221): the reply to the client
+    goes out once every file name has a result (controller.py:186).  A node-level reply (its
+    ``args[0]`` a list of files) stores its tar under the first file and
+    completes the others with ``None`` entries, which the tar of tars skips
+    (controller.py:195-197); ``''`` replies (the factorization-check early-out) are skipped
+    the same way (controller.py:175-179)."""
+
+    def __init__(self, filenames):
+        self.filenames = OrderedDict((f, None) for f in filenames)
+        self.results = OrderedDict()
+
+    def add_reply(self, args, data):
+        """One worker reply (its message's args and ``data``); True when the RPC is complete."""
+        names = list(args[0]) if isinstance(args[0], (list, tuple)) else [args[0]]
+        if not names:
+            raise ValueError('a reply without a file name')
+        for f in names:
+            if f not in self.filenames:
+                raise KeyError('reply for %r, which this RPC did not ask for' % (f,))
+        self.results[names[0]] = data if data else None
+        for other in names[1:]:
+            self.results[other] = None
+        return self.complete
+
+    @property
+    def complete(self):
+        return len(self.results) == len(self.filenames)
+
+    def tar(self):
+        """The reply's tar of tars (controller.py:192-209); only once complete."""
+        if not self.complete:
+            raise RuntimeError('%d of %d files have no result yet' % (len(self.filenames) - len(self.results),
+                                                                      len(self.filenames)))
+        return tar_of_tars(self.results)
 
 
 def read_shard_results(result_tar):

@@ -17,7 +17,8 @@
  *   worker.py:319  bcolz.fromiter(ct[cols].where(bool_arr), ...)   (aggregate=False)
  *                    -> bqg_select_rows
  * and the co-located cross-shard merge that the client does at bqueryd/rpc.py:164-173
- * ("we can only sum now") -> bqg_hash_partition + the all-to-all of bqueryd_amd/dist.py.
+ * ("we can only sum now") -> bqg_comm_init* + bqg_merge / bqg_merge_group (local re-group,
+ * hash partition, RCCL exchange over xGMI, re-group, gather to rank 0; all on device).
  *
  * Conventions
  *  - Every function returns 0 on success and a negative BQG_E_* code on failure; the
@@ -41,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BQG_ABI_VERSION 5
+#define BQG_ABI_VERSION 6
 
 /* error codes */
 #define BQG_OK 0
@@ -123,6 +124,9 @@ typedef struct {
   int32_t specialized;   /* 1: the scan ran a query-specialised (run-time compiled) kernel */
   int32_t narrow;        /* partitioned mode: 1 when the summed values travelled as exact 32-bit
                             integer codes (ABI 5) */
+  int32_t regrows;       /* times the last query was re-run after its group hash table or
+                            count_distinct set filled past half, each time with twice the slots
+                            (ABI 6) */
 } bqg_timing;
 
 /* ---------------- lifecycle ---------------- */
@@ -137,6 +141,33 @@ int bqg_set_stream(bqg_ctx* ctx, void* hip_stream);
 int bqg_synchronize(bqg_ctx* ctx);
 int bqg_enable_timing(bqg_ctx* ctx, int on);
 int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
+
+/* Engine options (ABI 6): launch shapes and path choices the planner otherwise makes by
+ * itself -- for tests and profiling; every value gives the same results.  Per context; read
+ * once from the environment when the context is created (BQGPU_OPTIONS="name=value,...";
+ * BQGPU_JIT=0 and BQGPU_JIT_MIN_ROWS=<n> set "jit" / "jit_min_rows"), never on the query path.
+ *   jit            1  run-time specialised (hiprtc) scans            0 | 1
+ *   jit_min_rows   4Mi  ... for tables of at least this many rows
+ *   partition      1  partitioned aggregation for large dense slot spaces   0 | 1
+ *   part_wbits     0  slots per partition 2^wbits (0: auto)           0 | 6..13
+ *   part_k         0  4-row chunks per scatter thread (0: auto)        0 | 1 | 2
+ *   part_threads   0  scatter workgroup size (0: auto)                 0 | 256 | 512 | 1024
+ *   part_per_cu    0  scatter workgroups per CU (0: auto)              0..8
+ *   part_splits    0  aggregate workgroups per partition (0: auto)
+ *   part_narrow    1  exact 32-bit value codes in partition entries     0 | 1
+ *   fused_scd      1  one fused pass for count / distinct queries       0 | 1
+ *   scd_compact    1  ... with 32-bit value codes when they fit         0 | 1
+ *   scd_pack16     1  ... first value and first row in one LDS word     0 | 1
+ *   priv_ahead     0  private scan: tiles in flight (0: default)       0..4
+ *   private_per_cu 0  private scan: workgroups per CU cap (0: auto)    0..8
+ *   small_emit     1  one-workgroup emit for <= 8192 slots              0 | 1
+ *   hash_slots     0  initial group hash-table slots (0: from rows)    0..2^31
+ *   distinct_slots 0  initial count_distinct set slots (0: from rows)  0..2^31
+ * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
+ * the defaults (then the environment's values). */
+int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);
+int bqg_get_option(bqg_ctx* ctx, const char* name, int64_t* value);
+int bqg_reset_options(bqg_ctx* ctx);
 
 /* ---------------- pinned host memory ---------------- */
 int bqg_alloc_pinned(bqg_ctx* ctx, size_t bytes, void** out);

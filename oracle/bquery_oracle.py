@@ -18,12 +18,18 @@ The arithmetic itself lives in the external ``bquery`` package (pinned only as
 Its algorithm is restated from the public bquery 0.2.x design as summarised in SURVEY.md
 §3.2 / §8a rows A6-A10; every such rule is tagged ``[ext-bquery, unverified]``.
 
-Parity status (also in DESIGN.md):
-* PINNED against the reference's own test oracle (pandas, ``tests/test_simple_rpc.py:139-190``):
-  single-key ``sum`` / ``mean`` / ``count`` without a filter, and full-vs-sharded counts.
-* UNPINNED (restated semantics only): where_terms ops, multi-column keys, count_distinct,
-  sorted_count_distinct, std, the skip-slot rules, aggregate=True merge, raw-row mode,
-  expand_filter_column.  No bquery/bcolz build or golden vectors exist in this container.
+Parity status (also in DESIGN.md §4; the pins are ``tests/test_oracle.py``):
+* PINNED against the reference's own test oracle, pandas (``tests/test_simple_rpc.py:139-190``):
+  the reference's cases (single-key ``sum`` / ``mean`` / ``count`` without a filter, and
+  full-vs-sharded counts), and every rule pandas can express: multi-key first-appearance
+  group order (``groupby(sort=False)``), where-term filters and the skip slot (``df[mask]``),
+  count_distinct (``nunique``), std (``std(ddof=0)``), raw rows (``aggregate=False``),
+  basket expansion (``transform('any')`` over runs), the ``aggregate=True`` client merge
+  (concat + ``groupby(sort=False).sum()``), and sorted_count_distinct up to its zero-init rule.
+* PARITY UNPINNED (bquery-only rules; bquery / bcolz are absent and no reference-held golden
+  vectors exist): sorted_count_distinct's zero-initialised ``last`` rule, the
+  bit pattern of Knuth's incremental mean, float32 row-order sums, and the factorization
+  check's exact operator semantics.
 
 All row-order-dependent reductions (float sums, Knuth mean, Welford std,
 sorted_count_distinct) are evaluated strictly in row order, as bquery's Cython loops do.

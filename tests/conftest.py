@@ -24,3 +24,17 @@ def oracle_c():
 def gpu_device():
     from bqueryd_amd.engine import get_device
     return get_device()
+
+
+@pytest.fixture
+def engine_options():
+    """Set engine options (include/bqgpu.h, bqg_set_option) on the process's default context
+    for one test; the defaults are restored afterwards."""
+    from bqueryd_amd.engine import get_device
+    dev = get_device()
+
+    def set_options(**kw):
+        for k, v in kw.items():
+            dev.set_option(k, v)
+    yield set_options
+    dev.reset_options()

@@ -1,8 +1,10 @@
-"""Cross-rank merge protocol (bqueryd_amd/dist.py) under gloo, world_size 2, on CPU.
+"""Cross-rank merge protocol under gloo, world_size 2, on CPU.
 
-The per-rank partition/reduce steps use the oracle as the backend (test infrastructure); the
-exchange, the partition bookkeeping and the gather are the product code.  The merged result
-must equal the reference client merge (rpc.py:164-173) of all shards."""
+``tests/merge_protocol.py`` is the host-side specification of the protocol libbqgpu's
+``bqg_merge`` runs on device buffers (partition, count exchange, row exchange, reduce, gather);
+here its per-rank partition / reduce steps use the oracle as the backend and the exchange runs
+over torch.distributed (gloo).  The merged result must equal the reference client merge
+(rpc.py:164-173) of all shards."""
 import os
 import socket
 from collections import OrderedDict
@@ -13,6 +15,7 @@ import pytest
 from bqueryd_amd import dist as bdist
 from bqueryd_amd import synth
 from oracle import bquery_oracle as bo
+from tests import merge_protocol as mp_
 from tests.helpers import assert_tables_equal, sort_by_keys
 
 AGGS = [['fare_amount', 'sum', 'fare_sum'], ['fare_amount', 'count', 'n'], ['fare_amount', 'mean', 'fm']]
@@ -23,7 +26,7 @@ NSHARDS = 5
 class OracleBackend:
     def reduce(self, table, groupby_cols, agg_list):
         if isinstance(table, list):
-            table = bdist.concat_tables(table)
+            table = mp_.concat_tables(table)
         return bo.groupby(table, groupby_cols, bdist.sum_spec(agg_list))
 
     def partition(self, table, groupby_cols, nparts):
@@ -51,7 +54,7 @@ def _worker(rank, world, port, q):
         results = shard_results()
         mine = [r for i, r in enumerate(results) if i % world == rank]
         dtypes = OrderedDict((k, v.dtype) for k, v in results[0].items())
-        merged = bdist.merge_partials(mine, KEYS, AGGS, dtypes, OracleBackend(), bdist.Exchange(dist))
+        merged = mp_.merge_partials(mine, KEYS, AGGS, dtypes, OracleBackend(), mp_.Exchange(dist))
         q.put((rank, None if merged is None else {k: v.tolist() for k, v in merged.items()}))
     finally:
         dist.destroy_process_group()
@@ -89,11 +92,11 @@ def test_merge_partials_single_rank():
     """World of one: the merge is one reduce of every local table, in client order."""
     results = shard_results()
     dtypes = OrderedDict((k, v.dtype) for k, v in results[0].items())
-    merged = bdist.merge_partials(results + [''], KEYS, AGGS, dtypes, OracleBackend(), bdist.LocalExchange())
+    merged = mp_.merge_partials(results + [''], KEYS, AGGS, dtypes, OracleBackend(), mp_.LocalExchange())
     ref = bo.client_merge(results, KEYS, AGGS, aggregate=True)
     # same first-appearance order as the client's appended-then-regrouped table
     assert_tables_equal(merged, ref)
-    empty = bdist.merge_partials([], KEYS, AGGS, dtypes, OracleBackend(), bdist.LocalExchange())
+    empty = mp_.merge_partials([], KEYS, AGGS, dtypes, OracleBackend(), mp_.LocalExchange())
     assert all(len(v) == 0 and v.dtype == dtypes[k] for k, v in empty.items())
 
 

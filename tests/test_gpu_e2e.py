@@ -153,6 +153,20 @@ def test_node_level_calc_matches_per_shard_replies(tmp_path, aggs, where, expand
     per_file = rpc.uncompress_groupby_to_df(rpc.tar_of_tars(replies), keys, aggs, where, aggregate=True)
     per_file = OrderedDict((c, per_file[c].values) for c in per_file.columns)
     assert_tables_equal(sort_by_keys(per_file, keys), sort_by_keys(ref, keys))
+    # the patched controller (restated in rpc.fan_out / rpc.CalcSegment):
+    # files 0-2 on a GPU node (one message, one reply), files 3-4 per file; the RPC completes
+    # when every file is covered and the client merge of the gathered tar is the same answer
+    seg = rpc.CalcSegment(files)
+    sent = rpc.fan_out([files, keys, aggs, where], kwargs, {'gpu-node': files[:3]})
+    assert sent[0][0] == files[:3] and len(sent) == 3
+    for a in reversed(sent):
+        assert not seg.complete
+        reply = calc.handle_work(_calc_msg(a[0], keys, aggs, where, **kwargs))
+        done = seg.add_reply(reply.get_args_kwargs()[0], reply['data'])
+    assert done
+    mixed = rpc.uncompress_groupby_to_df(seg.tar(), keys, aggs, where, aggregate=True)
+    mixed = OrderedDict((c, mixed[c].values) for c in mixed.columns)
+    assert_tables_equal(sort_by_keys(mixed, keys), sort_by_keys(ref, keys))
 
 
 def test_node_level_calc_needs_explicit_aggregate(tmp_path):

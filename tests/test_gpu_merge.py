@@ -23,18 +23,21 @@ KEYS = ['pickup_location', 'vendor_id']
     [['fare_amount', 'mean', 'fm'], ['passenger_count', 'count_distinct', 'pcd']],
 ])
 def test_gpu_single_rank_merge(aggs):
+    """The product merge (bqg_merge at world 1) of six shards' device-resident results, every
+    aggregation's finalized values summed as the client does -- in its first-appearance order."""
+    from bqueryd_amd.engine import get_device
     cols = ('pickup_location', 'vendor_id', 'fare_amount', 'passenger_count')
     shards = [synth.taxi_shard(150_000, config_id=5, n_shards=6, shard=i, columns=cols) for i in range(6)]
     for s in shards:
         s['pickup_location'] = (s['pickup_location'] % 20_000).astype(s['pickup_location'].dtype)
-    per = []
-    for s in shards:
-        t = ShardTable(s)
-        out, _ = t.groupby(KEYS, aggs)
-        t.close()
-        per.append(out)
-    dtypes = OrderedDict((k, np.asarray(v).dtype) for k, v in per[0].items())
-    merged = bdist.merge_partials(per, KEYS, aggs, dtypes, bdist.GpuBackend(), bdist.LocalExchange())
+    per = _device_results(shards, aggs=aggs)
+    comm = bdist.RcclComm(get_device())
+    try:
+        merged = bdist.merge_partials_device(per, KEYS, aggs, _dtypes(aggs), comm)
+    finally:
+        comm.close()
+        for p in per:
+            p.close()
     ref = bo.client_merge([bo.handle_work(s, KEYS, aggs, []) for s in shards], KEYS, aggs, aggregate=True)
     assert_tables_equal(merged, ref)
 

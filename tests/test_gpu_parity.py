@@ -280,12 +280,12 @@ def test_partitioned_four_sums(oracle_c):
 
 @pytest.mark.parametrize('jit', [False, True])
 @pytest.mark.parametrize('n', [1, 255, 257, 70_001, 400_000])
-def test_fused_distinct_pass(n, jit, oracle_c, monkeypatch):
+def test_fused_distinct_pass(n, jit, oracle_c, engine_options):
     """count + count_distinct + sorted_count_distinct on different columns: one fused pass
     (k_scd_fused; precompiled or run-time specialised), checked against the oracle and against
     the unfused kernels."""
     if jit:
-        monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
+        engine_options(jit_min_rows=0)
     rng = np.random.default_rng(n)
     cols = OrderedDict(k=rng.integers(0, 50, n).astype(np.int16), a=rng.integers(-5, 40, n).astype(np.int32),
                        b=np.repeat(rng.integers(0, 4, (n + 9) // 10), 10)[:n].astype(np.int64),
@@ -293,11 +293,11 @@ def test_fused_distinct_pass(n, jit, oracle_c, monkeypatch):
     aggs = [['a', 'count', 'n'], ['a', 'count_distinct', 'acd'], ['b', 'sorted_count_distinct', 'bscd']]
     for terms in ([], [('f', '>', 2)], [('f', 'in', [0, 8])]):
         got = run_both(cols, ['k'], aggs, terms, oracle_c)
-        monkeypatch.setenv('BQGPU_NO_FUSED_SCD', '1')
+        engine_options(fused_scd=0)
         t = ShardTable(cols)
         ref, _ = t.groupby(['k'], aggs, where_terms=terms)
         t.close()
-        monkeypatch.delenv('BQGPU_NO_FUSED_SCD')
+        engine_options(fused_scd=1)
         assert_tables_equal(got, ref)
     # float value column for the sorted distinct, first row filtered out
     cols['b'] = (cols['b'] * 0.5).astype(np.float64)
@@ -306,10 +306,10 @@ def test_fused_distinct_pass(n, jit, oracle_c, monkeypatch):
 
 
 @pytest.mark.parametrize('case', range(6))
-def test_specialised_private_scan(case, oracle_c, monkeypatch):
+def test_specialised_private_scan(case, oracle_c, engine_options):
     """The run-time specialised (hiprtc) private scan against the oracle, forced on at small
     sizes; the precompiled generic kernel must give the same table."""
-    monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
+    engine_options(jit_min_rows=0)
     n = 300_001
     rng = np.random.default_rng(100 + case)
     cols = synth.taxi_shard(n, config_id=2, columns=('payment_type', 'passenger_count', 'fare_amount'))
@@ -331,7 +331,7 @@ def test_specialised_private_scan(case, oracle_c, monkeypatch):
     t = ShardTable(cols)
     t.groupby(keys, aggs, where_terms=terms)
     assert t.dev.last_timing()['specialized'], 'specialised kernel did not run'
-    monkeypatch.setenv('BQGPU_JIT', '0')
+    engine_options(jit=0)
     ref, _ = t.groupby(keys, aggs, where_terms=terms)
     assert not t.dev.last_timing()['specialized']
     t.close()
@@ -339,10 +339,10 @@ def test_specialised_private_scan(case, oracle_c, monkeypatch):
 
 
 @pytest.mark.parametrize('case', range(3))
-def test_specialised_partitioned(case, oracle_c, monkeypatch):
+def test_specialised_partitioned(case, oracle_c, engine_options):
     """The run-time specialised (hiprtc) partition scatter kernel against the oracle, forced on
     at small sizes; the precompiled generic kernel must give the same table."""
-    monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
+    engine_options(jit_min_rows=0)
     n = 500_003
     rng = np.random.default_rng(200 + case)
     cols = synth.taxi_shard(n, config_id=3, columns=synth.query_columns(C3) + ['passenger_count'])
@@ -360,7 +360,7 @@ def test_specialised_partitioned(case, oracle_c, monkeypatch):
     t.groupby(keys, aggs, where_terms=terms)
     timing = t.dev.last_timing()
     assert timing['mode'] == 4 and timing['specialized'], timing
-    monkeypatch.setenv('BQGPU_JIT', '0')
+    engine_options(jit=0)
     ref, _ = t.groupby(keys, aggs, where_terms=terms)
     assert not t.dev.last_timing()['specialized']
     t.close()
@@ -369,11 +369,11 @@ def test_specialised_partitioned(case, oracle_c, monkeypatch):
 
 @pytest.mark.parametrize('jit', [False, True])
 @pytest.mark.parametrize('low_ranges', [(2, 4), (3,), (4, 3), (8192,), (16384,)])
-def test_partition_key_layouts(jit, low_ranges, oracle_c, monkeypatch):
+def test_partition_key_layouts(jit, low_ranges, oracle_c, engine_options):
     """Multi-column keys whose trailing columns stay inside one partition (range products that
     are powers of two <= 2^wbits) and ones that do not; terms on a trailing key column."""
     if jit:
-        monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
+        engine_options(jit_min_rows=0)
     rng = np.random.default_rng(sum(low_ranges) + jit)
     n = 300_007
     kr = 40_000 if int(np.prod(low_ranges)) <= 8 else 500  # keep the slot space dense
@@ -389,15 +389,15 @@ def test_partition_key_layouts(jit, low_ranges, oracle_c, monkeypatch):
 
 
 @pytest.mark.parametrize('threads,splits,per_cu', [(256, None, None), (512, 3, 1), (1024, 64, 8), (1024, 1, 2)])
-def test_partitioned_launch_shapes(threads, splits, per_cu, oracle_c, monkeypatch):
+def test_partitioned_launch_shapes(threads, splits, per_cu, oracle_c, engine_options):
     """Tile sizes (256 / 512 / 1024 scatter threads: 1024- to 4096-row tiles), aggregate tile
     splits (one, three, more splits than some partitions have tiles) and scatter workgroups per
     CU give the same table; a partial last tile and a filter that empties whole tiles."""
-    monkeypatch.setenv('BQGPU_PART_THREADS', str(threads))
+    engine_options(part_threads=threads)
     if splits:
-        monkeypatch.setenv('BQGPU_PART_SPLITS', str(splits))
+        engine_options(part_splits=splits)
     if per_cu:
-        monkeypatch.setenv('BQGPU_PART_PER_CU', str(per_cu))
+        engine_options(part_per_cu=per_cu)
     rng = np.random.default_rng(threads + (splits or 0))
     n = 123_457
     cols = OrderedDict(k=rng.integers(0, 200_000, n).astype(np.int32), v=np.round(rng.normal(size=n) * 64) / 64,
@@ -406,25 +406,20 @@ def test_partitioned_launch_shapes(threads, splits, per_cu, oracle_c, monkeypatc
     run_both(cols, ['k'], [['v', 'sum', 's'], ['v', 'mean', 'm']], [('f', '>', 0)], oracle_c, exact=True)
 
 
-def _groupby_info(cols, keys, aggs, env=None, monkeypatch=None):
-    if env:
-        for k_, v_ in env.items():
-            monkeypatch.setenv(k_, v_)
+def _groupby_info(cols, keys, aggs, opts=None):
     t = ShardTable(cols)
     try:
-        got, _ = t.groupby(keys, aggs)
-        info = t.dev.last_timing()
+        with t.dev.options(**(opts or {})):
+            got, _ = t.groupby(keys, aggs)
+            info = t.dev.last_timing()
     finally:
         t.close()
-        if env:
-            for k_ in env:
-                monkeypatch.delenv(k_)
     return got, info
 
 
 @pytest.mark.parametrize('kind', ['dyadic', 'cents', 'f32_dyadic', 'two_sums', 'neg_zero', 'nan', 'huge', 'int_sum',
                                   'int8_only', 'uint32_full', 'int64_wide', 'uint64'])
-def test_partitioned_narrow_codes(kind, oracle_c, monkeypatch):
+def test_partitioned_narrow_codes(kind, oracle_c, engine_options):
     """Partitioned sums over float columns whose values all have an exact 32-bit integer code
     (dyadic: v * 2^k; cents: rint(v * 100)) travel as 8-byte entries and are summed as
     integers: dyadic sums bit-exact (and bit-identical to the 64-bit entry path), cents within
@@ -483,7 +478,7 @@ def test_partitioned_narrow_codes(kind, oracle_c, monkeypatch):
         exact.add('ws')
     assert_tables_equal(got, ref, exact_cols=exact)
     if narrow:
-        wide, winfo = _groupby_info(cols, ['k'], aggs, {'BQGPU_PART_NARROW': '0'}, monkeypatch)
+        wide, winfo = _groupby_info(cols, ['k'], aggs, {'part_narrow': 0})
         assert not winfo['narrow']
         if kind in ('dyadic', 'f32_dyadic', 'neg_zero', 'int_sum', 'int8_only', 'uint32_full'):
             np.testing.assert_array_equal(got['vs'], wide['vs'])
@@ -492,14 +487,14 @@ def test_partitioned_narrow_codes(kind, oracle_c, monkeypatch):
 
 
 @pytest.mark.parametrize('vrange,no_pack', [(7, False), (7, True), (65_536, False), (200_000, False)])
-def test_fused_distinct_value_widths(vrange, no_pack, oracle_c, monkeypatch):
+def test_fused_distinct_value_widths(vrange, no_pack, oracle_c, engine_options):
     """The fused distinct pass with 32-bit value codes: first value and first row share one
     LDS word when the codes fit 16 bits (value range <= 2^16), two words otherwise (or with
-    BQGPU_SCD_NO_PACK16); every width against the oracle, at a size that runs the
+    option scd_pack16=0); every width against the oracle, at a size that runs the
     specialised kernel over several chunks."""
-    monkeypatch.setenv('BQGPU_JIT_MIN_ROWS', '0')
+    engine_options(jit_min_rows=0)
     if no_pack:
-        monkeypatch.setenv('BQGPU_SCD_NO_PACK16', '1')
+        engine_options(scd_pack16=0)
     rng = np.random.default_rng(vrange)
     n = 600_000
     v = rng.integers(-3, vrange - 3, n).astype(np.int32)
@@ -507,3 +502,61 @@ def test_fused_distinct_value_widths(vrange, no_pack, oracle_c, monkeypatch):
     cols = OrderedDict(k=rng.integers(0, 200, n).astype(np.int16),
                        v=np.repeat(v[: n // 3], 3)[:n].astype(np.int32))
     run_both(cols, ['k'], [['v', 'count', 'n'], ['v', 'sorted_count_distinct', 'vscd']], [], oracle_c)
+
+
+def _regrows_run(cols, keys, aggs, terms, oracle_c):
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(keys, aggs, where_terms=terms)
+        timing = t.dev.last_timing()
+    finally:
+        t.close()
+    ref = oracle_c.groupby(cols, keys, aggs, oracle_c.where_terms(cols, terms) if terms else None)
+    assert_tables_equal(got, ref, exact_cols={a[2] for a in aggs if a[1] == 'sum'})
+    return timing
+
+
+@pytest.mark.parametrize('keys', [['k'], ['k', 'f']])
+def test_hash_table_grows(keys, oracle_c, engine_options):
+    """A group hash table started far too small (option hash_slots = 1024) for 40 k distinct
+    keys fills past half: the query re-runs with twice the slots until it fits, as bquery's
+    khash factorize has no cardinality ceiling (worker.py:313).  Packed keys (hash mode 1) and
+    wide keys with a float column (mode 2), filtered and not, against the oracle."""
+    engine_options(hash_slots=1024)
+    rng = np.random.default_rng(len(keys))
+    n = 200_000
+    pool = rng.integers(-2**40, 2**40, 40_000)
+    cols = OrderedDict(k=pool[rng.integers(0, len(pool), n)], f=np.round(rng.normal(size=n)) / 4,
+                       v=np.round(rng.normal(size=n) * 64) / 64)
+    aggs = [['v', 'sum', 's'], ['v', 'count', 'n'], ['v', 'mean', 'm']]
+    for terms in ([], [('v', '>', -0.5)]):
+        timing = _regrows_run(cols, keys, aggs, terms, oracle_c)
+        assert timing['mode'] == 3 and timing['regrows'] >= 5, timing
+    engine_options(hash_slots=0)
+    assert _regrows_run(cols, keys, aggs, [], oracle_c)['regrows'] == 0
+
+
+def test_distinct_set_grows(oracle_c, engine_options):
+    """A count_distinct (group, value) set started at 1024 slots for ~50 k distinct pairs
+    (the pair space is too wide for the bitmap) grows the same way."""
+    engine_options(distinct_slots=1024)
+    rng = np.random.default_rng(3)
+    n = 150_000
+    cols = OrderedDict(k=rng.integers(0, 12, n).astype(np.int32), w=rng.integers(0, 2**40, 5_000)[rng.integers(0, 5_000, n)])
+    timing = _regrows_run(cols, ['k'], [['w', 'count_distinct', 'wcd'], ['w', 'count', 'n']], [], oracle_c)
+    assert timing['regrows'] >= 5, timing
+
+
+def test_engine_options_validate(gpu_device):
+    from bqueryd_amd import _lib
+    for name in _lib.OPTIONS:
+        v = gpu_device.get_option(name)
+        gpu_device.set_option(name, v)
+    with pytest.raises(_lib.BqgError):
+        gpu_device.set_option('no_such_option', 1)
+    with pytest.raises(_lib.BqgError):
+        gpu_device.set_option('part_threads', 300)
+    with pytest.raises(_lib.BqgError):
+        gpu_device.set_option('part_wbits', 3)
+    gpu_device.reset_options()
+    assert gpu_device.get_option('jit') in (0, 1) and gpu_device.get_option('part_narrow') == 1

@@ -135,6 +135,64 @@ def test_tar_of_tars_and_concat_merge(tmp_path):
     assert rpc.merge_tables([], ['k'], [], aggregate=True) is None
 
 
+@pytest.mark.parametrize('nrows', [0, 1, 70_000])
+def test_ctable_tar_matches_tar_of_written_ctable(tmp_path, nrows):
+    """The in-memory result tar has the members, order and contents of tarfile.add over the
+    ctable directory write_ctable creates (worker.py:335-346) -- also for a zero-row result,
+    whose columns have no chunk file but keep their data/ and meta/ directories."""
+    rng = np.random.default_rng(nrows)
+    cols = OrderedDict(k=rng.integers(0, 9, nrows).astype(np.int32), s=rng.normal(size=nrows),
+                       n=np.arange(nrows, dtype=np.int64))
+    d = str(tmp_path / 'result_abcdefgh')
+    bcolz_io.write_ctable(d, cols)
+    ref = worker.tar_directory(d)
+    got = bcolz_io.ctable_tar(cols, 'result_abcdefgh')
+    with tarfile.open(fileobj=io.BytesIO(ref)) as a, tarfile.open(fileobj=io.BytesIO(got)) as b:
+        ma, mb = a.getmembers(), b.getmembers()
+        assert [(m.name, m.isdir()) for m in ma] == [(m.name, m.isdir()) for m in mb]
+        for x, y in zip(ma, mb):
+            if x.isfile():
+                assert a.extractfile(x).read() == b.extractfile(y).read(), x.name
+    assert 'result_abcdefgh/k/data' in [m.name for m in mb]
+    back = rpc.read_shard_results(rpc.tar_of_tars(OrderedDict([('f.bcolzs', got)])))
+    assert len(back) == 1
+    for c in cols:
+        np.testing.assert_array_equal(back[0][c], cols[c])
+
+
+def test_fan_out_and_gather_accounting(tmp_path):
+    """controller.py:471-508 scatter and 146-221 gather, with the node-level patch: the RPC
+    completes only when every file is covered, by its own reply or by a node reply."""
+    files = ['f%d.bcolzs' % i for i in range(5)]
+    spec = [files, ['k'], [['s', 'sum', 's']], []]
+    # without aggregate=True (or without GPU nodes) every file gets its own message
+    assert [a[0] for a in rpc.fan_out(spec, {})] == files
+    assert [a[0] for a in rpc.fan_out(spec, {'aggregate': False}, {'n': files[:3]})] == files
+    msgs = rpc.fan_out(spec, {'aggregate': True}, {'gpu0': files[:3], 'gpu1': ['other.bcolzs']})
+    assert msgs[0][0] == files[:3] and [m[0] for m in msgs[1:]] == files[3:]
+    assert all(m[1:] == spec[1:] for m in msgs)
+    with pytest.raises(ValueError):
+        rpc.fan_out([[], ['k'], [], []], {})
+    tables = []
+    for i in range(3):
+        t = OrderedDict(k=np.array([i, 7], np.int32), s=np.array([1.0, 2.0]))
+        tables.append(t)
+    seg = rpc.CalcSegment(files)
+    assert not seg.add_reply(msgs[1], bcolz_io.ctable_tar(tables[1], 'result_a'))
+    with pytest.raises(RuntimeError):
+        seg.tar()
+    assert not seg.add_reply(msgs[2], '')  # factorization-check early-out: no member
+    with pytest.raises(KeyError):
+        seg.add_reply([['nope.bcolzs']] + spec[1:], b'x')
+    assert seg.add_reply(msgs[0], bcolz_io.ctable_tar(tables[0], 'result_b'))  # covers f0..f2
+    back = rpc.read_shard_results(seg.tar())
+    assert len(back) == 2
+    got = bo.client_merge(back, ['k'], [['s', 'sum', 's']], aggregate=True)
+    ref = bo.client_merge([tables[0], tables[1]], ['k'], [['s', 'sum', 's']], aggregate=True)
+    for c in ref:
+        np.testing.assert_array_equal(np.sort(got[c]), np.sort(ref[c]))
+
+
 # ---------------------------------------------------------------------------- C ABI
 def test_library_exports_every_declared_symbol():
     header = open(os.path.join(os.path.dirname(__file__), '..', 'include', 'bqgpu.h')).read()
@@ -144,7 +202,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(declared) == set(_lib._PROTOS), set(declared) ^ set(_lib._PROTOS)
-    assert lib.bqg_abi_version() == 5
+    assert lib.bqg_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_library_fails_loudly_without_gpu():
