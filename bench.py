@@ -174,6 +174,161 @@ def _load_traffic(config, rows):
     return None, None
 
 
+def _c5_local_ranks(args):
+    """C5 at its full shape on ONE GPU: 80 shards x 12.5 M rows = 1 B rows over
+    ``--local-ranks`` ranks (10 shards each, one libbqgpu context per rank, all on this GPU),
+    each rank's shards aggregated in one pass over their union, then the W-rank
+    ``aggregate=True`` merge (bqg_merge_group over the in-process transport: the code RCCL
+    runs, device copies as the wire).  ``value`` is the measured rate of the whole 1 B-row job
+    on this one GPU (ranks run one after another); the line also projects the 8-GPU node from
+    the measured parts: each rank's shard pass (as it runs alone on a GPU) + the W-rank merge
+    (measured with all ranks sharing this GPU: an upper bound for the merge over xGMI), and
+    measures the one-GPU C5 step (one rank's 10 shards + the world-1 RCCL merge) for the
+    x-over-one-GPU ratio of north_star."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from bqueryd_amd import dist as bdist
+    from bqueryd_amd import synth
+    from bqueryd_amd.engine import Device, ShardTable
+
+    cfg = synth.CONFIGS['c5']
+    W = args.local_ranks
+    per_rank = max(1, cfg['shards'] // 8)  # the 8-GPU layout: 10 shards per rank
+    shard_rows = args.rows or cfg['rows'] // cfg['shards']
+    n_shards = W * per_rank
+    devs = [Device(int(os.environ.get('BQGPU_BENCH_DEVICE', 0))) for _ in range(W)]
+    tables = [[] for _ in range(W)]
+
+    def make(i):
+        return synth.taxi_shard(shard_rows, config_id=5, n_shards=max(cfg['shards'], n_shards), shard=i,
+                                variant=args.variant, columns=synth.query_columns(cfg))
+    with ThreadPoolExecutor(16) as ex:  # numpy's generators release the GIL
+        for i, s in enumerate(ex.map(make, range(n_shards))):
+            tables[i // per_rank].append(ShardTable(s, device=devs[i // per_rank]))
+            del s
+    colos = [bdist.ColocatedShards(t) for t in tables]
+    for c in colos:
+        c.union(synth.query_columns(cfg))  # each rank's shard set, resident once (untimed, like the load)
+    probe, _ = colos[0].groupby_tables(cfg['groupby'], cfg['aggs'])
+    dtypes = {n: np.dtype(probe[0].dtypes[n]) for n in probe[0].names}
+    for p_ in probe:
+        p_.close()
+    group = bdist.CommGroup(devs, transport='local')
+    shard_s = [[] for _ in range(W)]
+    merge_s, timings = [], []
+
+    def step():
+        per = []
+        for r, c in enumerate(colos):
+            t0 = time.perf_counter()
+            p, reduced = c.groupby_tables(cfg['groupby'], cfg['aggs'])
+            shard_s[r].append(time.perf_counter() - t0)
+            timings.append(devs[r].last_timing())
+            per.append(p)
+        t1 = time.perf_counter()
+        merged = bdist.merge_group_device(per, cfg['groupby'], cfg['aggs'], dtypes, group, reduced=True)
+        merge_s.append(time.perf_counter() - t1)
+        for tabs in per:
+            for p in tabs:
+                p.close()
+        return merged
+
+    for _ in range(args.warmup):
+        out = step()
+    if int(out['n'].sum()) != n_shards * shard_rows:
+        raise SystemExit('sanity check failed: %d merged rows' % int(out['n'].sum()))
+    for d in devs:
+        d.enable_timing(True)
+    for lst in shard_s + [merge_s, timings]:
+        del lst[:]
+    for d in devs:
+        d.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    for d in devs:
+        d.synchronize()
+    elapsed = time.perf_counter() - t0
+    group.close()
+
+    # the one-GPU C5 step: rank 0's shards + the world-1 RCCL merge
+    with _stdout_to_stderr():
+        rccl = bdist.RcclComm(devs[0])
+    one_s, one_merge_s = [], []
+    for k in range(args.warmup + args.steps):
+        t0 = time.perf_counter()
+        per, reduced = colos[0].groupby_tables(cfg['groupby'], cfg['aggs'])
+        t1 = time.perf_counter()
+        bdist.merge_partials_device(per, cfg['groupby'], cfg['aggs'], dtypes, rccl, reduced=reduced)
+        for p in per:
+            p.close()
+        if k >= args.warmup:
+            one_s.append(time.perf_counter() - t0)
+            one_merge_s.append(time.perf_counter() - t1)
+    rccl.close()
+    for c in colos:
+        c.close()
+
+    rank_ms = [1e3 * float(np.mean(s)) for s in shard_s]
+    merge_ms = 1e3 * float(np.mean(merge_s))
+    one_ms = 1e3 * float(np.mean(one_s))
+    proj_ms = max(rank_ms) + merge_ms
+    total_rows = n_shards * shard_rows
+    one_rate = per_rank * shard_rows / (one_ms * 1e-3)
+    proj_rate = total_rows / (proj_ms * 1e-3)
+    scan_avg = float(np.mean([t['scan_ms'] for t in timings]))
+    bytes_per_launch = timings[-1]['bytes']
+    achieved = bytes_per_launch / (scan_avg * 1e-3) / 1e9
+    line = {
+        'metric': 'groupby rows/sec (whole node) + achieved HBM GB/s vs peak, 1/2/4/8 GPUs',
+        'value': total_rows * args.steps / elapsed,
+        'unit': 'rows/s',
+        'n_gpus': 1,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': elapsed / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f64',
+        'data': 'synthetic taxi-shaped shards (SURVEY.md §8d generator, %s variant), resident in HBM' % args.variant,
+        'config': {
+            'workload': ('C5 full shape: %d shards x %d rows = %d rows, %d ranks as %d libbqgpu contexts on ONE GPU '
+                         '(in-process transport), groupby %s, aggs %s, aggregate=True merge across the ranks; value = '
+                         'the whole job on this one GPU, ranks one after another' % (
+                             n_shards, shard_rows, total_rows, W, W, cfg['groupby'], [a[1] for a in cfg['aggs']])),
+            'rows_per_rank': per_rank * shard_rows,
+            'parallelism': '%d in-process ranks on one GPU' % W,
+            'shard_pass_ms_per_rank': rank_ms,
+            'merge_ms_all_ranks': merge_ms,
+            'merge': 'bqg_merge_group at world %d: pack kernel, count all-gather, per-column exchange, reduce, '
+                     'gather to rank 0, copy to host; every rank\'s work on this one GPU' % W,
+            'one_gpu': {'ms_per_step': one_ms, 'rows_per_s': one_rate, 'merge_ms_world1': 1e3 * float(np.mean(one_merge_s)),
+                        'what': 'one rank\'s %d shards in one pass + the world-1 RCCL merge (bench.py --config c5 at N=1)'
+                                % per_rank},
+            'projected_node': {'gpus': W, 'ms_per_step': proj_ms, 'rows_per_s': proj_rate,
+                               'x_over_one_gpu': proj_rate / one_rate,
+                               'basis': 'max over ranks of the measured shard pass (each as alone on its GPU) + the '
+                                        'measured %d-rank merge with every rank on one GPU (an upper bound for the '
+                                        'merge over xGMI); not an 8-GPU measurement' % W},
+        },
+        'roofline': {
+            'bound': 'hbm',
+            'achieved': achieved,
+            'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s',
+            'frac': achieved / HBM_PEAK_GBS,
+            'traffic': None,
+            'traffic_source': None,
+            'kernel': KERNELS[timings[-1]['mode'] or 0],
+            'kernel_avg_ms': scan_avg,
+            'algorithmic_bytes_per_launch': bytes_per_launch,
+        },
+        'cpu_baseline': None,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -186,7 +341,11 @@ def main(argv=None):
     ap.add_argument('--rows', type=int, default=None, help='override rows per shard')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--variant', default='exact', choices=['exact', 'raw'])
+    ap.add_argument('--local-ranks', type=int, default=1,
+                    help='C5: the full 80-shard workload over this many ranks as contexts on one GPU')
     args = ap.parse_args(argv)
+    if args.config == 'c5' and args.local_ranks > 1:
+        return _c5_local_ranks(args)
 
     ws, rank, local = _dist_env()
     comm = _Comm(ws)

@@ -306,7 +306,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -330,6 +330,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"small_emit", 1, 0, 1},                // one-workgroup emit for <= 8192 slots
     {"hash_slots", 0, 0, 1ll << 31},        // initial hash-table slots (0: from the row count)
     {"distinct_slots", 0, 0, 1ll << 31},    // initial count_distinct set slots (0: from rows)
+    {"part_pack", 1, 0, 1},                 // packed 4-byte partition entries when they fit
 };
 
 static int opt_index(const char* name) {
@@ -1058,47 +1059,108 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
           L.enc_off[q] = cs.empty ? 0 : cs.imin;
         }
       }
-      const bool nw = L.narrow != 0;
-      c->last.narrow = L.narrow;
-      // scatter workgroup: the widest whose staged tile fits in LDS (option part_threads caps it)
-      L.threads = c->opt[kOptPartThreads] ? (int)c->opt[kOptPartThreads] : 1024;
-      while (L.threads > 256 && part_scatter_lds(L.nparts, L.threads, nsum, 1, nw) > 150 * 1024) L.threads >>= 1;
-      // 8192-row tiles (two 4-row chunks per thread) when the staged tile fits: the aggregate's
-      // per-tile partition segments are twice as long (option part_k=1|2 forces the choice)
-      L.k = (L.threads == 1024 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw) <= 150 * 1024) ? 2 : 1;
-      if (c->opt[kOptPartK])
-        L.k = (c->opt[kOptPartK] == 2 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw) <= 150 * 1024) ? 2 : 1;
-      L.tile_rows = L.threads * kRowsPerThread * L.k;
+      // packed 4-byte entries (option part_pack): no summed column, or one narrow-coded
+      // column whose codes span at most 2^16 values -- {code16, slot_low} per entry
+      L.pack = 0;
+      uint64_t span16 = 0;
+      if (c->opt[kOptPartPack] && pl.wbits <= 16 && (nsum == 0 || (nsum == 1 && L.narrow))) {
+        L.pack = 1;
+        L.enc_base16 = 0;
+        const ColStats& cs = nsum ? t->cols[pl.tcol[0]].stats : ColStats{};
+        if (nsum && !cs.empty) {
+          if (L.enc_kind[0] == 3) {
+            span16 = (uint64_t)cs.imax - (uint64_t)cs.imin;  // codes are v - min already
+          } else {
+            // the device's code of a value is monotonic in it: the codes of min and max bound all
+            const double lo = cs.fmin * L.enc_mul[0], hi = cs.fmax * L.enc_mul[0];
+            const int64_t clo = (int64_t)(L.enc_kind[0] == 1 ? lo : std::rint(lo));
+            const int64_t chi = (int64_t)(L.enc_kind[0] == 1 ? hi : std::rint(hi));
+            span16 = (uint64_t)(chi - clo);
+            L.enc_base16 = clo;
+          }
+          if (span16 > 0xFFFFull) L.pack = 0;
+        }
+      }
+      auto bit_width = [](uint64_t v) {
+        int b = 0;
+        while (v) {
+          ++b;
+          v >>= 1;
+        }
+        return b;
+      };
+      auto shape = [&]() {
+        const bool nw = L.narrow != 0, pk = L.pack != 0;
+        // scatter workgroup: the widest whose staged tile fits in LDS (option part_threads caps it)
+        L.threads = c->opt[kOptPartThreads] ? (int)c->opt[kOptPartThreads] : 1024;
+        while (L.threads > 256 && part_scatter_lds(L.nparts, L.threads, nsum, 1, nw, pk) > 150 * 1024) L.threads >>= 1;
+        // 8192-row tiles (two 4-row chunks per thread) when the staged tile fits: the aggregate's
+        // per-tile partition segments are twice as long (option part_k=1|2 forces the choice)
+        L.k = (L.threads == 1024 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw, pk) <= 150 * 1024) ? 2 : 1;
+        if (c->opt[kOptPartK])
+          L.k = (c->opt[kOptPartK] == 2 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw, pk) <= 150 * 1024) ? 2 : 1;
+        L.tile_rows = L.threads * kRowsPerThread * L.k;
+        const int64_t tr = L.tile_rows;
+        L.ntiles = (N + tr - 1) / tr;
+        // contiguous whole-tile row ranges, as many scatter workgroups per CU as fit in LDS
+        int per_cu = L.k == 2 ? 1 : 2;
+        if (c->opt[kOptPartPerCu]) per_cu = (int)c->opt[kOptPartPerCu];
+        L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, L.ntiles));
+        L.rows_per_block = ((L.ntiles + L.blocks - 1) / L.blocks) * tr;
+        L.blocks = (int)((N + L.rows_per_block - 1) / L.rows_per_block);
+        // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
+        // slot table allows one per CU)
+        const size_t agg_lds = part_agg_lds(L.wbits, nsum, pk);
+        const int fit = std::max(1, (int)((160 * 1024) / agg_lds));
+        L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, (c->cu * fit + L.nparts / 2) / L.nparts));
+        if (c->opt[kOptPartSplits]) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, c->opt[kOptPartSplits]));
+        if (pk) {
+          // the packed accumulator of one split: count < 2^cbits, code16 sum < 2^(64 - cbits);
+          // more splits (fewer rows each) until both fields fit, else the 8-byte entries
+          for (;;) {
+            const uint64_t R = (uint64_t)((L.ntiles + L.splits - 1) / L.splits) * (uint64_t)tr;
+            const int cbits = bit_width(R);
+            L.sbits = 64 - cbits;
+            const bool fits = span16 == 0 || (R <= (~0ull) / span16 && bit_width(R * span16) <= L.sbits);
+            if (fits) break;
+            if (L.splits >= L.ntiles) {
+              L.pack = 0;
+              return false;
+            }
+            L.splits = (int)std::min<int64_t>(L.ntiles, 2 * (int64_t)L.splits);
+          }
+        }
+        return true;
+      };
+      if (!shape()) shape();
+      const bool nw = L.narrow != 0, pk = L.pack != 0;
+      c->last.narrow = pk ? 2 : L.narrow;
       const int64_t tr = L.tile_rows;
-      L.ntiles = (N + tr - 1) / tr;
-      // contiguous whole-tile row ranges, as many scatter workgroups per CU as fit in LDS
-      int per_cu = L.k == 2 ? 1 : 2;
-      if (c->opt[kOptPartPerCu]) per_cu = (int)c->opt[kOptPartPerCu];
-      L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, L.ntiles));
-      L.rows_per_block = ((L.ntiles + L.blocks - 1) / L.blocks) * tr;
-      L.blocks = (int)((N + L.rows_per_block - 1) / L.rows_per_block);
-      // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
-      // slot table allows one per CU)
-      const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)nsum);
-      const int fit = std::max(1, (int)((160 * 1024) / agg_lds));
-      L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, (c->cu * fit + L.nparts / 2) / L.nparts));
-      if (c->opt[kOptPartSplits]) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, c->opt[kOptPartSplits]));
       L.capacity = (uint64_t)L.ntiles * (uint64_t)tr;
       L.hdr = (uint16_t*)c->prefix.ensure((size_t)L.ntiles * (size_t)(L.nparts + 1) * 2 + 256);
       // one scratch block: entry values | entry meta | split partial tables | arrival counters
-      const size_t vbytes = ((size_t)L.capacity * (nw ? 4 : 8) * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
+      // (| pack: first tiles, tile marks)
+      const size_t vbytes = pk ? 0 : ((size_t)L.capacity * (nw ? 4 : 8) * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
       const size_t mbytes = ((size_t)L.capacity * 4 + 255) & ~size_t(255);
-      L.partial_bytes = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)nsum);
+      L.partial_bytes = (part_agg_lds(L.wbits, nsum, pk) + 255) & ~size_t(255);
       const size_t pbytes = L.splits > 1 ? (size_t)L.nparts * L.splits * L.partial_bytes : 0;
-      unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + mbytes + pbytes + (size_t)L.nparts * 4 + 512);
+      const size_t abytes = ((size_t)L.nparts * 4 + 255) & ~size_t(255);
+      const size_t fbytes = pk ? (((size_t)L.nparts << L.wbits) * 4 + 255) & ~size_t(255) : 0;
+      unsigned char* eb =
+          (unsigned char*)c->bitmap.ensure(vbytes + mbytes + pbytes + abytes + fbytes + (pk ? (size_t)L.ntiles : 0) + 512);
       L.vals = (unsigned long long*)eb;
       L.meta = (uint32_t*)(eb + vbytes);
       L.partial = eb + vbytes + mbytes;
       L.arrive = (unsigned int*)(eb + vbytes + mbytes + pbytes);
+      if (pk) {
+        L.first_tile = (uint32_t*)(eb + vbytes + mbytes + pbytes + abytes);
+        L.tile_mark = eb + vbytes + mbytes + pbytes + abytes + fbytes;
+      }
       hipFunction_t fs = nullptr;
       if (c->opt[kOptJit] && N >= c->opt[kOptJitMinRows]) {
         fs = jit_function("bq_jit_part_scatter", jit_spec(pl.p) + "#define BQ_PART_K " + std::to_string(L.k) +
-                                                      "\n#define BQ_PART_NARROW " + std::to_string(L.narrow) + "\n");
+                                                      "\n#define BQ_PART_NARROW " + std::to_string(L.narrow) +
+                                                      "\n#define BQ_PART_PACK " + std::to_string(L.pack) + "\n");
         c->last.specialized = fs ? 1 : 0;
       }
       launch_partitioned(pl.p, sa, L, st, fs);
@@ -1117,28 +1179,19 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
 
   // ---- std: centered second moments
   if (nsum2) {
-    // means per slot into scratch: centers[v][s] = acc[v][s] / cnt[s]  (computed on host side of
-    // a tiny kernel would be nicer; use a D2H/H2D round trip only for small S, else device)
-    DevBuf& mb = c->misc;
-    double* centers = (double*)mb.ensure((size_t)nsum2 * S * 8 + 64);
-    std::vector<double> hc((size_t)nsum2 * S);
-    std::vector<unsigned long long> hcnt(S), hacc((size_t)nsum * S);
-    HIPCHECK(hipMemcpyAsync(hcnt.data(), sa.cnt, S * 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(hacc.data(), sa.acc, (size_t)nsum * S * 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    // means per slot, on device: centers[i][s] = acc[v][s] / cnt[s] for the i-th std column v
+    double* centers = (double*)c->misc.ensure((size_t)nsum2 * S * 8 + 64);
+    StdCenters sc{};
+    sc.n = nsum2;
+    if (nsum2 > kMaxSums) fail(BQG_E_UNSUPPORTED, "more than %d std columns", kMaxSums);
     for (int i = 0; i < nsum2; ++i) {
       const int v = pl.std_cols[i];
       const int dt = t->cols[pl.tcol[v]].dtype;
-      for (uint64_t s = 0; s < S; ++s) {
-        double sum;
-        if (dtype_is_float(dt)) memcpy(&sum, &hacc[(size_t)v * S + s], 8);
-        else if (dt == BQG_U64) sum = (double)(uint64_t)hacc[(size_t)v * S + s];
-        else sum = (double)(int64_t)hacc[(size_t)v * S + s];
-        hc[(size_t)i * S + s] = hcnt[s] ? sum / (double)hcnt[s] : 0.0;
-      }
+      sc.state[i] = v;
+      sc.conv[i] = dtype_is_float(dt) ? 0 : dt == BQG_U64 ? 2 : 1;
     }
-    HIPCHECK(hipMemcpyAsync(centers, hc.data(), hc.size() * 8, hipMemcpyHostToDevice, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    launch_std_centers(sa.cnt, sa.acc, sc, S, centers, st);
+    HIPCHECK(hipGetLastError());
     Plan p2 = pl;
     // sum states of pass 2: the std columns, centered, in std order (they are the first
     // nsum2 scan columns after re-ordering)
@@ -1864,14 +1917,17 @@ int bqg_table_sync(bqg_table* t) {
 }
 
 int bqg_table_nrows(bqg_table* t, int64_t* nrows) {
+  if (!t) return BQG_E_INVALID;
   return guard(t->ctx, [&] { *nrows = t->nrows; });
 }
 
 int bqg_table_ncols(bqg_table* t, int32_t* ncols) {
+  if (!t) return BQG_E_INVALID;
   return guard(t->ctx, [&] { *ncols = (int32_t)t->cols.size(); });
 }
 
 int bqg_table_dtype(bqg_table* t, int32_t col, int32_t* dtype) {
+  if (!t) return BQG_E_INVALID;
   return guard(t->ctx, [&] {
     if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
     *dtype = t->cols[col].dtype;
@@ -1879,6 +1935,7 @@ int bqg_table_dtype(bqg_table* t, int32_t col, int32_t* dtype) {
 }
 
 int bqg_table_column_ptr(bqg_table* t, int32_t col, void** dev_ptr) {
+  if (!t) return BQG_E_INVALID;
   return guard(t->ctx, [&] {
     if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
     *dev_ptr = t->cols[col].dev;
@@ -2120,10 +2177,12 @@ int bqg_factorize(bqg_ctx* c, bqg_table* t, int32_t col, int64_t* labels, void* 
     if (col < 0 || col >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", col);
     if (!n_values) fail(BQG_E_INVALID, "null n_values");
     Column& k = t->cols[col];
-    if (dtype_is_float(k.dtype) || k.dtype == BQG_BOOL) fail(BQG_E_UNSUPPORTED, "factor cache of a float / bool column");
     compute_stats(t, col);
-    const uint64_t range = k.stats.empty ? 1 : (uint64_t)k.stats.imax - (uint64_t)k.stats.imin + 1;
-    if (range == 0 || range > (1ull << 27)) fail(BQG_E_UNSUPPORTED, "factor cache of a column spanning more than 2^27 values");
+    // labels by a lookup table lut[v - min] for integer columns spanning at most 2^27 values,
+    // else (floats, bools, wider spans) by a hash of the canonical key bits
+    const bool integer = !dtype_is_float(k.dtype) && k.dtype != BQG_BOOL;
+    const uint64_t range = (!integer || k.stats.empty) ? 1 : (uint64_t)k.stats.imax - (uint64_t)k.stats.imin + 1;
+    const bool use_lut = integer && range != 0 && range <= (1ull << 27);
     // distinct values in first-appearance order: a groupby over the column with no aggregation
     bqg_table* vt = nullptr;
     {
@@ -2146,15 +2205,23 @@ int bqg_factorize(bqg_ctx* c, bqg_table* t, int32_t col, int64_t* labels, void* 
     *n_values = G;
     if (values && G > values_cap) fail(BQG_E_INVALID, "values buffer holds %lld, column has %lld distinct values",
                                        (long long)values_cap, (long long)G);
-    const int64_t vmin = k.stats.empty ? 0 : k.stats.imin;
-    int32_t* lut = (int32_t*)c->misc.ensure(range * 4 + 256);
+    const int64_t vmin = (!integer || k.stats.empty) ? 0 : k.stats.imin;
     const bool dev_out = labels && mem_kind(labels) == 2;
     long long* out = nullptr;
     if (labels) out = dev_out ? (long long*)labels : (long long*)c->outcols.ensure((size_t)t->nrows * 8 + 256);
     const Column& vc = vt->cols[0];
     if (labels) {
-      launch_factor_labels(DevCol{vc.dev, vc.dtype, dtype_lg(vc.dtype)}, G, DevCol{k.dev, k.dtype, dtype_lg(k.dtype)},
-                           t->nrows, vmin, lut, out, c->stream);
+      const DevCol dvals{vc.dev, vc.dtype, dtype_lg(vc.dtype)}, dcol{k.dev, k.dtype, dtype_lg(k.dtype)};
+      if (use_lut) {
+        int32_t* lut = (int32_t*)c->misc.ensure(range * 4 + 256);
+        launch_factor_labels(dvals, G, dcol, t->nrows, vmin, lut, out, c->stream);
+      } else {
+        uint64_t cap = 64;
+        while (cap < 2 * (uint64_t)G) cap <<= 1;
+        unsigned char* hb = (unsigned char*)c->misc.ensure(cap * 12 + 256);
+        launch_factor_hash_labels(dvals, G, dcol, t->nrows, cap, (unsigned long long*)hb, (uint32_t*)(hb + cap * 8), out,
+                                  c->stream);
+      }
       HIPCHECK(hipGetLastError());
       if (!dev_out && t->nrows)
         HIPCHECK(hipMemcpyAsync(labels, out, (size_t)t->nrows * 8, hipMemcpyDeviceToHost, c->stream));

@@ -7,20 +7,23 @@
 //   1. local:     this rank's shard tables are concatenated (device to device) and summed by
 //                 key (bqg_groupby_table) -- skipped when the caller's one table is already
 //                 reduced (a co-located one-pass groupby over the rank's shards);
-//   2. partition: every row goes to rank hash(key values) mod nranks (bqg_hash_partition: a
-//                 pure function of the values, identical on every rank) -- packed per
-//                 destination, column by column, into one send buffer;
-//   3. exchange:  the [nranks x nranks] row-count matrix (ncclAllGather), then the payload
-//                 (grouped ncclSend / ncclRecv, one message per peer, self included);
+//   2. partition: every row goes to rank hash(key values) mod nranks (the partition function
+//                 of bqg_hash_partition: a pure function of the values, identical on every
+//                 rank) -- one stable scatter (k_mpack_*) writes each row straight into its
+//                 destination's packed block, whose row counts land on the device;
+//   3. exchange:  the [nranks x nranks] row-count matrix (ncclAllGather, then the one host
+//                 read of the exchange), then the payload (grouped ncclSend / ncclRecv, one
+//                 message per peer and column, self included) straight into the receiving
+//                 rank's table columns;
 //   4. reduce:    the received rows are summed by key again (keys are disjoint across ranks);
-//   5. gather:    the reduced partitions travel to rank 0 (grouped send / recv) and are
-//                 concatenated there in rank order.
+//   5. gather:    the reduced partitions travel to rank 0 column by column (grouped send /
+//                 recv), straight into the result table, in rank order.
 // Only the row counts cross to the host (to size buffers).  librccl is loaded with dlopen on
 // first use, so libbqgpu itself loads where RCCL is absent; every entry here then fails with
 // a message instead.
 //
-// The merge is built from the library's own public entry points (groupby, partition,
-// select, push); this file adds the communicator and the exchange.  It runs any number of
+// The merge is built from the library's own public entry points (groupby, push) plus the pack
+// kernels; this file adds the communicator and the exchange.  It runs any number of
 // local ranks from ONE host thread: bqg_merge drives one rank of a multi-process job (one
 // process per GPU), bqg_merge_group every rank of a process that owns several GPUs, with the
 // collective calls of all of them inside one ncclGroupStart / ncclGroupEnd.
@@ -37,6 +40,7 @@
 #include <vector>
 
 #include "ctx_internal.h"
+#include "kernels.h"
 
 namespace {
 
@@ -138,7 +142,7 @@ struct Buf {
 struct CommState {
   ncclComm_t comm = nullptr;  // RCCL transport; nullptr = in-process transport (see below)
   int rank = 0, nranks = 1;
-  Buf send, recv, counts;
+  Buf send, scratch, counts;  // packed send blocks, pack scratch, row counts
 };
 
 std::mutex g_mu;
@@ -156,7 +160,7 @@ void destroy_state(CommState* s) {
   if (s->comm) (void)rccl().CommDestroy(s->comm);
   if (s->comm == nullptr) (void)hipDeviceSynchronize();  // in-process copies may target its buffers
   s->send.release();
-  s->recv.release();
+  s->scratch.release();
   s->counts.release();
   delete s;
 }
@@ -262,40 +266,28 @@ struct Local {
   std::vector<bqg_table*> tables;
   CommState* st = nullptr;
   hipStream_t stream = nullptr;
-  TableOwner L;                   // this rank's reduced rows (+ partition column)
+  TableOwner L;                   // this rank's reduced rows (when the caller's are not)
   bqg_table* Lv = nullptr;        // the table whose rows this rank sends (L, or the caller's)
+  int64_t nl = 0;                 // rows of Lv
   std::vector<int64_t> to_peer;   // rows for each destination rank
-  std::vector<size_t> send_off;   // byte offset of each destination's block
+  std::vector<int64_t> from_peer; // rows from each source rank
   TableOwner R;                   // rows received from every rank, then reduced
-  int64_t n_recv = 0;
   bqg_table** out = nullptr;
 };
 
-// bytes of a packed block of `rows` rows: columns one after another, 16-byte aligned
-size_t block_bytes(const std::vector<int32_t>& dts, int64_t rows) {
-  size_t b = 0;
-  for (int32_t dt : dts) b += align16((size_t)rows * dt_size(dt));
-  return b;
-}
-
-// copy the first `rows` rows of every column of `t` into a packed block at `dst`
-void pack_block(bqg_ctx* c, hipStream_t st, bqg_table* t, const std::vector<int32_t>& dts, int64_t rows,
-                unsigned char* dst) {
-  for (int j = 0; j < (int)dts.size(); ++j) {
-    const size_t nb = (size_t)rows * dt_size(dts[j]);
-    if (nb) HIPCK(hipMemcpyAsync(dst, col_ptr(c, t, j), nb, hipMemcpyDeviceToDevice, st));
-    dst += align16(nb);
+int lg_of(int32_t dt) {
+  switch (dt_size(dt)) {
+    case 1: return 0;
+    case 2: return 1;
+    case 4: return 2;
+    default: return 3;
   }
 }
 
-// append a packed block of `rows` rows to table `t` at row `off`
-void unpack_block(bqg_ctx* c, bqg_table* t, const std::vector<int32_t>& dts, int64_t rows, int64_t off,
-                  const unsigned char* src) {
-  for (int j = 0; j < (int)dts.size(); ++j) {
-    const size_t nb = (size_t)rows * dt_size(dts[j]);
-    if (nb) ck(c, bqg_push_chunk(t, j, src, rows, off));
-    src += align16(nb);
-  }
+// one 64-bit count into device memory without a host round trip (two 32-bit fills)
+void put_count(int64_t* dst, int64_t v, hipStream_t st) {
+  HIPCK(hipMemsetD32Async((hipDeviceptr_t)dst, (int)(uint32_t)(uint64_t)v, 1, st));
+  HIPCK(hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)dst + 1), (int)(uint32_t)((uint64_t)v >> 32), 1, st));
 }
 
 
@@ -304,6 +296,8 @@ void unpack_block(bqg_ctx* c, bqg_table* t, const std::vector<int32_t>& dts, int
 // of this call (bqg_comm_init_local: one process driving several contexts, possibly on one
 // GPU -- the test harness for the exchange logic on a one-GPU machine)
 // ------------------------------------------------------------------------------------
+// one message; the messages between one (sender, receiver) pair are matched in the order they
+// are posted, as RCCL matches grouped send / receive operations with the same peer
 struct P2P {
   int peer;
   void* ptr;
@@ -349,7 +343,7 @@ void xfer_allgather_i64(std::vector<Local>& ranks, size_t count) {
   sync_all(ranks);
 }
 
-// grouped point-to-point: sends[i] / recvs[i] of local rank i (matching pairs on both sides)
+// grouped point-to-point: sends[i] / recvs[i] of local rank i (matching lists on both sides)
 void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& sends,
               const std::vector<std::vector<P2P>>& recvs) {
   if (ranks[0].st->comm) {
@@ -367,13 +361,19 @@ void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& se
   for (size_t i = 0; i < ranks.size(); ++i) {
     Local& d = ranks[i];
     HIPCK(hipSetDevice(bqg_internal_device(d.ctx)));
+    std::vector<size_t> taken(ranks.size(), 0);  // messages of each sender matched so far
     for (const P2P& x : recvs[i]) {
       size_t j = 0;
       while (j < ranks.size() && ranks[j].st->rank != x.peer) ++j;
       if (j == ranks.size()) comm_fail(BQG_E_STATE, "in-process transport: peer rank not in this merge call");
       const P2P* m = nullptr;
+      size_t k = 0;
       for (const P2P& y : sends[j])
-        if (y.peer == d.st->rank) m = &y;
+        if (y.peer == d.st->rank && k++ == taken[j]) {
+          m = &y;
+          break;
+        }
+      ++taken[j];
       if (!m || m->bytes != x.bytes) comm_fail(BQG_E_STATE, "in-process transport: unmatched send / receive");
       HIPCK(hipMemcpyAsync(x.ptr, m->ptr, x.bytes, hipMemcpyDefault, d.stream));
     }
@@ -383,8 +383,10 @@ void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& se
 
 void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t>& dts, int reduced) {
   const int ncols = (int)dts.size();
-  if (n_keys < 1 || n_keys > ncols) comm_fail(BQG_E_INVALID, "merge needs 1..ncols key columns");
+  if (n_keys < 1 || n_keys > ncols || n_keys > bqg::kMaxKeys) comm_fail(BQG_E_INVALID, "merge needs 1..4 key columns");
+  if (ncols > bqg::kMergeMaxCols) comm_fail(BQG_E_UNSUPPORTED, "merge schema has too many columns");
   const int W = ranks[0].st->nranks;
+  if (W > bqg::kMergeMaxRanks) comm_fail(BQG_E_UNSUPPORTED, "merge across more than 256 ranks");
   for (Local& l : ranks) {
     if (l.st->nranks != W) comm_fail(BQG_E_INVALID, "local ranks of one merge must share a communicator size");
     for (bqg_table* t : l.tables) {
@@ -398,197 +400,181 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       }
     }
   }
-  // 1-2. local reduce and partition by destination
-  std::vector<int32_t> key_idx(n_keys);
-  for (int k = 0; k < n_keys; ++k) key_idx[k] = k;
-  std::vector<int32_t> sel(ncols);
-  for (int j = 0; j < ncols; ++j) sel[j] = j;
+  std::vector<int> lg(ncols);
+  size_t row_bytes = 0;
+  for (int j = 0; j < ncols; ++j) {
+    lg[j] = lg_of(dts[j]);
+    row_bytes += dt_size(dts[j]);
+  }
+  // byte offset of column j of destination d's packed block (k_mpack_scan's layout)
+  auto packed_base = [&](const std::vector<int64_t>& rows, int d, int j) {
+    size_t off = 0;
+    for (int dd = 0; dd <= d; ++dd)
+      for (int jj = 0; jj < ncols; ++jj) {
+        if (dd == d && jj == j) return off;
+        off += align16((size_t)rows[dd] << lg[jj]);
+      }
+    return off;
+  };
+  // 1-2. local reduce, then every row straight into its destination's packed block
   for (Local& l : ranks) {
     HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-    l.to_peer.assign(W, 0);
     std::vector<bqg_table*> parts;
     for (bqg_table* t : l.tables)
       if (nrows_of(l.ctx, t) > 0) parts.push_back(t);
     if (!parts.empty()) {
-      if (reduced && parts.size() == 1 && W == 1) {
-        l.Lv = parts[0];  // one rank, keys already unique: the caller's table is sent as it is
+      if (reduced && parts.size() == 1) {
+        l.Lv = parts[0];  // keys already unique (a one-pass groupby over the rank's shards)
       } else {
         TableOwner cat;
         cat.t = concat_tables(l.ctx, parts, dts);
-        if (reduced && parts.size() == 1) l.L.t = cat.release();
-        else l.L.t = regroup(l.ctx, cat.t, n_keys, ncols);
+        l.L.t = regroup(l.ctx, cat.t, n_keys, ncols);
         l.Lv = l.L.t;
       }
     }
-    const int64_t nl = l.Lv ? nrows_of(l.ctx, l.Lv) : 0;
-    std::vector<bqg_table*> per(W, nullptr);
-    struct PerOwner {
-      std::vector<bqg_table*>& v;
-      ~PerOwner() {
-        for (bqg_table* t : v)
-          if (t) (void)bqg_table_destroy(t);
+    l.nl = l.Lv ? nrows_of(l.ctx, l.Lv) : 0;
+    int64_t* cnt = (int64_t*)l.st->counts.ensure(sizeof(int64_t) * ((size_t)W * (W + 1) + 2));
+    if (W == 1) {
+      put_count(cnt, l.nl, l.stream);  // one rank: every row goes to itself, sent as it is
+    } else if (l.nl == 0) {
+      HIPCK(hipMemsetAsync(cnt, 0, sizeof(int64_t) * W, l.stream));
+    } else {
+      bqg::MergePack m{};
+      m.keys.nkeys = n_keys;
+      for (int k = 0; k < n_keys; ++k)
+        m.keys.cols[k] = bqg::DevCol{(const unsigned char*)col_ptr(l.ctx, l.Lv, k), dts[k], lg[k]};
+      for (int j = 0; j < ncols; ++j) {
+        m.cols[j] = (const unsigned char*)col_ptr(l.ctx, l.Lv, j);
+        m.lg[j] = lg[j];
       }
-    } per_owner{per};
-    if (nl > 0 && W == 1) {
-      l.to_peer[0] = nl;  // one rank: every row goes to itself, no partition pass
-    } else if (nl > 0) {
-      int32_t pcol = -1;
-      ck(l.ctx, bqg_table_add_column(l.L.t, BQG_U32, &pcol));
-      ck(l.ctx, bqg_hash_partition(l.ctx, l.L.t, n_keys, key_idx.data(), W, pcol, l.to_peer.data()));
-      for (int d = 0; d < W; ++d) {
-        if (!l.to_peer[d]) continue;
-        const int64_t dv = d;
-        bqg_term term{pcol, BQG_T_EQ, 1, &dv, nullptr};
-        bqg_query q{};
-        q.n_terms = 1;
-        q.terms = &term;
-        q.mask_col = -1;
-        ck(l.ctx, bqg_select_rows_table(l.ctx, l.L.t, &q, ncols, sel.data(), &per[d]));
-      }
+      m.ncols = ncols;
+      m.nranks = W;
+      m.nrows = l.nl;
+      bqg::merge_pack_grid(l.nl, &m.nblocks, &m.rows_per_block);
+      const size_t dest_b = align16((size_t)l.nl), hist_b = align16((size_t)m.nblocks * W * 4);
+      unsigned char* scr = (unsigned char*)l.st->scratch.ensure(dest_b + hist_b + (size_t)W * ncols * 8);
+      m.dest = scr;
+      m.block_hist = (uint32_t*)(scr + dest_b);
+      m.colbase = (unsigned long long*)(scr + dest_b + hist_b);
+      m.to_peer = (unsigned long long*)cnt;
+      m.send = (unsigned char*)l.st->send.ensure((size_t)l.nl * row_bytes + (size_t)W * ncols * 16);
+      bqg::launch_merge_pack(m, l.stream);
+      HIPCK(hipGetLastError());
     }
-    l.send_off.assign(W + 1, 0);
-    for (int d = 0; d < W; ++d) l.send_off[d + 1] = l.send_off[d] + block_bytes(dts, l.to_peer[d]);
-    unsigned char* sb = (unsigned char*)l.st->send.ensure(l.send_off[W]);
-    for (int d = 0; d < W; ++d)
-      if (l.to_peer[d]) pack_block(l.ctx, l.stream, W == 1 ? l.Lv : per[d], dts, l.to_peer[d], sb + l.send_off[d]);
-    // the row counts this rank sends, for the count exchange
-    int64_t* cnt = (int64_t*)l.st->counts.ensure(sizeof(int64_t) * (size_t)W * (W + 2));
-    HIPCK(hipMemcpyAsync(cnt, l.to_peer.data(), sizeof(int64_t) * W, hipMemcpyHostToDevice, l.stream));
-    HIPCK(hipStreamSynchronize(l.stream));  // to_peer (host) is read by the copy; per[] is freed next
   }
   // 3a. count matrix: every rank's row counts per destination
   xfer_allgather_i64(ranks, (size_t)W);
-  std::vector<std::vector<int64_t>> from_peer(ranks.size(), std::vector<int64_t>(W, 0));
-  for (size_t i = 0; i < ranks.size(); ++i) {
-    Local& l = ranks[i];
+  for (Local& l : ranks) {
     HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
     std::vector<int64_t> m((size_t)W * W);
     HIPCK(hipMemcpyAsync(m.data(), (int64_t*)l.st->counts.p + W, sizeof(int64_t) * W * W, hipMemcpyDeviceToHost,
                          l.stream));
     HIPCK(hipStreamSynchronize(l.stream));
-    for (int s = 0; s < W; ++s) from_peer[i][s] = m[(size_t)s * W + l.st->rank];
+    l.to_peer.assign(m.begin() + (size_t)l.st->rank * W, m.begin() + (size_t)(l.st->rank + 1) * W);
+    l.from_peer.assign(W, 0);
+    for (int s = 0; s < W; ++s) l.from_peer[s] = m[(size_t)s * W + l.st->rank];
   }
-  // 3b. payload: one packed block per (source, destination) pair
-  std::vector<std::vector<size_t>> recv_off(ranks.size());
-  for (size_t i = 0; i < ranks.size(); ++i) {
-    Local& l = ranks[i];
-    recv_off[i].assign(W + 1, 0);
-    for (int s = 0; s < W; ++s) recv_off[i][s + 1] = recv_off[i][s] + block_bytes(dts, from_peer[i][s]);
-    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-    l.st->recv.ensure(recv_off[i][W]);
-  }
+  // 3b. payload: column by column, straight into the receiving rank's table
   {
     std::vector<std::vector<P2P>> sends(ranks.size()), recvs(ranks.size());
     for (size_t i = 0; i < ranks.size(); ++i) {
       Local& l = ranks[i];
-      unsigned char* sb = (unsigned char*)l.st->send.p;
-      unsigned char* rb = (unsigned char*)l.st->recv.p;
-      for (int p = 0; p < W; ++p) {
-        const size_t sbytes = l.send_off[p + 1] - l.send_off[p];
-        const size_t rbytes = recv_off[i][p + 1] - recv_off[i][p];
-        if (sbytes) sends[i].push_back(P2P{p, sb + l.send_off[p], sbytes});
-        if (rbytes) recvs[i].push_back(P2P{p, rb + recv_off[i][p], rbytes});
+      HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+      for (int d = 0; d < W; ++d) {
+        if (!l.to_peer[d]) continue;
+        for (int j = 0; j < ncols; ++j) {
+          void* src = W == 1 ? col_ptr(l.ctx, l.Lv, j) : (unsigned char*)l.st->send.p + packed_base(l.to_peer, d, j);
+          sends[i].push_back(P2P{d, src, (size_t)l.to_peer[d] << lg[j]});
+        }
+      }
+      int64_t total = 0;
+      for (int s = 0; s < W; ++s) total += l.from_peer[s];
+      if (!total) continue;
+      ck(l.ctx, bqg_table_create(l.ctx, total, ncols, dts.data(), &l.R.t));
+      int64_t off = 0;
+      for (int s = 0; s < W; ++s) {
+        if (!l.from_peer[s]) continue;
+        for (int j = 0; j < ncols; ++j)
+          recvs[i].push_back(P2P{s, (unsigned char*)col_ptr(l.ctx, l.R.t, j) + ((size_t)off << lg[j]),
+                                 (size_t)l.from_peer[s] << lg[j]});
+        off += l.from_peer[s];
       }
     }
     xfer_p2p(ranks, sends, recvs);
   }
-  // 4. reduce the received rows
-  std::vector<int64_t> reduced_rows(ranks.size(), 0);
-  for (size_t i = 0; i < ranks.size(); ++i) {
-    Local& l = ranks[i];
-    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-    l.L.reset();  // the local rows have been sent
-    l.Lv = nullptr;
-    int64_t total = 0;
-    for (int s = 0; s < W; ++s) total += from_peer[i][s];
-    l.n_recv = total;
-    if (!total) continue;
-    TableOwner got;
-    ck(l.ctx, bqg_table_create(l.ctx, total, ncols, dts.data(), &got.t));
-    int64_t off = 0;
-    for (int s = 0; s < W; ++s) {
-      unpack_block(l.ctx, got.t, dts, from_peer[i][s], off, (const unsigned char*)l.st->recv.p + recv_off[i][s]);
-      off += from_peer[i][s];
-    }
-    // one source's rows are already unique by key: only rows from two or more sources
-    // need the re-group
-    int sources = 0;
-    for (int s = 0; s < W; ++s) sources += from_peer[i][s] > 0;
-    l.R.t = sources > 1 ? regroup(l.ctx, got.t, n_keys, ncols) : got.release();
-    reduced_rows[i] = nrows_of(l.ctx, l.R.t);
-  }
-  // 5. gather to rank 0: counts, then the packed partitions
+  // 4. reduce the received rows: one source's rows are already unique by key, only rows from
+  // two or more sources need the re-group
   for (Local& l : ranks) {
     HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+    l.L.reset();  // sent (stream-ordered before any later use of its memory)
+    l.Lv = nullptr;
+    int sources = 0;
+    for (int s = 0; s < W; ++s) sources += l.from_peer[s] > 0;
+    if (sources > 1) {
+      TableOwner got;
+      got.t = l.R.release();
+      l.R.t = regroup(l.ctx, got.t, n_keys, ncols);
+    }
     int64_t* cnt = (int64_t*)l.st->counts.p;
-    const int64_t mine = l.R.t ? nrows_of(l.ctx, l.R.t) : 0;
-    HIPCK(hipMemcpyAsync(cnt, &mine, sizeof(int64_t), hipMemcpyHostToDevice, l.stream));
-    HIPCK(hipStreamSynchronize(l.stream));
+    put_count(cnt, l.R.t ? nrows_of(l.ctx, l.R.t) : 0, l.stream);
   }
+  // 5. gather to rank 0: counts, then the reduced partitions column by column
   xfer_allgather_i64(ranks, 1);
   std::vector<int64_t> part_rows(W, 0);
-  std::vector<size_t> goff(W + 1, 0);
-  for (Local& l : ranks) {
-    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-    HIPCK(hipMemcpyAsync(part_rows.data(), (int64_t*)l.st->counts.p + W, sizeof(int64_t) * W, hipMemcpyDeviceToHost,
-                         l.stream));
-    HIPCK(hipStreamSynchronize(l.stream));
-    // pack this rank's reduced partition into the send buffer (rank 0 keeps its own table)
-    if (l.R.t && l.st->rank != 0)
-      pack_block(l.ctx, l.stream, l.R.t, dts, nrows_of(l.ctx, l.R.t),
-                 (unsigned char*)l.st->send.ensure(block_bytes(dts, nrows_of(l.ctx, l.R.t))));
-  }
-  for (int s = 0; s < W; ++s) goff[s + 1] = goff[s] + block_bytes(dts, part_rows[s]);
   for (Local& l : ranks)
     if (l.st->rank == 0) {
       HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-      l.st->recv.ensure(goff[W]);
+      HIPCK(hipMemcpyAsync(part_rows.data(), (int64_t*)l.st->counts.p + W, sizeof(int64_t) * W,
+                           hipMemcpyDeviceToHost, l.stream));
+      HIPCK(hipStreamSynchronize(l.stream));
     }
+  if (ranks.size() < (size_t)W || ranks[0].st->rank != 0) {
+    // a process driving only some ranks (one process per GPU): non-root ranks learn the
+    // gather sizes they need (their own) locally
+    for (Local& l : ranks)
+      if (l.st->rank != 0) part_rows[l.st->rank] = l.R.t ? nrows_of(l.ctx, l.R.t) : 0;
+  }
+  int64_t others = 0;
+  for (int s = 1; s < W; ++s) others += part_rows[s];
   {
     std::vector<std::vector<P2P>> sends(ranks.size()), recvs(ranks.size());
     for (size_t i = 0; i < ranks.size(); ++i) {
       Local& l = ranks[i];
-      const size_t mine = block_bytes(dts, part_rows[l.st->rank]);
-      if (l.st->rank == 0) {
-        unsigned char* rb = (unsigned char*)l.st->recv.p;
-        for (int s = 1; s < W; ++s)
-          if (part_rows[s]) recvs[i].push_back(P2P{s, rb + goff[s], goff[s + 1] - goff[s]});
-      } else if (mine) {
-        sends[i].push_back(P2P{0, l.st->send.p, mine});
+      HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+      if (l.st->rank != 0) {
+        const int64_t mine = l.R.t ? nrows_of(l.ctx, l.R.t) : 0;
+        for (int j = 0; mine && j < ncols; ++j)
+          sends[i].push_back(P2P{0, col_ptr(l.ctx, l.R.t, j), (size_t)mine << lg[j]});
+        continue;
       }
+      if (others == 0) continue;  // every merged row is in rank 0's own partition
+      int64_t total = 0;
+      for (int s = 0; s < W; ++s) total += part_rows[s];
+      TableOwner res;
+      ck(l.ctx, bqg_table_create(l.ctx, total, ncols, dts.data(), &res.t));
+      if (part_rows[0])
+        for (int j = 0; j < ncols; ++j) ck(l.ctx, bqg_push_chunk(res.t, j, col_ptr(l.ctx, l.R.t, j), part_rows[0], 0));
+      int64_t off = part_rows[0];
+      for (int s = 1; s < W; ++s) {
+        if (!part_rows[s]) continue;
+        for (int j = 0; j < ncols; ++j)
+          recvs[i].push_back(P2P{s, (unsigned char*)col_ptr(l.ctx, res.t, j) + ((size_t)off << lg[j]),
+                                 (size_t)part_rows[s] << lg[j]});
+        off += part_rows[s];
+      }
+      l.R.reset();
+      l.R.t = res.release();
     }
     xfer_p2p(ranks, sends, recvs);
   }
   for (Local& l : ranks) {
     HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-    if (l.st->rank != 0) {
-      HIPCK(hipStreamSynchronize(l.stream));  // the send buffer is reused by the next merge
-      *l.out = nullptr;
-      continue;
-    }
-    int64_t total = 0, others = 0;
-    for (int s = 0; s < W; ++s) total += part_rows[s];
-    others = total - part_rows[0];
-    if (others == 0 && l.R.t) {  // every merged row is in rank 0's own partition
-      HIPCK(hipStreamSynchronize(l.stream));
-      *l.out = l.R.release();
-      continue;
-    }
-    TableOwner res;
-    ck(l.ctx, bqg_table_create(l.ctx, total, ncols, dts.data(), &res.t));
-    int64_t off = 0;
-    for (int s = 0; s < W; ++s) {
-      if (part_rows[s] && s == 0) {
-        for (int j = 0; j < ncols; ++j) ck(l.ctx, bqg_push_chunk(res.t, j, col_ptr(l.ctx, l.R.t, j), part_rows[0], 0));
-      } else if (part_rows[s]) {
-        unpack_block(l.ctx, res.t, dts, part_rows[s], off, (const unsigned char*)l.st->recv.p + goff[s]);
-      }
-      off += part_rows[s];
-    }
-    HIPCK(hipStreamSynchronize(l.stream));
-    *l.out = res.release();
+    HIPCK(hipStreamSynchronize(l.stream));  // sends complete before their tables are released
+    if (l.st->rank == 0 && !l.R.t) ck(l.ctx, bqg_table_create(l.ctx, 0, ncols, dts.data(), &l.R.t));  // no rows anywhere
+    if (l.st->rank == 0) *l.out = l.R.release();
+    else *l.out = nullptr;
+    l.R.reset();
   }
-  for (Local& l : ranks) l.R.reset();
 }
 
 }  // namespace

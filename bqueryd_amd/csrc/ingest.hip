@@ -356,6 +356,9 @@ Plan plan_chunk(const unsigned char* file, const ChunkFile& f, uint64_t dst, uin
   }
   if ((size_t)nbytes != want) return Plan::kFallback;  // a padded last frame: host copies `want`
   if (nbytes == 0) return Plan::kTasks;
+  // flag bits the device decoder does not implement go to host libblosc: 0x8 (the delta
+  // filter of newer c-blosc 1.x) and the reserved 0x40 / 0x80 bits of non-codec use
+  if (flags & 0x8) return Plan::kFallback;
   const uint64_t frame_src = f.off + kBloscpackHeader;
   if (flags & 0x2) {  // memcpyed: the items follow the header as they are
     if (kBloscHeader + (size_t)nbytes > (size_t)cbytes) {

@@ -17,6 +17,9 @@
 #ifndef BQ_PART_NARROW
 #define BQ_PART_NARROW 0
 #endif
+#ifndef BQ_PART_PACK
+#define BQ_PART_PACK 0
+#endif
 
 namespace bqg {
 __device__ __forceinline__ void jit_specialize(ScanParams& p) { BQ_SPEC }
@@ -33,7 +36,7 @@ extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_scatter(bqg::Scan
   extern __shared__ __align__(16) unsigned char smem[];
   bqg::ScanParams p = pin;
   bqg::jit_specialize(p);
-  bqg::part_scatter_body<BQ_NC, BQ_PART_K, BQ_PART_NARROW != 0>(p, L, smem);
+  bqg::part_scatter_body<BQ_NC, BQ_PART_K, BQ_PART_NARROW != 0, BQ_PART_PACK != 0>(p, L, smem);
 }
 
 extern "C" __global__ __launch_bounds__(256) void bq_jit_scd_fused(bqg::ScanParams pin, bqg::ScdLaunch d) {

@@ -608,6 +608,19 @@ constexpr uint32_t kHashPartLds = 8192;
 // Hash partition of rows by their key VALUES (not codes: codes depend on per-shard
 // statistics), for the cross-rank merge: partition = mix(canonical key bits) mod nparts.
 // ------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t row_partition(const PartitionCols& k, int64_t row, uint32_t nparts) {
+  uint64_t h = 0x243F6A8885A308D3ull;
+  for (int j = 0; j < k.nkeys; ++j) {
+    Chunk c;
+    row_word_to_chunk(c, k.cols[j], row, load_row_word(k.cols[j], row));
+    uint64_t v[1];
+    decode<1>(c, k.cols[j].dtype, v);
+    const uint64_t bits = dtype_is_float(k.cols[j].dtype) ? canon_f64_bits(v[0]) : v[0];
+    h = mix64(h ^ mix64(bits + (uint64_t)j));
+  }
+  return (uint32_t)(h % nparts);
+}
+
 __global__ __launch_bounds__(kBlock) void k_hash_partition(PartitionCols k, int64_t nrows, uint32_t nparts,
                                                            uint32_t* out, unsigned long long* counts) {
   // per-workgroup LDS histogram (a single hot partition -- world size 1 or skewed keys --
@@ -618,16 +631,7 @@ __global__ __launch_bounds__(kBlock) void k_hash_partition(PartitionCols k, int6
     for (uint32_t i = threadIdx.x; i < nparts; i += kBlock) hist[i] = 0;
   __syncthreads();
   for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < nrows; row += (int64_t)gridDim.x * kBlock) {
-    uint64_t h = 0x243F6A8885A308D3ull;
-    for (int j = 0; j < k.nkeys; ++j) {
-      Chunk c;
-      row_word_to_chunk(c, k.cols[j], row, load_row_word(k.cols[j], row));
-      uint64_t v[1];
-      decode<1>(c, k.cols[j].dtype, v);
-      const uint64_t bits = dtype_is_float(k.cols[j].dtype) ? canon_f64_bits(v[0]) : v[0];
-      h = mix64(h ^ mix64(bits + (uint64_t)j));
-    }
-    const uint32_t p = (uint32_t)(h % nparts);
+    const uint32_t p = row_partition(k, row, nparts);
     out[row] = p;
     if (lds)
       atomicAdd(&hist[p], 1u);
@@ -639,6 +643,159 @@ __global__ __launch_bounds__(kBlock) void k_hash_partition(PartitionCols k, int6
     for (uint32_t i = threadIdx.x; i < nparts; i += kBlock)
       if (hist[i]) atomicAdd(&counts[i], (unsigned long long)hist[i]);
   }
+}
+
+// ------------------------------------------------------------------------------------
+// Cross-rank merge, send side: every row of a rank's reduced table goes straight into its
+// destination rank's packed block (the block's columns one after another, each 16-byte
+// aligned, rows in table order).  A stable counting partition in three launches: per-workgroup
+// destination histograms (each row's destination kept as one byte), an exclusive scan over
+// the workgroups per destination plus the block layout, then the ordered scatter.  It
+// replaces one row-selection pass per destination and a copy per column and destination.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_mpack_hist(MergePack m) {
+  __shared__ unsigned int hist[kMergeMaxRanks];
+  for (int i = threadIdx.x; i < m.nranks; i += kBlock) hist[i] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * m.rows_per_block;
+  const int64_t r1 = min(m.nrows, r0 + m.rows_per_block);
+  for (int64_t row = r0 + threadIdx.x; row < r1; row += kBlock) {
+    const uint32_t d = row_partition(m.keys, row, (uint32_t)m.nranks);
+    m.dest[row] = (unsigned char)d;
+    atomicAdd(&hist[d], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < m.nranks; i += kBlock) m.block_hist[(size_t)blockIdx.x * m.nranks + i] = hist[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_mpack_scan(MergePack m) {
+  // thread (c, d): destination d over the c-th run of workgroups (kBlock / nranks runs)
+  __shared__ unsigned int part[kBlock];
+  __shared__ unsigned long long tot[kMergeMaxRanks];
+  const int W = m.nranks;
+  const int C = kBlock / W;
+  const int per = (m.nblocks + C - 1) / C;
+  const int d = threadIdx.x % W, c = threadIdx.x / W;
+  const bool on = c < C;
+  const int b0 = c * per, b1 = min(m.nblocks, (c + 1) * per);
+  unsigned int s = 0;
+  if (on)
+    for (int b = b0; b < b1; ++b) s += m.block_hist[(size_t)b * W + d];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (on) {
+    unsigned int run = 0;
+    for (int c2 = 0; c2 < c; ++c2) run += part[c2 * W + d];
+    if (c == C - 1) {
+      tot[d] = run + s;
+      m.to_peer[d] = run + s;
+    }
+    for (int b = b0; b < b1; ++b) {
+      const size_t i = (size_t)b * W + d;
+      const unsigned int v = m.block_hist[i];
+      m.block_hist[i] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long off = 0;
+    for (int dd = 0; dd < W; ++dd)
+      for (int j = 0; j < m.ncols; ++j) {
+        m.colbase[dd * m.ncols + j] = off;
+        off += ((tot[dd] << m.lg[j]) + 15) & ~15ull;
+      }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_mpack_scatter(MergePack m) {
+  __shared__ unsigned int next[kMergeMaxRanks];               // next position of each destination
+  __shared__ unsigned int wcnt[kBlock / 64][kMergeMaxRanks];  // rows per (wave, destination) of a step
+  const int W = m.nranks;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < W; i += kBlock) next[i] = m.block_hist[(size_t)blockIdx.x * W + i];
+  const int64_t r0 = (int64_t)blockIdx.x * m.rows_per_block;
+  const int64_t r1 = min(m.nrows, r0 + m.rows_per_block);
+  for (int64_t c0 = r0; c0 < r1; c0 += kBlock) {
+    for (int i = threadIdx.x; i < (kBlock / 64) * W; i += kBlock) wcnt[i / W][i % W] = 0;
+    __syncthreads();
+    const int64_t row = c0 + threadIdx.x;
+    const bool valid = row < r1;
+    const uint32_t d = valid ? m.dest[row] : 0u;
+    // rank among the wave's rows of the same destination: one ballot per distinct destination
+    uint64_t todo = __ballot(valid);
+    uint32_t rank = 0;
+    while (todo) {
+      const int leader = __ffsll((unsigned long long)todo) - 1;
+      const uint32_t dd = (uint32_t)__shfl((int)d, leader);
+      const uint64_t same = __ballot(valid && d == dd);
+      if (valid && d == dd) rank = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+      if (lane == leader) wcnt[wave][dd] = (unsigned int)__popcll(same);
+      todo &= ~same;
+    }
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = next[d] + rank;
+      for (int w = 0; w < wave; ++w) pos += wcnt[w][d];
+      const unsigned long long* cb = m.colbase + (size_t)d * m.ncols;
+      for (int j = 0; j < m.ncols; ++j) {
+        unsigned char* dst = m.send + cb[j];
+        switch (m.lg[j]) {
+          case 0: dst[pos] = m.cols[j][row]; break;
+          case 1: ((uint16_t*)dst)[pos] = ((const uint16_t*)m.cols[j])[row]; break;
+          case 2: ((uint32_t*)dst)[pos] = ((const uint32_t*)m.cols[j])[row]; break;
+          default: ((uint64_t*)dst)[pos] = ((const uint64_t*)m.cols[j])[row]; break;
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < W; i += kBlock) {
+      unsigned int add = 0;
+      for (int w = 0; w < kBlock / 64; ++w) add += wcnt[w][i];
+      next[i] += add;
+    }
+    __syncthreads();
+  }
+}
+
+// std pass 2 centers: the mean of every slot of every std column, from pass 1's count and sum
+// (conv: 0 float bits, 1 signed, 2 unsigned integer sum), written where pass 2 reads them --
+// no host round trip between the passes
+__global__ __launch_bounds__(kBlock) void k_std_centers(const unsigned long long* cnt, const unsigned long long* acc,
+                                                        StdCenters sc, uint64_t nslots, double* centers) {
+  const uint64_t total = (uint64_t)sc.n * nslots;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (uint64_t)gridDim.x * kBlock) {
+    const int k = (int)(i / nslots);
+    const uint64_t s = i - (uint64_t)k * nslots;
+    const unsigned long long a = acc[(size_t)sc.state[k] * nslots + s];
+    const double sum = sc.conv[k] == 0 ? as_f64(a) : sc.conv[k] == 2 ? (double)a : (double)(long long)a;
+    const unsigned long long c = cnt[s];
+    centers[i] = c ? sum / (double)c : 0.0;
+  }
+}
+
+void launch_std_centers(const unsigned long long* cnt, const unsigned long long* acc, const StdCenters& sc,
+                        uint64_t nslots, double* centers, hipStream_t st) {
+  const uint64_t total = (uint64_t)sc.n * nslots;
+  if (!total) return;
+  const unsigned g = (unsigned)std::min<uint64_t>((total + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL(k_std_centers, dim3(g), dim3(kBlock), 0, st, cnt, acc, sc, nslots, centers);
+}
+
+void merge_pack_grid(int64_t nrows, int32_t* nblocks, int64_t* rows_per_block) {
+  int64_t nb = std::max<int64_t>(1, std::min<int64_t>(256, (nrows + 4095) / 4096));
+  int64_t rpb = (nrows + nb - 1) / nb;
+  rpb = std::max<int64_t>(kBlock, (rpb + kBlock - 1) / kBlock * kBlock);
+  nb = std::max<int64_t>(1, (nrows + rpb - 1) / rpb);
+  *nblocks = (int32_t)nb;
+  *rows_per_block = rpb;
+}
+
+void launch_merge_pack(const MergePack& m, hipStream_t st) {
+  if (m.nrows > 0) hipLaunchKernelGGL(k_mpack_hist, dim3(m.nblocks), dim3(kBlock), 0, st, m);
+  else (void)hipMemsetAsync(m.block_hist, 0, (size_t)m.nblocks * m.nranks * 4, st);
+  hipLaunchKernelGGL(k_mpack_scan, dim3(1), dim3(kBlock), 0, st, m);
+  if (m.nrows > 0) hipLaunchKernelGGL(k_mpack_scatter, dim3(m.nblocks), dim3(kBlock), 0, st, m);
 }
 
 void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, hipStream_t st) {  // out4: 5 words
@@ -710,6 +867,61 @@ __global__ __launch_bounds__(kBlock) void k_factor_labels(DevCol col, int64_t n,
     decode<1>(c, col.dtype, v);
     out[i] = (long long)lut[v[0] - (uint64_t)vmin];
   }
+}
+
+// Factor caches of any key column -- floats (khash identity: -0.0 == +0.0, NaN == NaN, the
+// canonical bits of the groupby's key), bools and integers spanning more than a lookup table
+// allows: an open-addressing table from the distinct values' canonical bits to their labels
+// (inserted without collisions between equal keys: the values are distinct), then one probe
+// per row.  labs[] holds label + 1 (0 = empty slot).
+__device__ __forceinline__ uint64_t factor_bits(const DevCol& c, int64_t i) {
+  Chunk ch;
+  row_word_to_chunk(ch, c, i, load_row_word(c, i));
+  uint64_t v[1];
+  decode<1>(ch, c.dtype, v);
+  return dtype_is_float(c.dtype) ? canon_f64_bits(v[0]) : v[0];
+}
+
+__global__ __launch_bounds__(kBlock) void k_factor_hash_build(DevCol vals, int64_t n, uint64_t mask,
+                                                              unsigned long long* keys, uint32_t* labs) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const uint64_t bits = factor_bits(vals, i);
+    for (uint64_t h = mix64(bits) & mask;; h = (h + 1) & mask)
+      if (atomicCAS(&labs[h], 0u, (uint32_t)(i + 1)) == 0u) {
+        keys[h] = bits;
+        break;
+      }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_factor_hash_labels(DevCol col, int64_t n, uint64_t mask,
+                                                               const unsigned long long* keys, const uint32_t* labs,
+                                                               long long* out) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const uint64_t bits = factor_bits(col, i);
+    long long lab = -1;  // every row's value is among the distinct values: not reached
+    for (uint64_t h = mix64(bits) & mask;; h = (h + 1) & mask) {
+      const uint32_t l = labs[h];
+      if (l == 0u) break;
+      if (keys[h] == bits) {
+        lab = (long long)l - 1;
+        break;
+      }
+    }
+    out[i] = lab;
+  }
+}
+
+void launch_factor_hash_labels(const DevCol& vals, int64_t nvals, const DevCol& col, int64_t nrows, uint64_t cap,
+                               unsigned long long* keys, uint32_t* labs, long long* out, hipStream_t st) {
+  auto grid = [](int64_t n) {
+    int64_t b = (n + kBlock - 1) / kBlock;
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(b, 8192));
+  };
+  (void)hipMemsetAsync(labs, 0, cap * 4, st);
+  if (nvals > 0) hipLaunchKernelGGL(k_factor_hash_build, dim3(grid(nvals)), dim3(kBlock), 0, st, vals, nvals, cap - 1, keys, labs);
+  if (nrows > 0)
+    hipLaunchKernelGGL(k_factor_hash_labels, dim3(grid(nrows)), dim3(kBlock), 0, st, col, nrows, cap - 1, keys, labs, out);
 }
 
 void launch_factor_labels(const DevCol& vals, int64_t nvals, const DevCol& col, int64_t nrows, int64_t vmin,

@@ -23,10 +23,10 @@
 
 namespace bqg {
 
-template <int NC, int K, bool NARROW>
+template <int NC, int K, bool NARROW, bool PACK>
 __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartLaunch L) {
   extern __shared__ __align__(16) unsigned char smem[];
-  part_scatter_body<NC, K, NARROW>(p, L, smem);
+  part_scatter_body<NC, K, NARROW, PACK>(p, L, smem);
 }
 
 // Aggregate over the tile layout.  Workgroup (partition, split): the split's tile range.  A
@@ -41,7 +41,11 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartL
 // aggregate -- it waited on each group's loads.  Workgroups are mapped XCD-aware: the
 // workgroups of one XCD (blockIdx % 8) take consecutive partitions over the same tile range,
 // so the edge lines their segments share are read once into that XCD's L2.
-template <int G, int U, int NSUM, bool NARROW>
+//
+// PACK entries (PartLaunch::pack): one 32-bit word {code16, slot_low}; the slot table is one
+// packed 64-bit accumulator (count << sbits | code16 sum: ONE LDS atomic per entry) and the
+// slot's first tile, and the combine leaves first rows to k_part_first_rows.
+template <int G, int U, int NSUM, bool NARROW, bool PACK = false>
 __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunch L, SlotArrays sa) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int P = L.nparts;
@@ -51,15 +55,16 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   if (part >= P || split >= L.splits) return;  // the whole workgroup
   const int W = 1 << L.wbits;
   constexpr int nsum = NSUM;
-  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][W]
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)nsum * W);    // [W]
-  uint32_t* fst = cnt + W;                                                 // [W]
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][W] (PACK: [W] packed)
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)(PACK ? 1 : nsum) * W);  // [W] (PACK: unused)
+  uint32_t* fst = PACK ? cnt : cnt + W;                                    // [W] first row (PACK: first tile)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = (int)(blockDim.x >> 6);
   for (int i = tid; i < W; i += blockDim.x) {
-    cnt[i] = 0;
+    if (!PACK) cnt[i] = 0;
     fst[i] = kNoRow;
   }
-  for (int i = tid; i < nsum * W; i += blockDim.x) acc[i] = 0;
+  for (int i = tid; i < (PACK ? 1 : nsum) * W; i += blockDim.x) acc[i] = 0;
+  const unsigned long long inc = PACK ? 1ull << L.sbits : 0ull;  // one row in the packed count field
   __syncthreads();
   const int64_t nt = L.ntiles;
   // (splits <= ntiles: every split's tile range is non-empty, and every split must reach the
@@ -82,6 +87,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     uint32_t ex[G];
     uint32_t dl, total;
     size_t gbase;
+    uint32_t tile0;
   };
   // one U x 64-entry load of a group
   struct Ent {
@@ -97,6 +103,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     for (int j = 0; j < G; ++j) g.ex[j] = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
     g.dl = (uint32_t)lane * TR + s0 - excl;
     g.gbase = (size_t)tg * TR;
+    g.tile0 = (uint32_t)tg;
   };
   // unconditional loads (an empty group -- past the range -- reads entry 0; the value array
   // exists even without a summed column): the same loads on every path, so the compiler
@@ -111,8 +118,9 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       for (int j = 1; j < G; ++j) j0 += ec >= g.ex[j] ? 1u : 0u;
       size_t idx = g.gbase + (uint32_t)__shfl((int)g.dl, (int)j0, 64) + ec;
       idx = g.total ? idx : 0;
-      en.rowb[u] = (uint32_t)g.gbase + j0 * TR;
+      en.rowb[u] = PACK ? g.tile0 + j0 : (uint32_t)g.gbase + j0 * TR;  // PACK: the tile
       en.m[u] = L.meta[idx];
+      if (PACK) continue;
 #pragma unroll
       for (int q = 0; q < NV; ++q) {
         if (NARROW) {  // the exact 32-bit code: float codes signed, integer offsets unsigned
@@ -130,6 +138,11 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       const uint32_t e = e0 + u * 64u + lane;
       if (e >= g.total) continue;
       const uint32_t sl = en.m[u] & lowmask;
+      if (PACK) {
+        atomicAdd(&acc[sl], inc + (unsigned long long)(en.m[u] >> 16));
+        if (fst[sl] > en.rowb[u]) atomicMin(&fst[sl], en.rowb[u]);
+        continue;
+      }
       const uint32_t row = en.rowb[u] + (en.m[u] >> L.wbits);
       atomicAdd(&cnt[sl], 1u);
       if (fst[sl] > row) atomicMin(&fst[sl], row);
@@ -186,9 +199,17 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   __shared__ unsigned int s_last;
   if (S > 1) {
     uint32_t* pc = reinterpret_cast<uint32_t*>(L.partial + ((size_t)part * S + split) * L.partial_bytes);
+    if (PACK) {  // [W] packed accumulators, then [W] first tiles
+      unsigned long long* pa = reinterpret_cast<unsigned long long*>(pc);
+      uint32_t* pf = reinterpret_cast<uint32_t*>(pa + W);
+      for (int s = tid; s < W; s += blockDim.x) {
+        pa[s] = acc[s];
+        pf[s] = fst[s];
+      }
+    }
     uint32_t* pf = pc + W;
     unsigned long long* pa = reinterpret_cast<unsigned long long*>(pf + W);
-    for (int s = tid; s < W; s += blockDim.x) {
+    for (int s = tid; !PACK && s < W; s += blockDim.x) {
       pc[s] = cnt[s];
       pf[s] = fst[s];
 #pragma unroll
@@ -209,6 +230,43 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     }
     __syncthreads();
     if (!s_last) return;
+  }
+  if (PACK) {
+    // unpack every split's accumulator before adding (the packed fields of a sum over splits
+    // could carry into each other); exact code sum = sum of code16 + count x enc_base16
+    const unsigned long long smask = (1ull << L.sbits) - 1ull;
+    for (int s = tid; s < nvalid; s += blockDim.x) {
+      unsigned long long c = 0, cs = 0;
+      uint32_t f = kNoRow;
+      for (int o = 0; o < S; ++o) {
+        unsigned long long a;
+        uint32_t of;
+        if (o == split) {
+          a = acc[s];
+          of = fst[s];
+        } else {
+          const unsigned long long* pa =
+              reinterpret_cast<const unsigned long long*>(L.partial + ((size_t)part * S + o) * L.partial_bytes);
+          a = pa[s];
+          of = reinterpret_cast<const uint32_t*>(pa + W)[s];
+        }
+        c += a >> L.sbits;
+        cs += a & smask;
+        f = of < f ? of : f;
+      }
+      const uint64_t gs = slot0 + s;
+      sa.cnt[gs] = c;
+      sa.fst[gs] = kNoRow;  // k_part_first_rows
+      L.first_tile[gs] = f;
+      if (f != kNoRow) L.tile_mark[f] = 1;
+      if (nsum) {
+        unsigned long long tot = cs + c * (unsigned long long)L.enc_base16;
+        if (L.enc_kind[0] == 3) tot += c * (unsigned long long)L.enc_off[0];
+        else tot = as_u64((double)(long long)tot / L.enc_mul[0]);
+        sa.acc[gs] = tot;
+      }
+    }
+    return;
   }
   for (int s = tid; s < nvalid; s += blockDim.x) {
     uint32_t c = 0, f = kNoRow;
@@ -255,6 +313,34 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   }
 }
 
+// First rows of the PACK path: a slot's first row lies in its first tile (first_tile, from
+// the aggregate), so only the tiles marked as some slot's first tile are read again -- their
+// key / filter columns, through the scan's own row -> slot code -- and every passing row whose
+// slot has this tile as its first one takes part in an atomicMin on the slot's first row.  On
+// random keys the marked tiles are the first ~10-15 % (each slot's first appearance falls
+// early); on sorted keys every tile is marked.
+template <int NC>
+__global__ __launch_bounds__(256) void k_part_first_rows(ScanParams p, PartLaunch L, SlotArrays sa) {
+  for (int64_t t = blockIdx.x; t < L.ntiles; t += gridDim.x) {
+    if (!L.tile_mark[t]) continue;
+    const int64_t base = t * (int64_t)L.tile_rows;
+    const int64_t end = min(p.nrows, base + (int64_t)L.tile_rows);
+    for (int64_t row0 = base + (int64_t)threadIdx.x * kRowsPerThread; row0 < end; row0 += 256 * kRowsPerThread) {
+      Chunk raw[NC];
+      load_rows4<NC>(p, row0, raw);
+      uint64_t v[NC][4], code[4];
+      decode_all<NC, 4>(p, raw, v);
+      uint32_t pass = vals_pass<NC, 4>(p, row0, v);
+      const int64_t rem = end - row0;
+      pass &= rem >= 4 ? 0xFu : ((1u << rem) - 1u);
+      vals_code<NC, 4>(p, v, code);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((pass >> r) & 1u && L.first_tile[code[r]] == (uint32_t)t) atomicMin(&sa.fst[code[r]], (uint32_t)(row0 + r));
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Multi-workgroup exclusive scan of uint32 (3 launches): per-1024-segment scan with segment
 // totals, scan of the totals (recursively small), add-back.
@@ -288,7 +374,7 @@ void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipSt
 #ifndef BQG_PART_MICRO  // tools/micro/part_micro.hip includes this file for the aggregate kernel
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,
                         hipFunction_t fscatter) {
-  const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum, L.k, L.narrow != 0);
+  const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum, L.k, L.narrow != 0, L.pack != 0);
   if (fscatter) {
     PartLaunch Lc = L;
     ScanParams pc = p;
@@ -296,24 +382,42 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
     (void)hipModuleLaunchKernel(fscatter, (unsigned)L.blocks, 1, 1, (unsigned)L.threads, 1, 1, (unsigned)scatter_lds,
                                 st, args, nullptr);
   } else {
-#define BQG_SCATTER(K, NW) BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC, K, NW>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L))
+#define BQG_SCATTER(K, NW, PK) BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC, K, NW, PK>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L))
     if (L.k == 2) {
-      if (L.narrow) {
-        BQG_SCATTER(2, true);
+      if (L.pack) {
+        BQG_SCATTER(2, true, true);
+      } else if (L.narrow) {
+        BQG_SCATTER(2, true, false);
       } else {
-        BQG_SCATTER(2, false);
+        BQG_SCATTER(2, false, false);
       }
     } else {
-      if (L.narrow) {
-        BQG_SCATTER(1, true);
+      if (L.pack) {
+        BQG_SCATTER(1, true, true);
+      } else if (L.narrow) {
+        BQG_SCATTER(1, true, false);
       } else {
-        BQG_SCATTER(1, false);
+        BQG_SCATTER(1, false, false);
       }
     }
 #undef BQG_SCATTER
   }
-  const size_t agg_lds = ((size_t)1 << L.wbits) * (8 + 8 * (size_t)p.nsum);
+  const size_t agg_lds = part_agg_lds(L.wbits, p.nsum, L.pack != 0);
   const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
+  if (L.pack) {
+    (void)hipMemsetAsync(L.tile_mark, 0, (size_t)L.ntiles, st);
+#define BQG_AGGP(G, U, NS) hipLaunchKernelGGL((k_part_aggregate<G, U, NS, true, true>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
+    const bool big = L.tile_rows > 4096;
+    if (p.nsum == 0) {
+      if (big) BQG_AGGP(4, 4, 0); else BQG_AGGP(8, 4, 0);
+    } else {
+      if (big) BQG_AGGP(4, 4, 1); else BQG_AGGP(8, 4, 1);
+    }
+#undef BQG_AGGP
+    const unsigned fgrid = (unsigned)std::min<int64_t>(L.ntiles, 65535);
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_first_rows<NC>), dim3(fgrid), dim3(256), 0, st, p, L, s));
+    return;
+  }
   // G tiles per wave group: ~8 x 4096 rows of segments whichever the tile size
 #define BQG_AGG2(G, U, NS, NW) hipLaunchKernelGGL((k_part_aggregate<G, U, NS, NW>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
 #define BQG_AGG(G, U, NS) do { if (L.narrow) BQG_AGG2(G, U, NS, true); else BQG_AGG2(G, U, NS, false); } while (0)

@@ -184,6 +184,18 @@ struct PartLaunch {
   int32_t enc_kind[kMaxSums];  // 1 dyadic, 2 cents, 3 integer offset
   double enc_mul[kMaxSums];
   int64_t enc_off[kMaxSums];
+  // packed entries (at most one summed column, its narrow codes spanning at most 2^16 values):
+  // one 32-bit word per entry, code16 = code - enc_base16 above the 16-bit slot_low; the
+  // aggregate's per-slot accumulator is count << sbits | sum of code16 (one 64-bit LDS atomic
+  // per entry; the planner picks sbits and splits so neither field can overflow), and it
+  // records each slot's first TILE: first_tile [nslots] (kNoRow = none), tile_mark [ntiles]
+  // (1 = some slot's first tile, zeroed before the aggregate), then k_part_first_rows re-reads
+  // only the marked tiles for the exact first rows
+  int pack;
+  int sbits;
+  int64_t enc_base16;
+  uint32_t* first_tile;
+  unsigned char* tile_mark;
   // aggregate combine (splits > 1): per-partition arrival counters (zeroed by
   // launch_partitioned) and [nparts][splits] partial tables of partial_bytes each
   unsigned int* arrive;
@@ -192,8 +204,13 @@ struct PartLaunch {
 };
 // LDS bytes of a scatter workgroup: the staged tile (values, meta), tile counts (two
 // buffers) / offsets and two sets of scan totals
-inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1, bool narrow = false) {
-  return (size_t)threads * 4 * k * (4 + (narrow ? 4 : 8) * (size_t)nsum) + (size_t)nparts * 12 + 2 * 16 * 4;
+inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1, bool narrow = false, bool pack = false) {
+  return (size_t)threads * 4 * k * (4 + (pack ? 0 : (narrow ? 4 : 8) * (size_t)nsum)) + (size_t)nparts * 12 + 2 * 16 * 4;
+}
+// LDS bytes of an aggregate workgroup's slot table: count + first row + 8-byte sums, or
+// (pack) the packed 8-byte accumulator + first tile
+inline size_t part_agg_lds(int wbits, int nsum, bool pack) {
+  return ((size_t)1 << wbits) * (pack ? 12 : 8 + 8 * (size_t)nsum);
 }
 // fscatter: the query-specialised (JIT) scatter kernel, or nullptr for the precompiled one
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,
@@ -208,9 +225,45 @@ struct PartitionCols {
 void launch_hash_partition(const PartitionCols& k, int64_t nrows, uint32_t nparts, uint32_t* out,
                            unsigned long long* counts, hipStream_t st);
 
+// cross-rank merge, send side: rows -> destination rank hash(key values) mod nranks (the
+// partition of launch_hash_partition), packed per destination in one stable scatter
+constexpr int kMergeMaxRanks = 256;  // destinations are kept as one byte per row
+constexpr int kMergeMaxCols = kMaxKeys + kMaxAggs;
+struct MergePack {
+  PartitionCols keys;
+  const unsigned char* cols[kMergeMaxCols];  // every column of the table (keys included)
+  int32_t lg[kMergeMaxCols];                 // log2 of the element size
+  int32_t ncols;
+  int32_t nranks;
+  int32_t nblocks;                           // merge_pack_grid
+  int64_t nrows;
+  int64_t rows_per_block;
+  unsigned char* dest;                       // [nrows] scratch
+  uint32_t* block_hist;                      // [nblocks][nranks] scratch
+  unsigned long long* to_peer;               // [nranks] out: rows per destination
+  unsigned long long* colbase;               // [nranks][ncols] out: byte offset of each packed column
+  unsigned char* send;                       // packed blocks, destination order
+};
+void merge_pack_grid(int64_t nrows, int32_t* nblocks, int64_t* rows_per_block);
+void launch_merge_pack(const MergePack& m, hipStream_t st);
+
+// std: per-slot means of the std columns (pass 1 totals -> pass 2 centers), on device
+struct StdCenters {
+  int32_t n;                // std columns
+  int32_t state[kMaxSums];  // their sum-state index in SlotArrays::acc
+  int32_t conv[kMaxSums];   // 0 float bits, 1 signed integer, 2 unsigned integer
+};
+void launch_std_centers(const unsigned long long* cnt, const unsigned long long* acc, const StdCenters& sc,
+                        uint64_t nslots, double* centers, hipStream_t st);
+
 // factor cache labels (bquery auto_cache): lut [range] scratch, out [nrows] int64 labels
 void launch_factor_labels(const DevCol& vals, int64_t nvals, const DevCol& col, int64_t nrows, int64_t vmin,
                           int32_t* lut, long long* out, hipStream_t st);
+
+// ... any key column (floats, bools, wide integer spans): hash of canonical bits -> label;
+// cap a power of two >= 2 * nvals, keys [cap] / labs [cap] scratch
+void launch_factor_hash_labels(const DevCol& vals, int64_t nvals, const DevCol& col, int64_t nrows, uint64_t cap,
+                               unsigned long long* keys, uint32_t* labs, long long* out, hipStream_t st);
 
 int device_cu_count();
 

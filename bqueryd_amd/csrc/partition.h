@@ -99,7 +99,14 @@ __device__ __forceinline__ uint32_t part_enc(const ScanParams& p, const PartLaun
   return (uint32_t)(int32_t)(L.enc_kind[q] == 1 ? d : rint(d));
 }
 
-template <int NC, int K = 1, bool NARROW = false>
+// PACK (PartLaunch::pack): one 32-bit word per entry, the summed column's 16-bit code (if
+// any) above the 16-bit slot_low -- no row: first appearance comes from each slot's first
+// tile (k_part_aggregate) and a re-read of only those tiles (k_part_first_rows).
+__device__ __forceinline__ uint32_t part_code16(const ScanParams& p, const PartLaunch& L, uint64_t v) {
+  return (part_enc(p, L, 0, v) - (uint32_t)L.enc_base16) << 16;
+}
+
+template <int NC, int K = 1, bool NARROW = false, bool PACK = false>
 __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const PartLaunch& L, unsigned char* smem) {
   // K 4-row chunks per thread and tile (TR = T * 4 * K rows): chunk k of thread t covers rows
   // base + k * T * 4 + t * 4 .. + 3, so every chunk load of the workgroup is one coalesced block
@@ -110,7 +117,7 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   constexpr int NS = NC < kMaxSums ? NC : kMaxSums;
   unsigned long long* sval = reinterpret_cast<unsigned long long*>(smem);  // [nsum][TR] (wide)
   uint32_t* sval32 = reinterpret_cast<uint32_t*>(smem);                    // [nsum][TR] (narrow)
-  uint32_t* smeta = reinterpret_cast<uint32_t*>(smem) + (size_t)nsum * TR * (NARROW ? 1 : 2);  // [TR]
+  uint32_t* smeta = reinterpret_cast<uint32_t*>(smem) + (PACK ? 0 : (size_t)nsum * TR * (NARROW ? 1 : 2));  // [TR]
   uint32_t* hist2 = smeta + TR;                                            // [2][P] tile counts
   uint32_t* toff = hist2 + 2 * P;                                          // [P] tile offsets
   uint32_t* wsum2 = toff + P;                                              // [2][16] scan totals
@@ -183,6 +190,10 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
       for (int r = 0; r < 4; ++r) {
         if (!(pass[k] & (1u << r))) continue;
         const uint32_t pos = toff[part[k][r]] + rank[k][r];
+        if (PACK) {
+          smeta[pos] = (nsum ? part_code16(p, L, sv[0][k][r]) : 0u) | low[k][r];
+          continue;
+        }
         smeta[pos] = ((rit0 + r) << L.wbits) | low[k][r];
 #pragma unroll
         for (int s = 0; s < NS; ++s)
@@ -199,7 +210,7 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
       *reinterpret_cast<uint4*>(L.meta + base + 4 * (tid + k * T)) = *reinterpret_cast<const uint4*>(smeta + 4 * (tid + k * T));
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      if (s >= nsum) break;
+      if (PACK || s >= nsum) break;
       if (NARROW) {
         uint32_t* dv = reinterpret_cast<uint32_t*>(L.vals) + (size_t)s * L.capacity + base;
         const uint32_t* lv = sval32 + (size_t)s * TR;

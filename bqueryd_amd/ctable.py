@@ -229,8 +229,9 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
         caches of every groupby column that has none -- labels and values from the GPU
         (``bqg_factorize``), compressed and written by a background thread into temporary
         directories next to the columns and renamed into place (.factor before .values, so a
-        valid cache always has both).  Columns the kernel cannot factorize (floats, value
-        ranges above 2^27) get no cache, which only disables the early-out for them."""
+        valid cache always has both).  Every key dtype is cached: integer columns spanning at
+        most 2^27 values through a lookup table, floats (khash identity), bools and wider
+        spans through a hash of the canonical key bits."""
         if not (self.auto_cache and self.rootdir and os.access(self.rootdir, os.W_OK)):
             return
         pending = self.__dict__.setdefault('_caching', set())

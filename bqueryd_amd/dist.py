@@ -193,6 +193,11 @@ class ColocatedShards:
         self._union_key = key
         return self._union
 
+    def resident_bytes(self):
+        """HBM held by the union (0 when none is built)."""
+        u = self._union
+        return 0 if u is None else sum(u.nrows * dt.itemsize for dt in u.dtypes.values())
+
     def close(self):
         if self._union is not None:
             self._union.close()

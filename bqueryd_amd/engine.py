@@ -55,7 +55,7 @@ class Device:
         self.check(self._lib.bqg_last_timing(self.handle, ctypes.byref(t)))
         return {'scan_ms': t.scan_ms, 'scan_launches': t.scan_launches, 'total_ms': t.total_ms,
                 'rows': t.rows, 'bytes': t.bytes, 'mode': t.mode, 'specialized': bool(t.specialized),
-                'narrow': bool(t.narrow), 'regrows': t.regrows}
+                'narrow': bool(t.narrow), 'pack16': t.narrow == 2, 'regrows': t.regrows}
 
     def set_option(self, name, value):
         """One engine option of this context (include/bqgpu.h: launch shapes and path choices,

@@ -57,13 +57,18 @@ def result_name():
 
 
 class ShardCache:
-    """Device-resident shards, least-recently-used eviction by resident bytes."""
+    """Device-resident shards, least-recently-used eviction by resident bytes.  ``extra`` (set
+    by the node-level state) holds the other HBM this cache's budget covers -- the co-located
+    unions of the cached shards: ``extra.bytes()`` is what they hold, ``extra.drop_oldest()``
+    frees one (False when none is left), ``extra.forget(ct)`` drops the ones built over an
+    evicted shard."""
 
     def __init__(self, budget_bytes=None, device=None):
         self.budget = budget_bytes if budget_bytes is not None else int(
             float(os.environ.get('BQGPU_CACHE_GB', '64')) * (1 << 30))
         self.device = device
         self._items = OrderedDict()
+        self.extra = None
 
     def _key(self, rootdir):
         try:
@@ -85,9 +90,20 @@ class ShardCache:
         t = ct._table
         return 0 if t is None else sum(t.nrows * dt.itemsize for dt in t.dtypes.values())
 
+    def resident_bytes(self):
+        return sum(self._resident(c) for c in self._items.values()) + (self.extra.bytes() if self.extra else 0)
+
     def _evict(self):
-        while len(self._items) > 1 and sum(self._resident(c) for c in self._items.values()) > self.budget:
+        # unions go first (they are rebuilt from resident shards), then the least recently
+        # used shards, always keeping the one just opened
+        while self.resident_bytes() > self.budget:
+            if self.extra and self.extra.drop_oldest():
+                continue
+            if len(self._items) <= 1:
+                break
             _, ct = self._items.popitem(last=False)
+            if self.extra:
+                self.extra.forget(ct)
             ct.close()
 
 
@@ -168,8 +184,10 @@ class CalcPath:
                 for ct in cts:
                     ct._auto_cache(groupby_col_list)
                 colo = node.colocated(r, cts, tables)
-                per_rank[r].append(colo.union(cols).groupby_table(groupby_col_list, aggregation_list,
-                                                                 where_terms=where_terms_list or None))
+                union = colo.union(cols)
+                per_rank[r].append(union.groupby_table(groupby_col_list, aggregation_list,
+                                                       where_terms=where_terms_list or None))
+                node.union_built(r)
             else:
                 for ct in cts:
                     t = _shard_calc_device(ct, groupby_col_list, aggregation_list, where_terms_list,
@@ -217,6 +235,8 @@ class _NodeState:
         self._place = {}
         self._rows = [0] * len(self.devices)
         self._unions = OrderedDict()
+        for r, c in enumerate(self.caches):
+            c.extra = _RankUnions(self, r)
 
     def place(self, rootdir):
         r = self._place.get(rootdir)
@@ -237,11 +257,44 @@ class _NodeState:
             if colo is not None:
                 colo.close()
             colo = dist.ColocatedShards(tables)
+            colo.members = list(cts)
         self._unions[key] = colo
         while len(self._unions) > 4:
             _, old = self._unions.popitem(last=False)
             old.close()
         return colo
+
+    def union_built(self, rank):
+        """A union of ``rank`` was (re)built: its bytes now count against that GPU's cache."""
+        self.caches[rank]._evict()
+
+
+class _RankUnions:
+    """The co-located unions of one GPU, as the ``extra`` HBM of its shard cache."""
+
+    def __init__(self, node, rank):
+        self.node, self.rank = node, rank
+
+    def _mine(self):
+        return [(k, c) for k, c in self.node._unions.items() if k[0] == self.rank]
+
+    def bytes(self):
+        return sum(c.resident_bytes() for _, c in self._mine())
+
+    def drop_oldest(self):
+        mine = [(k, c) for k, c in self._mine() if c.resident_bytes()]
+        if not mine:
+            return False
+        k, c = mine[0]
+        del self.node._unions[k]
+        c.close()
+        return True
+
+    def forget(self, ct):
+        for k, c in self._mine():
+            if any(m is ct for m in getattr(c, 'members', ())):
+                del self.node._unions[k]
+                c.close()
 
 
 def _shard_mask(ct, where_terms_list, expand_filter_column):

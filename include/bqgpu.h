@@ -123,7 +123,8 @@ typedef struct {
                             4 partitioned, 5 fused distinct pass (sorted_count_distinct) */
   int32_t specialized;   /* 1: the scan ran a query-specialised (run-time compiled) kernel */
   int32_t narrow;        /* partitioned mode: 1 when the summed values travelled as exact 32-bit
-                            integer codes (ABI 5) */
+                            integer codes (ABI 5); 2 when the entries were packed 32-bit words
+                            {16-bit value code, slot} (no or one summed column) */
   int32_t regrows;       /* times the last query was re-run after its group hash table or
                             count_distinct set filled past half, each time with twice the slots
                             (ABI 6) */
@@ -163,6 +164,7 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *   small_emit     1  one-workgroup emit for <= 8192 slots              0 | 1
  *   hash_slots     0  initial group hash-table slots (0: from rows)    0..2^31
  *   distinct_slots 0  initial count_distinct set slots (0: from rows)  0..2^31
+ *   part_pack      1  packed 4-byte partition entries when they fit    0 | 1
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);

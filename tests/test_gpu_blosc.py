@@ -90,6 +90,24 @@ def test_memcpyed_frames(tmp_path):
     assert rep['host_chunks'] == 0
 
 
+def test_unimplemented_flag_bit_goes_to_host(tmp_path):
+    """A frame with header flag bit 0x8 set (reserved in c-blosc 1.x, the delta filter in later
+    blosc) is not decoded on the device, where the filter would be silently skipped: it goes
+    to host libblosc, which refuses it (1.21 here), so the call fails instead of returning
+    wrong column data."""
+    a = _array('int32', 50_000, 9, 'small')
+    d = str(tmp_path / 'col')
+    bcolz_io.write_carray(d, a, chunklen=8192, cname='lz4')
+    path = os.path.join(d, 'data', '__2.blp')
+    with open(path, 'r+b') as f:
+        f.seek(16 + 2)
+        flags = f.read(1)[0]
+        f.seek(16 + 2)
+        f.write(bytes([flags | 0x8]))
+    with pytest.raises(RuntimeError):
+        _load(d, a)
+
+
 @pytest.mark.parametrize('cname', ['zstd', 'zlib'])
 def test_other_codecs_fall_back_to_host(tmp_path, cname):
     a = _array('int32', 50_000, 3, 'small')

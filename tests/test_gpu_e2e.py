@@ -191,7 +191,7 @@ def test_auto_cache_factor_files_and_check(tmp_path):
         np.testing.assert_array_equal(bcolz_io.read_carray(os.path.join(root, col + '.factor')), labels)
         np.testing.assert_array_equal(bcolz_io.read_carray(os.path.join(root, col + '.values')), uniq)
         assert ct.cache_valid(col)
-    assert not ct.cache_valid('fare_amount')  # float columns get no cache
+    assert not ct.cache_valid('fare_amount')  # not a groupby column: no cache
     values = {c: bcolz_io.read_carray(os.path.join(root, c + '.values')) for c in ('passenger_count', 'vendor_id')}
     for terms in ([('passenger_count', '==', 42)], [('passenger_count', '==', 3)], [('passenger_count', '>', 9)],
                   [('passenger_count', '>=', 9)], [('passenger_count', '<', 0)], [('passenger_count', '<=', 0.5)],
@@ -203,6 +203,34 @@ def test_auto_cache_factor_files_and_check(tmp_path):
     msg = calc.handle_work(_calc_msg(files[0], ['vendor_id'], [['fare_amount', 'sum', 'f']],
                                      [('passenger_count', 'in', [11, 12])]))
     assert msg['data'] == ''
+
+
+def test_factor_cache_float_and_wide_columns(tmp_path):
+    """Factor caches of groupby columns the lookup table cannot cover -- a float column (with
+    -0.0 / +0.0 and NaN: khash identity) and an int64 column spanning more than 2^27 values --
+    through a hash of the canonical key bits; labels and values against the oracle's factorize,
+    and the factorization check over a float term column then answers the '' early-out."""
+    rng = np.random.default_rng(17)
+    n = 60_000
+    fl = np.array([2.5, -0.0, 0.0, np.nan, 7.25, 1e300, -3.5])
+    cols = OrderedDict(f=fl[rng.integers(0, len(fl), n)],
+                       w=rng.integers(-(1 << 40), 1 << 40, 900)[rng.integers(0, 900, n)].astype(np.int64),
+                       v=rng.integers(0, 9, n).astype(np.int32))
+    root = os.path.join(str(tmp_path), 's.bcolzs')
+    bcolz_io.write_ctable(root, cols)
+    calc = CalcPath(str(tmp_path))
+    calc.handle_work(_calc_msg('s.bcolzs', ['f', 'w'], [['v', 'sum', 'vs']], []))
+    ct = calc.cache.open(root)
+    ct.flush_caches()
+    for col in ('f', 'w'):
+        labels, uniq = bo.factorize(cols[col])
+        np.testing.assert_array_equal(bcolz_io.read_carray(os.path.join(root, col + '.factor')), labels)
+        np.testing.assert_array_equal(bcolz_io.read_carray(os.path.join(root, col + '.values')), uniq)
+        assert ct.cache_valid(col)
+    msg = calc.handle_work(_calc_msg('s.bcolzs', ['v'], [['v', 'count', 'n']], [('f', '==', 3.0)]))
+    assert msg['data'] == ''
+    msg = calc.handle_work(_calc_msg('s.bcolzs', ['v'], [['v', 'count', 'n']], [('f', '==', 7.25)]))
+    assert msg['data'] != ''
 
 
 def test_worker_mask_columns_stay_flat(tmp_path):

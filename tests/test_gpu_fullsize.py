@@ -14,6 +14,8 @@ The oracle sums every group strictly in row order (bquery's ``out[g] += v``,
 bqueryd/worker.py:313 -> ctable.groupby); the GPU sums in a different order, so the float64
 comparisons measure the reference's own rounding noise (~sqrt(n) ulp) as much as ours.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -155,5 +157,82 @@ def test_c5_full_size(variant, oracle_c):
     errs = {c: _rel_err(got[c], ref[c]) for c in _float_cols(cfg, got)}
     print('C5 %s: %d groups, max relative error %s' % (variant, len(ref['n']), errs))
     assert len(ref['n']) > 900_000
+    exact = {'fare_sum'} if variant == 'exact' else set()
+    assert_tables_equal(got, ref, rtol=1e-12, exact_cols=exact)
+
+
+def _c5_shard_and_result(i, variant, oracle_c):
+    """C5 generator shard i and bquery's per-shard result for it (the C restatement)."""
+    cfg = synth.CONFIGS['c5']
+    s = synth.taxi_shard(cfg['rows'] // cfg['shards'], config_id=5, n_shards=cfg['shards'], shard=i,
+                         variant=variant, columns=synth.query_columns(cfg))
+    return s, oracle_c.handle_work(s, cfg['groupby'], cfg['aggs'], cfg['where'])
+
+
+@pytest.mark.parametrize('variant', ['raw', 'exact'])
+def test_c5_full_shape_eight_ranks(variant, oracle_c):
+    """C5 at its stated workload: 80 shards x 12.5 M rows = 1 B rows over 8 ranks (10 shards
+    each, one libbqgpu context per rank, all on this box's one GPU), every rank's shards
+    aggregated in one pass over their union, then the 8-rank merge (bqg_merge_group: pack
+    kernel, count all-gather, per-column exchange, reduce, gather) over the in-process
+    transport -- the code path RCCL runs, with device copies as the wire.  Against the
+    reference client's merge (rpc.py:164-173, aggregate=True: concatenate the 80 per-shard
+    bquery results, group by the keys, sum) of the C restatement's per-shard results; the
+    client merge's groupby is the C restatement's too (the numpy one takes minutes on 80 M
+    rows, and the two agree bit for bit on every golden case).  Rows compared after sorting by
+    the keys (the merged order is by key hash; the client's is glob order, rpc.py:151):
+    keys and counts bit-exact, sums within 1e-12 (bit-exact on dyadic data)."""
+    from collections import OrderedDict
+    from concurrent.futures import ThreadPoolExecutor
+
+    from bqueryd_amd import dist as bdist
+    from bqueryd_amd.engine import Device
+    from tests.helpers import sort_by_keys
+    cfg = synth.CONFIGS['c5']
+    world = 8
+    per_rank = cfg['shards'] // world
+    devs = [Device(0) for _ in range(world)]
+    tables = [[] for _ in range(world)]
+    results = []
+    # shard generation and the per-shard oracle on host threads (numpy's generators and the C
+    # restatement release the GIL); each shard lands in its rank's context and is dropped
+    with ThreadPoolExecutor(min(16, os.cpu_count() or 4)) as ex:
+        for i, (s, r) in enumerate(ex.map(lambda i: _c5_shard_and_result(i, variant, oracle_c), range(cfg['shards']))):
+            tables[i // per_rank].append(ShardTable(s, device=devs[i // per_rank]))
+            results.append(r)
+            del s
+    colos = [bdist.ColocatedShards(t) for t in tables]
+    per = []
+    group = None
+    try:
+        for c in colos:
+            p, reduced = c.groupby_tables(cfg['groupby'], cfg['aggs'])
+            assert reduced
+            per.append(p)
+        dtypes = OrderedDict((k, per[0][0].dtypes[k]) for k in per[0][0].names)
+        group = bdist.CommGroup(devs, transport='local')
+        got = bdist.merge_group_device(per, cfg['groupby'], cfg['aggs'], dtypes, group, reduced=True)
+    finally:
+        if group is not None:
+            group.close()
+        for tabs in per:
+            for p in tabs:
+                p.close()
+        for c in colos:
+            c.close()
+        for ts in tables:
+            for t in ts:
+                t.close()
+    names = list(results[0].keys())
+    cat = OrderedDict((n, np.concatenate([r[n] for r in results])) for n in names)
+    del results
+    ref = oracle_c.groupby(cat, cfg['groupby'], bdist.sum_spec(cfg['aggs']))
+    got, ref = sort_by_keys(got, cfg['groupby']), sort_by_keys(ref, cfg['groupby'])
+    errs = {c: _rel_err(got[c], ref[c]) for c in _float_cols(cfg, got)}
+    print('C5 8 ranks %s: %d groups, %d rows, max relative error %s' % (variant, len(ref['n']), int(ref['n'].sum()), errs))
+    assert int(ref['n'].sum()) == cfg['rows']
+    assert len(ref['n']) > 990_000
+    for c, e in errs.items():
+        assert e <= 1e-12, (c, e)
     exact = {'fare_sum'} if variant == 'exact' else set()
     assert_tables_equal(got, ref, rtol=1e-12, exact_cols=exact)

@@ -486,6 +486,63 @@ def test_partitioned_narrow_codes(kind, oracle_c, engine_options):
             np.testing.assert_allclose(got['vs'], wide['vs'], rtol=1e-12, atol=0)
 
 
+@pytest.mark.parametrize('kind', ['count_only', 'dyadic', 'cents_neg', 'int_span_65535', 'int_span_65536', 'sorted_keys',
+                                  'filtered', 'one_split', 'jit'])
+def test_partitioned_packed_entries(kind, oracle_c, engine_options):
+    """Packed 4-byte partition entries {16-bit value code, slot}: no summed column, or one whose
+    narrow codes span at most 2^16 values.  First appearance comes from each slot's first tile
+    plus a re-read of the marked tiles (k_part_first_rows): group order, keys and counts
+    bit-exact against the oracle, sums bit-exact on dyadic data and identical to the 8-byte
+    entry path (part_pack=0); a span of 2^16 codes keeps the 8-byte entries; one aggregate
+    split over every tile (the packed count / sum fields sized for all rows)."""
+    rng = np.random.default_rng(abs(hash(kind)) % 1000)
+    n = 400_003
+    cols = OrderedDict(k=rng.integers(0, 300_000, n).astype(np.int32),
+                       v=np.round(rng.normal(size=n) * 300) / 64)
+    aggs = [['v', 'sum', 'vs'], ['v', 'count', 'n']]
+    terms = []
+    pack = True
+    if kind == 'count_only':
+        aggs = [['v', 'count', 'n']]
+    elif kind == 'cents_neg':
+        cols['v'] = np.round(rng.normal(size=n) * 30, 2)  # codes about -15000 .. 15000: base16 < 0
+    elif kind == 'int_span_65535':
+        cols['v'] = rng.integers(-7, 65_529, n).astype(np.int32)
+        cols['v'][:2] = [-7, 65_528]
+    elif kind == 'int_span_65536':
+        cols['v'] = rng.integers(-7, 65_530, n).astype(np.int32)
+        cols['v'][:2] = [-7, 65_529]
+        pack = False
+    elif kind == 'sorted_keys':  # every tile holds some group's first row
+        order = np.argsort(cols['k'], kind='stable')
+        cols = OrderedDict((c, a[order]) for c, a in cols.items())
+    elif kind == 'filtered':
+        cols['f'] = rng.integers(0, 5, n).astype(np.int8)
+        terms = [('f', '>', 1)]
+    elif kind == 'one_split':
+        engine_options(part_splits=1)
+        cols['v'] = rng.integers(0, 60_000, n).astype(np.int64)
+    elif kind == 'jit':
+        engine_options(jit_min_rows=0)
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(['k'], aggs, where_terms=terms)
+        info = t.dev.last_timing()
+        with t.dev.options(part_pack=0):
+            wide, _ = t.groupby(['k'], aggs, where_terms=terms)
+            winfo = t.dev.last_timing()
+    finally:
+        t.close()
+    assert info['mode'] == 4 and info['pack16'] == pack, info
+    assert not winfo['pack16']
+    if kind == 'jit':
+        assert info['specialized']
+    ref = oracle_c.groupby(cols, ['k'], aggs, oracle_c.where_terms(cols, terms) if terms else None)
+    exact = {'vs'} if kind not in ('cents_neg',) else set()
+    assert_tables_equal(got, ref, exact_cols=exact)
+    assert_tables_equal(got, wide, exact_float_sums=True)
+
+
 @pytest.mark.parametrize('vrange,no_pack', [(7, False), (7, True), (65_536, False), (200_000, False)])
 def test_fused_distinct_value_widths(vrange, no_pack, oracle_c, engine_options):
     """The fused distinct pass with 32-bit value codes: first value and first row share one

@@ -239,3 +239,55 @@ def test_groupby_plan_cache_key_is_exact():
     with pytest.raises(ValueError):  # bquery: `in` takes lists, sets or tuples
         t._plan(['a'], [['b', 'sum', 's']], [('a', 'in', np.arange(3))], None)
     assert len(t._plans) == 4
+
+
+def test_shard_cache_budget_counts_unions():
+    """The node-level unions of a GPU's shards count against its shard cache budget: over
+    budget, unions are dropped first, then the least recently used shards -- and a union built
+    over an evicted shard goes with it."""
+    class FakeTable:
+        def __init__(self, n):
+            self.nrows, self.dtypes = n, OrderedDict(a=np.dtype(np.int64))
+
+    class FakeCt:
+        def __init__(self, n):
+            self._table, self.closed = FakeTable(n), False
+
+        def close(self):
+            self.closed = True
+
+    class FakeUnions:
+        def __init__(self):
+            self.held = []  # (bytes, members)
+
+        def bytes(self):
+            return sum(b for b, _ in self.held)
+
+        def drop_oldest(self):
+            if not self.held:
+                return False
+            self.held.pop(0)
+            return True
+
+        def forget(self, ct):
+            self.held = [(b, m) for b, m in self.held if ct not in m]
+
+    cache = worker.ShardCache(budget_bytes=1000)
+    cache.extra = FakeUnions()
+    cts = {}
+    for name in ('a', 'b'):
+        cts[name] = FakeCt(40)  # 320 bytes each
+        cache._items[(name, None)] = cts[name]
+    cache.extra.held.append((300, [cts['a'], cts['b']]))
+    cache._evict()
+    assert cache.resident_bytes() == 940 and not cts['a'].closed
+    cts['c'] = FakeCt(40)
+    cache._items[('c', None)] = cts['c']
+    cache._evict()  # 1260 > 1000: the union goes first (960 left)
+    assert cache.extra.held == [] and not any(c.closed for c in cts.values())
+    cache.extra.held.append((100, [cts['a']]))
+    cts['d'] = FakeCt(10)
+    cache._items[('d', None)] = cts['d']
+    cache._evict()  # 1140: the union, then shard a (least recent)
+    assert cache.extra.held == [] and cts['a'].closed and not cts['b'].closed
+    assert cache.resident_bytes() <= 1000
