@@ -215,7 +215,7 @@ def _c5_local_ranks(args):
         p_.close()
     group = bdist.CommGroup(devs, transport='local')
     shard_s = [[] for _ in range(W)]
-    merge_s, timings = [], []
+    merge_s, timings, phases = [], [], []
 
     def step():
         per = []
@@ -228,6 +228,7 @@ def _c5_local_ranks(args):
         t1 = time.perf_counter()
         merged = bdist.merge_group_device(per, cfg['groupby'], cfg['aggs'], dtypes, group, reduced=True)
         merge_s.append(time.perf_counter() - t1)
+        phases.append([list(bdist.merge_phases(d).values()) for d in devs])
         for tabs in per:
             for p in tabs:
                 p.close()
@@ -239,7 +240,7 @@ def _c5_local_ranks(args):
         raise SystemExit('sanity check failed: %d merged rows' % int(out['n'].sum()))
     for d in devs:
         d.enable_timing(True)
-    for lst in shard_s + [merge_s, timings]:
+    for lst in shard_s + [merge_s, timings, phases]:
         del lst[:]
     for d in devs:
         d.synchronize()
@@ -271,8 +272,14 @@ def _c5_local_ranks(args):
 
     rank_ms = [1e3 * float(np.mean(s)) for s in shard_s]
     merge_ms = 1e3 * float(np.mean(merge_s))
+    ph = np.mean(np.array(phases), axis=0)  # [rank][phase] ms
+    phase_max = {n: float(ph[:, i].max()) for i, n in enumerate(bdist.MERGE_PHASES)}
+    # the merge as 8 GPUs would run it: each phase as long as its slowest rank (the collective
+    # steps measured as one in-process transfer of all ranks), + the result's copy to the host
+    host_copy_ms = max(0.0, merge_ms - float(ph[0].sum()))
+    merge_crit_ms = sum(phase_max.values()) + host_copy_ms
     one_ms = 1e3 * float(np.mean(one_s))
-    proj_ms = max(rank_ms) + merge_ms
+    proj_ms = max(rank_ms) + merge_crit_ms
     total_rows = n_shards * shard_rows
     one_rate = per_rank * shard_rows / (one_ms * 1e-3)
     proj_rate = total_rows / (proj_ms * 1e-3)
@@ -301,6 +308,9 @@ def _c5_local_ranks(args):
             'parallelism': '%d in-process ranks on one GPU' % W,
             'shard_pass_ms_per_rank': rank_ms,
             'merge_ms_all_ranks': merge_ms,
+            'merge_phase_ms_max_over_ranks': phase_max,
+            'merge_result_to_host_ms': host_copy_ms,
+            'merge_ms_critical_path': merge_crit_ms,
             'merge': 'bqg_merge_group at world %d: pack kernel, count all-gather, per-column exchange, reduce, '
                      'gather to rank 0, copy to host; every rank\'s work on this one GPU' % W,
             'one_gpu': {'ms_per_step': one_ms, 'rows_per_s': one_rate, 'merge_ms_world1': 1e3 * float(np.mean(one_merge_s)),
@@ -309,8 +319,10 @@ def _c5_local_ranks(args):
             'projected_node': {'gpus': W, 'ms_per_step': proj_ms, 'rows_per_s': proj_rate,
                                'x_over_one_gpu': proj_rate / one_rate,
                                'basis': 'max over ranks of the measured shard pass (each as alone on its GPU) + the '
-                                        'measured %d-rank merge with every rank on one GPU (an upper bound for the '
-                                        'merge over xGMI); not an 8-GPU measurement' % W},
+                                        'merge\'s critical path: every merge phase as long as its slowest rank '
+                                        '(host wall time per rank; the collective steps measured as one in-process '
+                                        'transfer of all %d ranks on this GPU) + the result\'s copy to the host; '
+                                        'not an 8-GPU measurement' % W},
         },
         'roofline': {
             'bound': 'hbm',

@@ -32,7 +32,7 @@ UNIQUE_ID_BYTES = 128
 ABI_VERSION = 6
 OPTIONS = ('jit', 'jit_min_rows', 'partition', 'part_wbits', 'part_k', 'part_threads', 'part_per_cu',
            'part_splits', 'part_narrow', 'fused_scd', 'scd_compact', 'scd_pack16', 'priv_ahead',
-           'private_per_cu', 'small_emit', 'hash_slots', 'distinct_slots', 'part_pack')
+           'private_per_cu', 'small_emit', 'hash_slots', 'distinct_slots', 'part_pack', 'scd_runs')
 
 
 class Term(ctypes.Structure):
@@ -130,6 +130,7 @@ _PROTOS = {
     'bqg_comm_init_local': ([_I32, _P], ctypes.c_int),
     'bqg_comm_destroy': ([_P], ctypes.c_int),
     'bqg_comm_info': ([_P, ctypes.POINTER(_I32), ctypes.POINTER(_I32)], ctypes.c_int),
+    'bqg_comm_last_phases': ([_P, ctypes.POINTER(ctypes.c_double), _I32], ctypes.c_int),
     'bqg_merge': ([_P, _I32, _P, _I32, _I32, _P, _I32, ctypes.POINTER(_P)], ctypes.c_int),
     'bqg_merge_group': ([_I32, _P, _P, _P, _I32, _I32, _P, _I32, _P], ctypes.c_int),
     'bqg_result_view_get': ([_P, ctypes.POINTER(ResultView)], ctypes.c_int),

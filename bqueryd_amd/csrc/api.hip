@@ -138,6 +138,7 @@ struct ColStats {
   // codes): 1 = dyadic, code = v * 2^enc_k; 2 = cents, code = rint(v * 100); 0 = none
   int enc = 0;
   int enc_k = 0;
+  int64_t runs = -1;  // value runs (rows differing from the row before + 1), -1 = not measured
 };
 
 struct Column {
@@ -306,7 +307,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -317,7 +318,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"jit_min_rows", 4ll << 20, 0, INT64_MAX},  // ... for tables of at least this many rows
     {"partition", 1, 0, 1},                 // partitioned aggregation for large dense slot spaces
     {"part_wbits", 0, 0, 13},               // slots per partition 2^wbits (0: auto, else 6..13)
-    {"part_k", 0, 0, 2},                    // 4-row chunks per scatter thread (0: auto)
+    {"part_k", 0, 0, 4},                    // 4-row chunks per scatter thread (0: auto; 4: packed entries only)
     {"part_threads", 0, 0, 1024},           // scatter workgroup size (0: auto; 256, 512, 1024)
     {"part_per_cu", 0, 0, 8},               // scatter workgroups per CU (0: auto)
     {"part_splits", 0, 0, 1 << 20},         // aggregate workgroups per partition (0: auto)
@@ -331,6 +332,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"hash_slots", 0, 0, 1ll << 31},        // initial hash-table slots (0: from the row count)
     {"distinct_slots", 0, 0, 1ll << 31},    // initial count_distinct set slots (0: from rows)
     {"part_pack", 1, 0, 1},                 // packed 4-byte partition entries when they fit
+    {"scd_runs", 1, 0, 1},                  // fused distinct pass: 256-row steps for clustered keys
 };
 
 static int opt_index(const char* name) {
@@ -414,6 +416,7 @@ void compute_stats(bqg_table* t, int col) {
   bqg_ctx* c = t->ctx;
   Column& k = t->cols[col];
   if (k.stats.valid) return;
+  k.stats.runs = -1;  // measured again on demand (column_runs)
   unsigned long long* d = (unsigned long long*)c->misc.ensure(8 * sizeof(unsigned long long));
   unsigned long long init[8] = {~0ull, 0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
   unsigned long long* h = (unsigned long long*)c->hhdr.ensure(128);
@@ -458,6 +461,24 @@ void compute_stats(bqg_table* t, int col) {
     }
   }
   k.stats.valid = true;
+}
+
+// value runs of a column (count_runs: one pass, cached with the statistics; a push or a
+// chunk load invalidates both)
+int64_t column_runs(bqg_table* t, int col) {
+  bqg_ctx* c = t->ctx;
+  Column& k = t->cols[col];
+  compute_stats(t, col);
+  if (k.stats.runs >= 0) return k.stats.runs;
+  unsigned long long* d = (unsigned long long*)c->misc.ensure(64);
+  HIPCHECK(hipMemsetAsync(d, 0, 8, c->stream));
+  launch_runs(DevCol{k.dev, k.dtype, dtype_lg(k.dtype)}, t->nrows, d, c->stream);
+  HIPCHECK(hipGetLastError());
+  unsigned long long* h = (unsigned long long*)c->hhdr.ensure(128);
+  HIPCHECK(hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  k.stats.runs = t->nrows > 0 ? (int64_t)h[0] + 1 : 0;
+  return k.stats.runs;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1097,8 +1118,14 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         // 8192-row tiles (two 4-row chunks per thread) when the staged tile fits: the aggregate's
         // per-tile partition segments are twice as long (option part_k=1|2 forces the choice)
         L.k = (L.threads == 1024 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw, pk) <= 150 * 1024) ? 2 : 1;
-        if (c->opt[kOptPartK])
-          L.k = (c->opt[kOptPartK] == 2 && part_scatter_lds(L.nparts, L.threads, nsum, 2, nw, pk) <= 150 * 1024) ? 2 : 1;
+        if (c->opt[kOptPartK]) {
+          // 1, 2 or (packed entries: 16384-row tiles) 4 chunks, the most that fit
+          int want = c->opt[kOptPartK] >= 4 ? 4 : (int)c->opt[kOptPartK];
+          while (want > 1 && !(L.threads == 1024 && (want != 4 || pk) &&
+                               part_scatter_lds(L.nparts, L.threads, nsum, want, nw, pk) <= 150 * 1024))
+            want >>= 1;
+          L.k = want;
+        }
         L.tile_rows = L.threads * kRowsPerThread * L.k;
         const int64_t tr = L.tile_rows;
         L.ntiles = (N + tr - 1) / tr;
@@ -1385,6 +1412,11 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
           waves = need;
         }
       }
+      // clustered keys (runs of 512 rows and more on average in the first key column) and no
+      // row filter: the RUNS loop (256-row steps)
+      if (fused && d.compact && c->opt[kOptScdRuns] && pc.p.nterms == 0 && pc.p.mask_col < 0 && q->n_keys > 0 &&
+          column_runs(t, q->key_cols[0]) * 512 <= N)
+        d.runs = 1;
       d.waves = (int)waves;
       d.chunk_rows = (((int64_t)((N + waves - 1) / waves)) + grain - 1) / grain * grain;
       d.lds_state = (S * 24 * (kBlock / 64) <= 64 * 1024) ? 1 : 0;
@@ -1416,7 +1448,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         std::string spec = jit_spec(pc.p) + "#define BQ_SCD_CD " + std::to_string(cd_mode) + "\n#define BQ_SCD_VC " +
                            std::to_string(vc) + "\n#define BQ_SCD_CC " + std::to_string(cc) + "\n#define BQ_SCD_P16 " +
                            std::to_string(d.pack16) + "\n";
-        sfn = jit_function(d.compact ? "bq_jit_scd_fused32" : "bq_jit_scd_fused", spec);
+        sfn = jit_function(d.runs ? "bq_jit_scd_runs32" : d.compact ? "bq_jit_scd_fused32" : "bq_jit_scd_fused", spec);
         c->last.specialized = sfn ? 1 : 0;
       }
       if (fused && c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));

@@ -32,6 +32,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -139,11 +140,17 @@ struct Buf {
   }
 };
 
+constexpr int kMergePhases = 6;  // bqg_comm_last_phases
 struct CommState {
   ncclComm_t comm = nullptr;  // RCCL transport; nullptr = in-process transport (see below)
   int rank = 0, nranks = 1;
   Buf send, scratch, counts;  // packed send blocks, pack scratch, row counts
+  double phase_ms[kMergePhases] = {};  // host wall time of this rank's part of the last merge
 };
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 std::mutex g_mu;
 std::map<bqg_ctx*, CommState*> g_comms;
@@ -317,6 +324,73 @@ Local& by_rank(std::vector<Local>& ranks, int r) {
   comm_fail(BQG_E_STATE, "in-process transport: a rank of the communicator is not part of this merge call");
 }
 
+// In-process transport on one GPU: every copy of a transfer step in ONE kernel launch (a
+// descriptor per copy; 16-, 4- or 1-byte moves by alignment) instead of one hipMemcpyAsync
+// per (rank, peer, column) -- the host cost of hundreds of small copies would otherwise swamp
+// the exchange being measured.
+struct CopyDesc {
+  const unsigned char* src;
+  unsigned char* dst;
+  unsigned long long bytes;
+};
+
+__global__ __launch_bounds__(256) void k_batch_copy(const CopyDesc* d) {
+  const CopyDesc c = d[blockIdx.y];
+  const unsigned long long stride = (unsigned long long)gridDim.x * 256;
+  const uintptr_t al = (uintptr_t)c.src | (uintptr_t)c.dst | (uintptr_t)c.bytes;
+  if ((al & 15) == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(c.src);
+    uint4* d4 = reinterpret_cast<uint4*>(c.dst);
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < c.bytes / 16; i += stride)
+      d4[i] = s4[i];
+  } else if ((al & 3) == 0) {
+    const uint32_t* s1 = reinterpret_cast<const uint32_t*>(c.src);
+    uint32_t* d1 = reinterpret_cast<uint32_t*>(c.dst);
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < c.bytes / 4; i += stride)
+      d1[i] = s1[i];
+  } else {
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < c.bytes; i += stride)
+      c.dst[i] = c.src[i];
+  }
+}
+
+bool one_device(std::vector<Local>& ranks) {
+  for (Local& l : ranks)
+    if (bqg_internal_device(l.ctx) != bqg_internal_device(ranks[0].ctx)) return false;
+  return true;
+}
+
+// the copies of one in-process transfer step, on rank 0's stream (the caller syncs every rank
+// before and after); contexts on different GPUs copy one by one on the receiver's stream
+void batch_copies(std::vector<Local>& ranks, const std::vector<std::pair<size_t, CopyDesc>>& copies) {
+  if (copies.empty()) return;
+  if (!one_device(ranks)) {
+    for (const auto& rc : copies) {
+      Local& d = ranks[rc.first];
+      HIPCK(hipSetDevice(bqg_internal_device(d.ctx)));
+      HIPCK(hipMemcpyAsync(rc.second.dst, rc.second.src, rc.second.bytes, hipMemcpyDefault, d.stream));
+    }
+    return;
+  }
+  Local& l = ranks[0];
+  HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+  std::vector<CopyDesc> h;
+  unsigned long long most = 0;
+  for (const auto& rc : copies) {
+    h.push_back(rc.second);
+    most = std::max<unsigned long long>(most, rc.second.bytes);
+  }
+  for (size_t i0 = 0; i0 < h.size(); i0 += 65535) {
+    const size_t n = std::min<size_t>(65535, h.size() - i0);
+    CopyDesc* dd = (CopyDesc*)l.st->scratch.ensure(sizeof(CopyDesc) * h.size());
+    HIPCK(hipMemcpyAsync(dd, h.data() + i0, sizeof(CopyDesc) * n, hipMemcpyHostToDevice, l.stream));
+    const unsigned gx = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>(512, (most / 16 + 255) / 256));
+    hipLaunchKernelGGL(k_batch_copy, dim3(gx, (unsigned)n), dim3(256), 0, l.stream, dd);
+    HIPCK(hipGetLastError());
+    HIPCK(hipStreamSynchronize(l.stream));  // the descriptors' host copy and scratch are reused
+  }
+}
+
 // every rank: `count` int64 at counts.p -> [nranks][count] at counts.p + nranks
 void xfer_allgather_i64(std::vector<Local>& ranks, size_t count) {
   const int W = ranks[0].st->nranks;
@@ -332,14 +406,17 @@ void xfer_allgather_i64(std::vector<Local>& ranks, size_t count) {
   }
   if ((int)ranks.size() != W) comm_fail(BQG_E_STATE, "in-process transport needs every rank in one merge call");
   sync_all(ranks);
-  for (Local& d : ranks) {
-    HIPCK(hipSetDevice(bqg_internal_device(d.ctx)));
+  std::vector<std::pair<size_t, CopyDesc>> copies;
+  for (size_t i = 0; i < ranks.size(); ++i) {
+    Local& d = ranks[i];
     for (int s = 0; s < W; ++s) {
       Local& src = by_rank(ranks, s);
-      HIPCK(hipMemcpyAsync((int64_t*)d.st->counts.p + W + (size_t)s * count, src.st->counts.p, count * sizeof(int64_t),
-                           hipMemcpyDefault, d.stream));
+      copies.push_back({i, CopyDesc{(const unsigned char*)src.st->counts.p,
+                                    (unsigned char*)((int64_t*)d.st->counts.p + W + (size_t)s * count),
+                                    count * sizeof(int64_t)}});
     }
   }
+  batch_copies(ranks, copies);
   sync_all(ranks);
 }
 
@@ -358,9 +435,9 @@ void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& se
     return;
   }
   sync_all(ranks);
+  std::vector<std::pair<size_t, CopyDesc>> copies;
   for (size_t i = 0; i < ranks.size(); ++i) {
     Local& d = ranks[i];
-    HIPCK(hipSetDevice(bqg_internal_device(d.ctx)));
     std::vector<size_t> taken(ranks.size(), 0);  // messages of each sender matched so far
     for (const P2P& x : recvs[i]) {
       size_t j = 0;
@@ -375,9 +452,10 @@ void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& se
         }
       ++taken[j];
       if (!m || m->bytes != x.bytes) comm_fail(BQG_E_STATE, "in-process transport: unmatched send / receive");
-      HIPCK(hipMemcpyAsync(x.ptr, m->ptr, x.bytes, hipMemcpyDefault, d.stream));
+      copies.push_back({i, CopyDesc{(const unsigned char*)m->ptr, (unsigned char*)x.ptr, x.bytes}});
     }
   }
+  batch_copies(ranks, copies);
   sync_all(ranks);
 }
 
@@ -416,8 +494,18 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       }
     return off;
   };
+  // phases (bqg_comm_last_phases): 0 local re-group + pack, 1 count exchange, 2 payload
+  // exchange, 3 reduce, 4 gather counts, 5 gather + final sync; a collective step's time is
+  // charged to every rank of the call
+  for (Local& l : ranks)
+    for (double& x : l.st->phase_ms) x = 0.0;
+  auto collective = [&](int ph, double t0) {
+    const double dt = now_ms() - t0;
+    for (Local& l : ranks) l.st->phase_ms[ph] += dt;
+  };
   // 1-2. local reduce, then every row straight into its destination's packed block
   for (Local& l : ranks) {
+    const double t0 = now_ms();
     HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
     std::vector<bqg_table*> parts;
     for (bqg_table* t : l.tables)
@@ -461,10 +549,14 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       bqg::launch_merge_pack(m, l.stream);
       HIPCK(hipGetLastError());
     }
+    l.st->phase_ms[0] += now_ms() - t0;
   }
   // 3a. count matrix: every rank's row counts per destination
+  double tc = now_ms();
   xfer_allgather_i64(ranks, (size_t)W);
+  collective(1, tc);
   for (Local& l : ranks) {
+    const double t0 = now_ms();
     HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
     std::vector<int64_t> m((size_t)W * W);
     HIPCK(hipMemcpyAsync(m.data(), (int64_t*)l.st->counts.p + W, sizeof(int64_t) * W * W, hipMemcpyDeviceToHost,
@@ -473,6 +565,7 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     l.to_peer.assign(m.begin() + (size_t)l.st->rank * W, m.begin() + (size_t)(l.st->rank + 1) * W);
     l.from_peer.assign(W, 0);
     for (int s = 0; s < W; ++s) l.from_peer[s] = m[(size_t)s * W + l.st->rank];
+    l.st->phase_ms[1] += now_ms() - t0;
   }
   // 3b. payload: column by column, straight into the receiving rank's table
   {
@@ -500,11 +593,14 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
         off += l.from_peer[s];
       }
     }
+    tc = now_ms();
     xfer_p2p(ranks, sends, recvs);
+    collective(2, tc);
   }
   // 4. reduce the received rows: one source's rows are already unique by key, only rows from
   // two or more sources need the re-group
   for (Local& l : ranks) {
+    const double t0 = now_ms();
     HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
     l.L.reset();  // sent (stream-ordered before any later use of its memory)
     l.Lv = nullptr;
@@ -517,8 +613,10 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     }
     int64_t* cnt = (int64_t*)l.st->counts.p;
     put_count(cnt, l.R.t ? nrows_of(l.ctx, l.R.t) : 0, l.stream);
+    l.st->phase_ms[3] += now_ms() - t0;
   }
   // 5. gather to rank 0: counts, then the reduced partitions column by column
+  tc = now_ms();
   xfer_allgather_i64(ranks, 1);
   std::vector<int64_t> part_rows(W, 0);
   for (Local& l : ranks)
@@ -528,6 +626,8 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
                            hipMemcpyDeviceToHost, l.stream));
       HIPCK(hipStreamSynchronize(l.stream));
     }
+  collective(4, tc);
+  tc = now_ms();
   if (ranks.size() < (size_t)W || ranks[0].st->rank != 0) {
     // a process driving only some ranks (one process per GPU): non-root ranks learn the
     // gather sizes they need (their own) locally
@@ -575,6 +675,7 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     else *l.out = nullptr;
     l.R.reset();
   }
+  collective(5, tc);
 }
 
 }  // namespace
@@ -675,6 +776,14 @@ int bqg_comm_info(bqg_ctx* ctx, int32_t* rank, int32_t* nranks) {
     CommState* s = state_of(ctx);
     if (rank) *rank = s->rank;
     if (nranks) *nranks = s->nranks;
+  });
+}
+
+int bqg_comm_last_phases(bqg_ctx* ctx, double* ms, int32_t n) {
+  return comm_guard(ctx, [&] {
+    if (!ms || n < 0) comm_fail(BQG_E_INVALID, "null output");
+    CommState* s = state_of(ctx);
+    for (int i = 0; i < n && i < kMergePhases; ++i) ms[i] = s->phase_ms[i];
   });
 }
 

@@ -69,6 +69,20 @@ __device__ __forceinline__ void load_rows4(const ScanParams& p, int64_t row0, Ch
   for (int c = 0; c < NC; ++c) load_chunk(raw[c], p.cols[c], row0);
 }
 
+// A thread's 4-row chunk of the columns in `mask`, loaded unconditionally: a chunk at or past
+// `end` re-reads the block's last chunk (its rows are masked off by the caller), and a column
+// outside `mask` re-reads its own first chunk at `home` (one cache line for the whole wave:
+// no HBM traffic to speak of).  Every path keeps the same number of loads in flight, so the
+// compiler waits for exactly the chunk it consumes (vmcnt(N)) instead of draining the
+// prefetch (vmcnt(0)).
+template <int NC>
+__device__ __forceinline__ void load_rows4_clamped(const ScanParams& p, int64_t row0, int64_t end, Chunk (&raw)[NC],
+                                                   uint32_t mask, int64_t home) {
+  const int64_t r = row0 < end ? row0 : ((end - 1) & ~(int64_t)(kRowsPerThread - 1));
+#pragma unroll
+  for (int c = 0; c < NC; ++c) load_chunk(raw[c], p.cols[c], ((mask >> c) & 1u) ? r : home);
+}
+
 __device__ __forceinline__ void load_one(Chunk& c, const DevCol& col, int64_t row) {
   c.sh = 0;
   switch (col.lg) {

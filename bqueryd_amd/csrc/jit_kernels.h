@@ -52,3 +52,10 @@ extern "C" __global__ __launch_bounds__(256) void bq_jit_scd_fused32(bqg::ScanPa
   bqg::jit_specialize(p);
   bqg::scd_fused_body<BQ_NC, true>(p, d, smem);
 }
+
+extern "C" __global__ __launch_bounds__(256) void bq_jit_scd_runs32(bqg::ScanParams pin, bqg::ScdLaunch d) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  bqg::ScanParams p = pin;
+  bqg::jit_specialize(p);
+  bqg::scd_fused_body<BQ_NC, true, true>(p, d, smem);
+}

@@ -226,10 +226,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_scd(ScanParams p, SlotArrays sa, 
 
 // k_scd_fused: sorted_count_distinct + per-slot rows / first rows (+ one count_distinct) in
 // one pass -- body in scd.h
-template <int NC, bool COMPACT>
+template <int NC, bool COMPACT, bool RUNS = false>
 __global__ __launch_bounds__(kBlock) void k_scd_fused(ScanParams p, ScdLaunch d) {
   extern __shared__ __align__(16) unsigned char smem[];
-  scd_fused_body<NC, COMPACT>(p, d, smem);
+  scd_fused_body<NC, COMPACT, RUNS>(p, d, smem);
 }
 
 struct ScdState {
@@ -364,7 +364,9 @@ void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hi
       void* args[] = {(void*)&p, (void*)&d};
       (void)hipModuleLaunchKernel(fused_fn, (unsigned)blocks, 1, 1, kBlock, 1, 1, (unsigned)lds, st, args, nullptr);
     } else {
-      if (d.compact) {
+      if (d.compact && d.runs) {
+        BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd_fused<NC, true, true>), dim3(blocks), dim3(kBlock), lds, st, p, d));
+      } else if (d.compact) {
         BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd_fused<NC, true>), dim3(blocks), dim3(kBlock), lds, st, p, d));
       } else {
         BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_scd_fused<NC, false>), dim3(blocks), dim3(kBlock), lds, st, p, d));

@@ -798,6 +798,43 @@ void launch_merge_pack(const MergePack& m, hipStream_t st) {
   if (m.nrows > 0) hipLaunchKernelGGL(k_mpack_scatter, dim3(m.nblocks), dim3(kBlock), 0, st, m);
 }
 
+// value runs: rows whose value differs from the previous row's (canonical bits: a float
+// column's -0.0 / +0.0 and NaN count as one value, like a group key)
+__global__ __launch_bounds__(kBlock) void k_runs(DevCol c, int64_t nrows, unsigned long long* out) {
+  unsigned long long n = 0;
+  for (int64_t row = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kRowsPerThread; row < nrows;
+       row += (int64_t)gridDim.x * kBlock * kRowsPerThread) {
+    Chunk ch;
+    load_chunk(ch, c, row);
+    uint64_t v[4];
+    decode<4>(ch, c.dtype, v);
+    uint64_t prev = 0;
+    if (row > 0) {
+      Chunk pc;
+      row_word_to_chunk(pc, c, row - 1, load_row_word(c, row - 1));
+      uint64_t pv[1];
+      decode<1>(pc, c.dtype, pv);
+      prev = pv[0];
+    }
+    const bool isf = dtype_is_float(c.dtype);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint64_t x = isf ? canon_f64_bits(v[r]) : v[r];
+      const uint64_t y = isf ? canon_f64_bits(prev) : prev;
+      if (row + r < nrows && row + r > 0 && x != y) ++n;
+      prev = v[r];
+    }
+  }
+  n = wave_sum_u64(n);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(out, n);
+}
+
+void launch_runs(const DevCol& c, int64_t nrows, unsigned long long* out, hipStream_t st) {
+  int64_t blocks = (nrows + kTileRows - 1) / kTileRows;
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 2048));
+  if (nrows > 0) hipLaunchKernelGGL(k_runs, dim3((unsigned)blocks), dim3(kBlock), 0, st, c, nrows, out);
+}
+
 void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, hipStream_t st) {  // out4: 5 words
   int64_t blocks = (nrows + kTileRows - 1) / kTileRows;
   if (blocks > 1024) blocks = 1024;

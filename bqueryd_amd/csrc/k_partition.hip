@@ -85,7 +85,8 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   // (lane j: entry index of tile j's segment start minus its flattened position) and the total
   struct Grp {
     uint32_t ex[G];
-    uint32_t dl, total;
+    uint32_t dl[G];  // per tile j: entry index of its segment start minus its flattened position
+    uint32_t total;
     size_t gbase;
     uint32_t tile0;
   };
@@ -99,9 +100,12 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     const uint32_t incl = wave_incl_scan_u32(len, lane);
     const uint32_t excl = incl - len;
     g.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, G - 1);
+    const uint32_t dl = (uint32_t)lane * TR + s0 - excl;
 #pragma unroll
-    for (int j = 0; j < G; ++j) g.ex[j] = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
-    g.dl = (uint32_t)lane * TR + s0 - excl;
+    for (int j = 0; j < G; ++j) {
+      g.ex[j] = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
+      g.dl[j] = (uint32_t)__builtin_amdgcn_readlane((int)dl, j);
+    }
     g.gbase = (size_t)tg * TR;
     g.tile0 = (uint32_t)tg;
   };
@@ -113,10 +117,16 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     for (int u = 0; u < U; ++u) {
       const uint32_t e = e0 + u * 64u + lane;
       const uint32_t ec = e < g.total ? e : (g.total ? g.total - 1u : 0u);
-      uint32_t j0 = 0;
+      // the entry's tile: the last j whose segment starts at or before it (wave-uniform starts
+      // and bases: compares and selects, no lane shuffle)
+      uint32_t j0 = 0, dsel = g.dl[0];
 #pragma unroll
-      for (int j = 1; j < G; ++j) j0 += ec >= g.ex[j] ? 1u : 0u;
-      size_t idx = g.gbase + (uint32_t)__shfl((int)g.dl, (int)j0, 64) + ec;
+      for (int j = 1; j < G; ++j) {
+        const bool in = ec >= g.ex[j];
+        j0 += in ? 1u : 0u;
+        dsel = in ? g.dl[j] : dsel;
+      }
+      size_t idx = g.gbase + dsel + ec;
       idx = g.total ? idx : 0;
       en.rowb[u] = PACK ? g.tile0 + j0 : (uint32_t)g.gbase + j0 * TR;  // PACK: the tile
       en.m[u] = L.meta[idx];
@@ -320,23 +330,37 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
 // random keys the marked tiles are the first ~10-15 % (each slot's first appearance falls
 // early); on sorted keys every tile is marked.
 template <int NC>
-__global__ __launch_bounds__(256) void k_part_first_rows(ScanParams p, PartLaunch L, SlotArrays sa) {
+__global__ __launch_bounds__(1024) void k_part_first_rows(ScanParams p, PartLaunch L, SlotArrays sa) {
+  // only the key, term and mask columns are read (the others re-read one line per wave)
+  uint32_t need = p.mask_col >= 0 ? 1u << p.mask_col : 0u;
+  for (int k = 0; k < p.nkeys; ++k) need |= 1u << p.keys[k].col;
+  for (int i = 0; i < p.nterms; ++i) need |= 1u << p.terms[i].col;
+  const int64_t TR = L.tile_rows;
   for (int64_t t = blockIdx.x; t < L.ntiles; t += gridDim.x) {
     if (!L.tile_mark[t]) continue;
-    const int64_t base = t * (int64_t)L.tile_rows;
-    const int64_t end = min(p.nrows, base + (int64_t)L.tile_rows);
-    for (int64_t row0 = base + (int64_t)threadIdx.x * kRowsPerThread; row0 < end; row0 += 256 * kRowsPerThread) {
-      Chunk raw[NC];
-      load_rows4<NC>(p, row0, raw);
+    const int64_t base = t * TR;
+    const int64_t end = min(p.nrows, base + TR);
+    // a tile is at most 4 x 1024 4-row chunks, taken two at a time: both loads in flight
+    // before either is used
+    for (int k0 = 0; (int64_t)k0 * 1024 * kRowsPerThread < TR; k0 += 2) {
+    Chunk raw[2][NC];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      load_rows4_clamped<NC>(p, base + ((int64_t)threadIdx.x + (k0 + k) * 1024) * kRowsPerThread, end, raw[k], need, base);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int64_t row0 = base + ((int64_t)threadIdx.x + (k0 + k) * 1024) * kRowsPerThread;
+      if (row0 >= end) continue;
       uint64_t v[NC][4], code[4];
-      decode_all<NC, 4>(p, raw, v);
+      decode_all<NC, 4>(p, raw[k], v);
       uint32_t pass = vals_pass<NC, 4>(p, row0, v);
       const int64_t rem = end - row0;
       pass &= rem >= 4 ? 0xFu : ((1u << rem) - 1u);
       vals_code<NC, 4>(p, v, code);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if ((pass >> r) & 1u && L.first_tile[code[r]] == (uint32_t)t) atomicMin(&sa.fst[code[r]], (uint32_t)(row0 + r));
+        if (((pass >> r) & 1u) && L.first_tile[code[r]] == (uint32_t)t) atomicMin(&sa.fst[code[r]], (uint32_t)(row0 + r));
+    }
     }
   }
 }
@@ -383,7 +407,9 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
                                 st, args, nullptr);
   } else {
 #define BQG_SCATTER(K, NW, PK) BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_scatter<NC, K, NW, PK>), dim3(L.blocks), dim3(L.threads), scatter_lds, st, p, L))
-    if (L.k == 2) {
+    if (L.k == 4) {
+      BQG_SCATTER(4, true, true);  // 16384-row tiles: packed entries only (LDS)
+    } else if (L.k == 2) {
       if (L.pack) {
         BQG_SCATTER(2, true, true);
       } else if (L.narrow) {
@@ -414,8 +440,9 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
       if (big) BQG_AGGP(4, 4, 1); else BQG_AGGP(8, 4, 1);
     }
 #undef BQG_AGGP
-    const unsigned fgrid = (unsigned)std::min<int64_t>(L.ntiles, 65535);
-    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_first_rows<NC>), dim3(fgrid), dim3(256), 0, st, p, L, s));
+    // grid-stride over the tiles (the marked ones are mostly a prefix on random keys)
+    const unsigned fgrid = (unsigned)std::min<int64_t>(L.ntiles, 2048);
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_first_rows<NC>), dim3(fgrid), dim3(1024), 0, st, p, L, s));
     return;
   }
   // G tiles per wave group: ~8 x 4096 rows of segments whichever the tile size

@@ -103,6 +103,7 @@ struct ScdLaunch {
   int compact;                       // fused: 32-bit value codes (integer values, range < 2^32)
   int pack16;                        // compact: value codes < 2^16, first value + first row in one word
   int64_t vmin;                      // compact: value code = v - vmin
+  int runs;                          // compact: the RUNS loop (clustered keys, no terms / mask)
 };
 // LDS bytes per wave of k_scd_fused for a slot space of nslots: a 32-byte state per slot (20
 // bytes with compact 32-bit value codes) plus an 8-byte lane mask per slot
@@ -143,6 +144,9 @@ void launch_emit_small(const EmitParams& e, const SlotArrays& s, uint32_t nslots
 
 // column statistics (min / max / nan) of one column
 void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, hipStream_t st);
+// value runs of one column: rows whose value differs from the row before (out: one counter,
+// zeroed by the caller)
+void launch_runs(const DevCol& c, int64_t nrows, unsigned long long* out, hipStream_t st);
 
 // where_terms -> uint8 mask column, passing-row count
 void launch_where(const ScanParams& p, unsigned char* out_mask, unsigned long long* npass,

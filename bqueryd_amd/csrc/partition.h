@@ -64,20 +64,6 @@ __device__ __forceinline__ uint32_t block_excl_scan_1b(uint32_t v, uint32_t* wsu
 // scatter: workgroups of up to 1024 threads, each over a contiguous range of whole tiles
 constexpr int kPartBlock = 1024;
 
-// A thread's 4-row chunk of the columns in `mask`, loaded unconditionally: a chunk at or past
-// `end` re-reads the block's last chunk (its rows are masked off by the caller), and a column
-// outside `mask` re-reads its own first chunk at `home` (one cache line for the whole wave:
-// no HBM traffic to speak of).  Every path keeps the same number of loads in flight, so the
-// compiler waits for exactly the chunk it consumes (vmcnt(N)) instead of draining the
-// prefetch (vmcnt(0)).
-template <int NC>
-__device__ __forceinline__ void load_rows4_clamped(const ScanParams& p, int64_t row0, int64_t end, Chunk (&raw)[NC],
-                                                   uint32_t mask, int64_t home) {
-  const int64_t r = row0 < end ? row0 : ((end - 1) & ~(int64_t)(kRowsPerThread - 1));
-#pragma unroll
-  for (int c = 0; c < NC; ++c) load_chunk(raw[c], p.cols[c], ((mask >> c) & 1u) ? r : home);
-}
-
 // Tile-layout scatter.  A tile is T * 4 * K rows (TR).  The workgroup counting-sorts each of its
 // tiles by partition (slot >> wbits) in LDS and writes the sorted tile back LINEARLY to the
 // tile's own entry range [tile * TR, tile * TR + TR) with 16-byte stores of whole lines --

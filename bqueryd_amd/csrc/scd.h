@@ -80,7 +80,128 @@ __device__ __forceinline__ void scd_word_to_chunk(Chunk& c, const DevCol& col, i
   }
 }
 
-template <int NC, bool COMPACT>
+// count_distinct pair bit of (slot, value): LDS pre-filter (merged per workgroup) or the
+// device bitmap (first setter counts the pair)
+__device__ __forceinline__ void scd_cd_pair(const ScdLaunch& d, int cd_mode, unsigned int* cdb, uint32_t s, uint32_t vcd) {
+  // 32-bit arithmetic: the planner fuses pair spaces < 2^30 only
+  const uint32_t bit = s * (uint32_t)d.cd.vrange + (vcd - (uint32_t)d.cd.vmin);
+  const unsigned int m = 1u << (bit & 31);
+  if (cd_mode == 1) {
+    // read first: lanes of one word broadcast; only a new pair pays the (serialising)
+    // same-address atomic
+    if (!(cdb[bit >> 5] & m)) atomicOr(&cdb[bit >> 5], m);
+  } else if (!(d.cd.bitmap[bit >> 5] & m) && !(atomicOr(&d.cd.bitmap[bit >> 5], m) & m)) {
+    atomicAdd(&d.cd.out[s], 1ull);
+  }
+}
+
+// The RUNS loop of the compact fused pass (see scd_fused_body): 256-row steps of 16-byte loads,
+// uniform full steps folded in registers, every other step handed to `fold` as four 64-row
+// steps re-read one row per lane (`derive` decodes them like the 64-row loop).
+constexpr int kScdRunsAhead = 2;  // 256-row steps loaded ahead of the one being folded
+template <int NC, typename Fold, typename Derive>
+__device__ __forceinline__ void scd_runs_loop(const ScanParams& p, const ScdLaunch& d, int64_t start, int64_t end,
+                                              uint32_t nrel, int lane, int vc, int cc, bool do_cd, bool cd_runs,
+                                              int cd_mode, ScdSlot32* st32, uint32_t* fv32, uint32_t* fr32, bool p16,
+                                              unsigned int* cdb, Fold& fold, Derive& derive) {
+  if (!nrel) return;
+  const uint32_t all = (1u << NC) - 1u;
+  Chunk ring[kScdRunsAhead][NC];
+#pragma unroll
+  for (int a = 0; a < kScdRunsAhead; ++a)
+    load_rows4_clamped<NC>(p, start + 256 * a + 4 * lane, end, ring[a], all, start);
+  for (uint32_t gbase = 0; gbase < nrel; gbase += 256u * kScdRunsAhead) {
+#pragma unroll
+    for (int a = 0; a < kScdRunsAhead; ++a) {
+      const uint32_t rb = gbase + 256u * a;
+      const int64_t row0 = start + (int64_t)rb + 4 * lane;
+      uint64_t v[NC][4], code[4];
+      decode_all<NC, 4>(p, ring[a], v);
+      const uint32_t pass = vals_pass<NC, 4, false>(p, row0, v);
+      vals_code<NC, 4>(p, v, code);
+      uint32_t s[4], vb[4], vcd[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        uint64_t x = 0, y = 0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (vc == c) x = v[c][r];
+          if (cc == c) y = v[c][r];
+        }
+        s[r] = (uint32_t)code[r];
+        vb[r] = (uint32_t)(x - (uint64_t)d.vmin);
+        vcd[r] = (uint32_t)y;
+      }
+      // derived before the refill (ring[a] dead at the refill, as in the 64-row loop)
+      asm volatile("" : "+v"(s[0]), "+v"(s[1]), "+v"(s[2]), "+v"(s[3]), "+v"(vb[0]), "+v"(vb[1]), "+v"(vb[2]),
+                   "+v"(vb[3]));
+      __builtin_amdgcn_sched_barrier(0);
+      load_rows4_clamped<NC>(p, row0 + 256 * kScdRunsAhead, end, ring[a], all, start);
+      if (rb >= nrel) continue;
+      const int64_t rem = end - row0;
+      const uint32_t act4 = pass & (rem >= 4 ? 0xFu : (rem > 0 ? (1u << rem) - 1u : 0u));
+      const uint32_t s0 = __builtin_amdgcn_readfirstlane(s[0]);
+      const bool uni = __ballot(act4 != 0xFu || s[0] != s0 || s[1] != s0 || s[2] != s0 || s[3] != s0) == 0;
+      if (!uni) {
+        // a key boundary, a filtered row or the chunk's tail: four 64-row steps in row order
+#pragma unroll 1
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t rbt = rb + 64u * t;
+          if (rbt >= nrel) break;
+          uint2 w[NC];
+          scd_issue<NC>(p, start, rbt, nrel, lane, w);
+          const uint32_t rel = rbt + (uint32_t)lane;
+          const int64_t row = start + (int64_t)rel;
+          bool act;
+          uint32_t sl;
+          uint64_t x, y;
+          derive(w, rel, row, act, sl, x, y);
+          fold(rel, row, act, sl, (uint64_t)(uint32_t)(x - (uint64_t)d.vmin), (uint64_t)(uint32_t)y);
+        }
+        continue;
+      }
+      // one slot, 256 active rows: value changes inside each lane's 4 rows and across the lane
+      // boundary (the lane below's last row: a DPP wave shift)
+      const uint32_t pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)vb[3], 0x138, 0xF, 0xF, false);  // wave_shr:1
+      const bool d0 = lane > 0 && vb[0] != pv, d1 = vb[1] != vb[0], d2 = vb[2] != vb[1], d3 = vb[3] != vb[2];
+      const uint32_t add_ch = (uint32_t)(__popcll(__ballot(d0)) + __popcll(__ballot(d1)) + __popcll(__ballot(d2)) +
+                                         __popcll(__ballot(d3)));
+      const uint32_t lastv = (uint32_t)__builtin_amdgcn_readlane(vb[3], 63);
+      bool rs0 = d0;  // row 0 of the lane starts a value run of the slot
+      if (lane == 0) {
+        const ScdSlot32 cur = st32[s0];
+        const uint32_t rows = cur.rc & 0xFFFFu;
+        uint32_t ch = (cur.rc >> 16) + add_ch;
+        if (rows == 0) {
+          if (p16) {
+            fv32[s0] = (vb[0] & 0xFFFFu) | (rb << 16);
+          } else {
+            fv32[s0] = vb[0];
+            fr32[s0] = (uint32_t)(start + rb);
+          }
+          rs0 = true;
+        } else if (cur.last != vb[0]) {
+          ch += 1u;
+          rs0 = true;
+        }
+        st32[s0] = ScdSlot32{lastv, (rows + 256u) | (ch << 16)};
+      }
+      if (do_cd) {
+        const bool rs[4] = {rs0, d1, d2, d3};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (cd_runs ? rs[r] : true) scd_cd_pair(d, cd_mode, cdb, s0, vcd[r]);
+      }
+    }
+  }
+}
+
+// RUNS (compact only): clustered keys (the planner's run count of the key column) -- 256-row
+// steps, 4 rows per lane from 16-byte loads.  A step whose 256 rows are all active and carry
+// one slot (all but ~one step per key run) is folded without LDS: in-lane value changes, the
+// lane boundary's through a DPP shift, four ballots, one state update; any other step is
+// folded as four 64-row steps over the same rows re-read one per lane (L1 / L2 hits).
+template <int NC, bool COMPACT, bool RUNS = false>
 __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLaunch& d, unsigned char* smem) {
   const int S = (int)p.nslots;
   // wave-uniform in a register the compiler knows to be uniform: the chunk bounds and step
@@ -142,56 +263,11 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
   const bool isf = !COMPACT && dtype_is_float(p.cols[vc].dtype);
   const bool cd_runs = cc == vc;  // count_distinct of the sorted_count_distinct column
   const uint64_t lanes_below = (1ull << lane) - 1ull;
-  uint2 ring[kScdAhead][NC];
-  // rows of the chunk (< 2^32: N < kNoRow); the last waves' chunks may start past the end
-  const uint32_t nrel = end > start ? (uint32_t)(end - start) : 0u;
-  if (nrel) {
-#pragma unroll
-    for (int a = 0; a < kScdAhead; ++a) scd_issue<NC>(p, start, 64u * a, nrel, lane, ring[a]);
-  }
-  for (uint32_t gbase = 0; gbase < nrel; gbase += 64 * kScdAhead) {
-#pragma unroll
-    for (int a = 0; a < kScdAhead; ++a) {
-      const uint32_t rb = gbase + 64u * a;
-      const uint32_t rel = rb + (uint32_t)lane;
-      const int64_t row = start + (int64_t)rel;
-      Chunk raw[NC];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) scd_word_to_chunk(raw[c], p.cols[c], row, ring[a][c]);
-      uint64_t v[NC][1];
-      decode_all<NC, 1>(p, raw, v);
-      // everything the step needs from its rows is derived before ring[a]'s refill is issued,
-      // so ring[a] is dead at the refill and the loads land in the loop-carried registers
-      // (otherwise they land in fresh ones, copied back at the loop head behind a vmcnt(0)
-      // that drains the whole prefetch); rel < nrel is the row bound (32-bit), vals_pass
-      // applies the terms only
-      const bool act = rel < nrel && (vals_pass<NC, 1, false>(p, row, v) & 1u);
-      uint64_t code[1];
-      vals_code<NC, 1>(p, v, code);
-      uint64_t vb = 0, vcd = 0;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        if (vc == c) vb = v[c][0];
-        if (cc == c) vcd = v[c][0];
-      }
-      uint32_t s = (uint32_t)code[0];
-      if (COMPACT) {
-        // the derived 32-bit values are pinned here (an empty asm that redefines them): the
-        // compiler would otherwise sink their arithmetic below the refill, keeping ring[a] live
-        uint32_t vb32 = (uint32_t)(vb - (uint64_t)d.vmin), vcd32 = (uint32_t)vcd;
-        asm volatile("" : "+v"(s), "+v"(vb32), "+v"(vcd32));
-        vb = vb32;
-        vcd = vcd32;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // unconditional (clamped) prefetch: the same number of loads is in flight on every
-      // path, so the compiler waits for exactly the step it consumes (vmcnt(N), not vmcnt(0));
-      // steps past the chunk end skip their work but not their loads (no `break`, whose exit
-      // edge would merge a shorter load history into the loop header)
-      scd_issue<NC>(p, start, rb + 64u * kScdAhead, nrel, lane, ring[a]);
-      if (rb >= nrel) continue;
+  // one 64-row step in row order (lane = row - rb): the per-slot lane masks, the previous row of
+  // each row's slot, the slot's state update and the count_distinct pairs
+  auto fold = [&](uint32_t rel, int64_t row, bool act, uint32_t s, uint64_t vb, uint64_t vcd) {
       const uint64_t actm = __ballot(act);
-      if (actm == 0) continue;
+      if (actm == 0) return;
       // one slot for the whole step (sorted or clustered keys): the active lanes are its lanes,
       // and the LDS mask -- 64 same-address atomics, serialised -- is skipped
       const uint32_t s0 = __builtin_amdgcn_readlane(s, (uint32_t)__builtin_ctzll(actm));
@@ -295,7 +371,82 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
           atomicAdd(&d.cd.out[s], 1ull);
         }
       }
+  };
+  // rows of the chunk (< 2^32: N < kNoRow); the last waves' chunks may start past the end
+  const uint32_t nrel = end > start ? (uint32_t)(end - start) : 0u;
+  // one 64-row step's values, one row per lane: decoded and coded
+  auto derive = [&](const uint2 (&w)[NC], uint32_t rel, int64_t row, bool& act, uint32_t& s, uint64_t& vb,
+                    uint64_t& vcd) {
+    Chunk raw[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) scd_word_to_chunk(raw[c], p.cols[c], row, w[c]);
+    uint64_t v[NC][1];
+    decode_all<NC, 1>(p, raw, v);
+    act = rel < nrel && (vals_pass<NC, 1, false>(p, row, v) & 1u);
+    uint64_t code[1];
+    vals_code<NC, 1>(p, v, code);
+    vb = 0;
+    vcd = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (vc == c) vb = v[c][0];
+      if (cc == c) vcd = v[c][0];
     }
+    s = (uint32_t)code[0];
+  };
+  if (RUNS) {
+    scd_runs_loop<NC>(p, d, start, end, nrel, lane, vc, cc, do_cd, cd_runs, cd_mode, st32, fv32, fr32, p16, cdb, fold,
+                      derive);
+  } else {
+  uint2 ring[kScdAhead][NC];
+  if (nrel) {
+#pragma unroll
+    for (int a = 0; a < kScdAhead; ++a) scd_issue<NC>(p, start, 64u * a, nrel, lane, ring[a]);
+  }
+  for (uint32_t gbase = 0; gbase < nrel; gbase += 64 * kScdAhead) {
+#pragma unroll
+    for (int a = 0; a < kScdAhead; ++a) {
+      const uint32_t rb = gbase + 64u * a;
+      const uint32_t rel = rb + (uint32_t)lane;
+      const int64_t row = start + (int64_t)rel;
+      Chunk raw[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) scd_word_to_chunk(raw[c], p.cols[c], row, ring[a][c]);
+      uint64_t v[NC][1];
+      decode_all<NC, 1>(p, raw, v);
+      // everything the step needs from its rows is derived before ring[a]'s refill is issued,
+      // so ring[a] is dead at the refill and the loads land in the loop-carried registers
+      // (otherwise they land in fresh ones, copied back at the loop head behind a vmcnt(0)
+      // that drains the whole prefetch); rel < nrel is the row bound (32-bit), vals_pass
+      // applies the terms only
+      const bool act = rel < nrel && (vals_pass<NC, 1, false>(p, row, v) & 1u);
+      uint64_t code[1];
+      vals_code<NC, 1>(p, v, code);
+      uint64_t vb = 0, vcd = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (vc == c) vb = v[c][0];
+        if (cc == c) vcd = v[c][0];
+      }
+      uint32_t s = (uint32_t)code[0];
+      if (COMPACT) {
+        // the derived 32-bit values are pinned here (an empty asm that redefines them): the
+        // compiler would otherwise sink their arithmetic below the refill, keeping ring[a] live
+        uint32_t vb32 = (uint32_t)(vb - (uint64_t)d.vmin), vcd32 = (uint32_t)vcd;
+        asm volatile("" : "+v"(s), "+v"(vb32), "+v"(vcd32));
+        vb = vb32;
+        vcd = vcd32;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // unconditional (clamped) prefetch: the same number of loads is in flight on every
+      // path, so the compiler waits for exactly the step it consumes (vmcnt(N), not vmcnt(0));
+      // steps past the chunk end skip their work but not their loads (no `break`, whose exit
+      // edge would merge a shorter load history into the loop header)
+      scd_issue<NC>(p, start, rb + 64u * kScdAhead, nrel, lane, ring[a]);
+      if (rb >= nrel) continue;
+      fold(rel, row, act, s, vb, vcd);
+    }
+  }
   }
   // count_distinct: merge the workgroup's pair bitmap into the device bitmap; every pair bit
   // this workgroup sets first counts once for its slot

@@ -86,6 +86,18 @@ class CommGroup:
         self.devices = []
 
 
+MERGE_PHASES = ('local', 'counts', 'exchange', 'reduce', 'gather_counts', 'gather')
+
+
+def merge_phases(device):
+    """Host wall time (ms) of this context's rank in the last merge, per phase
+    (``bqg_comm_last_phases``; collective steps charged to every rank of the call)."""
+    from . import _lib as L
+    out = (ctypes.c_double * len(MERGE_PHASES))()
+    device.check(L.lib().bqg_comm_last_phases(device.handle, out, len(MERGE_PHASES)))
+    return OrderedDict(zip(MERGE_PHASES, list(out)))
+
+
 def _schema(groupby_cols, agg_list, dtypes):
     from . import _lib as L
     names = list(groupby_cols) + [x[2] for x in agg_list]

@@ -151,7 +151,7 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *   jit_min_rows   4Mi  ... for tables of at least this many rows
  *   partition      1  partitioned aggregation for large dense slot spaces   0 | 1
  *   part_wbits     0  slots per partition 2^wbits (0: auto)           0 | 6..13
- *   part_k         0  4-row chunks per scatter thread (0: auto)        0 | 1 | 2
+ *   part_k         0  4-row chunks per scatter thread (0: auto)        0 | 1 | 2 | 4 (packed)
  *   part_threads   0  scatter workgroup size (0: auto)                 0 | 256 | 512 | 1024
  *   part_per_cu    0  scatter workgroups per CU (0: auto)              0..8
  *   part_splits    0  aggregate workgroups per partition (0: auto)
@@ -165,6 +165,7 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *   hash_slots     0  initial group hash-table slots (0: from rows)    0..2^31
  *   distinct_slots 0  initial count_distinct set slots (0: from rows)  0..2^31
  *   part_pack      1  packed 4-byte partition entries when they fit    0 | 1
+ *   scd_runs       1  fused distinct pass in 256-row steps for clustered keys  0 | 1
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);
@@ -300,6 +301,10 @@ int bqg_comm_init_all(int32_t n, bqg_ctx* const* ctxs);
 int bqg_comm_init_local(int32_t n, bqg_ctx* const* ctxs);
 int bqg_comm_destroy(bqg_ctx* ctx);
 int bqg_comm_info(bqg_ctx* ctx, int32_t* rank, int32_t* nranks);
+/* Profiling: host wall time (ms) of this rank's part of the last merge, per phase -- 0 local
+ * re-group + pack, 1 count exchange, 2 payload exchange, 3 reduce, 4 gather counts, 5 gather
+ * to rank 0; a collective step is charged to every rank of the call.  Up to n values. */
+int bqg_comm_last_phases(bqg_ctx* ctx, double* ms, int32_t n);
 int bqg_merge(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int32_t n_keys, int32_t n_cols,
               const int32_t* dtypes, int32_t reduced, bqg_table** out);
 int bqg_merge_group(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,

@@ -89,6 +89,36 @@ def test_worker_controller_client_path(tmp_path):
     assert_tables_equal(back, ref, exact_float_sums=True)
 
 
+@pytest.mark.parametrize('variant', ['exact', 'raw'])
+def test_c1_full_shape_end_to_end(tmp_path, variant, oracle_c):
+    """C1 at its stated shape (BASELINE.json configs[0]): 10 bcolz shards x 1 M rows on disk,
+    one per-file calc message per shard through CalcPath.handle_work (cold, then warm from the
+    resident shard cache), the controller's tar of tars and the client's aggregate=True merge
+    -- against the reference client merge (rpc.py:164-173) of bquery's per-shard results
+    (the C restatement): keys exact, sums bit-exact on dyadic data, 1e-12 on cents."""
+    cfg = synth.CONFIGS['c1']
+    data_dir = str(tmp_path)
+    files, results = [], []
+    for i in range(cfg['shards']):
+        cols = synth.taxi_shard(cfg['rows'] // cfg['shards'], config_id=1, n_shards=cfg['shards'], shard=i,
+                                variant=variant, columns=synth.query_columns(cfg))
+        fn = 'tripdata-%d.bcolzs' % i
+        bcolz_io.write_ctable(os.path.join(data_dir, fn), cols)
+        files.append(fn)
+        results.append(oracle_c.handle_work(cols, cfg['groupby'], cfg['aggs'], cfg['where']))
+    ref = bo.client_merge(results, cfg['groupby'], cfg['aggs'], aggregate=True)
+    calc = CalcPath(data_dir)
+    for rep in ('cold', 'warm'):
+        replies = OrderedDict()
+        for fn in files:
+            replies[fn] = calc.handle_work(_calc_msg(fn, cfg['groupby'], cfg['aggs'], cfg['where']))['data']
+        df = rpc.uncompress_groupby_to_df(rpc.tar_of_tars(replies), cfg['groupby'], cfg['aggs'], cfg['where'],
+                                          aggregate=True)
+        got = OrderedDict((c, df[c].values) for c in df.columns)
+        got, exp = sort_by_keys(got, cfg['groupby']), sort_by_keys(ref, cfg['groupby'])
+        assert_tables_equal(got, exp, exact_cols={'fare_amount'} if variant == 'exact' else set())
+
+
 def test_worker_factorization_check_and_errors(tmp_path):
     cols = synth.taxi_shard(5000, config_id=2, columns=('payment_type', 'passenger_count', 'fare_amount'))
     root = os.path.join(str(tmp_path), 's.bcolzs')

@@ -486,6 +486,47 @@ def test_partitioned_narrow_codes(kind, oracle_c, engine_options):
             np.testing.assert_allclose(got['vs'], wide['vs'], rtol=1e-12, atol=0)
 
 
+@pytest.mark.parametrize('jit', [False, True])
+@pytest.mark.parametrize('case', ['sorted_taxi', 'short_runs', 'wide_values', 'cd_other_column', 'int64_values',
+                                  'one_key', 'ragged'])
+def test_fused_distinct_runs_loop(case, jit, oracle_c, engine_options):
+    """Clustered keys take the fused distinct pass's RUNS loop (256-row steps, 4 rows per lane):
+    runs of several lengths (key boundaries inside and across steps and wave chunks), value
+    codes above 2^16 (no packed first value), a count_distinct of another column, int64 values,
+    a single key value and a ragged row count -- against the oracle and against the 64-row loop
+    (scd_runs=0)."""
+    if jit:
+        engine_options(jit_min_rows=0)
+    rng = np.random.default_rng(abs(hash(case)) % 997)
+    n = 700_003 if case == 'ragged' else 600_000
+    keys = ['k']
+    if case == 'short_runs':  # runs of ~600 rows: many key boundaries per wave chunk
+        k = np.repeat(rng.integers(0, 300, n // 600 + 1), 600)[:n]
+    elif case == 'one_key':
+        k = np.zeros(n, np.int64)
+    else:
+        k = np.sort(rng.integers(0, 265, n))
+    cols = OrderedDict(k=k.astype(np.int32))
+    v = np.repeat(rng.integers(0, 10, n // 37 + 1), 37)[:n]  # value runs inside key runs
+    v[rng.random(n) < 0.05] = 7
+    if case == 'wide_values':
+        v = v * 30_000
+    cols['v'] = v.astype(np.int64 if case == 'int64_values' else np.int32)
+    cols['w'] = rng.integers(0, 12, n).astype(np.int16)
+    cd_col = 'w' if case == 'cd_other_column' else 'v'
+    aggs = [['v', 'sorted_count_distinct', 'scd'], [cd_col, 'count_distinct', 'cd'], ['v', 'count', 'n']]
+    got = run_both(cols, keys, aggs, [], oracle_c)
+    t = ShardTable(cols)
+    try:
+        t.groupby(keys, aggs)
+        assert t.dev.last_timing()['mode'] == 5
+        with t.dev.options(scd_runs=0):
+            ref, _ = t.groupby(keys, aggs)
+    finally:
+        t.close()
+    assert_tables_equal(got, ref)
+
+
 @pytest.mark.parametrize('kind', ['count_only', 'dyadic', 'cents_neg', 'int_span_65535', 'int_span_65536', 'sorted_keys',
                                   'filtered', 'one_split', 'jit'])
 def test_partitioned_packed_entries(kind, oracle_c, engine_options):

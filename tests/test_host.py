@@ -291,3 +291,39 @@ def test_shard_cache_budget_counts_unions():
     cache._evict()  # 1140: the union, then shard a (least recent)
     assert cache.extra.held == [] and cts['a'].closed and not cts['b'].closed
     assert cache.resident_bytes() <= 1000
+
+
+@pytest.mark.parametrize('nrows', [0, 3, 100_000])
+def test_ctable_tar_bytes_match_tarfile(nrows, monkeypatch):
+    """The hand-written ustar blocks of bcolz_io.ctable_tar are byte-identical to what
+    ``tarfile`` writes for the same members (directories first, entries sorted, depth first)."""
+    import time as _time
+    monkeypatch.setattr(_time, 'time', lambda: 1_700_000_000.25)
+    rng = np.random.default_rng(nrows)
+    cols = OrderedDict(k=rng.integers(0, 9, nrows).astype(np.int32), v=rng.normal(size=nrows))
+    got = bcolz_io.ctable_tar(cols, 'result_x1')
+    tree = {}
+    for n in cols:
+        tree.setdefault(n, {}).setdefault('data', {})
+        tree[n].setdefault('meta', {})
+    for rel, data in bcolz_io.ctable_files(cols):
+        node = tree
+        parts = rel.split('/')
+        for p in parts[:-1]:
+            node = node.setdefault(p, {})
+        node[parts[-1]] = data
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode='w') as tf:
+        def add(name, node):
+            info = tarfile.TarInfo(name)
+            info.mtime = 1_700_000_000
+            if isinstance(node, dict):
+                info.type, info.mode = tarfile.DIRTYPE, 0o755
+                tf.addfile(info)
+                for k in sorted(node):
+                    add(name + '/' + k, node[k])
+            else:
+                info.size, info.mode = len(node), 0o644
+                tf.addfile(info, io.BytesIO(node))
+        add('result_x1', tree)
+    assert got == buf.getvalue()

@@ -20,3 +20,24 @@ def test_specialised_scan_compiles():
     if rc == 1:
         pytest.skip('hiprtc not loadable here')
     assert rc == 0
+
+
+C4_SPEC = (b"#define BQ_NC 2\n#define BQ_SPEC p.ncols=2;"
+           b"p.cols[0].dtype=3;p.cols[0].lg=2;p.cols[1].dtype=3;p.cols[1].lg=2;"
+           b"p.nterms=0;p.nkeys=1;p.keys[0].col=0;p.keys[0].is_float=0;p.keys[0].stride=1ull;"
+           b"p.nsum=0;p.mask_col=-1;p.hash=0;\n"
+           b"#define BQ_SCD_CD 1\n#define BQ_SCD_VC 1\n#define BQ_SCD_CC 1\n#define BQ_SCD_P16 1\n")
+
+
+@pytest.mark.parametrize('extra', [b'', b'#define BQ_PART_K 4\n#define BQ_PART_NARROW 1\n#define BQ_PART_PACK 1\n',
+                                   b'#define BQ_PART_K 2\n#define BQ_PART_NARROW 1\n#define BQ_PART_PACK 0\n'])
+def test_specialised_distinct_and_partition_kernels_compile(extra):
+    """Every JIT entry point (the fused distinct pass in both loops, the partition scatter with
+    packed / narrow entries and 16384-row tiles) compiles for a C4-shaped query."""
+    f = _lib.lib().bqg_internal_jit_compile_check
+    f.argtypes = [ctypes.c_char_p]
+    f.restype = ctypes.c_int
+    rc = f(C4_SPEC + extra)
+    if rc == 1:
+        pytest.skip('hiprtc not loadable here')
+    assert rc == 0

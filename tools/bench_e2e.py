@@ -68,6 +68,8 @@ def main():
     ap.add_argument('--reps', type=int, default=5)
     ap.add_argument('--cpu-workers', type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument('--no-gpu', action='store_true')
+    ap.add_argument('--profile', default=None,
+                    help='write a cProfile summary of 50 warm per-file messages (handle_work) to this file')
     args = ap.parse_args()
 
     from bqueryd_amd import bcolz_io, messages, rpc, synth
@@ -120,6 +122,28 @@ def main():
 
             calc = CalcPath(data_dir, device=dev)
             gpu_query(calc)  # warm the cache
+            if args.profile:
+                import cProfile
+                import io
+                import pstats
+                msgs = [msg_for(fn) for fn in files] * 5
+                pr = cProfile.Profile()
+                t0 = time.perf_counter()
+                pr.enable()
+                for m in msgs:
+                    calc.handle_work(m)
+                pr.disable()
+                per_msg = (time.perf_counter() - t0) / len(msgs)
+                sio = io.StringIO()
+                pstats.Stats(pr, stream=sio).sort_stats('cumulative').print_stats(45)
+                t0 = time.perf_counter()
+                for m in msgs:
+                    calc.handle_work(m)
+                plain = (time.perf_counter() - t0) / len(msgs)
+                with open(args.profile, 'w') as f:
+                    f.write('warm per-file message: %.1f us (unprofiled), %.1f us under cProfile\n' % (
+                        plain * 1e6, per_msg * 1e6))
+                    f.write(sio.getvalue())
             warm = min((gpu_query(calc) for _ in range(args.reps)), key=lambda x: x[0])
             cold = min((gpu_query(CalcPath(data_dir, device=dev, cache=ShardCache(device=dev)))
                         for _ in range(args.reps)), key=lambda x: x[0])
