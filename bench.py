@@ -228,7 +228,7 @@ def _c5_local_ranks(args):
         t1 = time.perf_counter()
         merged = bdist.merge_group_device(per, cfg['groupby'], cfg['aggs'], dtypes, group, reduced=True)
         merge_s.append(time.perf_counter() - t1)
-        phases.append([list(bdist.merge_phases(d).values()) for d in devs])
+        phases.append([list(bdist.merge_phases(d).values()) for d in devs] + [[bdist.LAST_MERGE['to_host_ms']] * 6])
         for tabs in per:
             for p in tabs:
                 p.close()
@@ -272,11 +272,12 @@ def _c5_local_ranks(args):
 
     rank_ms = [1e3 * float(np.mean(s)) for s in shard_s]
     merge_ms = 1e3 * float(np.mean(merge_s))
-    ph = np.mean(np.array(phases), axis=0)  # [rank][phase] ms
+    ph = np.mean(np.array(phases), axis=0)  # [rank][phase] ms; last row: the copy to host
+    host_copy_ms = float(ph[-1][0])
+    ph = ph[:-1]
     phase_max = {n: float(ph[:, i].max()) for i, n in enumerate(bdist.MERGE_PHASES)}
     # the merge as 8 GPUs would run it: each phase as long as its slowest rank (the collective
     # steps measured as one in-process transfer of all ranks), + the result's copy to the host
-    host_copy_ms = max(0.0, merge_ms - float(ph[0].sum()))
     merge_crit_ms = sum(phase_max.values()) + host_copy_ms
     one_ms = 1e3 * float(np.mean(one_s))
     proj_ms = max(rank_ms) + merge_crit_ms

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import ctypes.util
+import functools
 import json
 import os
 import struct
@@ -186,14 +187,20 @@ def carray_files(arr, chunklen=None, clevel=5, shuffle=1, cname='lz4'):
         frame = compress_chunk(arr[lo:lo + chunklen], clevel, shuffle, cname)
         files.append(('data/__%d.blp' % i, bloscpack_header(1) + frame))
         cbytes += len(frame) + BLOSCPACK_HEADER
-    dflt = False if arr.dtype.kind == 'b' else (0.0 if arr.dtype.kind == 'f' else 0)
-    files.append(('meta/storage', _json_bytes({
-        'dtype': str(arr.dtype),
-        'cparams': {'clevel': clevel, 'shuffle': shuffle, 'cname': cname, 'quantize': 0},
-        'chunklen': int(chunklen), 'expectedlen': int(max(n, 1)), 'dflt': dflt})))
+    files.append(('meta/storage', _storage_json(arr.dtype, clevel, shuffle, cname, int(chunklen), int(max(n, 1)))))
     files.append(('meta/sizes', _json_bytes({'shape': [int(n)], 'nbytes': int(arr.nbytes), 'cbytes': int(cbytes)})))
-    files.append((ATTRS, _json_bytes({})))
+    files.append((ATTRS, _EMPTY_ATTRS))
     return files
+
+
+_EMPTY_ATTRS = b'{}\n'
+
+
+@functools.lru_cache(maxsize=1024)
+def _storage_json(dtype, clevel, shuffle, cname, chunklen, expectedlen):
+    dflt = False if dtype.kind == 'b' else (0.0 if dtype.kind == 'f' else 0)
+    return _json_bytes({'dtype': str(dtype), 'cparams': {'clevel': clevel, 'shuffle': shuffle, 'cname': cname, 'quantize': 0},
+                        'chunklen': chunklen, 'expectedlen': expectedlen, 'dflt': dflt})
 
 
 def _write_files(rootdir, files):
@@ -283,6 +290,9 @@ _TAR_DEVS = bytes(16)                    # devmajor, devminor: empty unless a de
 _TAR_FIXED_SUM = sum(_TAR_IDS) + sum(b' ' * 8) + sum(_TAR_MAGIC) + sum(_TAR_DEVS)
 
 
+_TAR_TAIL = bytes(100) + _TAR_MAGIC + bytes(64) + _TAR_DEVS + bytes(167)  # after the type flag
+
+
 def _tar_header(name, size, mode, mtime, dirtype):
     """One 512-byte ustar header exactly as ``tarfile`` (default PAX format, a name of at most
     100 bytes: no extended header) writes it for a TarInfo with uid / gid 0 and empty owner
@@ -294,46 +304,47 @@ def _tar_header(name, size, mode, mtime, dirtype):
     typ = b'5' if dirtype else b'0'  # directory / regular file
     # checksum: every byte of the header with the checksum field read as spaces
     cks = _TAR_FIXED_SUM + sum(nb) + sum(m) + sum(sz) + sum(mt) + typ[0]
-    return b''.join((nb, bytes(100 - len(nb)), m, _TAR_IDS, sz, mt, b'%06o\x00 ' % cks, typ, bytes(100),
-                     _TAR_MAGIC, bytes(64), _TAR_DEVS, bytes(167)))
+    return nb.ljust(100, b'\x00') + m + _TAR_IDS + sz + mt + (b'%06o\x00 ' % cks) + typ + _TAR_TAIL
 
 
 def ctable_tar(columns, arcname, chunklen=None, cname='lz4'):
     """Bytes of ``tarfile.open(mode='w').add(<ctable rootdir>, arcname=arcname)``
-    (worker.py:337-345), built in memory: the same members (directories first, then their
-    files) without writing the ctable to disk and reading it back.  The ustar blocks are
-    written directly (``_tar_header``, byte-identical to ``tarfile``'s, which took most of a
-    warm per-file message's host time)."""
+    (worker.py:337-345), built in memory: the same members as ``write_ctable`` + ``tarfile.add``
+    (the directory, then its entries sorted by name, depth first; every column has data/ and
+    meta/ even when a zero-row column has no chunk file -- the client appends to the first
+    result it opens, rpc.py:158-162, and bcolz then writes chunks into data/) without writing
+    the ctable to disk.  The ustar blocks are written directly (``_tar_header``, byte-identical
+    to ``tarfile``'s, which took most of a warm per-file message's host time)."""
     import time
-    files = ctable_files(columns, chunklen, cname)
     now = int(time.time())
-    # the directory tree write_ctable creates: every column has data/ and meta/ even when a
-    # zero-row column has no chunk file (the client appends to the first result it opens,
-    # rpc.py:158-162, and bcolz then writes chunks into data/)
-    tree = {}
-    for n in columns:
-        tree.setdefault(n, {}).setdefault('data', {})
-        tree[n].setdefault('meta', {})
-    for rel, data in files:
-        parts = rel.split('/')
-        node = tree
-        for p in parts[:-1]:
-            node = node.setdefault(p, {})
-        node[parts[-1]] = data
     out = []
 
-    # tarfile.add's order: the directory, then its entries sorted by name, depth first
-    def add(name, node):
-        if isinstance(node, dict):
-            out.append(_tar_header(name + '/', 0, 0o755, now, True))
-            for k in sorted(node):
-                add(name + '/' + k, node[k])
-        else:
-            out.append(_tar_header(name, len(node), 0o644, now, False))
-            out.append(node)
-            if len(node) % 512:
-                out.append(bytes(512 - len(node) % 512))
-    add(arcname, tree)
+    def member(name, data):
+        out.append(_tar_header(name, len(data), 0o644, now, False))
+        out.append(data)
+        if len(data) % 512:
+            out.append(bytes(512 - len(data) % 512))
+
+    def directory(name):
+        out.append(_tar_header(name + '/', 0, 0o755, now, True))
+
+    names = list(columns.keys())
+    root = {ATTRS: _json_bytes({}), ROOTDIRS: _json_bytes({'names': names, 'dirs': {n: n for n in names}})}
+    directory(arcname)
+    for entry in sorted(list(root) + names):
+        if entry in root and entry not in columns:
+            member(arcname + '/' + entry, root[entry])
+            continue
+        files = dict(carray_files(columns[entry], chunklen=chunklen, cname=cname))
+        cdir = arcname + '/' + entry
+        directory(cdir)
+        member(cdir + '/' + ATTRS, files.pop(ATTRS))
+        directory(cdir + '/data')  # '__attrs__' < 'data' < 'meta'
+        for rel in sorted(r for r in files if r.startswith('data/')):
+            member(cdir + '/' + rel, files[rel])
+        directory(cdir + '/meta')
+        member(cdir + '/meta/sizes', files['meta/sizes'])
+        member(cdir + '/meta/storage', files['meta/storage'])
     out.append(bytes(1024))  # end-of-archive: two zero blocks
     body = b''.join(out)
     return body + bytes(-len(body) % 10240)  # tarfile pads the archive to whole 20-block records

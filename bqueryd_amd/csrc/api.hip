@@ -1183,14 +1183,16 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         L.first_tile = (uint32_t*)(eb + vbytes + mbytes + pbytes + abytes);
         L.tile_mark = eb + vbytes + mbytes + pbytes + abytes + fbytes;
       }
-      hipFunction_t fs = nullptr;
+      hipFunction_t fs = nullptr, ff = nullptr;
       if (c->opt[kOptJit] && N >= c->opt[kOptJitMinRows]) {
-        fs = jit_function("bq_jit_part_scatter", jit_spec(pl.p) + "#define BQ_PART_K " + std::to_string(L.k) +
-                                                      "\n#define BQ_PART_NARROW " + std::to_string(L.narrow) +
-                                                      "\n#define BQ_PART_PACK " + std::to_string(L.pack) + "\n");
+        const std::string spec = jit_spec(pl.p) + "#define BQ_PART_K " + std::to_string(L.k) +
+                                 "\n#define BQ_PART_NARROW " + std::to_string(L.narrow) +
+                                 "\n#define BQ_PART_PACK " + std::to_string(L.pack) + "\n";
+        fs = jit_function("bq_jit_part_scatter", spec);
+        if (pk) ff = jit_function("bq_jit_part_first_rows", spec);
         c->last.specialized = fs ? 1 : 0;
       }
-      launch_partitioned(pl.p, sa, L, st, fs);
+      launch_partitioned(pl.p, sa, L, st, fs, ff);
     } else {
       launch_scan_global(pl.p, sa, scan_blocks(c, N, 8), st);
     }

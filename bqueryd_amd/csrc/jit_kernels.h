@@ -39,6 +39,13 @@ extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_scatter(bqg::Scan
   bqg::part_scatter_body<BQ_NC, BQ_PART_K, BQ_PART_NARROW != 0, BQ_PART_PACK != 0>(p, L, smem);
 }
 
+extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_first_rows(bqg::ScanParams pin, bqg::PartLaunch L,
+                                                                        bqg::SlotArrays sa) {
+  bqg::ScanParams p = pin;
+  bqg::jit_specialize(p);
+  bqg::part_first_rows_body<BQ_NC>(p, L, sa);
+}
+
 extern "C" __global__ __launch_bounds__(256) void bq_jit_scd_fused(bqg::ScanParams pin, bqg::ScdLaunch d) {
   extern __shared__ __align__(16) unsigned char smem[];
   bqg::ScanParams p = pin;

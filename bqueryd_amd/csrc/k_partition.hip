@@ -85,8 +85,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   // (lane j: entry index of tile j's segment start minus its flattened position) and the total
   struct Grp {
     uint32_t ex[G];
-    uint32_t dl[G];  // per tile j: entry index of its segment start minus its flattened position
-    uint32_t total;
+    uint32_t dl, total;
     size_t gbase;
     uint32_t tile0;
   };
@@ -100,12 +99,9 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     const uint32_t incl = wave_incl_scan_u32(len, lane);
     const uint32_t excl = incl - len;
     g.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, G - 1);
-    const uint32_t dl = (uint32_t)lane * TR + s0 - excl;
 #pragma unroll
-    for (int j = 0; j < G; ++j) {
-      g.ex[j] = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
-      g.dl[j] = (uint32_t)__builtin_amdgcn_readlane((int)dl, j);
-    }
+    for (int j = 0; j < G; ++j) g.ex[j] = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
+    g.dl = (uint32_t)lane * TR + s0 - excl;
     g.gbase = (size_t)tg * TR;
     g.tile0 = (uint32_t)tg;
   };
@@ -117,16 +113,10 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     for (int u = 0; u < U; ++u) {
       const uint32_t e = e0 + u * 64u + lane;
       const uint32_t ec = e < g.total ? e : (g.total ? g.total - 1u : 0u);
-      // the entry's tile: the last j whose segment starts at or before it (wave-uniform starts
-      // and bases: compares and selects, no lane shuffle)
-      uint32_t j0 = 0, dsel = g.dl[0];
+      uint32_t j0 = 0;
 #pragma unroll
-      for (int j = 1; j < G; ++j) {
-        const bool in = ec >= g.ex[j];
-        j0 += in ? 1u : 0u;
-        dsel = in ? g.dl[j] : dsel;
-      }
-      size_t idx = g.gbase + dsel + ec;
+      for (int j = 1; j < G; ++j) j0 += ec >= g.ex[j] ? 1u : 0u;
+      size_t idx = g.gbase + (uint32_t)__shfl((int)g.dl, (int)j0, 64) + ec;
       idx = g.total ? idx : 0;
       en.rowb[u] = PACK ? g.tile0 + j0 : (uint32_t)g.gbase + j0 * TR;  // PACK: the tile
       en.m[u] = L.meta[idx];
@@ -323,46 +313,9 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   }
 }
 
-// First rows of the PACK path: a slot's first row lies in its first tile (first_tile, from
-// the aggregate), so only the tiles marked as some slot's first tile are read again -- their
-// key / filter columns, through the scan's own row -> slot code -- and every passing row whose
-// slot has this tile as its first one takes part in an atomicMin on the slot's first row.  On
-// random keys the marked tiles are the first ~10-15 % (each slot's first appearance falls
-// early); on sorted keys every tile is marked.
 template <int NC>
 __global__ __launch_bounds__(1024) void k_part_first_rows(ScanParams p, PartLaunch L, SlotArrays sa) {
-  // only the key, term and mask columns are read (the others re-read one line per wave)
-  uint32_t need = p.mask_col >= 0 ? 1u << p.mask_col : 0u;
-  for (int k = 0; k < p.nkeys; ++k) need |= 1u << p.keys[k].col;
-  for (int i = 0; i < p.nterms; ++i) need |= 1u << p.terms[i].col;
-  const int64_t TR = L.tile_rows;
-  for (int64_t t = blockIdx.x; t < L.ntiles; t += gridDim.x) {
-    if (!L.tile_mark[t]) continue;
-    const int64_t base = t * TR;
-    const int64_t end = min(p.nrows, base + TR);
-    // a tile is at most 4 x 1024 4-row chunks, taken two at a time: both loads in flight
-    // before either is used
-    for (int k0 = 0; (int64_t)k0 * 1024 * kRowsPerThread < TR; k0 += 2) {
-    Chunk raw[2][NC];
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      load_rows4_clamped<NC>(p, base + ((int64_t)threadIdx.x + (k0 + k) * 1024) * kRowsPerThread, end, raw[k], need, base);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int64_t row0 = base + ((int64_t)threadIdx.x + (k0 + k) * 1024) * kRowsPerThread;
-      if (row0 >= end) continue;
-      uint64_t v[NC][4], code[4];
-      decode_all<NC, 4>(p, raw[k], v);
-      uint32_t pass = vals_pass<NC, 4>(p, row0, v);
-      const int64_t rem = end - row0;
-      pass &= rem >= 4 ? 0xFu : ((1u << rem) - 1u);
-      vals_code<NC, 4>(p, v, code);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (((pass >> r) & 1u) && L.first_tile[code[r]] == (uint32_t)t) atomicMin(&sa.fst[code[r]], (uint32_t)(row0 + r));
-    }
-    }
-  }
+  part_first_rows_body<NC>(p, L, sa);
 }
 
 // ------------------------------------------------------------------------------------
@@ -397,7 +350,7 @@ void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipSt
 
 #ifndef BQG_PART_MICRO  // tools/micro/part_micro.hip includes this file for the aggregate kernel
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,
-                        hipFunction_t fscatter) {
+                        hipFunction_t fscatter, hipFunction_t ffirst) {
   const size_t scatter_lds = part_scatter_lds(L.nparts, L.threads, p.nsum, L.k, L.narrow != 0, L.pack != 0);
   if (fscatter) {
     PartLaunch Lc = L;
@@ -442,7 +395,15 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
 #undef BQG_AGGP
     // grid-stride over the tiles (the marked ones are mostly a prefix on random keys)
     const unsigned fgrid = (unsigned)std::min<int64_t>(L.ntiles, 2048);
-    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_first_rows<NC>), dim3(fgrid), dim3(1024), 0, st, p, L, s));
+    if (ffirst) {
+      PartLaunch Lc = L;
+      ScanParams pc = p;
+      SlotArrays sc = s;
+      void* args[] = {(void*)&pc, (void*)&Lc, (void*)&sc};
+      (void)hipModuleLaunchKernel(ffirst, fgrid, 1, 1, 1024, 1, 1, 0, st, args, nullptr);
+    } else {
+      BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_first_rows<NC>), dim3(fgrid), dim3(1024), 0, st, p, L, s));
+    }
     return;
   }
   // G tiles per wave group: ~8 x 4096 rows of segments whichever the tile size

@@ -217,8 +217,9 @@ inline size_t part_agg_lds(int wbits, int nsum, bool pack) {
   return ((size_t)1 << wbits) * (pack ? 12 : 8 + 8 * (size_t)nsum);
 }
 // fscatter: the query-specialised (JIT) scatter kernel, or nullptr for the precompiled one
+// ffirst: the query-specialised (JIT) first-row pass of packed entries, or nullptr
 void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaunch& L, hipStream_t st,
-                        hipFunction_t fscatter = nullptr);
+                        hipFunction_t fscatter = nullptr, hipFunction_t ffirst = nullptr);
 void launch_exclusive_scan_u32(uint32_t* v, uint64_t n, uint32_t* scratch, hipStream_t st);
 
 // cross-rank merge: partition id of every row from its key values

@@ -215,4 +215,46 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   }
 }
 
+// First rows of the PACK path: a slot's first row lies in its first tile (first_tile, from
+// the aggregate), so only the tiles marked as some slot's first tile are read again -- their
+// key / filter columns, through the scan's own row -> slot code -- and every passing row whose
+// slot has this tile as its first one takes part in an atomicMin on the slot's first row.  On
+// random keys the marked tiles are the first ~10-15 % (each slot's first appearance falls
+// early); on sorted keys every tile is marked.
+template <int NC>
+__device__ __forceinline__ void part_first_rows_body(const ScanParams& p, const PartLaunch& L, const SlotArrays& sa) {
+  // only the key, term and mask columns are read (the others re-read one line per wave)
+  uint32_t need = p.mask_col >= 0 ? 1u << p.mask_col : 0u;
+  for (int k = 0; k < p.nkeys; ++k) need |= 1u << p.keys[k].col;
+  for (int i = 0; i < p.nterms; ++i) need |= 1u << p.terms[i].col;
+  const int64_t TR = L.tile_rows;
+  for (int64_t t = blockIdx.x; t < L.ntiles; t += gridDim.x) {
+    if (!L.tile_mark[t]) continue;
+    const int64_t base = t * TR;
+    const int64_t end = min(p.nrows, base + TR);
+    // a tile is at most 4 x 1024 4-row chunks, taken two at a time: both loads in flight
+    // before either is used
+    for (int k0 = 0; (int64_t)k0 * 1024 * kRowsPerThread < TR; k0 += 2) {
+    Chunk raw[2][NC];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      load_rows4_clamped<NC>(p, base + ((int64_t)threadIdx.x + (k0 + k) * 1024) * kRowsPerThread, end, raw[k], need, base);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int64_t row0 = base + ((int64_t)threadIdx.x + (k0 + k) * 1024) * kRowsPerThread;
+      if (row0 >= end) continue;
+      uint64_t v[NC][4], code[4];
+      decode_all<NC, 4>(p, raw[k], v);
+      uint32_t pass = vals_pass<NC, 4>(p, row0, v);
+      const int64_t rem = end - row0;
+      pass &= rem >= 4 ? 0xFu : ((1u << rem) - 1u);
+      vals_code<NC, 4>(p, v, code);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (((pass >> r) & 1u) && L.first_tile[code[r]] == (uint32_t)t) atomicMin(&sa.fst[code[r]], (uint32_t)(row0 + r));
+    }
+    }
+  }
+}
+
 }  // namespace bqg

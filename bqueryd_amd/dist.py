@@ -21,6 +21,7 @@ tests, ``tests/merge_protocol.py``.
 from __future__ import annotations
 
 import ctypes
+import time
 from collections import OrderedDict
 
 import numpy as np
@@ -151,9 +152,18 @@ def merge_group_device(tables_per_rank, groupby_cols, agg_list, dtypes, group, r
     ntab = (ctypes.c_int32 * w)(*counts)
     arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
     outs = (ctypes.c_void_p * w)()
+    t0 = time.perf_counter()
     group.devices[0].check(L.lib().bqg_merge_group(w, ctxs, ntab, arr, len(groupby_cols), len(names), codes,
                                                    1 if reduced else 0, outs))
-    return _merged_to_host(ctypes.c_void_p(outs[0]), names, dtypes, group.devices[0])
+    t1 = time.perf_counter()
+    out = _merged_to_host(ctypes.c_void_p(outs[0]), names, dtypes, group.devices[0])
+    LAST_MERGE.update(merge_ms=1e3 * (t1 - t0), to_host_ms=1e3 * (time.perf_counter() - t1))
+    return out
+
+
+# host wall time of the last merge_group_device: the library call and the result's copy to
+# host memory (profiling)
+LAST_MERGE = {}
 
 
 # aggregations whose client-side merge (a sum of the per-shard finalized values, rpc.py:170-172)

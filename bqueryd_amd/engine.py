@@ -502,23 +502,27 @@ class ShardTable:
 
     def factorize(self, col, labels=True):
         """bquery's factor cache of column ``col`` (``bqg_factorize``): (int64 first-appearance
-        label of every row, or None; distinct values in label order).  Integer columns spanning
-        at most 2^27 values (else NotImplementedError)."""
+        label of every row, or None; distinct values in label order).  Any key dtype: integer
+        columns spanning at most 2^27 values through a lookup table, floats (khash identity),
+        bools and wider spans through a hash of the canonical key bits."""
         s = self.slot(col)
         dt = np.dtype(self.dtypes[col])
-        if dt.kind not in 'iu':
-            raise NotImplementedError('factor cache of a %s column' % dt)
-        st = self.stats(col)
-        span = 1 if st['empty'] else int(st['max']) - int(st['min']) + 1
-        if span > 1 << 27:
-            raise NotImplementedError('factor cache of a column spanning more than 2^27 values')
-        cap = min(self.nrows, span)
-        values = np.empty(max(cap, 1), dtype=dt)
+        cap = min(self.nrows, 1 << 22)
+        if dt.kind in 'iu':
+            st = self.stats(col)
+            cap = min(self.nrows, 1 if st['empty'] else int(st['max']) - int(st['min']) + 1)
+        elif dt.kind == 'b':
+            cap = min(self.nrows, 2)
         lab = np.empty(self.nrows, np.int64) if labels else None
         n_values = ctypes.c_int64()
-        self.dev.check(self._lib.bqg_factorize(self.dev.handle, self.handle, s,
-                                               lab.ctypes.data if labels else None, values.ctypes.data,
-                                               len(values), ctypes.byref(n_values)))
+        for _ in range(2):
+            values = np.empty(max(cap, 1), dtype=dt)
+            rc = self._lib.bqg_factorize(self.dev.handle, self.handle, s, lab.ctypes.data if labels else None,
+                                         values.ctypes.data, len(values), ctypes.byref(n_values))
+            if rc == 0 or n_values.value <= len(values):
+                break
+            cap = n_values.value  # more distinct values than the first guess: once more, sized
+        self.dev.check(rc)
         return lab, values[:n_values.value]
 
     def select_rows(self, cols, where_terms=None, mask=None):

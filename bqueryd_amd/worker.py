@@ -68,14 +68,17 @@ class ShardCache:
             float(os.environ.get('BQGPU_CACHE_GB', '64')) * (1 << 30))
         self.device = device
         self._items = OrderedDict()
+        self._real = {}  # rootdir -> realpath (resolved once: a warm message's largest file-system cost)
         self.extra = None
 
     def _key(self, rootdir):
+        real = self._real.get(rootdir)
+        if real is None:
+            real = self._real[rootdir] = os.path.realpath(rootdir)
         try:
-            st = os.stat(os.path.join(rootdir, '__rootdirs__'))
-            return (os.path.realpath(rootdir), st.st_mtime_ns)
+            return (real, os.stat(os.path.join(rootdir, '__rootdirs__')).st_mtime_ns)
         except OSError:
-            return (os.path.realpath(rootdir), None)
+            return (real, None)
 
     def open(self, rootdir):
         key = self._key(rootdir)
