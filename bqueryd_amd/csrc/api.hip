@@ -412,23 +412,10 @@ int guard(bqg_ctx* ctx, F&& f) {
 // ------------------------------------------------------------------------------------
 // statistics
 // ------------------------------------------------------------------------------------
-void compute_stats(bqg_table* t, int col) {
-  bqg_ctx* c = t->ctx;
-  Column& k = t->cols[col];
-  if (k.stats.valid) return;
-  k.stats.runs = -1;  // measured again on demand (column_runs)
-  unsigned long long* d = (unsigned long long*)c->misc.ensure(8 * sizeof(unsigned long long));
-  unsigned long long init[8] = {~0ull, 0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
-  unsigned long long* h = (unsigned long long*)c->hhdr.ensure(128);
-  memcpy(h, init, sizeof(init));
-  HIPCHECK(hipMemcpyAsync(d, h, sizeof(init), hipMemcpyHostToDevice, c->stream));
-  DevCol dc{k.dev, k.dtype, dtype_lg(k.dtype)};
-  if (t->nrows > 0) launch_stats(dc, t->nrows, d, c->stream);
-  HIPCHECK(hipGetLastError());
-  HIPCHECK(hipMemcpyAsync(h + 8, d, sizeof(init), hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(hipStreamSynchronize(c->stream));
-  const unsigned long long mn = h[8], mx = h[9], lsb = h[11], enc = h[12];
-  k.stats.has_nan = h[10] != 0;
+// the k_stats result words of one column -> its ColStats (min / max / NaN / exact codes)
+void finish_stats(Column& k, const unsigned long long* r) {
+  const unsigned long long mn = r[0], mx = r[1], lsb = r[3], enc = r[4];
+  k.stats.has_nan = r[2] != 0;
   k.stats.empty = mn > mx;
   if (!k.stats.empty) {
     if (dtype_is_float(k.dtype)) {
@@ -461,6 +448,40 @@ void compute_stats(bqg_table* t, int col) {
     }
   }
   k.stats.valid = true;
+}
+
+// Statistics of several columns in one round trip: one k_stats launch per column without
+// valid statistics, then ONE copy back and ONE synchronisation (a re-group of a merge's
+// received rows otherwise paid a host round trip per column).
+void compute_stats_many(bqg_table* t, const std::vector<int>& cols) {
+  bqg_ctx* c = t->ctx;
+  std::vector<int> todo;
+  for (int col : cols)
+    if (col >= 0 && col < (int)t->cols.size() && !t->cols[col].stats.valid &&
+        std::find(todo.begin(), todo.end(), col) == todo.end())
+      todo.push_back(col);
+  if (todo.empty()) return;
+  const size_t n = todo.size();
+  unsigned long long* d = (unsigned long long*)c->misc.ensure(n * 8 * sizeof(unsigned long long));
+  unsigned long long* h = (unsigned long long*)c->hhdr.ensure(2 * n * 8 * sizeof(unsigned long long));
+  static const unsigned long long init[8] = {~0ull, 0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
+  for (size_t i = 0; i < n; ++i) memcpy(h + 8 * i, init, sizeof(init));
+  HIPCHECK(hipMemcpyAsync(d, h, n * sizeof(init), hipMemcpyHostToDevice, c->stream));
+  for (size_t i = 0; i < n; ++i) {
+    Column& k = t->cols[todo[i]];
+    k.stats.runs = -1;  // measured again on demand (column_runs)
+    DevCol dc{k.dev, k.dtype, dtype_lg(k.dtype)};
+    if (t->nrows > 0) launch_stats(dc, t->nrows, d + 8 * i, c->stream);
+  }
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemcpyAsync(h + 8 * n, d, n * sizeof(init), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < n; ++i) finish_stats(t->cols[todo[i]], h + 8 * n + 8 * i);
+}
+
+void compute_stats(bqg_table* t, int col) {
+  if (t->cols[col].stats.valid) return;
+  compute_stats_many(t, std::vector<int>{col});
 }
 
 // value runs of a column (count_runs: one pass, cached with the statistics; a push or a
@@ -601,6 +622,15 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     pl.p.mask_col = scan_col(pl, q->mask_col);
   }
   pl.has_filter = q->n_terms > 0 || q->mask_col >= 0;
+  {
+    // the statistics this plan reads (key ranges, value codes of summed and distinct columns),
+    // in one device round trip
+    std::vector<int> sc;
+    for (int k = 0; k < q->n_keys; ++k) sc.push_back(q->key_cols[k]);
+    for (int a = 0; a < q->n_aggs; ++a)
+      if (q->aggs[a].op != BQG_COUNT) sc.push_back(q->aggs[a].col);
+    compute_stats_many(t, sc);
+  }
   // 3. keys
   pl.p.nkeys = q->n_keys;
   bool any_float = false;
@@ -1166,22 +1196,22 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.capacity = (uint64_t)L.ntiles * (uint64_t)tr;
       L.hdr = (uint16_t*)c->prefix.ensure((size_t)L.ntiles * (size_t)(L.nparts + 1) * 2 + 256);
       // one scratch block: entry values | entry meta | split partial tables | arrival counters
-      // (| pack: first tiles, tile marks)
+      // (| pack: first tile tags, tile marks)
       const size_t vbytes = pk ? 0 : ((size_t)L.capacity * (nw ? 4 : 8) * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
       const size_t mbytes = ((size_t)L.capacity * 4 + 255) & ~size_t(255);
       L.partial_bytes = (part_agg_lds(L.wbits, nsum, pk) + 255) & ~size_t(255);
       const size_t pbytes = L.splits > 1 ? (size_t)L.nparts * L.splits * L.partial_bytes : 0;
       const size_t abytes = ((size_t)L.nparts * 4 + 255) & ~size_t(255);
-      const size_t fbytes = pk ? (((size_t)L.nparts << L.wbits) * 4 + 255) & ~size_t(255) : 0;
-      unsigned char* eb =
-          (unsigned char*)c->bitmap.ensure(vbytes + mbytes + pbytes + abytes + fbytes + (pk ? (size_t)L.ntiles : 0) + 512);
+      const size_t tbytes = pk ? (((size_t)L.nparts << L.wbits) + 255) & ~size_t(255) : 0;
+      unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + mbytes + pbytes + abytes + tbytes +
+                                                           (pk ? (size_t)L.ntiles : 0) + 512);
       L.vals = (unsigned long long*)eb;
       L.meta = (uint32_t*)(eb + vbytes);
       L.partial = eb + vbytes + mbytes;
       L.arrive = (unsigned int*)(eb + vbytes + mbytes + pbytes);
       if (pk) {
-        L.first_tile = (uint32_t*)(eb + vbytes + mbytes + pbytes + abytes);
-        L.tile_mark = eb + vbytes + mbytes + pbytes + abytes + fbytes;
+        L.first_tag = eb + vbytes + mbytes + pbytes + abytes;
+        L.tile_mark = L.first_tag + tbytes;
       }
       hipFunction_t fs = nullptr, ff = nullptr;
       if (c->opt[kOptJit] && N >= c->opt[kOptJitMinRows]) {

@@ -146,6 +146,13 @@ struct CommState {
   int rank = 0, nranks = 1;
   Buf send, scratch, counts;  // packed send blocks, pack scratch, row counts
   double phase_ms[kMergePhases] = {};  // host wall time of this rank's part of the last merge
+  // in-process transport: an event on this rank's stream, and (rank 0) the copy descriptors
+  // of a transfer step -- page-locked staging, its reuse guarded by desc_ev -- and their
+  // device copy
+  hipEvent_t ev = nullptr, desc_ev = nullptr;
+  void* hdesc = nullptr;
+  size_t hdesc_cap = 0;
+  Buf ddesc;
 };
 
 double now_ms() {
@@ -169,6 +176,10 @@ void destroy_state(CommState* s) {
   s->send.release();
   s->scratch.release();
   s->counts.release();
+  s->ddesc.release();
+  if (s->hdesc) (void)hipHostFree(s->hdesc);
+  if (s->ev) (void)hipEventDestroy(s->ev);
+  if (s->desc_ev) (void)hipEventDestroy(s->desc_ev);
   delete s;
 }
 
@@ -264,7 +275,15 @@ bqg_table* regroup(bqg_ctx* c, bqg_table* t, int n_keys, int ncols) {
   q.n_aggs = ncols - n_keys;
   q.aggs = aggs.data();
   bqg_table* out = nullptr;
-  ck(c, bqg_groupby_table(c, t, &q, &out));
+  // the merge's re-groups run the query-specialised kernels whatever the table size (the
+  // context's jit_min_rows keeps small ad-hoc queries off the compiler; a merge's shape
+  // repeats, and its compiled kernels are cached)
+  int64_t jit_min = 0;
+  ck(c, bqg_get_option(c, "jit_min_rows", &jit_min));
+  ck(c, bqg_set_option(c, "jit_min_rows", 0));
+  const int rc = bqg_groupby_table(c, t, &q, &out);
+  (void)bqg_set_option(c, "jit_min_rows", jit_min);
+  ck(c, rc);
   return out;
 }
 
@@ -360,35 +379,64 @@ bool one_device(std::vector<Local>& ranks) {
   return true;
 }
 
-// the copies of one in-process transfer step, on rank 0's stream (the caller syncs every rank
-// before and after); contexts on different GPUs copy one by one on the receiver's stream
+hipEvent_t event_of(CommState* st, hipEvent_t CommState::*which) {
+  if (!(st->*which)) HIPCK(hipEventCreateWithFlags(&(st->*which), hipEventDisableTiming));
+  return st->*which;
+}
+
+// The copies of one in-process transfer step, ordered on the ranks' streams the way RCCL
+// orders a collective, with no host synchronisation: rank 0's stream waits for every rank's
+// work so far, runs all the copies in one kernel, and every rank's stream waits for that
+// kernel.  Contexts on different GPUs fall back to one copy per message on the receiver's
+// stream between full synchronisations.
 void batch_copies(std::vector<Local>& ranks, const std::vector<std::pair<size_t, CopyDesc>>& copies) {
-  if (copies.empty()) return;
   if (!one_device(ranks)) {
+    sync_all(ranks);
     for (const auto& rc : copies) {
       Local& d = ranks[rc.first];
       HIPCK(hipSetDevice(bqg_internal_device(d.ctx)));
       HIPCK(hipMemcpyAsync(rc.second.dst, rc.second.src, rc.second.bytes, hipMemcpyDefault, d.stream));
     }
+    sync_all(ranks);
     return;
   }
+  if (copies.empty()) return;
   Local& l = ranks[0];
   HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-  std::vector<CopyDesc> h;
+  for (size_t i = 1; i < ranks.size(); ++i) {
+    hipEvent_t e = event_of(ranks[i].st, &CommState::ev);
+    HIPCK(hipEventRecord(e, ranks[i].stream));
+    HIPCK(hipStreamWaitEvent(l.stream, e, 0));
+  }
+  CommState* st = l.st;
+  const size_t bytes = sizeof(CopyDesc) * copies.size();
+  hipEvent_t de = event_of(st, &CommState::desc_ev);
+  HIPCK(hipEventSynchronize(de));  // the previous step's descriptor upload has read the staging
+  if (bytes > st->hdesc_cap) {
+    if (st->hdesc) HIPCK(hipHostFree(st->hdesc));
+    st->hdesc = nullptr;
+    st->hdesc_cap = 0;
+    HIPCK(hipHostMalloc(&st->hdesc, std::max<size_t>(bytes, 4096), hipHostMallocDefault));
+    st->hdesc_cap = std::max<size_t>(bytes, 4096);
+  }
+  CopyDesc* h = (CopyDesc*)st->hdesc;
   unsigned long long most = 0;
-  for (const auto& rc : copies) {
-    h.push_back(rc.second);
-    most = std::max<unsigned long long>(most, rc.second.bytes);
+  for (size_t i = 0; i < copies.size(); ++i) {
+    h[i] = copies[i].second;
+    most = std::max<unsigned long long>(most, h[i].bytes);
   }
-  for (size_t i0 = 0; i0 < h.size(); i0 += 65535) {
-    const size_t n = std::min<size_t>(65535, h.size() - i0);
-    CopyDesc* dd = (CopyDesc*)l.st->scratch.ensure(sizeof(CopyDesc) * h.size());
-    HIPCK(hipMemcpyAsync(dd, h.data() + i0, sizeof(CopyDesc) * n, hipMemcpyHostToDevice, l.stream));
-    const unsigned gx = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>(512, (most / 16 + 255) / 256));
-    hipLaunchKernelGGL(k_batch_copy, dim3(gx, (unsigned)n), dim3(256), 0, l.stream, dd);
+  CopyDesc* dd = (CopyDesc*)st->ddesc.ensure(bytes);
+  HIPCK(hipMemcpyAsync(dd, h, bytes, hipMemcpyHostToDevice, l.stream));
+  HIPCK(hipEventRecord(de, l.stream));
+  const unsigned gx = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>(512, (most / 16 + 255) / 256));
+  for (size_t i0 = 0; i0 < copies.size(); i0 += 65535) {
+    const size_t n = std::min<size_t>(65535, copies.size() - i0);
+    hipLaunchKernelGGL(k_batch_copy, dim3(gx, (unsigned)n), dim3(256), 0, l.stream, dd + i0);
     HIPCK(hipGetLastError());
-    HIPCK(hipStreamSynchronize(l.stream));  // the descriptors' host copy and scratch are reused
   }
+  hipEvent_t done = event_of(st, &CommState::ev);
+  HIPCK(hipEventRecord(done, l.stream));
+  for (size_t i = 1; i < ranks.size(); ++i) HIPCK(hipStreamWaitEvent(ranks[i].stream, done, 0));
 }
 
 // every rank: `count` int64 at counts.p -> [nranks][count] at counts.p + nranks
@@ -405,7 +453,6 @@ void xfer_allgather_i64(std::vector<Local>& ranks, size_t count) {
     return;
   }
   if ((int)ranks.size() != W) comm_fail(BQG_E_STATE, "in-process transport needs every rank in one merge call");
-  sync_all(ranks);
   std::vector<std::pair<size_t, CopyDesc>> copies;
   for (size_t i = 0; i < ranks.size(); ++i) {
     Local& d = ranks[i];
@@ -417,7 +464,6 @@ void xfer_allgather_i64(std::vector<Local>& ranks, size_t count) {
     }
   }
   batch_copies(ranks, copies);
-  sync_all(ranks);
 }
 
 // grouped point-to-point: sends[i] / recvs[i] of local rank i (matching lists on both sides)
@@ -434,7 +480,6 @@ void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& se
     NCCLCHECK(R.GroupEnd());
     return;
   }
-  sync_all(ranks);
   std::vector<std::pair<size_t, CopyDesc>> copies;
   for (size_t i = 0; i < ranks.size(); ++i) {
     Local& d = ranks[i];
@@ -456,7 +501,6 @@ void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& se
     }
   }
   batch_copies(ranks, copies);
-  sync_all(ranks);
 }
 
 void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t>& dts, int reduced) {

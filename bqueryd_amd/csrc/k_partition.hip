@@ -257,8 +257,10 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       const uint64_t gs = slot0 + s;
       sa.cnt[gs] = c;
       sa.fst[gs] = kNoRow;  // k_part_first_rows
-      L.first_tile[gs] = f;
-      if (f != kNoRow) L.tile_mark[f] = 1;
+      if (f != kNoRow) {
+        L.tile_mark[f] = 1;
+        L.first_tag[gs] = (unsigned char)f;
+      }
       if (nsum) {
         unsigned long long tot = cs + c * (unsigned long long)L.enc_base16;
         if (L.enc_kind[0] == 3) tot += c * (unsigned long long)L.enc_off[0];

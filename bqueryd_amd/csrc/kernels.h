@@ -192,14 +192,14 @@ struct PartLaunch {
   // one 32-bit word per entry, code16 = code - enc_base16 above the 16-bit slot_low; the
   // aggregate's per-slot accumulator is count << sbits | sum of code16 (one 64-bit LDS atomic
   // per entry; the planner picks sbits and splits so neither field can overflow), and it
-  // records each slot's first TILE: first_tile [nslots] (kNoRow = none), tile_mark [ntiles]
-  // (1 = some slot's first tile, zeroed before the aggregate), then k_part_first_rows re-reads
-  // only the marked tiles for the exact first rows
+  // marks each slot's first TILE: tile_mark [ntiles] (1 = some slot's first tile, zeroed
+  // before the aggregate) and first_tag [nslots] (its low 8 bits), then k_part_first_rows
+  // re-reads only the marked tiles for the exact first rows
   int pack;
   int sbits;
   int64_t enc_base16;
-  uint32_t* first_tile;
   unsigned char* tile_mark;
+  unsigned char* first_tag;
   // aggregate combine (splits > 1): per-partition arrival counters (zeroed by
   // launch_partitioned) and [nparts][splits] partial tables of partial_bytes each
   unsigned int* arrive;

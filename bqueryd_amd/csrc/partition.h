@@ -215,12 +215,16 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   }
 }
 
-// First rows of the PACK path: a slot's first row lies in its first tile (first_tile, from
-// the aggregate), so only the tiles marked as some slot's first tile are read again -- their
-// key / filter columns, through the scan's own row -> slot code -- and every passing row whose
-// slot has this tile as its first one takes part in an atomicMin on the slot's first row.  On
-// random keys the marked tiles are the first ~10-15 % (each slot's first appearance falls
-// early); on sorted keys every tile is marked.
+// First rows of the PACK path: a slot's first row lies in its first tile, and the aggregate
+// marks every slot's first tile (tile_mark) and keeps its low 8 bits per slot (first_tag);
+// the marked tiles are read again -- their key / filter columns, through the scan's own row ->
+// slot code -- and a passing row whose slot's tag matches the tile's takes part in an
+// atomicMin on the slot's first row (the combine set every slot to kNoRow): the slot's true
+// first row is among them, and any other row that passes the 8-bit check is later, so it
+// cannot win.  The per-row check reads a 1-byte tag (the array stays in L2) instead of
+// issuing a memory-side atomic per row.  On random keys the marked tiles are mostly a prefix
+// (each slot's first appearance falls early: ~10-15 % of the tiles at C3's 1 M groups); on
+// sorted keys every tile is marked.
 template <int NC>
 __device__ __forceinline__ void part_first_rows_body(const ScanParams& p, const PartLaunch& L, const SlotArrays& sa) {
   // only the key, term and mask columns are read (the others re-read one line per wave)
@@ -230,6 +234,7 @@ __device__ __forceinline__ void part_first_rows_body(const ScanParams& p, const 
   const int64_t TR = L.tile_rows;
   for (int64_t t = blockIdx.x; t < L.ntiles; t += gridDim.x) {
     if (!L.tile_mark[t]) continue;
+    const unsigned char tag = (unsigned char)t;
     const int64_t base = t * TR;
     const int64_t end = min(p.nrows, base + TR);
     // a tile is at most 4 x 1024 4-row chunks, taken two at a time: both loads in flight
@@ -251,7 +256,7 @@ __device__ __forceinline__ void part_first_rows_body(const ScanParams& p, const 
       vals_code<NC, 4>(p, v, code);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (((pass >> r) & 1u) && L.first_tile[code[r]] == (uint32_t)t) atomicMin(&sa.fst[code[r]], (uint32_t)(row0 + r));
+        if (((pass >> r) & 1u) && L.first_tag[code[r]] == tag) atomicMin(&sa.fst[code[r]], (uint32_t)(row0 + r));
     }
     }
   }
