@@ -1167,7 +1167,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         L.blocks = (int)((N + L.rows_per_block - 1) / L.rows_per_block);
         // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
         // slot table allows one per CU)
-        const size_t agg_lds = part_agg_lds(L.wbits, nsum, pk);
+        const size_t agg_lds = part_agg_lds_launch(L.wbits, nsum, pk);
         const int fit = std::max(1, (int)((160 * 1024) / agg_lds));
         L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, (c->cu * fit + L.nparts / 2) / L.nparts));
         if (c->opt[kOptPartSplits]) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, c->opt[kOptPartSplits]));
@@ -1195,22 +1195,20 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       const int64_t tr = L.tile_rows;
       L.capacity = (uint64_t)L.ntiles * (uint64_t)tr;
       L.hdr = (uint16_t*)c->prefix.ensure((size_t)L.ntiles * (size_t)(L.nparts + 1) * 2 + 256);
-      // one scratch block: entry values | entry meta | split partial tables | arrival counters
+      // one scratch block: entry values | entry meta | split partial tables
       // (| pack: first tile tags, tile marks)
       const size_t vbytes = pk ? 0 : ((size_t)L.capacity * (nw ? 4 : 8) * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
       const size_t mbytes = ((size_t)L.capacity * 4 + 255) & ~size_t(255);
       L.partial_bytes = (part_agg_lds(L.wbits, nsum, pk) + 255) & ~size_t(255);
       const size_t pbytes = L.splits > 1 ? (size_t)L.nparts * L.splits * L.partial_bytes : 0;
-      const size_t abytes = ((size_t)L.nparts * 4 + 255) & ~size_t(255);
       const size_t tbytes = pk ? (((size_t)L.nparts << L.wbits) + 255) & ~size_t(255) : 0;
-      unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + mbytes + pbytes + abytes + tbytes +
+      unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + mbytes + pbytes + tbytes +
                                                            (pk ? (size_t)L.ntiles : 0) + 512);
       L.vals = (unsigned long long*)eb;
       L.meta = (uint32_t*)(eb + vbytes);
       L.partial = eb + vbytes + mbytes;
-      L.arrive = (unsigned int*)(eb + vbytes + mbytes + pbytes);
       if (pk) {
-        L.first_tag = eb + vbytes + mbytes + pbytes + abytes;
+        L.first_tag = eb + vbytes + mbytes + pbytes;
         L.tile_mark = L.first_tag + tbytes;
       }
       hipFunction_t fs = nullptr, ff = nullptr;

@@ -45,7 +45,80 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartL
 // PACK entries (PartLaunch::pack): one 32-bit word {code16, slot_low}; the slot table is one
 // packed 64-bit accumulator (count << sbits | code16 sum: ONE LDS atomic per entry) and the
 // slot's first tile, and the combine leaves first rows to k_part_first_rows.
-template <int G, int U, int NSUM, bool NARROW, bool PACK = false>
+// One split's record of a slot: count, first row (PACK: first tile), sums (PACK: a[0] is the
+// packed count << sbits | code16 sum).
+template <int NV>
+struct PartRec {
+  unsigned long long a[NV];
+  uint32_t c, f;
+};
+
+// The final values of slot gs from its S split records (rec(o, r) fills split o's), added in
+// split order, written to the slot arrays.
+template <int NSUM, bool NARROW, bool PACK, typename Rec>
+__device__ __forceinline__ void part_finish_slot(const ScanParams& p, const PartLaunch& L, const SlotArrays& sa,
+                                                 uint64_t gs, int S, Rec rec) {
+  constexpr int NV = NSUM > 0 ? NSUM : 1;
+  constexpr int nsum = NSUM;
+  if (PACK) {
+    // unpack every split's accumulator before adding (the packed fields of a sum over splits
+    // could carry into each other); exact code sum = sum of code16 + count x enc_base16
+    const unsigned long long smask = (1ull << L.sbits) - 1ull;
+    unsigned long long c = 0, cs = 0;
+    uint32_t f = kNoRow;
+    for (int o = 0; o < S; ++o) {
+      PartRec<NV> r;
+      rec(o, r);
+      c += r.a[0] >> L.sbits;
+      cs += r.a[0] & smask;
+      f = r.f < f ? r.f : f;
+    }
+    sa.cnt[gs] = c;
+    sa.fst[gs] = kNoRow;  // k_part_first_rows
+    if (f != kNoRow) {
+      // a few hundred marked tiles take ~1 M marks (random keys): a read first (an L2 hit once
+      // the XCD has seen the line) instead of 1 M contended byte stores
+      if (!L.tile_mark[f]) L.tile_mark[f] = 1;
+      L.first_tag[gs] = (unsigned char)f;
+    }
+    if (nsum) {
+      unsigned long long tot = cs + c * (unsigned long long)L.enc_base16;
+      if (L.enc_kind[0] == 3) tot += c * (unsigned long long)L.enc_off[0];
+      else tot = as_u64((double)(long long)tot / L.enc_mul[0]);
+      sa.acc[gs] = tot;
+    }
+    return;
+  }
+  uint32_t c = 0, f = kNoRow;
+  unsigned long long a[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) a[q] = 0;
+  for (int o = 0; o < S; ++o) {
+    PartRec<NV> r;
+    rec(o, r);
+    c += r.c;
+    f = r.f < f ? r.f : f;
+#pragma unroll
+    for (int q = 0; q < nsum; ++q) {
+      if (!NARROW && p.sum_is_float[q]) a[q] = as_u64(as_f64(a[q]) + as_f64(r.a[q]));
+      else a[q] += r.a[q];
+    }
+  }
+  sa.cnt[gs] = c;
+  sa.fst[gs] = f;
+#pragma unroll
+  for (int q = 0; q < nsum; ++q) {
+    // narrow: the exact sum of the codes, scaled back once (dyadic: exact below 2^53), or
+    // shifted back by count x offset (integers, modulo 2^64 like the 64-bit accumulator)
+    if (NARROW) {
+      if (L.enc_kind[q] == 3) a[q] += (unsigned long long)c * (unsigned long long)L.enc_off[q];
+      else a[q] = as_u64((double)(long long)a[q] / L.enc_mul[q]);
+    }
+    sa.acc[(size_t)q * p.nslots + gs] = a[q];
+  }
+}
+
+template <int U, int AH, int NSUM, bool NARROW, bool PACK>
 __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunch L, SlotArrays sa) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int P = L.nparts;
@@ -72,246 +145,203 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   const int64_t t_lo = nt * split / L.splits, t_hi = nt * (split + 1) / L.splits;
   const uint32_t lowmask = (uint32_t)W - 1u;
   const uint32_t TR = (uint32_t)L.tile_rows;
-  auto hload = [&](int64_t tg, uint32_t& s0, uint32_t& s1) {
-    const int64_t t = tg + lane;
-    const bool valid = lane < G && t < t_hi;
-    const uint16_t* th = L.hdr + (size_t)(valid ? t : t_lo) * (size_t)(P + 1) + part;
-    const uint32_t a = th[0], b = th[1];
-    s0 = valid ? a : 0u;
-    s1 = valid ? b : 0u;
-  };
   constexpr int NV = NSUM > 0 ? NSUM : 1;
-  // one group of G tiles: flattened segment starts (wave-uniform), the per-lane index base
-  // (lane j: entry index of tile j's segment start minus its flattened position) and the total
-  struct Grp {
-    uint32_t ex[G];
-    uint32_t dl, total;
-    size_t gbase;
-    uint32_t tile0;
-  };
-  // one U x 64-entry load of a group
+  // the window's tiles: flattened segment start F[j] and entry-index base B[j] (entry index =
+  // B[j] + flattened position), K + 1 sentinels past the last tile
+  uint32_t* wF = reinterpret_cast<uint32_t*>(smem + part_agg_lds(L.wbits, nsum, PACK));
+  uint32_t* wB = wF + kAggWin + kAggK + 1;
+  // one chunk of at most U x 64 consecutive entries of a wave's range, spanning at most K
+  // tiles; an entry's tile (global index) or kNoRow past the chunk
   struct Ent {
-    uint32_t m[U], rowb[U];
+    uint32_t m[U], t[U];
     unsigned long long v[U][NV];
   };
-  auto prep = [&](int64_t tg, uint32_t s0, uint32_t s1, Grp& g) {
-    const uint32_t len = s1 - s0;
-    const uint32_t incl = wave_incl_scan_u32(len, lane);
-    const uint32_t excl = incl - len;
-    g.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, G - 1);
+  for (int64_t w0 = t_lo; w0 < t_hi; w0 += kAggWin) {
+    const int nw = (int)min((int64_t)kAggWin, t_hi - w0);
+    // headers of the window's tiles (two per thread, contiguous for the scan)
+    uint32_t len[2], beg[2];
 #pragma unroll
-    for (int j = 0; j < G; ++j) g.ex[j] = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
-    g.dl = (uint32_t)lane * TR + s0 - excl;
-    g.gbase = (size_t)tg * TR;
-    g.tile0 = (uint32_t)tg;
-  };
-  // unconditional loads (an empty group -- past the range -- reads entry 0; the value array
-  // exists even without a summed column): the same loads on every path, so the compiler
-  // waits for exactly the set it consumes
-  auto issue = [&](const Grp& g, uint32_t e0, Ent& en) {
+    for (int k = 0; k < 2; ++k) {
+      const int j = 2 * tid + k;
+      beg[k] = len[k] = 0;
+      if (j < nw) {
+        const uint16_t* th = L.hdr + (size_t)(w0 + j) * (size_t)(P + 1) + part;
+        beg[k] = th[0];
+        len[k] = (uint32_t)th[1] - beg[k];
+      }
+    }
+    uint32_t tot;
+    const uint32_t ex0 = block_excl_scan_1024(len[0] + len[1], &tot);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t e = e0 + u * 64u + lane;
-      const uint32_t ec = e < g.total ? e : (g.total ? g.total - 1u : 0u);
-      uint32_t j0 = 0;
+    for (int k = 0; k < 2; ++k) {
+      const int j = 2 * tid + k;
+      const uint32_t fj = ex0 + (k ? len[0] : 0u);
+      if (j < nw) {
+        wF[j] = fj;
+        wB[j] = (uint32_t)(w0 + j) * TR + beg[k] - fj;
+      }
+    }
+    for (int j = nw + tid; j <= nw + kAggK; j += blockDim.x) {
+      wF[j] = tot;
+      wB[j] = 0u;
+    }
+    lds_barrier();
+    // the wave's equal share of the window's entries, and the tile of its first entry
+    const uint32_t e_lo = (uint32_t)((uint64_t)tot * wave / NW), e_hi = (uint32_t)((uint64_t)tot * (wave + 1) / NW);
+    int jlo = 0, jhi = nw;  // largest j < nw with F[j] <= e_lo
+    while (jhi - jlo > 1) {
+      const int mid = (jlo + jhi) >> 1;
+      if (wF[mid] <= e_lo) jlo = mid; else jhi = mid;
+    }
+    uint32_t f_next = e_lo;
+    int j_next = __builtin_amdgcn_readfirstlane(jlo);
+    // issue the next chunk into `en`: lanes 0..K read the chunk's tile bounds, the chunk ends
+    // at U x 64 entries, the wave's range end or the K-th tile boundary
+    auto issue = [&](Ent& en) {
+      const uint32_t lf = wF[j_next + min(lane, kAggK)], lb = wB[j_next + min(lane, kAggK - 1)];
+      uint32_t Fk[kAggK + 1], Bk[kAggK];
 #pragma unroll
-      for (int j = 1; j < G; ++j) j0 += ec >= g.ex[j] ? 1u : 0u;
-      size_t idx = g.gbase + (uint32_t)__shfl((int)g.dl, (int)j0, 64) + ec;
-      idx = g.total ? idx : 0;
-      en.rowb[u] = PACK ? g.tile0 + j0 : (uint32_t)g.gbase + j0 * TR;  // PACK: the tile
-      en.m[u] = L.meta[idx];
-      if (PACK) continue;
+      for (int k = 0; k <= kAggK; ++k) Fk[k] = (uint32_t)__builtin_amdgcn_readlane((int)lf, k);
 #pragma unroll
-      for (int q = 0; q < NV; ++q) {
-        if (NARROW) {  // the exact 32-bit code: float codes signed, integer offsets unsigned
-          const uint32_t code = reinterpret_cast<const uint32_t*>(L.vals)[(size_t)q * L.capacity + idx];
-          en.v[u][q] = L.enc_kind[q] == 3 ? (unsigned long long)code : (unsigned long long)(long long)(int32_t)code;
+      for (int k = 0; k < kAggK; ++k) Bk[k] = (uint32_t)__builtin_amdgcn_readlane((int)lb, k);
+      const uint32_t fe = min(min(f_next + 64u * U, e_hi), max(Fk[kAggK], f_next));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t f = f_next + u * 64u + lane;
+        const bool valid = f < fe;
+        const uint32_t fc = valid ? f : f_next;
+        uint32_t j = 0, base = Bk[0];
+#pragma unroll
+        for (int k = 1; k < kAggK; ++k) {
+          const bool ge = fc >= Fk[k];
+          j = ge ? (uint32_t)k : j;
+          base = ge ? Bk[k] : base;
         }
-        else
-          en.v[u][q] = L.vals[(size_t)q * L.capacity + idx];
-      }
-    }
-  };
-  auto consume = [&](const Grp& g, uint32_t e0, const Ent& en) {
+        const uint32_t idx = f_next < fe ? base + fc : 0u;
+        en.t[u] = valid ? (uint32_t)w0 + (uint32_t)j_next + j : kNoRow;
+        en.m[u] = L.meta[idx];
+        if (PACK) continue;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t e = e0 + u * 64u + lane;
-      if (e >= g.total) continue;
-      const uint32_t sl = en.m[u] & lowmask;
-      if (PACK) {
-        atomicAdd(&acc[sl], inc + (unsigned long long)(en.m[u] >> 16));
-        if (fst[sl] > en.rowb[u]) atomicMin(&fst[sl], en.rowb[u]);
-        continue;
+        for (int q = 0; q < NV; ++q) {
+          if (NARROW) {  // the exact 32-bit code: float codes signed, integer offsets unsigned
+            const uint32_t code = reinterpret_cast<const uint32_t*>(L.vals)[(size_t)q * L.capacity + idx];
+            en.v[u][q] = L.enc_kind[q] == 3 ? (unsigned long long)code : (unsigned long long)(long long)(int32_t)code;
+          } else {
+            en.v[u][q] = L.vals[(size_t)q * L.capacity + idx];
+          }
+        }
       }
-      const uint32_t row = en.rowb[u] + (en.m[u] >> L.wbits);
-      atomicAdd(&cnt[sl], 1u);
-      if (fst[sl] > row) atomicMin(&fst[sl], row);
+      // the next chunk starts in the last tile whose start is <= fe (empty tiles skipped)
+      int adv = 0;
 #pragma unroll
-      for (int q = 0; q < nsum; ++q) {
-        if (!NARROW && p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][q], p.sum_conv[q]));
-        else atomicAdd(&acc[(size_t)q * W + sl], en.v[u][q]);
+      for (int k = 1; k <= kAggK; ++k) adv += Fk[k] <= fe ? 1 : 0;
+      j_next = min(j_next + adv, nw);
+      f_next = fe;
+    };
+    auto consume = [&](const Ent& en) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (en.t[u] == kNoRow) continue;
+        const uint32_t sl = en.m[u] & lowmask;
+        if (PACK) {
+          // fire-and-forget LDS atomics: nothing in the loop waits on the LDS
+          atomicAdd(&acc[sl], inc + (unsigned long long)(en.m[u] >> 16));
+          atomicMin(&fst[sl], en.t[u]);
+          continue;
+        }
+        const uint32_t row = en.t[u] * TR + (en.m[u] >> L.wbits);
+        atomicAdd(&cnt[sl], 1u);
+        atomicMin(&fst[sl], row);
+#pragma unroll
+        for (int q = 0; q < nsum; ++q) {
+          if (!NARROW && p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][q], p.sum_conv[q]));
+          else atomicAdd(&acc[(size_t)q * W + sl], en.v[u][q]);
+        }
+      }
+    };
+    // AH chunks in flight: each ring slot is consumed, then refilled in place (no exit
+    // inside the body: a copy of a pending load would wait for every load in flight)
+    Ent ring[AH];
+    uint32_t cstart[AH];
+#pragma unroll
+    for (int a = 0; a < AH; ++a) {
+      cstart[a] = f_next;
+      issue(ring[a]);
+    }
+    while (cstart[0] < e_hi) {
+#pragma unroll
+      for (int a = 0; a < AH; ++a) {
+        consume(ring[a]);
+        cstart[a] = f_next;
+        issue(ring[a]);
       }
     }
-  };
-  // entries of a group beyond its first U x 64 (segments longer than the typical tile share)
-  auto rest = [&](const Grp& g, Ent& en) {
-    for (uint32_t e0 = 64u * U; e0 < g.total; e0 += 64u * U) {
-      issue(g, e0, en);
-      consume(g, e0, en);
-    }
-  };
-  const int64_t stride = (int64_t)NW * G;
-  int64_t tg = t_lo + (int64_t)wave * G;
-  uint32_t ha0, ha1, hb0, hb1;  // headers of the groups two and three ahead, in turn
-  Grp ga, gb;
-  Ent ea, eb;
-  hload(tg, ha0, ha1);
-  hload(tg + stride, hb0, hb1);
-  prep(tg, ha0, ha1, ga);
-  issue(ga, 0, ea);
-  hload(tg + 2 * stride, ha0, ha1);
-  for (; tg < t_hi; tg += 2 * stride) {
-    // group tg in (ga, ea); group tg + stride's header in hb
-    prep(tg + stride, hb0, hb1, gb);
-    issue(gb, 0, eb);
-    hload(tg + 3 * stride, hb0, hb1);
-    consume(ga, 0, ea);
-    rest(ga, ea);
-    if (tg + stride >= t_hi) break;
-    // group tg + stride in (gb, eb); group tg + 2 * stride's header in ha
-    prep(tg + 2 * stride, ha0, ha1, ga);
-    issue(ga, 0, ea);
-    hload(tg + 4 * stride, ha0, ha1);
-    consume(gb, 0, eb);
-    rest(gb, eb);
+    lds_barrier();  // every wave is done with this window's bounds
   }
   __syncthreads();
-  // Combine the partition's split tables without device atomics (and without a slot-array
-  // initialisation pass): every split stores its table to its own partial record, the last
-  // split to arrive (one agent-scope counter per partition, zeroed before the launch) adds the
-  // records in split order -- the same sums whatever the arrival order -- and writes every slot
-  // of the partition, empty ones included.  Hand-off: plain stores, each wave drains, barrier,
-  // one lane's agent release, then the counter; the last arriver acquires before reading
-  // (cdna_hip_programming.md Guideline 16).  Nobody waits: no spin, no residency assumption.
+  // Split tables: with several splits per partition every workgroup stores its table to its own
+  // partial record and k_part_combine adds the records in split order (the same sums whatever
+  // the order the workgroups ran in); with one split the workgroup finishes its slots itself.
+  // (An in-kernel hand-off -- the last split to arrive adds the others' records after an agent
+  // release / acquire -- cost ~130 us at C3: every workgroup's release writes back its XCD's L2.)
   const uint64_t slot0 = (uint64_t)part << L.wbits;
   const int nvalid = (int)((uint64_t)W < p.nslots - slot0 ? (uint64_t)W : p.nslots - slot0);
-  const int S = L.splits;
-  __shared__ unsigned int s_last;
-  if (S > 1) {
-    uint32_t* pc = reinterpret_cast<uint32_t*>(L.partial + ((size_t)part * S + split) * L.partial_bytes);
+  if (L.splits > 1) {
+    unsigned char* rec = L.partial + ((size_t)part * L.splits + split) * L.partial_bytes;
     if (PACK) {  // [W] packed accumulators, then [W] first tiles
-      unsigned long long* pa = reinterpret_cast<unsigned long long*>(pc);
+      unsigned long long* pa = reinterpret_cast<unsigned long long*>(rec);
       uint32_t* pf = reinterpret_cast<uint32_t*>(pa + W);
-      for (int s = tid; s < W; s += blockDim.x) {
+      for (int s = tid; s < nvalid; s += blockDim.x) {
         pa[s] = acc[s];
         pf[s] = fst[s];
       }
-    }
-    uint32_t* pf = pc + W;
-    unsigned long long* pa = reinterpret_cast<unsigned long long*>(pf + W);
-    for (int s = tid; !PACK && s < W; s += blockDim.x) {
-      pc[s] = cnt[s];
-      pf[s] = fst[s];
+    } else {  // [W] counts, [W] first rows, then [nsum][W] sums
+      uint32_t* pc = reinterpret_cast<uint32_t*>(rec);
+      uint32_t* pf = pc + W;
+      unsigned long long* pa = reinterpret_cast<unsigned long long*>(pf + W);
+      for (int s = tid; s < nvalid; s += blockDim.x) {
+        pc[s] = cnt[s];
+        pf[s] = fst[s];
 #pragma unroll
-      for (int q = 0; q < nsum; ++q) pa[(size_t)q * W + s] = acc[(size_t)q * W + s];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned int old = __hip_atomic_fetch_add(&L.arrive[part], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = old == (unsigned int)(S - 1);
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      s_last = last ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!s_last) return;
-  }
-  if (PACK) {
-    // unpack every split's accumulator before adding (the packed fields of a sum over splits
-    // could carry into each other); exact code sum = sum of code16 + count x enc_base16
-    const unsigned long long smask = (1ull << L.sbits) - 1ull;
-    for (int s = tid; s < nvalid; s += blockDim.x) {
-      unsigned long long c = 0, cs = 0;
-      uint32_t f = kNoRow;
-      for (int o = 0; o < S; ++o) {
-        unsigned long long a;
-        uint32_t of;
-        if (o == split) {
-          a = acc[s];
-          of = fst[s];
-        } else {
-          const unsigned long long* pa =
-              reinterpret_cast<const unsigned long long*>(L.partial + ((size_t)part * S + o) * L.partial_bytes);
-          a = pa[s];
-          of = reinterpret_cast<const uint32_t*>(pa + W)[s];
-        }
-        c += a >> L.sbits;
-        cs += a & smask;
-        f = of < f ? of : f;
-      }
-      const uint64_t gs = slot0 + s;
-      sa.cnt[gs] = c;
-      sa.fst[gs] = kNoRow;  // k_part_first_rows
-      if (f != kNoRow) {
-        L.tile_mark[f] = 1;
-        L.first_tag[gs] = (unsigned char)f;
-      }
-      if (nsum) {
-        unsigned long long tot = cs + c * (unsigned long long)L.enc_base16;
-        if (L.enc_kind[0] == 3) tot += c * (unsigned long long)L.enc_off[0];
-        else tot = as_u64((double)(long long)tot / L.enc_mul[0]);
-        sa.acc[gs] = tot;
+        for (int q = 0; q < nsum; ++q) pa[(size_t)q * W + s] = acc[(size_t)q * W + s];
       }
     }
     return;
   }
   for (int s = tid; s < nvalid; s += blockDim.x) {
-    uint32_t c = 0, f = kNoRow;
-    unsigned long long a[NV];
+    PartRec<NV> r;
+    r.f = fst[s];
+    r.c = PACK ? 0u : cnt[s];
 #pragma unroll
-    for (int q = 0; q < NV; ++q) a[q] = 0;
-    for (int o = 0; o < S; ++o) {
-      uint32_t oc, of;
-      unsigned long long oa[NV];
-      if (o == split) {
-        oc = cnt[s];
-        of = fst[s];
-#pragma unroll
-        for (int q = 0; q < nsum; ++q) oa[q] = acc[(size_t)q * W + s];
+    for (int q = 0; q < (PACK ? 1 : nsum); ++q) r.a[q] = acc[(size_t)q * W + s];
+    part_finish_slot<NSUM, NARROW, PACK>(p, L, sa, slot0 + s, 1, [&](int, PartRec<NV>& o) { o = r; });
+  }
+}
+
+// The split records of a partition added in split order, one thread per slot (coalesced).
+template <int NSUM, bool NARROW, bool PACK>
+__global__ __launch_bounds__(256) void k_part_combine(ScanParams p, PartLaunch L, SlotArrays sa) {
+  constexpr int NV = NSUM > 0 ? NSUM : 1;
+  const int W = 1 << L.wbits, S = L.splits;
+  for (uint64_t gs = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; gs < p.nslots; gs += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t part = gs >> L.wbits;
+    const int s = (int)(gs & (uint64_t)(W - 1));
+    part_finish_slot<NSUM, NARROW, PACK>(p, L, sa, gs, S, [&](int o, PartRec<NV>& r) {
+      const unsigned char* rec = L.partial + ((size_t)part * S + o) * L.partial_bytes;
+      if (PACK) {
+        const unsigned long long* pa = reinterpret_cast<const unsigned long long*>(rec);
+        r.a[0] = pa[s];
+        r.f = reinterpret_cast<const uint32_t*>(pa + W)[s];
+        r.c = 0;
       } else {
-        const uint32_t* pc = reinterpret_cast<const uint32_t*>(L.partial + ((size_t)part * S + o) * L.partial_bytes);
+        const uint32_t* pc = reinterpret_cast<const uint32_t*>(rec);
         const unsigned long long* pa = reinterpret_cast<const unsigned long long*>(pc + 2 * W);
-        oc = pc[s];
-        of = pc[W + s];
+        r.c = pc[s];
+        r.f = pc[W + s];
 #pragma unroll
-        for (int q = 0; q < nsum; ++q) oa[q] = pa[(size_t)q * W + s];
+        for (int q = 0; q < NSUM; ++q) r.a[q] = pa[(size_t)q * W + s];
       }
-      c += oc;
-      f = of < f ? of : f;
-#pragma unroll
-      for (int q = 0; q < nsum; ++q) {
-        if (!NARROW && p.sum_is_float[q]) a[q] = as_u64(as_f64(a[q]) + as_f64(oa[q]));
-        else a[q] += oa[q];
-      }
-    }
-    const uint64_t gs = slot0 + s;
-    sa.cnt[gs] = c;
-    sa.fst[gs] = f;
-#pragma unroll
-    for (int q = 0; q < nsum; ++q) {
-      // narrow: the exact sum of the codes, scaled back once (dyadic: exact below 2^53), or
-      // shifted back by count x offset (integers, modulo 2^64 like the 64-bit accumulator)
-      if (NARROW) {
-        if (L.enc_kind[q] == 3) a[q] += (unsigned long long)c * (unsigned long long)L.enc_off[q];
-        else a[q] = as_u64((double)(long long)a[q] / L.enc_mul[q]);
-      }
-      sa.acc[(size_t)q * p.nslots + gs] = a[q];
-    }
+    });
   }
 }
 
@@ -383,18 +413,18 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
     }
 #undef BQG_SCATTER
   }
-  const size_t agg_lds = part_agg_lds(L.wbits, p.nsum, L.pack != 0);
+  const size_t agg_lds = part_agg_lds_launch(L.wbits, p.nsum, L.pack != 0);
   const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
+  const unsigned cgrid = (unsigned)std::min<uint64_t>((p.nslots + 255) / 256, 4096);
   if (L.pack) {
     (void)hipMemsetAsync(L.tile_mark, 0, (size_t)L.ntiles, st);
-#define BQG_AGGP(G, U, NS) hipLaunchKernelGGL((k_part_aggregate<G, U, NS, true, true>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
-    const bool big = L.tile_rows > 4096;
-    if (p.nsum == 0) {
-      if (big) BQG_AGGP(4, 4, 0); else BQG_AGGP(8, 4, 0);
-    } else {
-      if (big) BQG_AGGP(4, 4, 1); else BQG_AGGP(8, 4, 1);
-    }
+#define BQG_AGGP(NS) hipLaunchKernelGGL((k_part_aggregate<8, 2, NS, true, true>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
+    if (p.nsum == 0) BQG_AGGP(0); else BQG_AGGP(1);
 #undef BQG_AGGP
+    if (L.splits > 1) {
+      if (p.nsum == 0) hipLaunchKernelGGL((k_part_combine<0, true, true>), dim3(cgrid), dim3(256), 0, st, p, L, s);
+      else hipLaunchKernelGGL((k_part_combine<1, true, true>), dim3(cgrid), dim3(256), 0, st, p, L, s);
+    }
     // grid-stride over the tiles (the marked ones are mostly a prefix on random keys)
     const unsigned fgrid = (unsigned)std::min<int64_t>(L.ntiles, 2048);
     if (ffirst) {
@@ -408,16 +438,17 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
     }
     return;
   }
-  // G tiles per wave group: ~8 x 4096 rows of segments whichever the tile size
-#define BQG_AGG2(G, U, NS, NW) hipLaunchKernelGGL((k_part_aggregate<G, U, NS, NW>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
-#define BQG_AGG(G, U, NS) do { if (L.narrow) BQG_AGG2(G, U, NS, true); else BQG_AGG2(G, U, NS, false); } while (0)
-  const bool big = L.tile_rows > 4096;
+#define BQG_AGG2(U, NS, NW) do { \
+    hipLaunchKernelGGL((k_part_aggregate<U, 2, NS, NW, false>), dim3(grid), dim3(1024), agg_lds, st, p, L, s); \
+    if (L.splits > 1) hipLaunchKernelGGL((k_part_combine<NS, NW, false>), dim3(cgrid), dim3(256), 0, st, p, L, s); \
+  } while (0)
+#define BQG_AGG(U, NS) do { if (L.narrow) BQG_AGG2(U, NS, true); else BQG_AGG2(U, NS, false); } while (0)
   switch (p.nsum) {
-    case 0: if (big) BQG_AGG2(4, 4, 0, false); else BQG_AGG2(8, 4, 0, false); break;
-    case 1: if (big) BQG_AGG(4, 4, 1); else BQG_AGG(8, 4, 1); break;
-    case 2: if (big) BQG_AGG(4, 4, 2); else BQG_AGG(8, 4, 2); break;
-    case 3: if (big) BQG_AGG(4, 2, 3); else BQG_AGG(8, 2, 3); break;
-    default: if (big) BQG_AGG(4, 2, 4); else BQG_AGG(8, 2, 4); break;
+    case 0: BQG_AGG2(8, 0, false); break;
+    case 1: BQG_AGG(8, 1); break;
+    case 2: BQG_AGG(4, 2); break;
+    case 3: BQG_AGG(4, 3); break;
+    default: BQG_AGG(2, 4); break;
   }
 #undef BQG_AGG
 #undef BQG_AGG2

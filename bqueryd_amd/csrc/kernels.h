@@ -200,9 +200,7 @@ struct PartLaunch {
   int64_t enc_base16;
   unsigned char* tile_mark;
   unsigned char* first_tag;
-  // aggregate combine (splits > 1): per-partition arrival counters (zeroed by
-  // launch_partitioned) and [nparts][splits] partial tables of partial_bytes each
-  unsigned int* arrive;
+  // splits > 1: [nparts][splits] split tables of partial_bytes each, added by k_part_combine
   unsigned char* partial;
   size_t partial_bytes;      // 2^wbits * (8 + 8 * nsum)
 };
@@ -213,8 +211,15 @@ inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1, boo
 }
 // LDS bytes of an aggregate workgroup's slot table: count + first row + 8-byte sums, or
 // (pack) the packed 8-byte accumulator + first tile
-inline size_t part_agg_lds(int wbits, int nsum, bool pack) {
+__host__ __device__ inline size_t part_agg_lds(int wbits, int nsum, bool pack) {
   return ((size_t)1 << wbits) * (pack ? 12 : 8 + 8 * (size_t)nsum);
+}
+// the aggregate walks its split's tiles in windows of kAggWin tiles (their flattened segment
+// starts and entry bases in LDS); a chunk of entries spans at most kAggK tiles
+constexpr int kAggWin = 2048;
+constexpr int kAggK = 8;
+inline size_t part_agg_lds_launch(int wbits, int nsum, bool pack) {
+  return part_agg_lds(wbits, nsum, pack) + 2 * (size_t)(kAggWin + kAggK + 1) * 4;
 }
 // fscatter: the query-specialised (JIT) scatter kernel, or nullptr for the precompiled one
 // ffirst: the query-specialised (JIT) first-row pass of packed entries, or nullptr

@@ -107,10 +107,6 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   uint32_t* hist2 = smeta + TR;                                            // [2][P] tile counts
   uint32_t* toff = hist2 + 2 * P;                                          // [P] tile offsets
   uint32_t* wsum2 = toff + P;                                              // [2][16] scan totals
-  // the aggregate's per-partition arrival counters, zeroed here: the aggregate kernel runs
-  // after this one on the same stream (splits > 1 implies at least one scatter workgroup)
-  if (blockIdx.x == 0 && L.arrive)
-    for (int i = tid; i < P; i += T) L.arrive[i] = 0u;
   for (int i = tid; i < 2 * P; i += T) hist2[i] = 0;
   lds_barrier();
   const int64_t begin = (int64_t)blockIdx.x * L.rows_per_block;

@@ -514,7 +514,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&L.vals, L.capacity * 8 + 256));
   L.partial_bytes = ((size_t)1 << L.wbits) * 16;
   CK(hipMalloc(&L.partial, (size_t)L.nparts * 8 * L.partial_bytes + 256));
-  CK(hipMalloc(&L.arrive, (size_t)L.nparts * 4 + 256));
+
   const size_t slds = part_scatter_lds(L.nparts, L.threads, 1);
   CK(hipFuncSetAttribute((const void*)k_scatter_lib, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   auto agg_run = [&](auto agg, const char* what, int splits) {
@@ -525,7 +525,7 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(ev[0], 0));
       k_scatter_lib<<<L.blocks, L.threads, slds>>>(b.p, L);
       CK(hipEventRecord(ev[1], 0));
-      agg<<<grid, 1024, ((size_t)1 << L.wbits) * 16>>>(b.p, L, b.sa);
+      agg<<<grid, 1024, part_agg_lds_launch(L.wbits, 1, false)>>>(b.p, L, b.sa);
       CK(hipEventRecord(ev[2], 0));
       CK(hipEventSynchronize(ev[2]));
       float t[2];
@@ -534,7 +534,7 @@ int main(int argc, char** argv) {
     }
     same(ref, fetch(b), what);
   };
-  agg_run(k_part_aggregate<8, 4, 1, false>, "agg G8 U4 (library)", 2);
+  agg_run(k_part_aggregate<8, 2, 1, false, false>, "agg U8 (library; splits > 1 need k_part_combine)", 1);
 
   agg_run(k_agg_probe<8, 4, 1, 1>, "probe: loads only (no LDS atomics)", 2);
   agg_run(k_agg_probe<8, 4, 1, 2>, "probe: LDS atomics only (no entry loads)", 2);
