@@ -39,7 +39,7 @@ extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_scatter(bqg::Scan
   bqg::part_scatter_body<BQ_NC, BQ_PART_K, BQ_PART_NARROW != 0, BQ_PART_PACK != 0>(p, L, smem);
 }
 
-extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_first_rows(bqg::ScanParams pin, bqg::PartLaunch L,
+extern "C" __global__ __launch_bounds__(bqg::kFirstRowsBlock) void bq_jit_part_first_rows(bqg::ScanParams pin, bqg::PartLaunch L,
                                                                         bqg::SlotArrays sa) {
   bqg::ScanParams p = pin;
   bqg::jit_specialize(p);

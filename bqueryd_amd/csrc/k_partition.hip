@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void k_part_combine(ScanParams p, PartLaunch L
 }
 
 template <int NC>
-__global__ __launch_bounds__(1024) void k_part_first_rows(ScanParams p, PartLaunch L, SlotArrays sa) {
+__global__ __launch_bounds__(kFirstRowsBlock) void k_part_first_rows(ScanParams p, PartLaunch L, SlotArrays sa) {
   part_first_rows_body<NC>(p, L, sa);
 }
 
@@ -425,16 +425,18 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
       if (p.nsum == 0) hipLaunchKernelGGL((k_part_combine<0, true, true>), dim3(cgrid), dim3(256), 0, st, p, L, s);
       else hipLaunchKernelGGL((k_part_combine<1, true, true>), dim3(cgrid), dim3(256), 0, st, p, L, s);
     }
-    // grid-stride over the tiles (the marked ones are mostly a prefix on random keys)
-    const unsigned fgrid = (unsigned)std::min<int64_t>(L.ntiles, 2048);
+    // grid-stride over 4096-row units of the tiles (the marked ones are mostly a prefix on
+    // random keys)
+    const int64_t funits = L.ntiles * ((L.tile_rows + kFirstRowsUnit - 1) / kFirstRowsUnit);
+    const unsigned fgrid = (unsigned)std::min<int64_t>(funits, 8192);
     if (ffirst) {
       PartLaunch Lc = L;
       ScanParams pc = p;
       SlotArrays sc = s;
       void* args[] = {(void*)&pc, (void*)&Lc, (void*)&sc};
-      (void)hipModuleLaunchKernel(ffirst, fgrid, 1, 1, 1024, 1, 1, 0, st, args, nullptr);
+      (void)hipModuleLaunchKernel(ffirst, fgrid, 1, 1, kFirstRowsBlock, 1, 1, 0, st, args, nullptr);
     } else {
-      BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_first_rows<NC>), dim3(fgrid), dim3(1024), 0, st, p, L, s));
+      BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_part_first_rows<NC>), dim3(fgrid), dim3(kFirstRowsBlock), 0, st, p, L, s));
     }
     return;
   }

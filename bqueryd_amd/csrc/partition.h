@@ -221,6 +221,12 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
 // issuing a memory-side atomic per row.  On random keys the marked tiles are mostly a prefix
 // (each slot's first appearance falls early: ~10-15 % of the tiles at C3's 1 M groups); on
 // sorted keys every tile is marked.
+// Work unit: one 4096-row quarter of a tile (kFirstRowsBlock threads x 16 rows, every load of
+// the unit issued before the first is used); the grid strides over the units of the table, and
+// units of unmarked tiles return at once, so the few hundred marked tiles of a random-key query
+// spread over every CU instead of queueing behind one large workgroup each.
+constexpr int kFirstRowsBlock = 256;
+constexpr int kFirstRowsUnit = kFirstRowsBlock * 16;
 template <int NC>
 __device__ __forceinline__ void part_first_rows_body(const ScanParams& p, const PartLaunch& L, const SlotArrays& sa) {
   // only the key, term and mask columns are read (the others re-read one line per wave)
@@ -228,21 +234,21 @@ __device__ __forceinline__ void part_first_rows_body(const ScanParams& p, const 
   for (int k = 0; k < p.nkeys; ++k) need |= 1u << p.keys[k].col;
   for (int i = 0; i < p.nterms; ++i) need |= 1u << p.terms[i].col;
   const int64_t TR = L.tile_rows;
-  for (int64_t t = blockIdx.x; t < L.ntiles; t += gridDim.x) {
+  const int64_t per_tile = (TR + kFirstRowsUnit - 1) / kFirstRowsUnit;
+  const int64_t units = L.ntiles * per_tile;
+  for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const int64_t t = u / per_tile;
     if (!L.tile_mark[t]) continue;
     const unsigned char tag = (unsigned char)t;
-    const int64_t base = t * TR;
-    const int64_t end = min(p.nrows, base + TR);
-    // a tile is at most 4 x 1024 4-row chunks, taken two at a time: both loads in flight
-    // before either is used
-    for (int k0 = 0; (int64_t)k0 * 1024 * kRowsPerThread < TR; k0 += 2) {
-    Chunk raw[2][NC];
+    const int64_t base = t * TR + (u - t * per_tile) * kFirstRowsUnit;
+    const int64_t end = min(min(p.nrows, (t + 1) * TR), base + kFirstRowsUnit);
+    Chunk raw[4][NC];
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
-      load_rows4_clamped<NC>(p, base + ((int64_t)threadIdx.x + (k0 + k) * 1024) * kRowsPerThread, end, raw[k], need, base);
+    for (int k = 0; k < 4; ++k)
+      load_rows4_clamped<NC>(p, base + ((int64_t)threadIdx.x + k * kFirstRowsBlock) * kRowsPerThread, end, raw[k], need, base);
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int64_t row0 = base + ((int64_t)threadIdx.x + (k0 + k) * 1024) * kRowsPerThread;
+    for (int k = 0; k < 4; ++k) {
+      const int64_t row0 = base + ((int64_t)threadIdx.x + k * kFirstRowsBlock) * kRowsPerThread;
       if (row0 >= end) continue;
       uint64_t v[NC][4], code[4];
       decode_all<NC, 4>(p, raw[k], v);
@@ -253,7 +259,6 @@ __device__ __forceinline__ void part_first_rows_body(const ScanParams& p, const 
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (((pass >> r) & 1u) && L.first_tag[code[r]] == tag) atomicMin(&sa.fst[code[r]], (uint32_t)(row0 + r));
-    }
     }
   }
 }
