@@ -29,7 +29,7 @@ sys.path.insert(0, HERE)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 MODES = ['private-lds', 'shared-lds', 'global-dense', 'global-hash', 'partitioned', 'fused-distinct']
 KERNELS = ['k_scan_private', 'k_scan_shared', 'k_scan_global', 'k_scan_global<hash>',
-           'bq_jit_part_scatter+k_part_aggregate (tile scatter and aggregate, timed together)',
+           'bq_jit_part_scatter+k_part_aggregate+k_part_combine+bq_jit_part_first_rows (tile scatter, aggregate, split combine and first-row pass, timed together)',
            'k_scd_fused (rows + count_distinct + sorted_count_distinct in one pass)']
 
 
