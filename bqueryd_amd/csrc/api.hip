@@ -1132,14 +1132,6 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
           if (span16 > 0xFFFFull) L.pack = 0;
         }
       }
-      auto bit_width = [](uint64_t v) {
-        int b = 0;
-        while (v) {
-          ++b;
-          v >>= 1;
-        }
-        return b;
-      };
       auto shape = [&]() {
         const bool nw = L.narrow != 0, pk = L.pack != 0;
         // scatter workgroup: the widest whose staged tile fits in LDS (option part_threads caps it)
@@ -1172,20 +1164,11 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, (c->cu * fit + L.nparts / 2) / L.nparts));
         if (c->opt[kOptPartSplits]) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, c->opt[kOptPartSplits]));
         if (pk) {
-          // the packed accumulator of one split: count < 2^cbits, code16 sum < 2^(64 - cbits);
-          // more splits (fewer rows each) until both fields fit, else the 8-byte entries
-          for (;;) {
-            const uint64_t R = (uint64_t)((L.ntiles + L.splits - 1) / L.splits) * (uint64_t)tr;
-            const int cbits = bit_width(R);
-            L.sbits = 64 - cbits;
-            const bool fits = span16 == 0 || (R <= (~0ull) / span16 && bit_width(R * span16) <= L.sbits);
-            if (fits) break;
-            if (L.splits >= L.ntiles) {
-              L.pack = 0;
-              return false;
-            }
-            L.splits = (int)std::min<int64_t>(L.ntiles, 2 * (int64_t)L.splits);
-          }
+          // the packed accumulator: count << 40 | code16 sum, flushed every 2^23 entries (a
+          // count below 2^24, a sum below 2^23 x 65535 < 2^40) -- fixed widths, so the packing
+          // does not constrain the splits
+          L.sbits = 40;
+          L.pack_flush = 1ll << 23;
         }
         return true;
       };
@@ -1199,8 +1182,10 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       // (| pack: first tile tags, tile marks)
       const size_t vbytes = pk ? 0 : ((size_t)L.capacity * (nw ? 4 : 8) * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
       const size_t mbytes = ((size_t)L.capacity * 4 + 255) & ~size_t(255);
-      L.partial_bytes = (part_agg_lds(L.wbits, nsum, pk) + 255) & ~size_t(255);
-      const size_t pbytes = L.splits > 1 ? (size_t)L.nparts * L.splits * L.partial_bytes : 0;
+      // split records: [W] counts, [W] sums ([W] first rows / tiles); packed entries always
+      // have one (an aggregate that flushes its accumulators adds into it)
+      L.partial_bytes = ((pk ? ((size_t)1 << L.wbits) * 20 : part_agg_lds(L.wbits, nsum, pk)) + 255) & ~size_t(255);
+      const size_t pbytes = (L.splits > 1 || pk) ? (size_t)L.nparts * L.splits * L.partial_bytes : 0;
       const size_t tbytes = pk ? (((size_t)L.nparts << L.wbits) + 255) & ~size_t(255) : 0;
       unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + mbytes + pbytes + tbytes +
                                                            (pk ? (size_t)L.ntiles : 0) + 512);

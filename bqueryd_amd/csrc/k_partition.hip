@@ -45,11 +45,12 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartL
 // PACK entries (PartLaunch::pack): one 32-bit word {code16, slot_low}; the slot table is one
 // packed 64-bit accumulator (count << sbits | code16 sum: ONE LDS atomic per entry) and the
 // slot's first tile, and the combine leaves first rows to k_part_first_rows.
-// One split's record of a slot: count, first row (PACK: first tile), sums (PACK: a[0] is the
-// packed count << sbits | code16 sum).
+// One split's record of a slot: count, first row (PACK: first tile), sums (PACK: 64-bit count
+// c64 and the code16 sum a[0]).
 template <int NV>
 struct PartRec {
   unsigned long long a[NV];
+  unsigned long long c64;  // PACK: count
   uint32_t c, f;
 };
 
@@ -61,16 +62,15 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
   constexpr int NV = NSUM > 0 ? NSUM : 1;
   constexpr int nsum = NSUM;
   if (PACK) {
-    // unpack every split's accumulator before adding (the packed fields of a sum over splits
-    // could carry into each other); exact code sum = sum of code16 + count x enc_base16
-    const unsigned long long smask = (1ull << L.sbits) - 1ull;
+    // split records hold the unpacked count (c64) and code16 sum (a[0]); exact code sum =
+    // sum of code16 + count x enc_base16
     unsigned long long c = 0, cs = 0;
     uint32_t f = kNoRow;
     for (int o = 0; o < S; ++o) {
       PartRec<NV> r;
       rec(o, r);
-      c += r.a[0] >> L.sbits;
-      cs += r.a[0] & smask;
+      c += r.c64;
+      cs += r.a[0];
       f = r.f < f ? r.f : f;
     }
     sa.cnt[gs] = c;
@@ -156,8 +156,35 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     uint32_t m[U], t[U];
     unsigned long long v[U][NV];
   };
-  for (int64_t w0 = t_lo; w0 < t_hi; w0 += kAggWin) {
-    const int nw = (int)min((int64_t)kAggWin, t_hi - w0);
+  // PACK: the packed accumulator's fields hold L.pack_flush entries (count < 2^(64 - sbits),
+  // code16 sum < 2^sbits); a window holds at most that many entries, and before a window that
+  // would pass it the accumulators are flushed (unpacked, added) into the workgroup's own
+  // split record -- never at C3's ~400 K entries per workgroup, only for partitions with many
+  // millions of rows in one split (skewed keys)
+  unsigned long long* rec_cnt = nullptr;
+  unsigned long long* rec_sum = nullptr;
+  uint32_t* rec_fst = nullptr;
+  if (PACK) {
+    rec_cnt = reinterpret_cast<unsigned long long*>(L.partial + ((size_t)part * L.splits + split) * L.partial_bytes);
+    rec_sum = rec_cnt + W;
+    rec_fst = reinterpret_cast<uint32_t*>(rec_sum + W);
+  }
+  const unsigned long long smask = PACK ? (1ull << L.sbits) - 1ull : 0ull;
+  bool flushed = false;
+  uint64_t since = 0;
+  auto flush = [&]() {
+    for (int sl = tid; sl < W; sl += blockDim.x) {
+      const unsigned long long a = acc[sl];
+      const unsigned long long c = a >> L.sbits, sm = a & smask;
+      rec_cnt[sl] = flushed ? rec_cnt[sl] + c : c;
+      rec_sum[sl] = flushed ? rec_sum[sl] + sm : sm;
+      acc[sl] = 0ull;
+    }
+    flushed = true;
+    lds_barrier();
+  };
+  for (int64_t w0 = t_lo; w0 < t_hi;) {
+    int nw = (int)min((int64_t)kAggWin, t_hi - w0);
     // headers of the window's tiles (two per thread, contiguous for the scan)
     uint32_t len[2], beg[2];
 #pragma unroll
@@ -181,11 +208,31 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
         wB[j] = (uint32_t)(w0 + j) * TR + beg[k] - fj;
       }
     }
+    lds_barrier();
+    if (PACK && tot > L.pack_flush) {
+      // cut the window at the last tile boundary within pack_flush entries (one tile holds at
+      // most tile_rows <= pack_flush entries)
+      int lo = 1, hi = nw;  // largest j with F[j] <= pack_flush
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (wF[mid] <= L.pack_flush) lo = mid; else hi = mid;
+      }
+      tot = wF[lo];
+      nw = lo;
+      lds_barrier();
+    }
     for (int j = nw + tid; j <= nw + kAggK; j += blockDim.x) {
       wF[j] = tot;
       wB[j] = 0u;
     }
     lds_barrier();
+    if (PACK) {
+      if (since + tot > L.pack_flush) {
+        flush();
+        since = 0;
+      }
+      since += tot;
+    }
     // the wave's equal share of the window's entries, and the tile of its first entry
     const uint32_t e_lo = (uint32_t)((uint64_t)tot * wave / NW), e_hi = (uint32_t)((uint64_t)tot * (wave + 1) / NW);
     int jlo = 0, jhi = nw;  // largest j < nw with F[j] <= e_lo
@@ -277,6 +324,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       }
     }
     lds_barrier();  // every wave is done with this window's bounds
+    w0 += nw;
   }
   __syncthreads();
   // Split tables: with several splits per partition every workgroup stores its table to its own
@@ -286,16 +334,33 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   // release / acquire -- cost ~130 us at C3: every workgroup's release writes back its XCD's L2.)
   const uint64_t slot0 = (uint64_t)part << L.wbits;
   const int nvalid = (int)((uint64_t)W < p.nslots - slot0 ? (uint64_t)W : p.nslots - slot0);
+  if (PACK) {
+    // the workgroup's totals (flushed + LDS), unpacked: [W] counts, [W] code16 sums, [W] first
+    // tiles; one split finishes its slots itself
+    for (int s = tid; s < nvalid; s += blockDim.x) {
+      const unsigned long long a = acc[s];
+      unsigned long long c = a >> L.sbits, sm = a & smask;
+      if (flushed) {
+        c += rec_cnt[s];
+        sm += rec_sum[s];
+      }
+      if (L.splits > 1) {
+        rec_cnt[s] = c;
+        rec_sum[s] = sm;
+        rec_fst[s] = fst[s];
+      } else {
+        PartRec<NV> r;
+        r.c64 = c;
+        r.a[0] = sm;
+        r.f = fst[s];
+        part_finish_slot<NSUM, NARROW, PACK>(p, L, sa, slot0 + s, 1, [&](int, PartRec<NV>& o) { o = r; });
+      }
+    }
+    return;
+  }
   if (L.splits > 1) {
     unsigned char* rec = L.partial + ((size_t)part * L.splits + split) * L.partial_bytes;
-    if (PACK) {  // [W] packed accumulators, then [W] first tiles
-      unsigned long long* pa = reinterpret_cast<unsigned long long*>(rec);
-      uint32_t* pf = reinterpret_cast<uint32_t*>(pa + W);
-      for (int s = tid; s < nvalid; s += blockDim.x) {
-        pa[s] = acc[s];
-        pf[s] = fst[s];
-      }
-    } else {  // [W] counts, [W] first rows, then [nsum][W] sums
+    {  // [W] counts, [W] first rows, then [nsum][W] sums
       uint32_t* pc = reinterpret_cast<uint32_t*>(rec);
       uint32_t* pf = pc + W;
       unsigned long long* pa = reinterpret_cast<unsigned long long*>(pf + W);
@@ -329,10 +394,10 @@ __global__ __launch_bounds__(256) void k_part_combine(ScanParams p, PartLaunch L
     part_finish_slot<NSUM, NARROW, PACK>(p, L, sa, gs, S, [&](int o, PartRec<NV>& r) {
       const unsigned char* rec = L.partial + ((size_t)part * S + o) * L.partial_bytes;
       if (PACK) {
-        const unsigned long long* pa = reinterpret_cast<const unsigned long long*>(rec);
-        r.a[0] = pa[s];
-        r.f = reinterpret_cast<const uint32_t*>(pa + W)[s];
-        r.c = 0;
+        const unsigned long long* pc = reinterpret_cast<const unsigned long long*>(rec);
+        r.c64 = pc[s];
+        r.a[0] = pc[W + s];
+        r.f = reinterpret_cast<const uint32_t*>(pc + 2 * W)[s];
       } else {
         const uint32_t* pc = reinterpret_cast<const uint32_t*>(rec);
         const unsigned long long* pa = reinterpret_cast<const unsigned long long*>(pc + 2 * W);

@@ -191,12 +191,14 @@ struct PartLaunch {
   // packed entries (at most one summed column, its narrow codes spanning at most 2^16 values):
   // one 32-bit word per entry, code16 = code - enc_base16 above the 16-bit slot_low; the
   // aggregate's per-slot accumulator is count << sbits | sum of code16 (one 64-bit LDS atomic
-  // per entry; the planner picks sbits and splits so neither field can overflow), and it
+  // per entry; flushed into the split record every pack_flush entries so neither field can
+  // overflow), and it
   // marks each slot's first TILE: tile_mark [ntiles] (1 = some slot's first tile, zeroed
   // before the aggregate) and first_tag [nslots] (its low 8 bits), then k_part_first_rows
   // re-reads only the marked tiles for the exact first rows
   int pack;
   int sbits;
+  int64_t pack_flush;  // entries between flushes of the packed accumulators
   int64_t enc_base16;
   unsigned char* tile_mark;
   unsigned char* first_tag;

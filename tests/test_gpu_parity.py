@@ -528,16 +528,17 @@ def test_fused_distinct_runs_loop(case, jit, oracle_c, engine_options):
 
 
 @pytest.mark.parametrize('kind', ['count_only', 'dyadic', 'cents_neg', 'int_span_65535', 'int_span_65536', 'sorted_keys',
-                                  'filtered', 'one_split', 'jit'])
+                                  'filtered', 'one_split', 'jit', 'flush'])
 def test_partitioned_packed_entries(kind, oracle_c, engine_options):
     """Packed 4-byte partition entries {16-bit value code, slot}: no summed column, or one whose
     narrow codes span at most 2^16 values.  First appearance comes from each slot's first tile
     plus a re-read of the marked tiles (k_part_first_rows): group order, keys and counts
     bit-exact against the oracle, sums bit-exact on dyadic data and identical to the 8-byte
     entry path (part_pack=0); a span of 2^16 codes keeps the 8-byte entries; one aggregate
-    split over every tile (the packed count / sum fields sized for all rows)."""
+    split over every tile; 'flush': one split whose partition takes ~10.8 M entries, past the
+    2^23 entries after which the aggregate flushes its packed accumulators into its record."""
     rng = np.random.default_rng(abs(hash(kind)) % 1000)
-    n = 400_003
+    n = 400_003 if kind != 'flush' else 12_000_003
     cols = OrderedDict(k=rng.integers(0, 300_000, n).astype(np.int32),
                        v=np.round(rng.normal(size=n) * 300) / 64)
     aggs = [['v', 'sum', 'vs'], ['v', 'count', 'n']]
@@ -565,6 +566,10 @@ def test_partitioned_packed_entries(kind, oracle_c, engine_options):
         cols['v'] = rng.integers(0, 60_000, n).astype(np.int64)
     elif kind == 'jit':
         engine_options(jit_min_rows=0)
+    elif kind == 'flush':
+        engine_options(part_splits=1)
+        hot = rng.random(n) < 0.9
+        cols['k'][hot] = 7
     t = ShardTable(cols)
     try:
         got, _ = t.groupby(['k'], aggs, where_terms=terms)
