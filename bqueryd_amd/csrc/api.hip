@@ -1639,6 +1639,7 @@ void run_groupby_grow(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result**
 
 int bqg_internal_device(bqg_ctx* c) { return c->device; }
 hipStream_t bqg_internal_stream(bqg_ctx* c) { return c->stream; }
+bool bqg_internal_timing(bqg_ctx* c) { return c->timing; }
 void bqg_internal_set_error(bqg_ctx* c, const std::string& msg) {
   if (c) c->err = msg;
   g_err = msg;

@@ -593,6 +593,7 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       bqg::launch_merge_pack(m, l.stream);
       HIPCK(hipGetLastError());
     }
+    if (bqg_internal_timing(l.ctx)) HIPCK(hipStreamSynchronize(l.stream));
     l.st->phase_ms[0] += now_ms() - t0;
   }
   // 3a. count matrix: every rank's row counts per destination
