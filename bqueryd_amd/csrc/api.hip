@@ -462,7 +462,10 @@ void compute_stats_many(bqg_table* t, const std::vector<int>& cols) {
       todo.push_back(col);
   if (todo.empty()) return;
   const size_t n = todo.size();
-  unsigned long long* d = (unsigned long long*)c->misc.ensure(n * 8 * sizeof(unsigned long long));
+  // results [n][8] words, then one column's per-block partials at a time (the launches of
+  // one stream run in order)
+  unsigned long long* d = (unsigned long long*)c->misc.ensure((n * 8 + (size_t)kStatsMaxBlocks * 5) *
+                                                              sizeof(unsigned long long));
   unsigned long long* h = (unsigned long long*)c->hhdr.ensure(2 * n * 8 * sizeof(unsigned long long));
   static const unsigned long long init[8] = {~0ull, 0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
   for (size_t i = 0; i < n; ++i) memcpy(h + 8 * i, init, sizeof(init));
@@ -471,7 +474,7 @@ void compute_stats_many(bqg_table* t, const std::vector<int>& cols) {
     Column& k = t->cols[todo[i]];
     k.stats.runs = -1;  // measured again on demand (column_runs)
     DevCol dc{k.dev, k.dtype, dtype_lg(k.dtype)};
-    if (t->nrows > 0) launch_stats(dc, t->nrows, d + 8 * i, c->stream);
+    if (t->nrows > 0) launch_stats(dc, t->nrows, d + 8 * i, d + 8 * n, c->stream);
   }
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipMemcpyAsync(h + 8 * n, d, n * sizeof(init), hipMemcpyDeviceToHost, c->stream));

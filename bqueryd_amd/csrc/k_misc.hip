@@ -337,7 +337,7 @@ __device__ __forceinline__ unsigned long long ord_key_f(double d) {
 // every value is an integer multiple of 2^(out[3] - 4096); out[4]: bit 0 -- some value is
 // subnormal or infinite (no dyadic code), bit 1 -- some value is not a whole number of
 // hundredths (rint(v * 100) / 100 != v: no cents code).
-__global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsigned long long* out) {
+__global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsigned long long* partial) {
   unsigned long long mn = ~0ull, mx = 0ull, nan = 0ull, lsb = ~0ull, enc = 0ull;
   const bool isf = dtype_is_float(c.dtype);
   const bool u64 = c.dtype == BQG_U64;
@@ -400,13 +400,58 @@ __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsig
       lsb = min(lsb, slsb[q]);
       enc |= senc[q];
     }
-    atomicMin(&out[0], mn);
-    atomicMax(&out[1], mx);
-    if (nan) atomicOr(&out[2], 1ull);
-    if (isf) {
-      atomicMin(&out[3], lsb);
-      if (enc) atomicOr(&out[4], enc);
+    // the block's partial (k_stats_final reduces them: ~1000 blocks' same-address device
+    // atomics on five words serialised at the memory side, 25 us and more per column)
+    unsigned long long* o = partial + (size_t)blockIdx.x * 5;
+    o[0] = mn;
+    o[1] = mx;
+    o[2] = nan;
+    o[3] = lsb;
+    o[4] = enc;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_stats_final(const unsigned long long* partial, int blocks,
+                                                        unsigned long long* out) {
+  unsigned long long mn = ~0ull, mx = 0ull, nan = 0ull, lsb = ~0ull, enc = 0ull;
+  for (int b = threadIdx.x; b < blocks; b += kBlock) {
+    const unsigned long long* o = partial + (size_t)b * 5;
+    mn = min(mn, o[0]);
+    mx = max(mx, o[1]);
+    nan |= o[2];
+    lsb = min(lsb, o[3]);
+    enc |= o[4];
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    mn = min(mn, (unsigned long long)__shfl_xor(mn, o, 64));
+    mx = max(mx, (unsigned long long)__shfl_xor(mx, o, 64));
+    nan |= (unsigned long long)__shfl_xor(nan, o, 64);
+    lsb = min(lsb, (unsigned long long)__shfl_xor(lsb, o, 64));
+    enc |= (unsigned long long)__shfl_xor(enc, o, 64);
+  }
+  __shared__ unsigned long long s[5][kBlock / 64];
+  if ((threadIdx.x & 63) == 0) {
+    s[0][threadIdx.x >> 6] = mn;
+    s[1][threadIdx.x >> 6] = mx;
+    s[2][threadIdx.x >> 6] = nan;
+    s[3][threadIdx.x >> 6] = lsb;
+    s[4][threadIdx.x >> 6] = enc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < kBlock / 64; ++q) {
+      mn = min(mn, s[0][q]);
+      mx = max(mx, s[1][q]);
+      nan |= s[2][q];
+      lsb = min(lsb, s[3][q]);
+      enc |= s[4][q];
     }
+    out[0] = min(out[0], mn);
+    out[1] = max(out[1], mx);
+    out[2] |= nan ? 1ull : 0ull;
+    out[3] = min(out[3], lsb);
+    out[4] |= enc;
   }
 }
 
@@ -835,11 +880,13 @@ void launch_runs(const DevCol& c, int64_t nrows, unsigned long long* out, hipStr
   if (nrows > 0) hipLaunchKernelGGL(k_runs, dim3((unsigned)blocks), dim3(kBlock), 0, st, c, nrows, out);
 }
 
-void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, hipStream_t st) {  // out4: 5 words
+void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, unsigned long long* scratch,
+                  hipStream_t st) {  // out4: 5 words; scratch: kStatsMaxBlocks x 5 words
   int64_t blocks = (nrows + kTileRows - 1) / kTileRows;
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > kStatsMaxBlocks) blocks = kStatsMaxBlocks;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_stats, dim3((unsigned)blocks), dim3(kBlock), 0, st, c, nrows, out4);
+  hipLaunchKernelGGL(k_stats, dim3((unsigned)blocks), dim3(kBlock), 0, st, c, nrows, scratch);
+  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(kBlock), 0, st, scratch, (int)blocks, out4);
 }
 void launch_where(const ScanParams& p, unsigned char* out_mask, unsigned long long* npass, int blocks, hipStream_t st) {
   BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_where<NC>), dim3(blocks), dim3(kBlock), 0, st, p, out_mask, npass));
