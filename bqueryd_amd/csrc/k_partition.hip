@@ -146,21 +146,31 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   const uint32_t lowmask = (uint32_t)W - 1u;
   const uint32_t TR = (uint32_t)L.tile_rows;
   constexpr int NV = NSUM > 0 ? NSUM : 1;
-  // the window's tiles: flattened segment start F[j] and entry-index base B[j] (entry index =
-  // B[j] + flattened position), K + 1 sentinels past the last tile
+  // Entries are read in 16-byte granules (4 entries, a lane's one load; a segment's edge
+  // granules also hold neighbouring partitions' entries, masked off by their index in the tile):
+  // 4-byte loads kept too few bytes in flight -- a loads-only probe of the 4-byte version took
+  // 0.178 of the aggregate's 0.195 ms.  The window's tiles, in LDS: flattened granule start
+  // F[j], global granule base B[j] (granule = B[j] + flattened position), E[j] (entry index in
+  // the tile of a flattened granule's first entry = E[j] + 4 x position) and the segment's
+  // entry range AB[j] = a | b << 16; K + 1 sentinels past the last tile.
   uint32_t* wF = reinterpret_cast<uint32_t*>(smem + part_agg_lds(L.wbits, nsum, PACK));
   uint32_t* wB = wF + kAggWin + kAggK + 1;
-  // one chunk of at most U x 64 consecutive entries of a wave's range, spanning at most K
-  // tiles; an entry's tile (global index) or kNoRow past the chunk
+  uint32_t* wE = wB + kAggWin + kAggK + 1;
+  uint32_t* wAB = wE + kAggWin + kAggK + 1;
+  const uint32_t TG = TR >> 2;  // granules per tile
+  // one chunk of at most U x 64 consecutive granules of a wave's range, spanning at most K
+  // tiles: per granule its 4 entries, its tile (global index; kNoRow past the chunk), the tile
+  // index of its first entry and the segment's entry range
   struct Ent {
-    uint32_t m[U], t[U];
-    unsigned long long v[U][NV];
+    uint4 m[U];
+    uint32_t t[U], e0[U], ab[U];
+    unsigned long long v[U][4][NV];
   };
   // PACK: the packed accumulator's fields hold L.pack_flush entries (count < 2^(64 - sbits),
-  // code16 sum < 2^sbits); a window holds at most that many entries, and before a window that
-  // would pass it the accumulators are flushed (unpacked, added) into the workgroup's own
-  // split record -- never at C3's ~400 K entries per workgroup, only for partitions with many
-  // millions of rows in one split (skewed keys)
+  // code16 sum < 2^sbits); a window holds at most that many entries (4 per granule), and before
+  // a window that would pass it the accumulators are flushed (unpacked, added) into the
+  // workgroup's own split record -- never at C3's ~400 K entries per workgroup, only for
+  // partitions with many millions of rows in one split (skewed keys)
   unsigned long long* rec_cnt = nullptr;
   unsigned long long* rec_sum = nullptr;
   uint32_t* rec_fst = nullptr;
@@ -183,39 +193,44 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     flushed = true;
     lds_barrier();
   };
+  const uint32_t gflush = (uint32_t)(L.pack_flush >> 2);  // granules between flushes
   for (int64_t w0 = t_lo; w0 < t_hi;) {
     int nw = (int)min((int64_t)kAggWin, t_hi - w0);
     // headers of the window's tiles (two per thread, contiguous for the scan)
-    uint32_t len[2], beg[2];
+    uint32_t glen[2], ga[2], ab[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int j = 2 * tid + k;
-      beg[k] = len[k] = 0;
+      glen[k] = ga[k] = ab[k] = 0;
       if (j < nw) {
         const uint16_t* th = L.hdr + (size_t)(w0 + j) * (size_t)(P + 1) + part;
-        beg[k] = th[0];
-        len[k] = (uint32_t)th[1] - beg[k];
+        const uint32_t a = th[0], b = th[1];
+        ga[k] = a >> 2;
+        glen[k] = b > a ? ((b + 3u) >> 2) - ga[k] : 0u;
+        ab[k] = a | (b << 16);
       }
     }
     uint32_t tot;
-    const uint32_t ex0 = block_excl_scan_1024(len[0] + len[1], &tot);
+    const uint32_t ex0 = block_excl_scan_1024(glen[0] + glen[1], &tot);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int j = 2 * tid + k;
-      const uint32_t fj = ex0 + (k ? len[0] : 0u);
+      const uint32_t fj = ex0 + (k ? glen[0] : 0u);
       if (j < nw) {
         wF[j] = fj;
-        wB[j] = (uint32_t)(w0 + j) * TR + beg[k] - fj;
+        wB[j] = (uint32_t)(w0 + j) * TG + ga[k] - fj;
+        wE[j] = 4u * ga[k] - 4u * fj;
+        wAB[j] = ab[k];
       }
     }
     lds_barrier();
-    if (PACK && tot > L.pack_flush) {
+    if (PACK && tot > gflush) {
       // cut the window at the last tile boundary within pack_flush entries (one tile holds at
-      // most tile_rows <= pack_flush entries)
-      int lo = 1, hi = nw;  // largest j with F[j] <= pack_flush
+      // most tile_rows / 4 + 1 granules, and tile_rows + 4 <= pack_flush)
+      int lo = 1, hi = nw;  // largest j with F[j] <= gflush
       while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
-        if (wF[mid] <= L.pack_flush) lo = mid; else hi = mid;
+        if (wF[mid] <= gflush) lo = mid; else hi = mid;
       }
       tot = wF[lo];
       nw = lo;
@@ -224,16 +239,18 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     for (int j = nw + tid; j <= nw + kAggK; j += blockDim.x) {
       wF[j] = tot;
       wB[j] = 0u;
+      wE[j] = 0u;
+      wAB[j] = 0u;
     }
     lds_barrier();
     if (PACK) {
-      if (since + tot > L.pack_flush) {
+      if (since + tot > gflush) {
         flush();
         since = 0;
       }
       since += tot;
     }
-    // the wave's equal share of the window's entries, and the tile of its first entry
+    // the wave's equal share of the window's granules, and the tile of its first granule
     const uint32_t e_lo = (uint32_t)((uint64_t)tot * wave / NW), e_hi = (uint32_t)((uint64_t)tot * (wave + 1) / NW);
     int jlo = 0, jhi = nw;  // largest j < nw with F[j] <= e_lo
     while (jhi - jlo > 1) {
@@ -243,38 +260,55 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     uint32_t f_next = e_lo;
     int j_next = __builtin_amdgcn_readfirstlane(jlo);
     // issue the next chunk into `en`: lanes 0..K read the chunk's tile bounds, the chunk ends
-    // at U x 64 entries, the wave's range end or the K-th tile boundary
+    // at U x 64 granules, the wave's range end or the K-th tile boundary
     auto issue = [&](Ent& en) {
-      const uint32_t lf = wF[j_next + min(lane, kAggK)], lb = wB[j_next + min(lane, kAggK - 1)];
-      uint32_t Fk[kAggK + 1], Bk[kAggK];
+      const int jl = j_next + min(lane, kAggK);
+      const uint32_t lf = wF[jl], lb = wB[jl], le = wE[jl], lab = wAB[jl];
+      uint32_t Fk[kAggK + 1], Bk[kAggK], Ek[kAggK], ABk[kAggK];
 #pragma unroll
       for (int k = 0; k <= kAggK; ++k) Fk[k] = (uint32_t)__builtin_amdgcn_readlane((int)lf, k);
 #pragma unroll
-      for (int k = 0; k < kAggK; ++k) Bk[k] = (uint32_t)__builtin_amdgcn_readlane((int)lb, k);
+      for (int k = 0; k < kAggK; ++k) {
+        Bk[k] = (uint32_t)__builtin_amdgcn_readlane((int)lb, k);
+        Ek[k] = (uint32_t)__builtin_amdgcn_readlane((int)le, k);
+        ABk[k] = (uint32_t)__builtin_amdgcn_readlane((int)lab, k);
+      }
       const uint32_t fe = min(min(f_next + 64u * U, e_hi), max(Fk[kAggK], f_next));
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t f = f_next + u * 64u + lane;
         const bool valid = f < fe;
         const uint32_t fc = valid ? f : f_next;
-        uint32_t j = 0, base = Bk[0];
+        uint32_t j = 0, base = Bk[0], eb = Ek[0], abk = ABk[0];
 #pragma unroll
         for (int k = 1; k < kAggK; ++k) {
           const bool ge = fc >= Fk[k];
           j = ge ? (uint32_t)k : j;
           base = ge ? Bk[k] : base;
+          eb = ge ? Ek[k] : eb;
+          abk = ge ? ABk[k] : abk;
         }
-        const uint32_t idx = f_next < fe ? base + fc : 0u;
+        const uint32_t gidx = f_next < fe ? base + fc : 0u;
         en.t[u] = valid ? (uint32_t)w0 + (uint32_t)j_next + j : kNoRow;
-        en.m[u] = L.meta[idx];
+        en.e0[u] = eb + 4u * fc;
+        en.ab[u] = abk;
+        en.m[u] = reinterpret_cast<const uint4*>(L.meta)[gidx];
         if (PACK) continue;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
-          if (NARROW) {  // the exact 32-bit code: float codes signed, integer offsets unsigned
-            const uint32_t code = reinterpret_cast<const uint32_t*>(L.vals)[(size_t)q * L.capacity + idx];
-            en.v[u][q] = L.enc_kind[q] == 3 ? (unsigned long long)code : (unsigned long long)(long long)(int32_t)code;
+          if (NARROW) {  // the exact 32-bit codes: float codes signed, integer offsets unsigned
+            const uint4 c4 = reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(L.vals) + (size_t)q * L.capacity)[gidx];
+            const uint32_t cc[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              en.v[u][e][q] = L.enc_kind[q] == 3 ? (unsigned long long)cc[e] : (unsigned long long)(long long)(int32_t)cc[e];
           } else {
-            en.v[u][q] = L.vals[(size_t)q * L.capacity + idx];
+            const uint4* vp = reinterpret_cast<const uint4*>(L.vals + (size_t)q * L.capacity) + 2 * (size_t)gidx;
+            const uint4 v0 = vp[0], v1 = vp[1];
+            en.v[u][0][q] = ((unsigned long long)v0.y << 32) | v0.x;
+            en.v[u][1][q] = ((unsigned long long)v0.w << 32) | v0.z;
+            en.v[u][2][q] = ((unsigned long long)v1.y << 32) | v1.x;
+            en.v[u][3][q] = ((unsigned long long)v1.w << 32) | v1.z;
           }
         }
       }
@@ -289,20 +323,27 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (en.t[u] == kNoRow) continue;
-        const uint32_t sl = en.m[u] & lowmask;
-        if (PACK) {
-          // fire-and-forget LDS atomics: nothing in the loop waits on the LDS
-          atomicAdd(&acc[sl], inc + (unsigned long long)(en.m[u] >> 16));
-          atomicMin(&fst[sl], en.t[u]);
-          continue;
-        }
-        const uint32_t row = en.t[u] * TR + (en.m[u] >> L.wbits);
-        atomicAdd(&cnt[sl], 1u);
-        atomicMin(&fst[sl], row);
+        const uint32_t a = en.ab[u] & 0xFFFFu, b = en.ab[u] >> 16;
+        const uint32_t mm[4] = {en.m[u].x, en.m[u].y, en.m[u].z, en.m[u].w};
 #pragma unroll
-        for (int q = 0; q < nsum; ++q) {
-          if (!NARROW && p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][q], p.sum_conv[q]));
-          else atomicAdd(&acc[(size_t)q * W + sl], en.v[u][q]);
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t ei = en.e0[u] + (uint32_t)e;  // entry index in the tile
+          if (ei < a || ei >= b) continue;            // a neighbouring partition's entry
+          const uint32_t sl = mm[e] & lowmask;
+          if (PACK) {
+            // fire-and-forget LDS atomics: nothing in the loop waits on the LDS
+            atomicAdd(&acc[sl], inc + (unsigned long long)(mm[e] >> 16));
+            atomicMin(&fst[sl], en.t[u]);
+            continue;
+          }
+          const uint32_t row = en.t[u] * TR + (mm[e] >> L.wbits);
+          atomicAdd(&cnt[sl], 1u);
+          atomicMin(&fst[sl], row);
+#pragma unroll
+          for (int q = 0; q < nsum; ++q) {
+            if (!NARROW && p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][e][q], p.sum_conv[q]));
+            else atomicAdd(&acc[(size_t)q * W + sl], en.v[u][e][q]);
+          }
         }
       }
     };
@@ -483,7 +524,7 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
   const unsigned cgrid = (unsigned)std::min<uint64_t>((p.nslots + 255) / 256, 4096);
   if (L.pack) {
     (void)hipMemsetAsync(L.tile_mark, 0, (size_t)L.ntiles, st);
-#define BQG_AGGP(NS) hipLaunchKernelGGL((k_part_aggregate<8, 2, NS, true, true>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
+#define BQG_AGGP(NS) hipLaunchKernelGGL((k_part_aggregate<2, 2, NS, true, true>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
     if (p.nsum == 0) BQG_AGGP(0); else BQG_AGGP(1);
 #undef BQG_AGGP
     if (L.splits > 1) {
@@ -511,11 +552,11 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
   } while (0)
 #define BQG_AGG(U, NS) do { if (L.narrow) BQG_AGG2(U, NS, true); else BQG_AGG2(U, NS, false); } while (0)
   switch (p.nsum) {
-    case 0: BQG_AGG2(8, 0, false); break;
-    case 1: BQG_AGG(8, 1); break;
-    case 2: BQG_AGG(4, 2); break;
-    case 3: BQG_AGG(4, 3); break;
-    default: BQG_AGG(2, 4); break;
+    case 0: BQG_AGG2(2, 0, false); break;
+    case 1: BQG_AGG(2, 1); break;
+    case 2: BQG_AGG(1, 2); break;
+    case 3: BQG_AGG(1, 3); break;
+    default: BQG_AGG(1, 4); break;
   }
 #undef BQG_AGG
 #undef BQG_AGG2

@@ -218,12 +218,12 @@ inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1, boo
 __host__ __device__ inline size_t part_agg_lds(int wbits, int nsum, bool pack) {
   return ((size_t)1 << wbits) * (pack ? 12 : 8 + 8 * (size_t)nsum);
 }
-// the aggregate walks its split's tiles in windows of kAggWin tiles (their flattened segment
-// starts and entry bases in LDS); a chunk of entries spans at most kAggK tiles
-constexpr int kAggWin = 2048;
+// the aggregate walks its split's tiles in windows of kAggWin tiles (four words of bounds per
+// tile in LDS); a chunk of entry granules spans at most kAggK tiles
+constexpr int kAggWin = 1024;
 constexpr int kAggK = 8;
 inline size_t part_agg_lds_launch(int wbits, int nsum, bool pack) {
-  return part_agg_lds(wbits, nsum, pack) + 2 * (size_t)(kAggWin + kAggK + 1) * 4;
+  return part_agg_lds(wbits, nsum, pack) + 4 * (size_t)(kAggWin + kAggK + 1) * 4;
 }
 // fscatter: the query-specialised (JIT) scatter kernel, or nullptr for the precompiled one
 // ffirst: the query-specialised (JIT) first-row pass of packed entries, or nullptr

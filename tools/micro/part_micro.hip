@@ -534,7 +534,7 @@ int main(int argc, char** argv) {
     }
     same(ref, fetch(b), what);
   };
-  agg_run(k_part_aggregate<8, 2, 1, false, false>, "agg U8 (library; splits > 1 need k_part_combine)", 1);
+  agg_run(k_part_aggregate<2, 2, 1, false, false>, "agg U2 granules (library; splits > 1 need k_part_combine)", 1);
 
   agg_run(k_agg_probe<8, 4, 1, 1>, "probe: loads only (no LDS atomics)", 2);
   agg_run(k_agg_probe<8, 4, 1, 2>, "probe: LDS atomics only (no entry loads)", 2);
