@@ -181,9 +181,11 @@ def _c5_local_ranks(args):
     ``aggregate=True`` merge (bqg_merge_group over the in-process transport: the code RCCL
     runs, device copies as the wire).  ``value`` is the measured rate of the whole 1 B-row job
     on this one GPU (ranks run one after another); the line also projects the 8-GPU node from
-    the measured parts: each rank's shard pass (as it runs alone on a GPU) + the W-rank merge
-    (measured with all ranks sharing this GPU: an upper bound for the merge over xGMI), and
-    measures the one-GPU C5 step (one rank's 10 shards + the world-1 RCCL merge) for the
+    the measured parts: each rank's shard pass (as it runs alone on a GPU) + the W-rank merge's
+    critical path (every phase as long as its slowest rank, each rank's device work measured
+    on its own; the exchange is measured as one on-die copy of all ranks' messages, faster than
+    xGMI links, so the line also gives the exchange modelled from the bytes per link), and
+    measures the one-GPU C5 step (one rank's 10 shards + the world-1 merge) for the
     x-over-one-GPU ratio of north_star."""
     from concurrent.futures import ThreadPoolExecutor
 
@@ -228,7 +230,7 @@ def _c5_local_ranks(args):
         t1 = time.perf_counter()
         merged = bdist.merge_group_device(per, cfg['groupby'], cfg['aggs'], dtypes, group, reduced=True)
         merge_s.append(time.perf_counter() - t1)
-        phases.append([list(bdist.merge_phases(d).values()) for d in devs] + [[bdist.LAST_MERGE['to_host_ms']] * 6])
+        phases.append([list(bdist.merge_phases(d).values()) for d in devs])
         for tabs in per:
             for p in tabs:
                 p.close()
@@ -272,13 +274,19 @@ def _c5_local_ranks(args):
 
     rank_ms = [1e3 * float(np.mean(s)) for s in shard_s]
     merge_ms = 1e3 * float(np.mean(merge_s))
-    ph = np.mean(np.array(phases), axis=0)  # [rank][phase] ms; last row: the copy to host
-    host_copy_ms = float(ph[-1][0])
-    ph = ph[:-1]
+    ph = np.mean(np.array(phases), axis=0)  # [rank][phase] ms
     phase_max = {n: float(ph[:, i].max()) for i, n in enumerate(bdist.MERGE_PHASES)}
+    host_copy_ms = phase_max['gather']  # each rank's slice copied to host memory, measured alone
     # the merge as 8 GPUs would run it: each phase as long as its slowest rank (the collective
-    # steps measured as one in-process transfer of all ranks), + the result's copy to the host
-    merge_crit_ms = sum(phase_max.values()) + host_copy_ms
+    # steps measured as one in-process transfer of all ranks), the host copies included
+    # the exchange over xGMI instead of one on-die copy: a rank's reduced table holds at most
+    # every merged key; it sends 1/W of it to each of W-1 peers, one point-to-point link each
+    # at ~50 GB/s achieved (MI355X_MICROARCH.md: 7 links x ~153 GB/s peak), plus ~20 us of
+    # RCCL group latency; the projection takes the larger of the measured and modelled exchange
+    res_bytes = float(sum(np.dtype(dtypes[n]).itemsize for n in dtypes))
+    per_link = float(len(out[next(iter(out))])) / W * res_bytes
+    xgmi_ms = per_link / 50e9 * 1e3 + 0.02 if W > 1 else 0.0
+    merge_crit_ms = sum(phase_max.values()) - phase_max['exchange'] + max(phase_max['exchange'], xgmi_ms)
     one_ms = 1e3 * float(np.mean(one_s))
     proj_ms = max(rank_ms) + merge_crit_ms
     total_rows = n_shards * shard_rows
@@ -312,8 +320,10 @@ def _c5_local_ranks(args):
             'merge_phase_ms_max_over_ranks': phase_max,
             'merge_result_to_host_ms': host_copy_ms,
             'merge_ms_critical_path': merge_crit_ms,
-            'merge': 'bqg_merge_group at world %d: pack kernel, count all-gather, per-column exchange, reduce, '
-                     'gather to rank 0, copy to host; every rank\'s work on this one GPU' % W,
+            'merge_exchange_modelled_xgmi_ms': xgmi_ms,
+            'merge': 'bqg_merge_group_host at world %d: pack kernel, count all-gather, per-column exchange, hash '
+                     'reduce (partials in source order), each rank\'s partition copied straight into its slice '
+                     'of one pinned host result; every rank\'s work on this one GPU' % W,
             'one_gpu': {'ms_per_step': one_ms, 'rows_per_s': one_rate, 'merge_ms_world1': 1e3 * float(np.mean(one_merge_s)),
                         'what': 'one rank\'s %d shards in one pass + the world-1 RCCL merge (bench.py --config c5 at N=1)'
                                 % per_rank},
@@ -321,9 +331,10 @@ def _c5_local_ranks(args):
                                'x_over_one_gpu': proj_rate / one_rate,
                                'basis': 'max over ranks of the measured shard pass (each as alone on its GPU) + the '
                                         'merge\'s critical path: every merge phase as long as its slowest rank '
-                                        '(host wall time per rank; the collective steps measured as one in-process '
-                                        'transfer of all %d ranks on this GPU) + the result\'s copy to the host; '
-                                        'not an 8-GPU measurement' % W},
+                                        '(host wall time per rank, each rank\'s device work waited for on its own, '
+                                        'its slice of the result copied to host memory alone; the payload exchange '
+                                        'the larger of one in-process transfer of all %d ranks on this GPU and the '
+                                        'xGMI model); not an 8-GPU measurement' % W},
         },
         'roofline': {
             'bound': 'hbm',

@@ -357,6 +357,11 @@ struct bqg_ctx {
   ColumnPool colpool;
   IngestPool ingest;  // cold-path staging: streams + pinned double buffers per decode thread
   int cu = 256;
+  // the merge's re-groups run the query-specialised kernels at any size (their shape repeats
+  // and the compiled kernels are cached): a per-call override of jit_min_rows that leaves the
+  // user-visible option untouched (bqg_internal_jit_min_override; -1: none)
+  int64_t jit_min_override = -1;
+  int64_t jit_min_rows() const { return jit_min_override >= 0 ? jit_min_override : opt[kOptJitMinRows]; }
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
@@ -682,6 +687,18 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
         distinct.push_back(q->aggs[a].col);
     for (int tc : distinct) pl.alg_bytes += (int64_t)dtype_size(t->cols[tc].dtype) * t->nrows;
   }
+  if (pl.tcol.empty()) {
+    // no keys, terms, mask or summed columns (e.g. groupby([], count / count_distinct)): the
+    // scan kernels stream at least one column (NC >= 1) -- the first aggregation's, whose rows
+    // the count covers (not counted in alg_bytes: nothing is read from it)
+    if (ncols_t < 1) fail(BQG_E_INVALID, "table has no columns");
+    const int tc = q->n_aggs > 0 ? q->aggs[0].col : 0;
+    scan_col(pl, tc);
+    pl.p.ncols = 1;
+    const Column& col = t->cols[tc];
+    pl.p.cols[0] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
+  }
+  if (pl.p.ncols < 1 || pl.p.ncols > kMaxCols) fail(BQG_E_INVALID, "scan plan with %d columns", pl.p.ncols);
   pl.p.nrows = t->nrows;
   // 4. mode
   const uint64_t kDenseMax = std::max<uint64_t>(1ull << 24, std::min<uint64_t>(2ull * (uint64_t)t->nrows, 1ull << 27));
@@ -1020,7 +1037,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       for (int j = 0; j < e.ncols; ++j) e.cols[j].out = ob + 64 + (size_t)j * S * 8;
     }
     hipFunction_t jfn = nullptr;
-    if (c->opt[kOptJit] && N >= c->opt[kOptJitMinRows]) {
+    if (c->opt[kOptJit] && N >= c->jit_min_rows()) {
       std::string spec = jit_spec(pl.p);
       // tiles in flight per workgroup (profiling option; default in scan_private.h)
       if (c->opt[kOptPrivAhead]) spec += std::string("#define BQ_PRIV_AHEAD ") + std::to_string(c->opt[kOptPrivAhead]) + "\n";
@@ -1200,7 +1217,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         L.tile_mark = L.first_tag + tbytes;
       }
       hipFunction_t fs = nullptr, ff = nullptr;
-      if (c->opt[kOptJit] && N >= c->opt[kOptJitMinRows]) {
+      if (c->opt[kOptJit] && N >= c->jit_min_rows()) {
         const std::string spec = jit_spec(pl.p) + "#define BQ_PART_K " + std::to_string(L.k) +
                                  "\n#define BQ_PART_NARROW " + std::to_string(L.narrow) +
                                  "\n#define BQ_PART_PACK " + std::to_string(L.pack) + "\n";
@@ -1317,24 +1334,33 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       pc.p.ncols = (int)pc.tcol.size();
       pc.p.cols[d.vcol] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
       d.out = cd_out + (size_t)i * S;
-      if (dtype_is_float(col.dtype)) {
-        if (S != 1) fail(BQG_E_UNSUPPORTED, "count_distinct of a float column with groupby keys");
+      // pair identity: (slot, value code) packed into one 64-bit set key when the pair space
+      // allows (a bitmap when it is small), else slot << 32 | representative row (pair_rows)
+      const bool isf = dtype_is_float(col.dtype);
+      unsigned __int128 pairs;
+      if (isf) {
         d.vmin = 0;
-        d.vrange = 1;  // key = value bits (S == 1)
+        d.vrange = 1;  // S == 1: key = canonical value bits
+        d.pair_rows = S != 1;
+        pairs = (unsigned __int128)1 << 64;
       } else {
         d.vmin = col.stats.empty ? 0 : col.stats.imin;
         d.vrange = col.stats.empty ? 1 : (uint64_t)col.stats.imax - (uint64_t)col.stats.imin + 1;
-        if (d.vrange == 0) fail(BQG_E_UNSUPPORTED, "count_distinct value range too wide");
+        pairs = (unsigned __int128)S * (d.vrange ? d.vrange : ((unsigned __int128)1 << 64));
+        // a full-range 64-bit column (vrange wraps to 0) or S x range >= 2^63
+        if (pairs >= ((unsigned __int128)1 << 63)) {
+          d.pair_rows = 1;
+          d.vmin = 0;
+        }
       }
-      const unsigned __int128 pairs = (unsigned __int128)S * (dtype_is_float(col.dtype) ? 1 : d.vrange);
-      if (!dtype_is_float(col.dtype) && pairs <= ((unsigned __int128)1 << 30)) {
+      if (!isf && pairs <= ((unsigned __int128)1 << 30)) {
         const size_t words = (size_t)((pairs + 31) / 32);
         d.bitmap = (unsigned int*)c->bitmap.ensure(words * 4);
         HIPCHECK(hipMemsetAsync(d.bitmap, 0, words * 4, st));
         d.lds_bitmap_words = words * 4 <= 32 * 1024 ? (int)words : 0;
       } else {
-        if (!dtype_is_float(col.dtype) && pairs >= ((unsigned __int128)1 << 63))
-          fail(BQG_E_UNSUPPORTED, "count_distinct pair space wider than 63 bits");
+        if (d.pair_rows && (S >= 0xFFFFFFFFull || N > (int64_t)0xFFFFFFFFll))
+          fail(BQG_E_UNSUPPORTED, "count_distinct pair set: slot or row index beyond 32 bits");
         uint64_t cap = 1024;
         uint64_t est = std::min<uint64_t>((uint64_t)N, 1ull << 27);
         if (c->opt[kOptDistinctSlots]) est = (uint64_t)c->opt[kOptDistinctSlots] / 2;
@@ -1457,7 +1483,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       d.out_changes = so + (size_t)i * S * 2;
       d.out_first = d.out_changes + S;
       hipFunction_t sfn = nullptr;
-      if (fused && c->opt[kOptJit] && N >= c->opt[kOptJitMinRows]) {
+      if (fused && c->opt[kOptJit] && N >= c->jit_min_rows()) {
         const int cd_mode = d.cd.bitmap == nullptr ? 0 : (d.cd.lds_bitmap_words > 0 ? 1 : 2);
         // the value columns as constants (the same choice as the generic body's column loop)
         const int nc = pc.p.ncols;
@@ -1647,6 +1673,40 @@ void bqg_internal_set_error(bqg_ctx* c, const std::string& msg) {
   if (c) c->err = msg;
   g_err = msg;
 }
+int bqg_internal_table_set_rows(bqg_table* t, int64_t n) {
+  if (!t || n < 0 || n > t->nrows) return BQG_E_INVALID;
+  t->nrows = n;
+  for (Column& col : t->cols) col.stats.valid = false;
+  return BQG_OK;
+}
+int bqg_internal_host_result(bqg_ctx* c, int64_t n, const std::vector<int32_t>& dts, std::vector<void*>& cols,
+                             bqg_result** out) {
+  *out = nullptr;
+  try {
+    std::vector<size_t> offs;
+    size_t off = 0;
+    for (int32_t dt : dts) {
+      offs.push_back(off);
+      off += ((size_t)n * dtype_size(dt) + 255) & ~size_t(255);
+    }
+    BlockGuard blk;
+    blk.reset(c->pool, c->pool_get(off + 256));
+    std::vector<int> d(dts.begin(), dts.end());
+    bqg_result* r = block_result(c, blk.b, n, 0, d, offs);
+    blk.release();
+    cols.clear();
+    for (size_t j = 0; j < dts.size(); ++j) cols.push_back((unsigned char*)r->block.p + offs[j]);
+    *out = r;
+    return BQG_OK;
+  } catch (const ApiError& e) {
+    c->err = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    c->err = "host out of memory";
+    return BQG_E_OOM;
+  }
+}
+void bqg_internal_jit_min_override(bqg_ctx* c, int64_t rows) { c->jit_min_override = rows; }
 
 // ======================================================================================
 // C ABI

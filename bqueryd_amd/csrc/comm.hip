@@ -36,12 +36,14 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "ctx_internal.h"
 #include "kernels.h"
+#include "merge_schedule.h"
 
 namespace {
 
@@ -145,6 +147,15 @@ struct CommState {
   ncclComm_t comm = nullptr;  // RCCL transport; nullptr = in-process transport (see below)
   int rank = 0, nranks = 1;
   Buf send, scratch, counts;  // packed send blocks, pack scratch, row counts
+  Buf reduce;                 // receive-side reduce: hash table, sums, rank bitmap
+  void* hcnt = nullptr;       // page-locked staging of the reduce's key count (async D2H)
+  void* hcounts() {
+    if (!hcnt && hipHostMalloc(&hcnt, 64, hipHostMallocDefault) != hipSuccess) {
+      hcnt = nullptr;
+      comm_fail(BQG_E_OOM, "pinned staging for the merge counts failed");
+    }
+    return hcnt;
+  }
   double phase_ms[kMergePhases] = {};  // host wall time of this rank's part of the last merge
   // in-process transport: an event on this rank's stream, and (rank 0) the copy descriptors
   // of a transfer step -- page-locked staging, its reuse guarded by desc_ev -- and their
@@ -176,7 +187,9 @@ void destroy_state(CommState* s) {
   s->send.release();
   s->scratch.release();
   s->counts.release();
+  s->reduce.release();
   s->ddesc.release();
+  if (s->hcnt) (void)hipHostFree(s->hcnt);
   if (s->hdesc) (void)hipHostFree(s->hdesc);
   if (s->ev) (void)hipEventDestroy(s->ev);
   if (s->desc_ev) (void)hipEventDestroy(s->desc_ev);
@@ -278,11 +291,11 @@ bqg_table* regroup(bqg_ctx* c, bqg_table* t, int n_keys, int ncols) {
   // the merge's re-groups run the query-specialised kernels whatever the table size (the
   // context's jit_min_rows keeps small ad-hoc queries off the compiler; a merge's shape
   // repeats, and its compiled kernels are cached)
-  int64_t jit_min = 0;
-  ck(c, bqg_get_option(c, "jit_min_rows", &jit_min));
-  ck(c, bqg_set_option(c, "jit_min_rows", 0));
+  // (a per-call override: the context's option, as bqg_get_option reports it, is untouched;
+  // the first merge of a schema pays the specialisation's compile, cached afterwards)
+  bqg_internal_jit_min_override(c, 0);
   const int rc = bqg_groupby_table(c, t, &q, &out);
-  (void)bqg_set_option(c, "jit_min_rows", jit_min);
+  bqg_internal_jit_min_override(c, -1);
   ck(c, rc);
   return out;
 }
@@ -322,13 +335,10 @@ void put_count(int64_t* dst, int64_t v, hipStream_t st) {
 // of this call (bqg_comm_init_local: one process driving several contexts, possibly on one
 // GPU -- the test harness for the exchange logic on a one-GPU machine)
 // ------------------------------------------------------------------------------------
-// one message; the messages between one (sender, receiver) pair are matched in the order they
-// are posted, as RCCL matches grouped send / receive operations with the same peer
-struct P2P {
-  int peer;
-  void* ptr;
-  size_t bytes;
-};
+// one message (merge_schedule.h); the messages between one (sender, receiver) pair are
+// matched in the order they are posted, as RCCL matches grouped send / receive operations with
+// the same peer
+using bqg_sched::P2P;
 
 void sync_all(std::vector<Local>& ranks) {
   for (Local& l : ranks) {
@@ -503,7 +513,56 @@ void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& se
   batch_copies(ranks, copies);
 }
 
-void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t>& dts, int reduced) {
+// where the merged table goes: a new device table on rank 0 (bqg_merge / bqg_merge_group), a
+// host result on rank 0 after the gather (bqg_merge_host), or a host result that every rank
+// fills with its own partition (bqg_merge_group_host driving every rank: no gather)
+enum class MergeOut { kDeviceRoot, kHostRoot, kHostDirect };
+
+// the receive side's sum by key (MergeReduce, kernels.h) of a rank's received rows R (from
+// `sources` ranks, row blocks from_peer in rank order): launched on the rank's stream; the key
+// count lands in st->counts (read by the caller after a sync)
+void queue_reduce(Local& l, int n_keys, const std::vector<int32_t>& dts, const std::vector<int>& lg, int W,
+                  TableOwner& out) {
+  const int ncols = (int)dts.size();
+  const int64_t n = nrows_of(l.ctx, l.R.t);
+  ck(l.ctx, bqg_table_create(l.ctx, n, ncols, dts.data(), &out.t));
+  bqg::MergeReduce m{};
+  m.keys.nkeys = n_keys;
+  for (int k = 0; k < n_keys; ++k) {
+    m.keys.cols[k] = bqg::DevCol{(const unsigned char*)col_ptr(l.ctx, l.R.t, k), dts[k], lg[k]};
+    m.out_keys[k] = (unsigned char*)col_ptr(l.ctx, out.t, k);
+  }
+  m.nvals = ncols - n_keys;
+  for (int j = 0; j < m.nvals; ++j) {
+    m.vals[j] = (const unsigned char*)col_ptr(l.ctx, l.R.t, n_keys + j);
+    m.vdt[j] = dts[n_keys + j];
+    m.out_vals[j] = (unsigned char*)col_ptr(l.ctx, out.t, n_keys + j);
+  }
+  m.nrows = n;
+  const uint64_t cap = bqg::merge_reduce_cap(n);
+  m.mask = cap - 1;
+  const uint64_t nwords = ((uint64_t)n + 31) / 32, nblocks = (nwords + 1023) / 1024;
+  const size_t o_acc = align16(cap * 8), o_bits = o_acc + align16(cap * 8 * (size_t)std::max(1, m.nvals)),
+               o_wp = o_bits + align16(nwords * 4 + 4), o_bs = o_wp + align16(nwords * 4 + 4),
+               total = o_bs + align16(nblocks * 4 + 4);
+  unsigned char* b = (unsigned char*)l.st->reduce.ensure(total);
+  m.table = (unsigned long long*)b;
+  m.acc = (unsigned long long*)(b + o_acc);
+  m.rep_bits = (unsigned int*)(b + o_bits);
+  m.word_prefix = (unsigned int*)(b + o_wp);
+  m.block_sum = (unsigned int*)(b + o_bs);
+  int64_t* cnt = (int64_t*)l.st->counts.p;
+  m.groups = (unsigned long long*)cnt;                 // [0]: keys found
+  m.overflow = (unsigned int*)(cnt + 1);               // [1]: probe overflow flag
+  HIPCK(hipMemsetAsync(cnt + 1, 0, 8, l.stream));
+  std::vector<int64_t> off(W + 1, 0);
+  for (int s = 0; s < W; ++s) off[s + 1] = off[s] + l.from_peer[s];
+  bqg::launch_merge_reduce(m, off.data(), W, l.stream);
+  HIPCK(hipGetLastError());
+}
+
+void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t>& dts, int reduced, MergeOut mode,
+                bqg_result** host_out) {
   const int ncols = (int)dts.size();
   if (n_keys < 1 || n_keys > ncols || n_keys > bqg::kMaxKeys) comm_fail(BQG_E_INVALID, "merge needs 1..4 key columns");
   if (ncols > bqg::kMergeMaxCols) comm_fail(BQG_E_UNSUPPORTED, "merge schema has too many columns");
@@ -522,6 +581,9 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       }
     }
   }
+  const bool all_local = (int)ranks.size() == W;
+  if (mode == MergeOut::kHostDirect && !all_local) mode = MergeOut::kHostRoot;
+  const bool timing = bqg_internal_timing(ranks[0].ctx);
   std::vector<int> lg(ncols);
   size_t row_bytes = 0;
   for (int j = 0; j < ncols; ++j) {
@@ -540,12 +602,46 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
   };
   // phases (bqg_comm_last_phases): 0 local re-group + pack, 1 count exchange, 2 payload
   // exchange, 3 reduce, 4 gather counts, 5 gather + final sync; a collective step's time is
-  // charged to every rank of the call
+  // charged to every rank of the call (with timing on, after its device work has finished)
   for (Local& l : ranks)
     for (double& x : l.st->phase_ms) x = 0.0;
   auto collective = [&](int ph, double t0) {
+    if (timing) sync_all(ranks);
     const double dt = now_ms() - t0;
     for (Local& l : ranks) l.st->phase_ms[ph] += dt;
+  };
+  // a host result with the merged rows of every local rank's table `src` (rank order), each
+  // rank's slice copied on its own stream: per-rank phase 5 with timing (each copy alone)
+  auto to_host = [&](std::vector<bqg_table*> src) {
+    std::vector<int64_t> rows(ranks.size(), 0);
+    std::vector<size_t> order(ranks.size());  // slices in rank order
+    int64_t total = 0;
+    for (size_t i = 0; i < ranks.size(); ++i) {
+      rows[i] = src[i] ? nrows_of(ranks[i].ctx, src[i]) : 0;
+      total += rows[i];
+      order[i] = i;
+    }
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return ranks[a].st->rank < ranks[b].st->rank; });
+    std::vector<void*> cols;
+    bqg_result* r = nullptr;
+    ck(ranks[0].ctx, bqg_internal_host_result(ranks[0].ctx, total, dts, cols, &r));
+    std::unique_ptr<bqg_result, int (*)(bqg_result*)> own(r, bqg_result_free);
+    int64_t off = 0;
+    for (size_t i : order) {
+      Local& l = ranks[i];
+      const double t0 = now_ms();
+      HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+      for (int j = 0; rows[i] && j < ncols; ++j)
+        HIPCK(hipMemcpyAsync((unsigned char*)cols[j] + ((size_t)off << lg[j]), col_ptr(l.ctx, src[i], j),
+                             (size_t)rows[i] << lg[j], hipMemcpyDeviceToHost, l.stream));
+      if (timing) {
+        HIPCK(hipStreamSynchronize(l.stream));
+        l.st->phase_ms[5] += now_ms() - t0;
+      }
+      off += rows[i];
+    }
+    sync_all(ranks);
+    *host_out = own.release();
   };
   // 1-2. local reduce, then every row straight into its destination's packed block
   for (Local& l : ranks) {
@@ -593,8 +689,14 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       bqg::launch_merge_pack(m, l.stream);
       HIPCK(hipGetLastError());
     }
-    if (bqg_internal_timing(l.ctx)) HIPCK(hipStreamSynchronize(l.stream));
+    if (timing) HIPCK(hipStreamSynchronize(l.stream));
     l.st->phase_ms[0] += now_ms() - t0;
+  }
+  // world 1 with a host result: the rank's reduced rows are the answer (no exchange)
+  if (W == 1 && mode != MergeOut::kDeviceRoot) {
+    to_host({ranks[0].Lv});
+    for (Local& l : ranks) l.L.reset();
+    return;
   }
   // 3a. count matrix: every rank's row counts per destination
   double tc = now_ms();
@@ -618,67 +720,83 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     for (size_t i = 0; i < ranks.size(); ++i) {
       Local& l = ranks[i];
       HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-      for (int d = 0; d < W; ++d) {
-        if (!l.to_peer[d]) continue;
-        for (int j = 0; j < ncols; ++j) {
-          void* src = W == 1 ? col_ptr(l.ctx, l.Lv, j) : (unsigned char*)l.st->send.p + packed_base(l.to_peer, d, j);
-          sends[i].push_back(P2P{d, src, (size_t)l.to_peer[d] << lg[j]});
-        }
-      }
       int64_t total = 0;
       for (int s = 0; s < W; ++s) total += l.from_peer[s];
-      if (!total) continue;
-      ck(l.ctx, bqg_table_create(l.ctx, total, ncols, dts.data(), &l.R.t));
-      int64_t off = 0;
-      for (int s = 0; s < W; ++s) {
-        if (!l.from_peer[s]) continue;
-        for (int j = 0; j < ncols; ++j)
-          recvs[i].push_back(P2P{s, (unsigned char*)col_ptr(l.ctx, l.R.t, j) + ((size_t)off << lg[j]),
-                                 (size_t)l.from_peer[s] << lg[j]});
-        off += l.from_peer[s];
-      }
+      if (total) ck(l.ctx, bqg_table_create(l.ctx, total, ncols, dts.data(), &l.R.t));
+      std::vector<void*> dst(ncols);
+      for (int j = 0; j < ncols; ++j) dst[j] = total ? col_ptr(l.ctx, l.R.t, j) : nullptr;
+      bqg_sched::exchange_schedule(W, ncols, lg, l.to_peer, l.from_peer, [&](int d, int j) {
+        return W == 1 ? col_ptr(l.ctx, l.Lv, j) : (void*)((unsigned char*)l.st->send.p + packed_base(l.to_peer, d, j));
+      }, dst, sends[i], recvs[i]);
     }
     tc = now_ms();
     xfer_p2p(ranks, sends, recvs);
     collective(2, tc);
   }
-  // 4. reduce the received rows: one source's rows are already unique by key, only rows from
-  // two or more sources need the re-group
-  for (Local& l : ranks) {
-    const double t0 = now_ms();
-    HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-    l.L.reset();  // sent (stream-ordered before any later use of its memory)
-    l.Lv = nullptr;
-    int sources = 0;
-    for (int s = 0; s < W; ++s) sources += l.from_peer[s] > 0;
-    if (sources > 1) {
-      TableOwner got;
-      got.t = l.R.release();
-      l.R.t = regroup(l.ctx, got.t, n_keys, ncols);
-    }
-    int64_t* cnt = (int64_t*)l.st->counts.p;
-    put_count(cnt, l.R.t ? nrows_of(l.ctx, l.R.t) : 0, l.stream);
-    l.st->phase_ms[3] += now_ms() - t0;
-  }
-  // 5. gather to rank 0: counts, then the reduced partitions column by column
-  tc = now_ms();
-  xfer_allgather_i64(ranks, 1);
-  std::vector<int64_t> part_rows(W, 0);
-  for (Local& l : ranks)
-    if (l.st->rank == 0) {
+  // 4. reduce the received rows: one source's rows are already unique by key, rows from two or
+  // more sources are summed by key (MergeReduce: one hash table, source order)
+  {
+    std::vector<TableOwner> red(ranks.size());
+    for (size_t i = 0; i < ranks.size(); ++i) {
+      Local& l = ranks[i];
+      const double t0 = now_ms();
       HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-      HIPCK(hipMemcpyAsync(part_rows.data(), (int64_t*)l.st->counts.p + W, sizeof(int64_t) * W,
-                           hipMemcpyDeviceToHost, l.stream));
-      HIPCK(hipStreamSynchronize(l.stream));
+      int sources = 0;
+      for (int s = 0; s < W; ++s) sources += l.from_peer[s] > 0;
+      if (sources > 1) {
+        queue_reduce(l, n_keys, dts, lg, W, red[i]);
+        HIPCK(hipMemcpyAsync(l.st->hcounts(), l.st->counts.p, 16, hipMemcpyDeviceToHost, l.stream));
+      }
+      if (timing) HIPCK(hipStreamSynchronize(l.stream));
+      l.st->phase_ms[3] += now_ms() - t0;
     }
-  collective(4, tc);
+    for (size_t i = 0; i < ranks.size(); ++i) {
+      Local& l = ranks[i];
+      const double t0 = now_ms();
+      HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+      HIPCK(hipStreamSynchronize(l.stream));
+      l.L.reset();  // sent (stream-ordered before any later use of its memory)
+      l.Lv = nullptr;
+      if (red[i].t) {
+        const int64_t* hc = (const int64_t*)l.st->hcounts();
+        if (hc[1] & 0xFFFFFFFFll) comm_fail(BQG_E_HIP, "merge reduce: hash table overflow");
+        ck(l.ctx, bqg_internal_table_set_rows(red[i].t, hc[0]));
+        l.R.reset();
+        l.R.t = red[i].release();
+      }
+      l.st->phase_ms[3] += now_ms() - t0;
+    }
+  }
+  if (mode == MergeOut::kHostDirect) {
+    // 5. every rank's partition straight into its slice of the host result
+    std::vector<bqg_table*> src;
+    for (Local& l : ranks) src.push_back(l.R.t);
+    to_host(src);
+    for (Local& l : ranks) l.R.reset();
+    return;
+  }
+  // 5. gather to rank 0: the partitions' row counts (all-local: known here; else an
+  // all-gather), then the reduced partitions column by column
+  std::vector<int64_t> part_rows(W, 0);
   tc = now_ms();
-  if (ranks.size() < (size_t)W || ranks[0].st->rank != 0) {
-    // a process driving only some ranks (one process per GPU): non-root ranks learn the
-    // gather sizes they need (their own) locally
+  if (all_local) {
+    for (Local& l : ranks) part_rows[l.st->rank] = l.R.t ? nrows_of(l.ctx, l.R.t) : 0;
+  } else {
+    for (Local& l : ranks) put_count((int64_t*)l.st->counts.p, l.R.t ? nrows_of(l.ctx, l.R.t) : 0, l.stream);
+    xfer_allgather_i64(ranks, 1);
+    for (Local& l : ranks)
+      if (l.st->rank == 0) {
+        HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+        HIPCK(hipMemcpyAsync(part_rows.data(), (int64_t*)l.st->counts.p + W, sizeof(int64_t) * W,
+                             hipMemcpyDeviceToHost, l.stream));
+        HIPCK(hipStreamSynchronize(l.stream));
+      }
+    // non-root ranks learn the gather sizes they need (their own) locally
     for (Local& l : ranks)
       if (l.st->rank != 0) part_rows[l.st->rank] = l.R.t ? nrows_of(l.ctx, l.R.t) : 0;
   }
+  collective(4, tc);
+  tc = now_ms();
   int64_t others = 0;
   for (int s = 1; s < W; ++s) others += part_rows[s];
   {
@@ -686,10 +804,10 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     for (size_t i = 0; i < ranks.size(); ++i) {
       Local& l = ranks[i];
       HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+      std::vector<void*> src(ncols, nullptr), dst(ncols, nullptr);
       if (l.st->rank != 0) {
-        const int64_t mine = l.R.t ? nrows_of(l.ctx, l.R.t) : 0;
-        for (int j = 0; mine && j < ncols; ++j)
-          sends[i].push_back(P2P{0, col_ptr(l.ctx, l.R.t, j), (size_t)mine << lg[j]});
+        for (int j = 0; l.R.t && j < ncols; ++j) src[j] = col_ptr(l.ctx, l.R.t, j);
+        bqg_sched::gather_schedule(l.st->rank, W, ncols, lg, part_rows, src, dst, sends[i], recvs[i]);
         continue;
       }
       if (others == 0) continue;  // every merged row is in rank 0's own partition
@@ -699,14 +817,8 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       ck(l.ctx, bqg_table_create(l.ctx, total, ncols, dts.data(), &res.t));
       if (part_rows[0])
         for (int j = 0; j < ncols; ++j) ck(l.ctx, bqg_push_chunk(res.t, j, col_ptr(l.ctx, l.R.t, j), part_rows[0], 0));
-      int64_t off = part_rows[0];
-      for (int s = 1; s < W; ++s) {
-        if (!part_rows[s]) continue;
-        for (int j = 0; j < ncols; ++j)
-          recvs[i].push_back(P2P{s, (unsigned char*)col_ptr(l.ctx, res.t, j) + ((size_t)off << lg[j]),
-                                 (size_t)part_rows[s] << lg[j]});
-        off += part_rows[s];
-      }
+      for (int j = 0; j < ncols; ++j) dst[j] = col_ptr(l.ctx, res.t, j);
+      bqg_sched::gather_schedule(0, W, ncols, lg, part_rows, src, dst, sends[i], recvs[i]);
       l.R.reset();
       l.R.t = res.release();
     }
@@ -716,11 +828,62 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
     HIPCK(hipStreamSynchronize(l.stream));  // sends complete before their tables are released
     if (l.st->rank == 0 && !l.R.t) ck(l.ctx, bqg_table_create(l.ctx, 0, ncols, dts.data(), &l.R.t));  // no rows anywhere
+  }
+  collective(5, tc);
+  if (mode == MergeOut::kHostRoot) {
+    for (Local& l : ranks)
+      if (l.st->rank == 0) {
+        const double t0 = now_ms();
+        // the gathered table to host memory on rank 0's stream
+        std::vector<void*> cols;
+        bqg_result* r = nullptr;
+        const int64_t n = nrows_of(l.ctx, l.R.t);
+        ck(l.ctx, bqg_internal_host_result(l.ctx, n, dts, cols, &r));
+        std::unique_ptr<bqg_result, int (*)(bqg_result*)> own(r, bqg_result_free);
+        HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+        for (int j = 0; n && j < ncols; ++j)
+          HIPCK(hipMemcpyAsync(cols[j], col_ptr(l.ctx, l.R.t, j), (size_t)n << lg[j], hipMemcpyDeviceToHost, l.stream));
+        HIPCK(hipStreamSynchronize(l.stream));
+        *host_out = own.release();
+        l.st->phase_ms[4] += now_ms() - t0;
+      }
+    for (Local& l : ranks) {
+      l.R.reset();
+      *l.out = nullptr;
+    }
+    return;
+  }
+  for (Local& l : ranks) {
     if (l.st->rank == 0) *l.out = l.R.release();
     else *l.out = nullptr;
     l.R.reset();
   }
-  collective(5, tc);
+}
+
+int merge_entry(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,
+                int32_t n_keys, int32_t n_cols, const int32_t* dtypes, int32_t reduced, bqg_table** out,
+                MergeOut mode, bqg_result** host_out) {
+  bqg_ctx* c0 = n_local > 0 && ctxs ? ctxs[0] : nullptr;
+  return comm_guard(c0, [&] {
+    if (n_local < 1 || !ctxs || !n_tables || !out || !dtypes || n_cols < 1 || (mode != MergeOut::kDeviceRoot && !host_out))
+      comm_fail(BQG_E_INVALID, "bad merge arguments");
+    if (host_out) *host_out = nullptr;
+    std::vector<int32_t> dts(dtypes, dtypes + n_cols);
+    for (int32_t dt : dts)
+      if (dt < BQG_BOOL || dt > BQG_F64) comm_fail(BQG_E_INVALID, "unknown dtype in the merge schema");
+    std::vector<Local> ranks(n_local);
+    size_t k = 0;
+    for (int i = 0; i < n_local; ++i) {
+      ranks[i].ctx = ctxs[i];
+      ranks[i].st = state_of(ctxs[i]);
+      ranks[i].stream = bqg_internal_stream(ctxs[i]);
+      ranks[i].out = &out[i];
+      out[i] = nullptr;
+      if (n_tables[i] < 0) comm_fail(BQG_E_INVALID, "negative table count");
+      for (int j = 0; j < n_tables[i]; ++j) ranks[i].tables.push_back(tables[k++]);
+    }
+    merge_impl(ranks, n_keys, dts, reduced, mode, host_out);
+  });
 }
 
 }  // namespace
@@ -839,26 +1002,21 @@ int bqg_merge(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int32_t 
 
 int bqg_merge_group(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,
                     int32_t n_keys, int32_t n_cols, const int32_t* dtypes, int32_t reduced, bqg_table** out) {
-  bqg_ctx* c0 = n_local > 0 && ctxs ? ctxs[0] : nullptr;
-  return comm_guard(c0, [&] {
-    if (n_local < 1 || !ctxs || !n_tables || !out || !dtypes || n_cols < 1)
-      comm_fail(BQG_E_INVALID, "bad merge arguments");
-    std::vector<int32_t> dts(dtypes, dtypes + n_cols);
-    for (int32_t dt : dts)
-      if (dt < BQG_BOOL || dt > BQG_F64) comm_fail(BQG_E_INVALID, "unknown dtype in the merge schema");
-    std::vector<Local> ranks(n_local);
-    size_t k = 0;
-    for (int i = 0; i < n_local; ++i) {
-      ranks[i].ctx = ctxs[i];
-      ranks[i].st = state_of(ctxs[i]);
-      ranks[i].stream = bqg_internal_stream(ctxs[i]);
-      ranks[i].out = &out[i];
-      out[i] = nullptr;
-      if (n_tables[i] < 0) comm_fail(BQG_E_INVALID, "negative table count");
-      for (int j = 0; j < n_tables[i]; ++j) ranks[i].tables.push_back(tables[k++]);
-    }
-    merge_impl(ranks, n_keys, dts, reduced);
-  });
+  return merge_entry(n_local, ctxs, n_tables, tables, n_keys, n_cols, dtypes, reduced, out, MergeOut::kDeviceRoot,
+                     nullptr);
+}
+
+int bqg_merge_host(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int32_t n_keys, int32_t n_cols,
+                   const int32_t* dtypes, int32_t reduced, bqg_result** out) {
+  bqg_table* unused = nullptr;
+  return merge_entry(1, &ctx, &n_tables, tables, n_keys, n_cols, dtypes, reduced, &unused, MergeOut::kHostRoot, out);
+}
+
+int bqg_merge_group_host(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,
+                         int32_t n_keys, int32_t n_cols, const int32_t* dtypes, int32_t reduced, bqg_result** out) {
+  std::vector<bqg_table*> unused((size_t)std::max(n_local, 1), nullptr);
+  return merge_entry(n_local, ctxs, n_tables, tables, n_keys, n_cols, dtypes, reduced, unused.data(),
+                     MergeOut::kHostDirect, out);
 }
 
 }  // extern "C"

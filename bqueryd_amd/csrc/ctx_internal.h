@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/bqgpu.h"
 
@@ -18,3 +19,13 @@ bool bqg_internal_timing(bqg_ctx* c);
 void bqg_internal_set_error(bqg_ctx* c, const std::string& msg);
 // comm.hip: drop the context's RCCL communicator, if any (called by bqg_destroy)
 void bqg_internal_comm_release(bqg_ctx* c);
+// comm.hip: lower a library table's row count to n <= its rows (the merge emits into a table
+// sized by an upper bound); the column memory is kept
+int bqg_internal_table_set_rows(bqg_table* t, int64_t n);
+// a host result of n rows of the given dtypes in one pinned block of the context's pool
+// (device-mapped); cols[j] receives column j's host address (BQG_OK or an error code, with
+// the context's message set)
+int bqg_internal_host_result(bqg_ctx* c, int64_t n, const std::vector<int32_t>& dts, std::vector<void*>& cols,
+                             bqg_result** out);
+// per-call override of the jit_min_rows option (-1: none), not visible through bqg_get_option
+void bqg_internal_jit_min_override(bqg_ctx* c, int64_t rows);

@@ -387,6 +387,21 @@ __device__ __forceinline__ uint64_t slot_lookup(const ScanParams& p, const SlotA
   return kEmpty;
 }
 
+// 64-bit hash of the canonical key VALUES of a row (not codes: codes depend on per-table
+// statistics) -- the cross-rank merge's partition function (mod nranks) and its reduce table
+__device__ __forceinline__ uint64_t key_hash_row(const PartitionCols& k, int64_t row) {
+  uint64_t h = 0x243F6A8885A308D3ull;
+  for (int j = 0; j < k.nkeys; ++j) {
+    Chunk c;
+    row_word_to_chunk(c, k.cols[j], row, load_row_word(k.cols[j], row));
+    uint64_t v[1];
+    decode<1>(c, k.cols[j].dtype, v);
+    const uint64_t bits = dtype_is_float(k.cols[j].dtype) ? canon_f64_bits(v[0]) : v[0];
+    h = mix64(h ^ mix64(bits + (uint64_t)j));
+  }
+  return h;
+}
+
 // ------------------------------------------------------------------------------------
 // Emit helpers (shared by the private finish kernel and the generic emit kernel)
 // ------------------------------------------------------------------------------------

@@ -38,12 +38,44 @@ __global__ __launch_bounds__(kBlock, 4) void k_count_distinct(ScanParams p, Slot
         if (s == kEmpty) continue;
       }
       uint64_t vcode = 0;
+      bool vfloat = false;
 #pragma unroll
       for (int c = 0; c < NC; ++c)
         if (d.vcol == c) {
           const int dt = p.cols[c].dtype;
-          vcode = dtype_is_float(dt) ? canon_f64_bits(v[c][r]) : v[c][r] - (uint64_t)d.vmin;
+          vfloat = dtype_is_float(dt);
+          vcode = vfloat ? canon_f64_bits(v[c][r]) : v[c][r] - (uint64_t)d.vmin;
         }
+      if (d.pair_rows) {
+        // vmin == 0 here: vcode is the value's full canonical identity
+        const uint32_t row = (uint32_t)(row0 + r);
+        const unsigned long long mine = (s << 32) | row;
+        uint64_t pos = mix64(vcode ^ mix64(s + 0x9E3779B97F4A7C15ull)) & d.set_mask;
+        for (uint64_t i = 0; i <= d.set_mask; ++i) {
+          unsigned long long k = d.set[pos];
+          if (k == kEmpty) {
+            const unsigned long long prev = atomicCAS(&d.set[pos], kEmpty, mine);
+            if (prev == kEmpty) {
+              atomicAdd(&d.out[s], 1ull);
+              const unsigned int f = atomicAdd(d.set_fill, 1u);
+              if ((uint64_t)(f + 1) * 2 > d.set_mask + 1) atomicOr(d.overflow, 1u);
+              break;
+            }
+            k = prev;
+          }
+          if ((k >> 32) == s) {
+            const uint32_t rep = (uint32_t)k;
+            uint64_t rv = 0;
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+              if (d.vcol == c) rv = key_at_row(p.cols[c], vfloat, rep);
+            if (rv == vcode) break;
+          }
+          pos = (pos + 1) & d.set_mask;
+          if (i == d.set_mask) atomicOr(d.overflow, 1u);
+        }
+        continue;
+      }
       if (d.bitmap) {
         const uint64_t bit = s * d.vrange + vcode;
         const unsigned int m = 1u << (bit & 31);

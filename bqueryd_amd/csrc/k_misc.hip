@@ -3,7 +3,7 @@
 
 #include <algorithm>
 
-#include "device.h"
+#include "partition.h"  // device.h + block_excl_scan_1024
 
 namespace bqg {
 
@@ -654,16 +654,7 @@ constexpr uint32_t kHashPartLds = 8192;
 // statistics), for the cross-rank merge: partition = mix(canonical key bits) mod nparts.
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t row_partition(const PartitionCols& k, int64_t row, uint32_t nparts) {
-  uint64_t h = 0x243F6A8885A308D3ull;
-  for (int j = 0; j < k.nkeys; ++j) {
-    Chunk c;
-    row_word_to_chunk(c, k.cols[j], row, load_row_word(k.cols[j], row));
-    uint64_t v[1];
-    decode<1>(c, k.cols[j].dtype, v);
-    const uint64_t bits = dtype_is_float(k.cols[j].dtype) ? canon_f64_bits(v[0]) : v[0];
-    h = mix64(h ^ mix64(bits + (uint64_t)j));
-  }
-  return (uint32_t)(h % nparts);
+  return (uint32_t)(key_hash_row(k, row) % nparts);
 }
 
 __global__ __launch_bounds__(kBlock) void k_hash_partition(PartitionCols k, int64_t nrows, uint32_t nparts,
@@ -841,6 +832,144 @@ void launch_merge_pack(const MergePack& m, hipStream_t st) {
   else (void)hipMemsetAsync(m.block_hist, 0, (size_t)m.nblocks * m.nranks * 4, st);
   hipLaunchKernelGGL(k_mpack_scan, dim3(1), dim3(kBlock), 0, st, m);
   if (m.nrows > 0) hipLaunchKernelGGL(k_mpack_scatter, dim3(m.nblocks), dim3(kBlock), 0, st, m);
+}
+
+// ------------------------------------------------------------------------------------
+// Cross-rank merge, receive side (MergeReduce, kernels.h): the received rows summed by key.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mred_val(const unsigned char* col, int dt, int64_t row) {
+  const DevCol c{col, dt, dtype_lg(dt)};
+  Chunk ch;
+  row_word_to_chunk(ch, c, row, load_row_word(c, row));
+  uint64_t v[1];
+  decode<1>(ch, dt, v);
+  return v[0];
+}
+
+__device__ __forceinline__ bool mred_same_keys(const PartitionCols& k, int64_t a, int64_t b) {
+  bool same = true;
+  for (int j = 0; j < k.nkeys; ++j) {
+    const bool f = dtype_is_float(k.cols[j].dtype);
+    same &= key_at_row(k.cols[j], f, (uint32_t)a) == key_at_row(k.cols[j], f, (uint32_t)b);
+  }
+  return same;
+}
+
+// one source block [row0, row1): claim or find each row's slot, then store (new key) or add
+// (key of an earlier source) its values -- plain accesses, a key occurs once per source
+__global__ __launch_bounds__(kBlock) void k_mred_insert(MergeReduce m) {
+  for (int64_t row = m.row0 + (int64_t)blockIdx.x * kBlock + threadIdx.x; row < m.row1;
+       row += (int64_t)gridDim.x * kBlock) {
+    const uint64_t h = key_hash_row(m.keys, row);
+    const uint32_t hi = (uint32_t)(h >> 32);
+    // the table position from a second mix: the rows of one rank share h mod nranks
+    uint64_t pos = mix64(h ^ 0x9E3779B97F4A7C15ull) & m.mask;
+    bool fresh = false;
+    uint64_t i = 0;
+    for (; i <= m.mask; ++i) {
+      unsigned long long w = m.table[pos];
+      if (w == kEmpty) {
+        const unsigned long long mine = ((unsigned long long)hi << 32) | (uint32_t)row;
+        const unsigned long long prev = atomicCAS(&m.table[pos], kEmpty, mine);
+        if (prev == kEmpty) {
+          fresh = true;
+          break;
+        }
+        w = prev;
+      }
+      if ((uint32_t)(w >> 32) == hi && mred_same_keys(m.keys, (int64_t)(uint32_t)w, row)) break;
+      pos = (pos + 1) & m.mask;
+    }
+    if (i > m.mask) {
+      atomicOr(m.overflow, 1u);
+      continue;
+    }
+    if (fresh) atomicOr(&m.rep_bits[row >> 5], 1u << (row & 31));
+    for (int j = 0; j < m.nvals; ++j) {
+      const int dt = m.vdt[j];
+      const uint64_t v = mred_val(m.vals[j], dt, row);
+      unsigned long long* a = m.acc + (size_t)j * (m.mask + 1) + pos;
+      if (fresh) *a = v;
+      else if (dtype_is_float(dt)) *a = as_u64(as_f64(*a) + as_f64(v));
+      else *a = *a + v;  // two's complement: wraps like bquery's typed sum at the output width
+    }
+  }
+}
+
+// rank scan of the representative-row bitmap: exclusive popcount prefix per word inside
+// blocks of 1024 words, block totals
+__global__ __launch_bounds__(1024) void k_mred_word_scan(MergeReduce m, uint64_t nwords) {
+  const uint64_t w = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  const unsigned int c = w < nwords ? (unsigned int)__popc(m.rep_bits[w]) : 0u;
+  unsigned int tot;
+  const unsigned int e = block_excl_scan_1024(c, &tot);
+  if (w < nwords) m.word_prefix[w] = e;
+  if (threadIdx.x == 0) m.block_sum[blockIdx.x] = tot;
+}
+
+// exclusive scan of the block totals (one workgroup, any count) and the key count
+__global__ __launch_bounds__(1024) void k_mred_block_scan(MergeReduce m, uint64_t nblocks) {
+  __shared__ unsigned int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint64_t base = 0; base < nblocks; base += 1024) {
+    const uint64_t i = base + threadIdx.x;
+    const unsigned int c = i < nblocks ? m.block_sum[i] : 0u;
+    unsigned int tot;
+    const unsigned int e = block_excl_scan_1024(c, &tot);
+    if (i < nblocks) m.block_sum[i] = carry + e;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *m.groups = carry;
+}
+
+// every occupied slot writes its output row at the rank of its representative row: keys as
+// stored at that row, sums converted to the column's dtype (integers wrap, float32 rounds once)
+__global__ __launch_bounds__(kBlock) void k_mred_emit(MergeReduce m) {
+  const uint64_t cap = m.mask + 1;
+  for (uint64_t pos = (uint64_t)blockIdx.x * kBlock + threadIdx.x; pos < cap; pos += (uint64_t)gridDim.x * kBlock) {
+    const unsigned long long w = m.table[pos];
+    if (w == kEmpty) continue;
+    const uint32_t rep = (uint32_t)w;
+    const uint32_t wi = rep >> 5;
+    const uint64_t r = (uint64_t)m.block_sum[wi >> 10] + m.word_prefix[wi] +
+                       (unsigned int)__popc(m.rep_bits[wi] & ((1u << (rep & 31)) - 1u));
+    for (int k = 0; k < m.keys.nkeys; ++k) {
+      const DevCol& c = m.keys.cols[k];
+      switch (c.lg) {
+        case 0: m.out_keys[k][r] = c.ptr[rep]; break;
+        case 1: reinterpret_cast<uint16_t*>(m.out_keys[k])[r] = reinterpret_cast<const uint16_t*>(c.ptr)[rep]; break;
+        case 2: reinterpret_cast<uint32_t*>(m.out_keys[k])[r] = reinterpret_cast<const uint32_t*>(c.ptr)[rep]; break;
+        default: reinterpret_cast<uint64_t*>(m.out_keys[k])[r] = reinterpret_cast<const uint64_t*>(c.ptr)[rep]; break;
+      }
+    }
+    for (int j = 0; j < m.nvals; ++j) {
+      unsigned long long a = m.acc[(size_t)j * cap + pos];
+      if (m.vdt[j] == BQG_F32) a = __float_as_uint((float)as_f64(a));
+      store_elem(m.out_vals[j], m.vdt[j], r, a);
+    }
+  }
+}
+
+void launch_merge_reduce(MergeReduce m, const int64_t* src_off, int nsrc, hipStream_t st) {
+  const uint64_t cap = m.mask + 1;
+  const uint64_t nwords = ((uint64_t)m.nrows + 31) / 32;
+  const uint64_t nblocks = (nwords + 1023) / 1024;
+  (void)hipMemsetAsync(m.table, 0xFF, cap * 8, st);
+  (void)hipMemsetAsync(m.rep_bits, 0, nwords * 4 + 4, st);
+  for (int s = 0; s < nsrc; ++s) {
+    m.row0 = src_off[s];
+    m.row1 = src_off[s + 1];
+    if (m.row1 <= m.row0) continue;
+    const unsigned g = (unsigned)std::min<int64_t>((m.row1 - m.row0 + kBlock - 1) / kBlock, 2048);
+    hipLaunchKernelGGL(k_mred_insert, dim3(g), dim3(kBlock), 0, st, m);
+  }
+  if (nwords) hipLaunchKernelGGL(k_mred_word_scan, dim3((unsigned)nblocks), dim3(1024), 0, st, m, nwords);
+  hipLaunchKernelGGL(k_mred_block_scan, dim3(1), dim3(1024), 0, st, m, nblocks);
+  const unsigned ge = (unsigned)std::min<uint64_t>((cap + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL(k_mred_emit, dim3(ge), dim3(kBlock), 0, st, m);
 }
 
 // value runs: rows whose value differs from the previous row's (canonical bits: a float

@@ -75,6 +75,10 @@ struct DistinctLaunch {
   unsigned int* overflow;
   unsigned long long* out;  // [nslots] distinct counts
   int lds_bitmap_words;     // > 0: per-workgroup LDS pre-filter of this many words
+  // pair_rows (float values with group keys, integer pair spaces of 2^63 and more): set
+  // entries are slot << 32 | representative row, probed at hash(slot, canonical value) and
+  // matched by re-reading the value column at the representative row (full compare)
+  int pair_rows;
 };
 void launch_count_distinct(const ScanParams& p, const SlotArrays& s, const DistinctLaunch& d,
                            int blocks, hipStream_t st);
@@ -260,6 +264,43 @@ struct MergePack {
 };
 void merge_pack_grid(int64_t nrows, int32_t* nblocks, int64_t* rows_per_block);
 void launch_merge_pack(const MergePack& m, hipStream_t st);
+
+// cross-rank merge, receive side: the rows a rank received from every source rank (each
+// source's rows already unique by key) summed by key in one hash table -- no statistics, no
+// planner, no first-appearance sort.  Sources are inserted one launch each, in source order,
+// so every key's sums are added in source order (deterministic) with plain stores: within one
+// source a key occurs once, so no two rows of a launch touch one slot's accumulators.  The
+// table word is hash_hi32 << 32 | representative row (the key's first row, in the lowest
+// source holding it); keys compare in full at the representative row.  Output rows come in
+// representative-row order: first appearance in the received rows, as a re-group would give.
+constexpr int kMergeMaxVals = kMergeMaxCols;
+struct MergeReduce {
+  PartitionCols keys;                         // key columns of the received table
+  const unsigned char* vals[kMergeMaxVals];   // value (sum) columns
+  int32_t vdt[kMergeMaxVals];                 // their dtypes (the output dtype too)
+  int32_t nvals;
+  int64_t nrows;                              // received rows
+  int64_t row0, row1;                         // this launch's source block
+  unsigned long long* table;                  // [cap] kEmpty or hash_hi32 << 32 | rep row
+  uint64_t mask;                              // cap - 1
+  unsigned long long* acc;                    // [nvals][cap] 64-bit sums (f64 bits for floats)
+  unsigned int* rep_bits;                     // [ceil(nrows / 32)] rows that represent a key
+  unsigned int* word_prefix;                  // [ceil(nrows / 32)] rank-scan scratch
+  unsigned int* block_sum;                    // [ceil(nrows / 32768)] rank-scan scratch
+  unsigned int* overflow;                     // a probe ran past the table (cannot at load <= 1/2)
+  unsigned long long* groups;                 // out: keys found
+  unsigned char* out_keys[kMaxKeys];          // out columns, capacity nrows
+  unsigned char* out_vals[kMergeMaxVals];
+};
+// table capacity for `rows` received rows (load <= 1/2)
+inline uint64_t merge_reduce_cap(int64_t rows) {
+  uint64_t cap = 1024;
+  while (cap < 2 * (uint64_t)rows) cap <<= 1;
+  return cap;
+}
+// every launch of the reduce on `st`: table init, one insert per non-empty source block
+// (src_off[0..nsrc]), rank scan, emit; `groups` receives the key count on the device
+void launch_merge_reduce(MergeReduce m, const int64_t* src_off, int nsrc, hipStream_t st);
 
 // std: per-slot means of the std columns (pass 1 totals -> pass 2 centers), on device
 struct StdCenters {

@@ -106,41 +106,59 @@ def _schema(groupby_cols, agg_list, dtypes):
     return names, codes
 
 
-def _merged_to_host(handle, names, dtypes, device):
-    from .engine import ShardTable
-    t = ShardTable._wrap(handle, names, [dtypes[n] for n in names], device)
-    try:
-        return t.to_host(names)
-    finally:
-        t.close()
-
-
 def merge_partials_device(local_tables, groupby_cols, agg_list, dtypes, comm, reduced=False):
     """The client's ``aggregate=True`` merge (rpc.py:164-173) of every rank's shard results,
-    in HBM over RCCL (``bqg_merge``): ``local_tables`` are this rank's finalized shard tables
-    as device ShardTables (``ShardTable.groupby_table``), keys first.  Returns the merged table
-    (host columns) on rank 0, None elsewhere.  ``reduced``: ``local_tables`` is ONE table with
-    unique keys (``ColocatedShards`` one-pass groupby): the local re-group is skipped.  Rows
-    come grouped by key hash; the reference's order is the client's file-system glob order
-    (rpc.py:151), so compare after sorting by the keys."""
+    in HBM over RCCL (``bqg_merge_host``): ``local_tables`` are this rank's finalized shard
+    tables as device ShardTables (``ShardTable.groupby_table``), keys first.  Returns the merged
+    table (host columns, zero-copy views of the library's pinned result) on rank 0, None
+    elsewhere.  ``reduced``: ``local_tables`` is ONE table with unique keys
+    (``ColocatedShards`` one-pass groupby): the local re-group is skipped.  Rows come grouped by
+    key hash; the reference's order is the client's file-system glob order (rpc.py:151), so
+    compare after sorting by the keys."""
     from . import _lib as L
+    from .engine import _result_to_columns
     names, codes = _schema(groupby_cols, agg_list, dtypes)
     tabs = [t for t in local_tables if t is not None]
     arr = (ctypes.c_void_p * max(1, len(tabs)))(*[t.handle.value for t in tabs])
     out = ctypes.c_void_p()
     dev = comm.device
-    dev.check(L.lib().bqg_merge(dev.handle, len(tabs), arr, len(groupby_cols), len(names), codes,
-                                1 if reduced else 0, ctypes.byref(out)))
-    if comm.rank != 0:
+    dev.check(L.lib().bqg_merge_host(dev.handle, len(tabs), arr, len(groupby_cols), len(names), codes,
+                                     1 if reduced else 0, ctypes.byref(out)))
+    if comm.rank != 0 or not out.value:
         return None
-    return _merged_to_host(out, names, dtypes, dev)
+    return _result_to_columns(dev, out, names)[0]
 
 
 def merge_group_device(tables_per_rank, groupby_cols, agg_list, dtypes, group, reduced=False):
     """``merge_partials_device`` for every rank of a ``CommGroup`` from one host thread
-    (``bqg_merge_group``): ``tables_per_rank[i]`` are rank i's device tables (on
-    ``group.devices[i]``).  Returns the merged table (host columns)."""
+    (``bqg_merge_group_host``): ``tables_per_rank[i]`` are rank i's device tables (on
+    ``group.devices[i]``).  Every rank copies its reduced partition straight into its slice of
+    one pinned host result (no gather to rank 0).  Returns the merged table (host columns)."""
     from . import _lib as L
+    from .engine import _result_to_columns
+    names, codes = _schema(groupby_cols, agg_list, dtypes)
+    flat, counts = [], []
+    for tabs in tables_per_rank:
+        tabs = [t for t in tabs if t is not None]
+        counts.append(len(tabs))
+        flat += [t.handle.value for t in tabs]
+    w = group.world
+    ctxs = (ctypes.c_void_p * w)(*[d.handle.value for d in group.devices])
+    ntab = (ctypes.c_int32 * w)(*counts)
+    arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
+    out = ctypes.c_void_p()
+    t0 = time.perf_counter()
+    group.devices[0].check(L.lib().bqg_merge_group_host(w, ctxs, ntab, arr, len(groupby_cols), len(names), codes,
+                                                        1 if reduced else 0, ctypes.byref(out)))
+    LAST_MERGE.update(merge_ms=1e3 * (time.perf_counter() - t0))
+    return _result_to_columns(group.devices[0], out, names)[0]
+
+
+def merge_group_device_table(tables_per_rank, groupby_cols, agg_list, dtypes, group, reduced=False):
+    """The device-result variant (``bqg_merge_group``): the merged table gathered to rank 0 as
+    a device ShardTable (a later query can run on it in HBM)."""
+    from . import _lib as L
+    from .engine import ShardTable
     names, codes = _schema(groupby_cols, agg_list, dtypes)
     flat, counts = [], []
     for tabs in tables_per_rank:
@@ -152,17 +170,12 @@ def merge_group_device(tables_per_rank, groupby_cols, agg_list, dtypes, group, r
     ntab = (ctypes.c_int32 * w)(*counts)
     arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
     outs = (ctypes.c_void_p * w)()
-    t0 = time.perf_counter()
     group.devices[0].check(L.lib().bqg_merge_group(w, ctxs, ntab, arr, len(groupby_cols), len(names), codes,
                                                    1 if reduced else 0, outs))
-    t1 = time.perf_counter()
-    out = _merged_to_host(ctypes.c_void_p(outs[0]), names, dtypes, group.devices[0])
-    LAST_MERGE.update(merge_ms=1e3 * (t1 - t0), to_host_ms=1e3 * (time.perf_counter() - t1))
-    return out
+    return ShardTable._wrap(ctypes.c_void_p(outs[0]), names, [dtypes[n] for n in names], group.devices[0])
 
 
-# host wall time of the last merge_group_device: the library call and the result's copy to
-# host memory (profiling)
+# host wall time of the last merge_group_device (profiling)
 LAST_MERGE = {}
 
 

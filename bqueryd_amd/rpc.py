@@ -39,29 +39,78 @@ def tar_of_tars(results):
     return buf.getvalue()
 
 
-def fan_out(args, kwargs, gpu_node_files=None):
+def _is_calc_worker(info):
+    # find_free_worker skips the download / movebcolz workers (controller.py:119-121)
+    return info.get('workertype') not in ('download', 'movebcolz')
+
+
+def fan_out(args, kwargs, worker_map=None, files_map=None):
     """The controller's scatter of one groupby RPC (``handle_calc_message``,
-    controller.py:471-508) with the node-level patch of INTEGRATION.md §4: the argument lists of
-    the worker messages, in send order.  ``gpu_node_files``: {node: [its files]} for GPU nodes
-    that take all of their files in one message; used only when the client merges by sum
-    (``kwargs['aggregate'] is True``), else every file gets its own message as in the
-    reference."""
+    controller.py:471-508) with the node-level patch of INTEGRATION.md §4.
+
+    Returns the outgoing messages in send order as dicts ``{'args', 'filename', 'worker_id'}``
+    (the fields ``handle_out`` reads, controller.py:248-257).  ``worker_map`` /
+    ``files_map`` are the controller's own maps (controller.py:322-330): a calc worker that
+    registered with ``'gpu_node': True`` takes, in ONE message pinned to it by ``worker_id``,
+    every file of the RPC that ``files_map`` lists for that very worker -- so the message can
+    only reach a worker that holds all of its files, whoever else also holds the first one.
+    Used only when the client merges by sum (``kwargs['aggregate'] is True``) and a GPU worker
+    holds at least two of the files; every other file gets its own unpinned message
+    (``worker_id`` None: ``find_free_worker`` by file name), exactly as in the reference."""
     args = list(args)
     if len(args) != 4:
         raise ValueError('expecting: path_list, groupby_col_list, measure_col_list, where_terms_list')
     filenames = list(args[0])
     if not filenames:
         raise ValueError('no filenames given')
+    files_map = files_map or {}
     out = []
     covered = set()
-    if kwargs.get('aggregate') is True and gpu_node_files:
-        for node, files in gpu_node_files.items():
-            files = [f for f in files if f in filenames and f not in covered]
-            if files:
-                out.append([files] + args[1:])
-                covered.update(files)
-    out += [[f] + args[1:] for f in filenames if f not in covered]
+    if kwargs.get('aggregate') is True and worker_map:
+        for wid in sorted(worker_map):
+            info = worker_map[wid]
+            if not info.get('gpu_node') or not _is_calc_worker(info):
+                continue
+            files = [f for f in filenames if f not in covered and wid in files_map.get(f, ())]
+            if len(files) < 2:
+                continue
+            out.append({'args': [files] + args[1:], 'filename': files[0], 'worker_id': wid})
+            covered.update(files)
+    out += [{'args': [f] + args[1:], 'filename': f, 'worker_id': None} for f in filenames if f not in covered]
     return out
+
+
+def find_free_worker(worker_map, files_map, filename=None, needs_local=False, node_name=None, rng=None):
+    """``ControllerNode.find_free_worker`` (controller.py:113-144): a random non-busy calc
+    worker that has ``filename`` (a local one when ``needs_local``); None when there is none."""
+    import random
+    rng = rng or random
+    free, local = [], []
+    for wid, info in worker_map.items():
+        if not _is_calc_worker(info) or info.get('busy'):
+            continue
+        if filename and wid not in files_map.get(filename, ()):
+            continue
+        free.append(wid)
+        if info.get('node') == node_name:
+            local.append(wid)
+    if not free:
+        return None
+    if needs_local:
+        return rng.choice(local) if local else None
+    return rng.choice(free)
+
+
+def route(msg, worker_map, files_map, node_name=None, rng=None):
+    """The worker choice of ``handle_out`` (controller.py:248-257): a pinned ``worker_id`` is
+    used as is (the reference does not re-check it), ``'__needs_local__'`` and None go through
+    ``find_free_worker`` by the message's ``filename``."""
+    wid = msg.get('worker_id')
+    if wid == '__needs_local__':
+        return find_free_worker(worker_map, files_map, msg.get('filename'), True, node_name, rng)
+    if wid is None:
+        return find_free_worker(worker_map, files_map, msg.get('filename'), rng=rng)
+    return wid
 
 
 class CalcSegment:

@@ -42,7 +42,10 @@
 extern "C" {
 #endif
 
-#define BQG_ABI_VERSION 6
+/* ABI history: 5 -- bqg_timing.narrow (exact 32-bit codes on the partitioned path);
+ * 6 -- bqg_timing.narrow == 2 (packed entries) and the engine options (bqg_set_option);
+ * 7 -- bqg_merge_host / bqg_merge_group_host (merged table straight to host memory). */
+#define BQG_ABI_VERSION 7
 
 /* error codes */
 #define BQG_OK 0
@@ -267,8 +270,10 @@ int bqg_result_free(bqg_result* r);
  * time it groups by `col` (read back by where_terms_factorization_check, worker.py:298):
  * labels[nrows] (int64, host or device memory; NULL to skip) = first-appearance rank of each
  * row's value over ALL rows; values[*n_values] (column dtype; NULL to skip; at most
- * values_cap) = the distinct values in label order.  Integer columns spanning at most 2^27
- * values; otherwise BQG_E_UNSUPPORTED (no cache is written). */
+ * values_cap) = the distinct values in label order.  Every column dtype: integer columns
+ * spanning at most 2^27 values through a lookup table, any other column (floats with khash
+ * identity -0.0 == +0.0 and NaN == NaN, bools, wider integer spans) through a hash of its
+ * canonical bits.  BQG_E_INVALID when `values` holds fewer than the distinct values. */
 int bqg_factorize(bqg_ctx* ctx, bqg_table* t, int32_t col, int64_t* labels, void* values, int64_t values_cap,
                   int64_t* n_values);
 
@@ -293,7 +298,15 @@ int bqg_factorize(bqg_ctx* ctx, bqg_table* t, int32_t col, int64_t* labels, void
  *                        reference, rpc.py:151); compare after sorting by the keys.
  *   bqg_merge_group      the same for n_local ranks driven from one host thread (a process
  *                        owning several GPUs, after bqg_comm_init_all); n_tables[i] tables
- *                        of rank i follow each other in `tables`; out[i] per rank. */
+ *                        of rank i follow each other in `tables`; out[i] per rank.
+ *   bqg_merge_host       bqg_merge with the merged table returned as a host result (rank 0;
+ *                        NULL elsewhere): the gather to rank 0, then one copy to host memory.
+ *   bqg_merge_group_host bqg_merge_group with a host result: when every rank of the
+ *                        communicator is driven by this call, each rank copies its reduced
+ *                        partition straight into its slice of one pinned host result over
+ *                        its own link (no gather to rank 0); rows come in rank order.
+ * The receive-side reduce sums each key's partials in source-rank order (deterministic), and
+ * a rank's rows come in first-appearance order of the rows it received. */
 #define BQG_UNIQUE_ID_BYTES 128
 int bqg_comm_unique_id(void* out);
 int bqg_comm_init(bqg_ctx* ctx, int32_t rank, int32_t nranks, const void* unique_id);
@@ -303,12 +316,19 @@ int bqg_comm_destroy(bqg_ctx* ctx);
 int bqg_comm_info(bqg_ctx* ctx, int32_t* rank, int32_t* nranks);
 /* Profiling: host wall time (ms) of this rank's part of the last merge, per phase -- 0 local
  * re-group + pack, 1 count exchange, 2 payload exchange, 3 reduce, 4 gather counts, 5 gather
- * to rank 0; a collective step is charged to every rank of the call.  Up to n values. */
+ * to rank 0 (host results: 5 is this rank's copy to host memory, 4 the copy of the gathered
+ * table); a collective step is charged to every rank of the call.  With bqg_enable_timing
+ * every step waits for the device work it queued, so each phase holds its own device time.
+ * Up to n values. */
 int bqg_comm_last_phases(bqg_ctx* ctx, double* ms, int32_t n);
 int bqg_merge(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int32_t n_keys, int32_t n_cols,
               const int32_t* dtypes, int32_t reduced, bqg_table** out);
 int bqg_merge_group(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,
                     int32_t n_keys, int32_t n_cols, const int32_t* dtypes, int32_t reduced, bqg_table** out);
+int bqg_merge_host(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int32_t n_keys, int32_t n_cols,
+                   const int32_t* dtypes, int32_t reduced, bqg_result** out);
+int bqg_merge_group_host(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,
+                         int32_t n_keys, int32_t n_cols, const int32_t* dtypes, int32_t reduced, bqg_result** out);
 
 #ifdef __cplusplus
 }

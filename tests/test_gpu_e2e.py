@@ -183,15 +183,22 @@ def test_node_level_calc_matches_per_shard_replies(tmp_path, aggs, where, expand
     per_file = rpc.uncompress_groupby_to_df(rpc.tar_of_tars(replies), keys, aggs, where, aggregate=True)
     per_file = OrderedDict((c, per_file[c].values) for c in per_file.columns)
     assert_tables_equal(sort_by_keys(per_file, keys), sort_by_keys(ref, keys))
-    # the patched controller (restated in rpc.fan_out / rpc.CalcSegment):
-    # files 0-2 on a GPU node (one message, one reply), files 3-4 per file; the RPC completes
-    # when every file is covered and the client merge of the gathered tar is the same answer
+    # the patched controller (restated in rpc.fan_out / rpc.route /
+    # rpc.CalcSegment): files 0-2 on the GPU worker (one message pinned to it, one reply), files
+    # 3-4 per file on a CPU worker; file 0 is replicated on the CPU worker too, so an unpinned
+    # node message could have reached a worker without files 1-2.  The RPC completes when every
+    # file is covered and the client merge of the gathered tar is the same answer
+    workers = {'gpu-w': {'workertype': 'calc', 'gpu_node': True}, 'cpu-w': {'workertype': 'calc'}}
+    fmap = {f: {'gpu-w'} for f in files[:3]}
+    fmap.update({f: {'cpu-w'} for f in files[3:]})
+    fmap[files[0]] = {'gpu-w', 'cpu-w'}
     seg = rpc.CalcSegment(files)
-    sent = rpc.fan_out([files, keys, aggs, where], kwargs, {'gpu-node': files[:3]})
-    assert sent[0][0] == files[:3] and len(sent) == 3
-    for a in reversed(sent):
+    sent = rpc.fan_out([files, keys, aggs, where], kwargs, workers, fmap)
+    assert sent[0]['args'][0] == files[:3] and len(sent) == 3
+    assert [rpc.route(m, workers, fmap) for m in sent] == ['gpu-w', 'cpu-w', 'cpu-w']
+    for m in reversed(sent):
         assert not seg.complete
-        reply = calc.handle_work(_calc_msg(a[0], keys, aggs, where, **kwargs))
+        reply = calc.handle_work(_calc_msg(m['args'][0], keys, aggs, where, **kwargs))
         done = seg.add_reply(reply.get_args_kwargs()[0], reply['data'])
     assert done
     mixed = rpc.uncompress_groupby_to_df(seg.tar(), keys, aggs, where, aggregate=True)

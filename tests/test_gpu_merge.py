@@ -216,3 +216,72 @@ def test_colocated_shards_single_rank(aggs, where):
         t.close()
     ref = bo.client_merge([bo.handle_work(s, KEYS, aggs, where) for s in shards], KEYS, aggs, aggregate=True)
     assert_tables_equal(merged, ref)
+
+
+def _rank_tables(world, seed, n_tables=3, rows=40_000):
+    """Finalized per-shard tables of mixed dtypes (each table's keys unique, as a shard result
+    is): an int16 and a float64 key (-0.0 / +0.0 and NaN among them), an int32 sum that wraps,
+    a float32 sum, a raw (non-dyadic) float64 sum and an int64 count."""
+    rng = np.random.default_rng(seed)
+    fkeys = np.array([0.0, -0.0, np.nan, 1.5, -2.25, 1e300, 3.0])
+    out = []
+    for r in range(world):
+        tabs = []
+        for _ in range(n_tables):
+            a = rng.integers(-300, 300, rows).astype(np.int16)
+            f = fkeys[rng.integers(0, len(fkeys), rows)]
+            t = OrderedDict(a=a, f=f)
+            # unique keys per table: keep each (a, canonical f) once
+            code = (a.astype(np.int64) + 300) * 8 + np.searchsorted(np.array([-2.25, 0.0, 1.5, 3.0, 1e300]), np.nan_to_num(f, nan=9e300))
+            _, first = np.unique(code, return_index=True)
+            first.sort()
+            t = OrderedDict((k, v[first]) for k, v in t.items())
+            m = len(first)
+            t['s32'] = rng.integers(-2**31, 2**31 - 1, m).astype(np.int32)
+            t['f32'] = (rng.normal(size=m) * 100).astype(np.float32)
+            t['f64'] = np.round(rng.lognormal(2.3, 0.6, m), 2)
+            t['n'] = rng.integers(0, 1000, m).astype(np.int64)
+            tabs.append(t)
+        out.append(tabs)
+    return out
+
+
+@pytest.mark.parametrize('world', [1, 2, 3, 5])
+def test_merge_reduce_dtypes_and_determinism(world):
+    """The receive-side reduce (MergeReduce: one hash table, partials added in source-rank
+    order) over mixed key / value dtypes: keys compare by value (-0.0 == +0.0, NaN == NaN),
+    int32 sums wrap, float32 sums round once; the same merge twice gives bit-identical rows in
+    the same order (deterministic sums and order), and the device-table variant (gather to
+    rank 0, bqg_merge_group) gives the same rows."""
+    from bqueryd_amd.engine import Device
+    keys = ['a', 'f']
+    aggs = [['s32', 'sum', 's32'], ['f32', 'sum', 'f32'], ['f64', 'sum', 'f64'], ['n', 'sum', 'n']]
+    host = _rank_tables(world, 50 + world)
+    dtypes = OrderedDict((k, v.dtype) for k, v in host[0][0].items())
+    devs = [Device(0) for _ in range(world)]
+    per = [[ShardTable(t, device=devs[r]) for t in host[r]] for r in range(world)]
+    group = bdist.CommGroup(devs, transport='local')
+    try:
+        m1 = bdist.merge_group_device(per, keys, aggs, dtypes, group)
+        m2 = bdist.merge_group_device(per, keys, aggs, dtypes, group)
+        t3 = bdist.merge_group_device_table(per, keys, aggs, dtypes, group)
+        m3 = t3.to_host()
+        t3.close()
+    finally:
+        group.close()
+        for tabs in per:
+            for p in tabs:
+                p.close()
+    for c in m1:
+        np.testing.assert_array_equal(m1[c].view(np.uint8), m2[c].view(np.uint8), err_msg=c)
+    flat = [t for tabs in host for t in tabs]
+    ref = bo.client_merge(flat, keys, aggs, aggregate=True)
+    for got in (m1, m3):
+        g, r = sort_by_keys(got, keys), sort_by_keys(ref, keys)
+        assert list(g) == list(r)
+        for c in r:
+            if c in ('f32', 'f64'):
+                tol = 1e-6 if c == 'f32' else 1e-12
+                np.testing.assert_allclose(g[c], r[c], rtol=tol, atol=tol * float(np.abs(r[c]).max()), err_msg=c)
+            else:
+                np.testing.assert_array_equal(g[c], r[c], err_msg=c)

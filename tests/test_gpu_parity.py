@@ -186,6 +186,9 @@ def test_zero_keys_and_empty(oracle_c):
     run_both(cols, [], aggs, [('passenger_count', '>', 3)], oracle_c)
     run_both(cols, [], aggs, [('passenger_count', '>', 30)], oracle_c)
     run_both(cols, ['payment_type'], aggs, [('passenger_count', '>', 30)], oracle_c)
+    # no key, term or summed column: the scan still streams one column (count / distinct only)
+    run_both(cols, [], [['passenger_count', 'count', 'c']], [], oracle_c)
+    run_both(cols, [], [['passenger_count', 'count_distinct', 'cd'], ['fare_amount', 'count', 'c']], [], oracle_c)
     empty = OrderedDict((k, v[:0]) for k, v in cols.items())
     got, _ = ShardTable(empty).groupby([], aggs)
     ref = bo.groupby(empty, [], aggs)
@@ -224,6 +227,54 @@ def test_count_distinct_hash_set(oracle_c):
     cols = OrderedDict(k=rng.integers(0, 50, n).astype(np.int32),
                        v=rng.integers(-2**40, 2**40, 500, dtype=np.int64)[rng.integers(0, 500, n)])
     run_both(cols, ['k'], [['v', 'count_distinct', 'cd'], ['v', 'sorted_count_distinct', 'scd']], [], oracle_c)
+
+
+def _distinct_value_cols(n, seed):
+    rng = np.random.default_rng(seed)
+    fv = np.concatenate([np.array([0.0, -0.0, np.nan, -np.nan, np.inf, -np.inf, 1e-300, -1e-300]),
+                         np.round(rng.normal(size=600) * 64) / 64 + 0.001 * rng.integers(0, 3, 600)])
+    i64 = rng.integers(-2**63, 2**63 - 1, 700, dtype=np.int64)
+    i64[:2] = [-2**63, 2**63 - 1]
+    u64 = rng.integers(0, 2**64 - 1, 500, dtype=np.uint64)
+    u64[:2] = [0, 2**64 - 1]
+    return OrderedDict(
+        k1=rng.integers(0, 40, n).astype(np.int32), k2=rng.integers(0, 7, n).astype(np.int16),
+        kw=rng.integers(-2**62, 2**62, 300, dtype=np.int64)[rng.integers(0, 300, n)],
+        f64=fv[rng.integers(0, len(fv), n)], f32=fv[rng.integers(0, len(fv), n)].astype(np.float32),
+        i64=i64[rng.integers(0, len(i64), n)], u64=u64[rng.integers(0, len(u64), n)],
+        w41=rng.integers(-2**41, 2**41, 900, dtype=np.int64)[rng.integers(0, 900, n)],
+        p=rng.integers(0, 10, n).astype(np.int32))
+
+
+@pytest.mark.parametrize('keys', [['k1'], ['k1', 'k2'], ['kw'], ['kw', 'k2'], []])
+@pytest.mark.parametrize('terms', [[], [('p', '>=', 3)]])
+def test_count_distinct_float_and_wide_values(keys, terms, oracle_c):
+    """count_distinct of float values under group keys (NaN one value, -0.0 == +0.0) and of
+    integer values whose (slot x value range) pair space reaches 2^63 (full-range int64 /
+    uint64, 2^42-wide values under a multi-key group): the pair set keyed by slot and
+    representative row (bquery answers these with its per-group hash sets, worker.py:313)."""
+    cols = _distinct_value_cols(60_000, 31 + len(keys))
+    aggs = [['f64', 'count_distinct', 'cf'], ['f32', 'count_distinct', 'cf32'], ['i64', 'count_distinct', 'ci'],
+            ['u64', 'count_distinct', 'cu'], ['w41', 'count_distinct', 'cw'], ['p', 'count', 'n']]
+    run_both(cols, keys, aggs, terms, oracle_c)
+
+
+def test_count_distinct_pair_set_grows(oracle_c, engine_options):
+    """The pair set starts too small and is regrown (query re-run) until it holds every pair."""
+    cols = _distinct_value_cols(80_000, 77)
+    engine_options(distinct_slots=1024)
+    run_both(cols, ['k1', 'k2'], [['f64', 'count_distinct', 'cf'], ['i64', 'count_distinct', 'ci']], [], oracle_c)
+
+
+def test_count_distinct_c4_fare(oracle_c):
+    """C4's query shape with fare_amount (float64, cent-rounded) as the distinct column."""
+    cols = synth.taxi_shard(300_000, config_id=4, columns=('pu_location_id', 'passenger_count', 'fare_amount'),
+                            variant='raw')
+    run_both(cols, ['pu_location_id'], [['fare_amount', 'count_distinct', 'fcd'],
+                                        ['passenger_count', 'sorted_count_distinct', 'pscd']], [], oracle_c)
+    run_both(cols, ['pu_location_id'], [['fare_amount', 'count_distinct', 'fcd'],
+                                        ['fare_amount', 'sorted_count_distinct', 'fscd']],
+             [('passenger_count', '>', 1)], oracle_c)
 
 
 @pytest.mark.parametrize('krange', [300, 20_000, 400_000])
@@ -404,6 +455,42 @@ def test_partitioned_launch_shapes(threads, splits, per_cu, oracle_c, engine_opt
                        f=np.where(np.arange(n) // 5000 % 3 == 1, 0, rng.integers(1, 5, n)).astype(np.int16))
     run_both(cols, ['k'], [['v', 'sum', 's'], ['v', 'count', 'c']], [], oracle_c, exact=True)
     run_both(cols, ['k'], [['v', 'sum', 's'], ['v', 'mean', 'm']], [('f', '>', 0)], oracle_c, exact=True)
+
+
+@pytest.mark.parametrize('splits', [1, 2, 3])
+@pytest.mark.parametrize('entries', ['packed', 'narrow', 'wide'])
+def test_partitioned_aggregate_window_boundaries(splits, entries, oracle_c, engine_options):
+    """The aggregate's window walk at its edges (k_part_aggregate: kAggWin = 1024 tiles of
+    bounds per window, chunks of <= 8 tiles): 1024-row tiles (256 scatter threads, part_k 1)
+    over 2,500,037 rows = 2442 tiles, so one split walks windows of 1024 + 1024 + 394 tiles and
+    two splits 1024 + 197 each -- more tiles per split than one window, a last window that ends
+    inside a chunk, a partial last tile -- and three splits (more splits than tiles / kAggWin)
+    one window each; for packed, narrow (8-byte) and wide (12-byte) entries.  (Round-3 record:
+    an illegal address in an aggregate experiment never committed; this pins the kept kernel's
+    window / sentinel / granule indexing at these shapes.)"""
+    engine_options(part_threads=256, part_k=1, part_splits=splits)
+    if entries != 'packed':
+        engine_options(part_pack=0)
+    if entries == 'wide':
+        engine_options(part_narrow=0)
+    rng = np.random.default_rng(1000 + splits)
+    n = 2_500_037
+    cols = OrderedDict(k=rng.integers(0, 400_000, n).astype(np.int32),
+                       v=np.round(rng.normal(size=n) * 300) / 64,
+                       f=rng.integers(0, 4, n).astype(np.int8))
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(['k'], [['v', 'sum', 'vs'], ['v', 'count', 'n']])
+        info = t.dev.last_timing()
+        got_f, _ = t.groupby(['k'], [['v', 'sum', 'vs']], where_terms=[('f', '>', 0)])
+    finally:
+        t.close()
+    assert info['mode'] == 4 and bool(info['pack16']) == (entries == 'packed')
+    assert bool(info['narrow']) == (entries != 'wide')
+    ref = oracle_c.groupby(cols, ['k'], [['v', 'sum', 'vs'], ['v', 'count', 'n']], None)
+    ref_f = oracle_c.groupby(cols, ['k'], [['v', 'sum', 'vs']], oracle_c.where_terms(cols, [('f', '>', 0)]))
+    assert_tables_equal(got, ref, exact_cols={'vs'})
+    assert_tables_equal(got_f, ref_f, exact_cols={'vs'})
 
 
 def _groupby_info(cols, keys, aggs, opts=None):

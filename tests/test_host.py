@@ -160,17 +160,64 @@ def test_ctable_tar_matches_tar_of_written_ctable(tmp_path, nrows):
         np.testing.assert_array_equal(back[0][c], cols[c])
 
 
+def test_node_message_routing_pins_the_gpu_worker():
+    """The node-level message is pinned to the GPU calc worker that holds ALL of its files,
+    so handle_out (controller.py:248-257) cannot hand it to another worker that holds only the
+    first file; replicated files on a CPU worker keep their per-file path."""
+    import random
+    files = ['f%d.bcolzs' % i for i in range(6)]
+    spec = [files, ['k'], [['s', 'sum', 's']], []]
+    workers = {
+        'cpu0': {'workertype': 'calc', 'node': 'n0'},            # holds f0 (and f5) too
+        'dl0': {'workertype': 'download', 'node': 'n1'},
+        'gpuA': {'workertype': 'calc', 'node': 'n1', 'gpu_node': True},
+        'gpuB': {'workertype': 'calc', 'node': 'n2', 'gpu_node': True},  # holds only f4
+    }
+    fmap = {'f0.bcolzs': {'cpu0', 'gpuA'}, 'f1.bcolzs': {'gpuA'}, 'f2.bcolzs': {'gpuA', 'dl0'},
+            'f3.bcolzs': {'gpuA'}, 'f4.bcolzs': {'gpuB'}, 'f5.bcolzs': {'cpu0'}}
+    out = rpc.fan_out(spec, {'aggregate': True}, workers, fmap)
+    node = [m for m in out if isinstance(m['args'][0], list)]
+    assert len(node) == 1 and node[0]['worker_id'] == 'gpuA'
+    assert node[0]['args'][0] == files[:4] and node[0]['filename'] == 'f0.bcolzs'
+    per_file = [m for m in out if not isinstance(m['args'][0], list)]
+    assert [m['filename'] for m in per_file] == ['f4.bcolzs', 'f5.bcolzs']  # gpuB holds one file only
+    for seed in range(50):
+        rng = random.Random(seed)
+        # pinned: whichever workers are free, the node message goes to gpuA
+        assert rpc.route(node[0], workers, fmap, rng=rng) == 'gpuA'
+        # an unpinned message for f0 (the pre-patch behaviour) may reach cpu0 -- the bug the pin fixes
+        assert rpc.route({'filename': 'f0.bcolzs', 'worker_id': None}, workers, fmap, rng=rng) in ('cpu0', 'gpuA')
+        assert rpc.route(per_file[0], workers, fmap, rng=rng) == 'gpuB'
+        assert rpc.route(per_file[1], workers, fmap, rng=rng) == 'cpu0'
+    seen = {rpc.route({'filename': 'f0.bcolzs', 'worker_id': None}, workers, fmap, rng=random.Random(s))
+            for s in range(50)}
+    assert seen == {'cpu0', 'gpuA'}
+    # busy workers are skipped by find_free_worker (controller.py:123-124); needs_local keeps the node
+    busy = dict(workers, cpu0=dict(workers['cpu0'], busy=True))
+    assert rpc.route({'filename': 'f5.bcolzs', 'worker_id': None}, busy, fmap) is None
+    assert rpc.route({'filename': 'f1.bcolzs', 'worker_id': '__needs_local__'}, workers, fmap, node_name='n1') == 'gpuA'
+    assert rpc.route({'filename': 'f1.bcolzs', 'worker_id': '__needs_local__'}, workers, fmap, node_name='n0') is None
+    # a GPU worker never gets a node message for files it does not hold: no files -> per-file only
+    assert all(m['worker_id'] is None for m in rpc.fan_out([['f5.bcolzs', 'f4.bcolzs'], ['k'], [], []],
+                                                           {'aggregate': True}, workers, fmap))
+
+
 def test_fan_out_and_gather_accounting(tmp_path):
     """controller.py:471-508 scatter and 146-221 gather, with the node-level patch: the RPC
     completes only when every file is covered, by its own reply or by a node reply."""
     files = ['f%d.bcolzs' % i for i in range(5)]
     spec = [files, ['k'], [['s', 'sum', 's']], []]
+    workers = {'gpu0': {'gpu_node': True, 'workertype': 'calc'}, 'gpu1': {'gpu_node': True, 'workertype': 'calc'}}
+    fmap = {f: {'gpu0'} for f in files[:3]}
+    fmap['other.bcolzs'] = {'gpu1'}
     # without aggregate=True (or without GPU nodes) every file gets its own message
-    assert [a[0] for a in rpc.fan_out(spec, {})] == files
-    assert [a[0] for a in rpc.fan_out(spec, {'aggregate': False}, {'n': files[:3]})] == files
-    msgs = rpc.fan_out(spec, {'aggregate': True}, {'gpu0': files[:3], 'gpu1': ['other.bcolzs']})
-    assert msgs[0][0] == files[:3] and [m[0] for m in msgs[1:]] == files[3:]
-    assert all(m[1:] == spec[1:] for m in msgs)
+    assert [m['args'][0] for m in rpc.fan_out(spec, {})] == files
+    assert [m['args'][0] for m in rpc.fan_out(spec, {'aggregate': False}, workers, fmap)] == files
+    out = rpc.fan_out(spec, {'aggregate': True}, workers, fmap)
+    assert out[0]['args'][0] == files[:3] and out[0]['worker_id'] == 'gpu0'
+    assert [m['args'][0] for m in out[1:]] == files[3:] and all(m['worker_id'] is None for m in out[1:])
+    assert all(m['args'][1:] == spec[1:] for m in out)
+    msgs = [m['args'] for m in out]
     with pytest.raises(ValueError):
         rpc.fan_out([[], ['k'], [], []], {})
     tables = []
@@ -202,7 +249,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(declared) == set(_lib._PROTOS), set(declared) ^ set(_lib._PROTOS)
-    assert lib.bqg_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.bqg_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_library_fails_loudly_without_gpu():
