@@ -174,17 +174,38 @@ def _json_bytes(obj):
     return json.dumps(obj, ensure_ascii=True).encode('ascii') + b'\n'
 
 
-def carray_files(arr, chunklen=None, clevel=5, shuffle=1, cname='lz4'):
-    """The files of a carray directory: [(path relative to the carray rootdir, bytes)]."""
+# Compression pool: a result's chunks are compressed in parallel (libblosc releases the GIL
+# through ctypes), one blosc context per chunk -- the frames are byte-identical to a serial
+# compression.  bqueryd compresses results on the worker's one thread (bcolz.set_nthreads(1),
+# worker.py:40): a 1 M-group result took ~29 ms of host time that way, >90 % of a C3 message.
+_POOL = None
+_PARALLEL_MIN_BYTES = 4 << 20
+
+
+def _pool():
+    global _POOL
+    if _POOL is None:
+        _POOL = ThreadPoolExecutor(max_workers=max(1, min(16, os.cpu_count() or 1)),
+                                   thread_name_prefix='bqgpu-blosc')
+    return _POOL
+
+
+def carray_files(arr, chunklen=None, clevel=5, shuffle=1, cname='lz4', frames=None):
+    """The files of a carray directory: [(path relative to the carray rootdir, bytes)].
+    ``frames``: the column's compressed chunks when the caller already has them."""
     arr = np.ascontiguousarray(arr)
     if arr.dtype.kind not in 'biuf':
         raise NotImplementedError('bcolz writer: dtype %s' % arr.dtype)
     n = len(arr)
     chunklen = chunklen or _chunklen_for(arr.dtype.itemsize, n)
+    if frames is None:
+        los = range(0, n, chunklen)
+        comp = lambda lo: compress_chunk(arr[lo:lo + chunklen], clevel, shuffle, cname)  # noqa: E731
+        frames = list(_pool().map(comp, los)) if arr.nbytes >= _PARALLEL_MIN_BYTES and len(los) > 1 else \
+            [comp(lo) for lo in los]
     files = []
     cbytes = 0
-    for i, lo in enumerate(range(0, n, chunklen)):
-        frame = compress_chunk(arr[lo:lo + chunklen], clevel, shuffle, cname)
+    for i, frame in enumerate(frames):
         files.append(('data/__%d.blp' % i, bloscpack_header(1) + frame))
         cbytes += len(frame) + BLOSCPACK_HEADER
     files.append(('meta/storage', _storage_json(arr.dtype, clevel, shuffle, cname, int(chunklen), int(max(n, 1)))))
@@ -329,13 +350,30 @@ def ctable_tar(columns, arcname, chunklen=None, cname='lz4'):
         out.append(_tar_header(name + '/', 0, 0o755, now, True))
 
     names = list(columns.keys())
+    # every column's chunks, compressed on the pool when the result is large
+    arrays = {n: np.ascontiguousarray(columns[n]) for n in names}
+    for n, a in arrays.items():
+        if a.dtype.kind not in 'biuf':
+            raise NotImplementedError('bcolz writer: dtype %s' % a.dtype)
+    clen = {n: chunklen or _chunklen_for(a.dtype.itemsize, len(a)) for n, a in arrays.items()}
+    jobs = [(n, lo) for n in names for lo in range(0, len(arrays[n]), clen[n])]
+    total = sum(a.nbytes for a in arrays.values())
+
+    def comp(job):
+        n, lo = job
+        return compress_chunk(arrays[n][lo:lo + clen[n]], 5, 1, cname)
+
+    done = list(_pool().map(comp, jobs)) if total >= _PARALLEL_MIN_BYTES and len(jobs) > 1 else [comp(j) for j in jobs]
+    frames = {n: [] for n in names}
+    for (n, _), f in zip(jobs, done):
+        frames[n].append(f)
     root = {ATTRS: _json_bytes({}), ROOTDIRS: _json_bytes({'names': names, 'dirs': {n: n for n in names}})}
     directory(arcname)
     for entry in sorted(list(root) + names):
         if entry in root and entry not in columns:
             member(arcname + '/' + entry, root[entry])
             continue
-        files = dict(carray_files(columns[entry], chunklen=chunklen, cname=cname))
+        files = dict(carray_files(arrays[entry], chunklen=clen[entry], cname=cname, frames=frames[entry]))
         cdir = arcname + '/' + entry
         directory(cdir)
         member(cdir + '/' + ATTRS, files.pop(ATTRS))

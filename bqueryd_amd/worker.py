@@ -28,6 +28,7 @@ import os
 import random
 import shutil
 import string
+import time
 from collections import OrderedDict
 
 import numpy as np
@@ -127,6 +128,7 @@ class CalcPath:
         self.device = device or get_device()
         self.cache = cache if cache is not None else ShardCache(device=self.device)
         self._node = None  # node-level state, created by the first multi-file message
+        self.last_stages = {}  # host wall time per stage of the last message
 
     def handle_work(self, msg):
         if msg.isa('execute_code'):
@@ -142,10 +144,16 @@ class CalcPath:
         rootdir = os.path.join(self.data_dir, filename)
         if not os.path.exists(rootdir):
             raise Exception('Path %s does not exist' % rootdir)
+        t0 = time.perf_counter()
         ct = self.cache.open(rootdir)
+        t1 = time.perf_counter()
         result = _shard_calc(ct, groupby_col_list, aggregation_list, where_terms_list, expand_filter_column,
                              aggregate)
+        t2 = time.perf_counter()
         msg['data'] = '' if result is None else bcolz_io.ctable_tar(result, result_name())
+        # per-message stage timings (the reference only logs the RPC's wall time)
+        self.last_stages = {'open_s': t1 - t0, 'calc_s': t2 - t1, 'result_tar_s': time.perf_counter() - t2,
+                            'groups': 0 if result is None else len(next(iter(result.values()), ()))}
         return msg
 
     # ---- node-level calc (co-located shards)
@@ -173,6 +181,7 @@ class CalcPath:
             if where_terms_list and not ct.where_terms_factorization_check(where_terms_list):
                 continue  # this shard's reply would be '' (worker.py:298-301): nothing to merge
             shards[r].append(ct)
+        t_open = time.perf_counter()
         names = list(groupby_col_list) + [x[2] for x in aggregation_list]
         dtypes = None
         fused = dist.decomposable(aggregation_list) and not expand_filter_column
@@ -200,6 +209,7 @@ class CalcPath:
             if dtypes is None and per_rank[r]:
                 t0 = per_rank[r][0]
                 dtypes = OrderedDict((n, t0.dtypes[n]) for n in t0.names)
+        t_calc = time.perf_counter()
         try:
             if dtypes is None:
                 msg['data'] = ''  # no shard can contribute a row
@@ -210,9 +220,12 @@ class CalcPath:
             for tabs in per_rank:
                 for t in tabs:
                     t.close()
+        t_merge = time.perf_counter()
         merged = OrderedDict((n, np.asarray(merged[n])) for n in names)
         msg['data'] = bcolz_io.ctable_tar(merged, result_name())
         msg['filenames'] = list(filenames)
+        self.last_stages = {'calc_s': t_calc - t_open, 'merge_s': t_merge - t_calc,
+                            'result_tar_s': time.perf_counter() - t_merge, 'groups': len(merged[names[0]])}
         return msg
 
     def _node_state(self):

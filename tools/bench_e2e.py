@@ -61,16 +61,79 @@ def _cpu_task(args):
     return data, time.perf_counter() - t0
 
 
+def _large_message(args):
+    """C3 / C5 message-level cost on one GPU: the bcolz shard(s) on disk, resident in HBM after
+    a first message (the worker's steady state), then per message: shard-cache lookup, the
+    query (device passes + the result's copy to host memory) and the result ctable + tar
+    (worker.py:335-346), timed per stage (CalcPath.last_stages); and the unchanged client's
+    untar + merge of that one reply (rpc.py:134-179).
+      c3: one 100 M-row shard, groupby (pickup_location, vendor_id), sum / count (~1 M groups);
+      c5: one node-level message over one GPU's 10 x 12.5 M-row shards (one pass over the
+          union + the world-1 merge, ~1 M groups) -- a rank's share of C5."""
+    from bqueryd_amd import bcolz_io, messages, rpc, synth
+    from bqueryd_amd.engine import get_device
+    from bqueryd_amd.worker import CalcPath
+    cfg = synth.CONFIGS[args.config]
+    cols_needed = synth.query_columns(cfg)
+    if args.config == 'c3':
+        n_shards, rows = 1, args.rows or cfg['rows']
+    else:
+        n_shards, rows = args.shards or 10, args.rows or cfg['rows'] // cfg['shards']
+    data_dir = tempfile.mkdtemp(prefix='bqgpu_%s_' % args.config)
+    try:
+        files = []
+        for i in range(n_shards):
+            cols = synth.taxi_shard(rows, config_id=synth.CONFIG_ID[args.config], n_shards=max(n_shards, cfg.get('shards', 1)),
+                                    shard=i, columns=cols_needed)
+            fn = 'tripdata-%d.bcolzs' % i
+            bcolz_io.write_ctable(os.path.join(data_dir, fn), cols)
+            files.append(fn)
+            del cols
+        dev = get_device()
+        calc = CalcPath(data_dir, device=dev)
+        m = messages.CalcMessage({'payload': 'groupby', 'token': 'ab' * 8, 'filename': files[0]})
+        m.set_args_kwargs([files[0] if args.config == 'c3' else list(files), cfg['groupby'], cfg['aggs'], cfg['where']],
+                          {'aggregate': True})
+        calc.handle_work(m)  # load + warm
+        best = None
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            data = calc.handle_work(m)['data']
+            t1 = time.perf_counter()
+            df = rpc.uncompress_groupby_to_df(rpc.tar_of_tars({files[0]: data}), cfg['groupby'], cfg['aggs'],
+                                              cfg['where'], aggregate=True, device=dev)
+            t2 = time.perf_counter()
+            if best is None or t1 - t0 < best['message_s']:
+                best = dict(message_s=t1 - t0, client_merge_s=t2 - t1, reply_bytes=len(data),
+                            groups=int(len(df)), **calc.last_stages)
+        total = n_shards * rows
+        line = {'workload': '%s message level: %d bcolz shard(s) x %d rows resident in HBM, groupby %s, aggs %s, '
+                            'aggregate=True%s' % (args.config.upper(), n_shards, rows, cfg['groupby'],
+                                                 [a[1] for a in cfg['aggs']],
+                                                 ', one node-level message (world 1)' if args.config == 'c5' else ''),
+                'rows': total, 'gpu_warm': dict(best, rows_per_s=total / best['message_s']),
+                'host_threads_for_result_compression': bcolz_io._pool()._max_workers}
+        print(json.dumps(line), flush=True)
+    finally:
+        shutil.rmtree(data_dir, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--shards', type=int, default=10)
-    ap.add_argument('--rows', type=int, default=1_000_000)
+    ap.add_argument('--config', default='c1', choices=['c1', 'c3', 'c5'])
+    ap.add_argument('--shards', type=int, default=None)
+    ap.add_argument('--rows', type=int, default=None)
     ap.add_argument('--reps', type=int, default=5)
-    ap.add_argument('--cpu-workers', type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument('--cpu-workers', type=int, default=None,
+                    help='C1 CPU port: worker processes (default: 2, as BASELINE configs[0] states, and all cores)')
     ap.add_argument('--no-gpu', action='store_true')
     ap.add_argument('--profile', default=None,
                     help='write a cProfile summary of 50 warm per-file messages (handle_work) to this file')
     args = ap.parse_args()
+    if args.config != 'c1':
+        return _large_message(args)
+    args.shards = args.shards or 10
+    args.rows = args.rows or 1_000_000
 
     from bqueryd_amd import bcolz_io, messages, rpc, synth
     from oracle import bquery_oracle as bo
@@ -173,25 +236,30 @@ def main():
                                      'note': 'one node-level message (args[0] = the files, aggregate=True): one '
                                              'pass over the resident shard union + RCCL merge, one reply'}
 
-        # CPU: the reference's architecture (one calc per shard on a pool of worker processes)
+        # CPU: the reference's architecture (one calc per shard on a pool of worker processes):
+        # 2 workers as BASELINE configs[0] states ("CPU controller + 2 workers"), and all cores
+        from oracle import cpu_cluster
         ctx = mp.get_context('spawn')  # no fork of a process that initialised the GPU
-        with ctx.Pool(args.cpu_workers) as pool:
-            pool.map(_cpu_task, [(os.path.join(data_dir, files[0]),)])
-            best = None
-            for _ in range(args.reps):
-                t0 = time.perf_counter()
-                res = pool.map(_cpu_task, [(os.path.join(data_dir, fn),) for fn in files])
-                reply = rpc.tar_of_tars(OrderedDict((fn, r[0]) for fn, r in zip(files, res)))
-                merged = bo.client_merge(rpc.read_shard_results(reply), GROUPBY, AGGS, aggregate=True)
-                dt = time.perf_counter() - t0
-                calc_s = sum(r[1] for r in res)
-                if best is None or dt < best[0]:
-                    best = (dt, calc_s)
-            check(merged)
-        line['cpu_port'] = {'s_per_query': best[0], 'rows_per_s': total_rows / best[0],
-                            'calc_core_s': best[1], 'workers': args.cpu_workers, 'kind': 'port',
-                            'note': 'per shard in worker processes: bcolz decode (1 thread) + oracle/cbquery.c '
-                                    'calc + result ctable + tar; tar of tars; client untar + oracle merge'}
+        counts = [args.cpu_workers] if args.cpu_workers else sorted({2, cpu_cluster.host_cores()})
+        for nw in counts:
+            with ctx.Pool(nw) as pool:
+                pool.map(_cpu_task, [(os.path.join(data_dir, files[0]),)])
+                best = None
+                for _ in range(args.reps):
+                    t0 = time.perf_counter()
+                    res = pool.map(_cpu_task, [(os.path.join(data_dir, fn),) for fn in files])
+                    reply = rpc.tar_of_tars(OrderedDict((fn, r[0]) for fn, r in zip(files, res)))
+                    merged = bo.client_merge(rpc.read_shard_results(reply), GROUPBY, AGGS, aggregate=True)
+                    dt = time.perf_counter() - t0
+                    calc_s = sum(r[1] for r in res)
+                    if best is None or dt < best[0]:
+                        best = (dt, calc_s)
+                check(merged)
+            key = 'cpu_port' if nw == 2 or len(counts) == 1 else 'cpu_port_all_cores'
+            line[key] = {'s_per_query': best[0], 'rows_per_s': total_rows / best[0],
+                         'calc_core_s': best[1], 'workers': nw, 'kind': 'port', 'cpu_model': cpu_cluster.cpu_model(),
+                         'note': 'per shard in worker processes: bcolz decode (1 thread) + oracle/cbquery.c '
+                                 'calc + result ctable + tar; tar of tars; client untar + oracle merge'}
         print(json.dumps(line), flush=True)
     finally:
         shutil.rmtree(data_dir, ignore_errors=True)
