@@ -139,6 +139,7 @@ _PROTOS = {
     'bqg_hash_partition': ([_P, _P, _I32, _P, _I32, _I32, _P], ctypes.c_int),
     'bqg_result_free': ([_P], ctypes.c_int),
     'bqg_factorize': ([_P, _P, _I32, _P, _P, _I64, ctypes.POINTER(_I64)], ctypes.c_int),
+    'bqg_encode_bytes': ([_P, _P, _I32, _P, _I32, _P, _I64, ctypes.POINTER(_I64)], ctypes.c_int),
 }
 
 _lib = None

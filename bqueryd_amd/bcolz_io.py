@@ -194,7 +194,7 @@ def carray_files(arr, chunklen=None, clevel=5, shuffle=1, cname='lz4', frames=No
     """The files of a carray directory: [(path relative to the carray rootdir, bytes)].
     ``frames``: the column's compressed chunks when the caller already has them."""
     arr = np.ascontiguousarray(arr)
-    if arr.dtype.kind not in 'biuf':
+    if arr.dtype.kind not in _WRITABLE_KINDS:
         raise NotImplementedError('bcolz writer: dtype %s' % arr.dtype)
     n = len(arr)
     chunklen = chunklen or _chunklen_for(arr.dtype.itemsize, n)
@@ -215,11 +215,14 @@ def carray_files(arr, chunklen=None, clevel=5, shuffle=1, cname='lz4', frames=No
 
 
 _EMPTY_ATTRS = b'{}\n'
+# numeric, bool, fixed-width bytes / unicode and datetime64 / timedelta64 columns (the dtypes a
+# bqueryd shard built with ctable.fromdataframe holds; blosc's typesize is the element size)
+_WRITABLE_KINDS = 'biufSUMm'
 
 
 @functools.lru_cache(maxsize=1024)
 def _storage_json(dtype, clevel, shuffle, cname, chunklen, expectedlen):
-    dflt = False if dtype.kind == 'b' else (0.0 if dtype.kind == 'f' else 0)
+    dflt = False if dtype.kind == 'b' else (0.0 if dtype.kind == 'f' else ('' if dtype.kind in 'SU' else 0))
     return _json_bytes({'dtype': str(dtype), 'cparams': {'clevel': clevel, 'shuffle': shuffle, 'cname': cname, 'quantize': 0},
                         'chunklen': chunklen, 'expectedlen': expectedlen, 'dflt': dflt})
 
@@ -353,7 +356,7 @@ def ctable_tar(columns, arcname, chunklen=None, cname='lz4'):
     # every column's chunks, compressed on the pool when the result is large
     arrays = {n: np.ascontiguousarray(columns[n]) for n in names}
     for n, a in arrays.items():
-        if a.dtype.kind not in 'biuf':
+        if a.dtype.kind not in _WRITABLE_KINDS:
             raise NotImplementedError('bcolz writer: dtype %s' % a.dtype)
     clen = {n: chunklen or _chunklen_for(a.dtype.itemsize, len(a)) for n, a in arrays.items()}
     jobs = [(n, lo) for n in names for lo in range(0, len(arrays[n]), clen[n])]

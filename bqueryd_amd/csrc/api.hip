@@ -357,11 +357,7 @@ struct bqg_ctx {
   ColumnPool colpool;
   IngestPool ingest;  // cold-path staging: streams + pinned double buffers per decode thread
   int cu = 256;
-  // the merge's re-groups run the query-specialised kernels at any size (their shape repeats
-  // and the compiled kernels are cached): a per-call override of jit_min_rows that leaves the
-  // user-visible option untouched (bqg_internal_jit_min_override; -1: none)
-  int64_t jit_min_override = -1;
-  int64_t jit_min_rows() const { return jit_min_override >= 0 ? jit_min_override : opt[kOptJitMinRows]; }
+  int64_t jit_min_rows() const { return opt[kOptJitMinRows]; }
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
@@ -372,6 +368,7 @@ struct bqg_ctx {
   int stage_i = 0;
   // scratch
   DevBuf partials, counter, hdr, slots, terms, outcols, lists, bitmap, prefix, cdbuf, scdbuf, mask, misc, done;
+  DevBuf strings;  // bqg_encode_bytes: the staged bytes and the dictionary's work arrays
   HostBuf hhdr, hout;
   // pinned blocks for results (returned by bqg_result_free); shared with outstanding results
   // so a result may outlive its context
@@ -1706,7 +1703,6 @@ int bqg_internal_host_result(bqg_ctx* c, int64_t n, const std::vector<int32_t>& 
     return BQG_E_OOM;
   }
 }
-void bqg_internal_jit_min_override(bqg_ctx* c, int64_t rows) { c->jit_min_override = rows; }
 
 // ======================================================================================
 // C ABI
@@ -2279,6 +2275,65 @@ int bqg_hash_partition(bqg_ctx* c, bqg_table* t, int32_t n_keys, const int32_t* 
     HIPCHECK(hipMemcpyAsync(counts, d, (size_t)nparts * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
     t->cols[out_col].stats.valid = false;
+  });
+}
+
+int bqg_encode_bytes(bqg_ctx* c, bqg_table* t, int32_t out_col, const void* bytes, int32_t width, void* values,
+                     int64_t values_cap, int64_t* n_values) {
+  return guard(c, [&] {
+    if (!t || out_col < 0 || out_col >= (int)t->cols.size() || t->cols[out_col].dtype != BQG_I32)
+      fail(BQG_E_INVALID, "bqg_encode_bytes: output must be an INT32 column of the table");
+    if (width < 1 || width > 4096) fail(BQG_E_INVALID, "bqg_encode_bytes: width %d out of range", width);
+    if (!n_values || (t->nrows > 0 && !bytes)) fail(BQG_E_INVALID, "bqg_encode_bytes: null argument");
+    const int64_t n = t->nrows;
+    *n_values = 0;
+    Column& out = t->cols[out_col];
+    out.stats.valid = false;
+    if (n == 0) return;
+    if ((uint64_t)n >= 0xFFFFFFFFull) fail(BQG_E_UNSUPPORTED, "bqg_encode_bytes: 2^32 rows or more");
+    uint64_t cap = 1024;
+    while (cap < 2 * (uint64_t)n) cap <<= 1;
+    const uint64_t nwords = ((uint64_t)n + 31) / 32, nblocks = (nwords + 1023) / 1024;
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t o_data = 0, o_table = al((size_t)n * width), o_first = o_table + al(cap * 8),
+                 o_slot = o_first + al(cap * 4), o_bits = o_slot + al((size_t)n * 4),
+                 o_wp = o_bits + al(nwords * 4 + 4), o_bs = o_wp + al(nwords * 4 + 4),
+                 o_cnt = o_bs + al(nblocks * 4 + 4), o_vals = o_cnt + 256, total = o_vals + al((size_t)n * width);
+    unsigned char* b = (unsigned char*)c->strings.ensure(total);
+    hipStream_t st = c->stream;
+    HIPCHECK(hipMemcpyAsync(b + o_data, bytes, (size_t)n * width,
+                            mem_kind(bytes) == 2 ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    BytesEncode e{};
+    e.data = b + o_data;
+    e.n = n;
+    e.width = width;
+    e.table = (unsigned long long*)(b + o_table);
+    e.mask = cap - 1;
+    e.first = (uint32_t*)(b + o_first);
+    e.row_slot = (uint32_t*)(b + o_slot);
+    e.rep_bits = (unsigned int*)(b + o_bits);
+    e.word_prefix = (unsigned int*)(b + o_wp);
+    e.block_sum = (unsigned int*)(b + o_bs);
+    e.groups = (unsigned long long*)(b + o_cnt);
+    e.overflow = (unsigned int*)(b + o_cnt + 8);
+    e.codes = (int32_t*)out.dev;
+    e.values = b + o_vals;
+    HIPCHECK(hipMemsetAsync(e.overflow, 0, 8, st));
+    launch_bytes_encode(e, st);
+    HIPCHECK(hipGetLastError());
+    unsigned long long* h = (unsigned long long*)c->hhdr.ensure(64);
+    HIPCHECK(hipMemcpyAsync(h, e.groups, 16, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (h[1] & 0xFFFFFFFFull) fail(BQG_E_HIP, "bqg_encode_bytes: dictionary table overflow");
+    const int64_t G = (int64_t)h[0];
+    *n_values = G;
+    if (values) {
+      if (G > values_cap) fail(BQG_E_INVALID, "values buffer holds %lld, column has %lld distinct values",
+                               (long long)values_cap, (long long)G);
+      HIPCHECK(hipMemcpyAsync(values, e.values, (size_t)G * width,
+                              mem_kind(values) == 2 ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+    }
   });
 }
 

@@ -5,8 +5,8 @@
 // re-grouped with `sum` of every column ("we can only sum now", bqueryd/rpc.py:164-173).  For
 // shards that live on one node's GPUs the same merge runs here, on device buffers:
 //   1. local:     this rank's shard tables are concatenated (device to device) and summed by
-//                 key (bqg_groupby_table) -- skipped when the caller's one table is already
-//                 reduced (a co-located one-pass groupby over the rank's shards);
+//                 key (MergeReduce: one hash table, tables in order) -- skipped when the
+//                 caller's one table is already reduced (a co-located one-pass groupby);
 //   2. partition: every row goes to rank hash(key values) mod nranks (the partition function
 //                 of bqg_hash_partition: a pure function of the values, identical on every
 //                 rank) -- one stable scatter (k_mpack_*) writes each row straight into its
@@ -15,15 +15,18 @@
 //                 read of the exchange), then the payload (grouped ncclSend / ncclRecv, one
 //                 message per peer and column, self included) straight into the receiving
 //                 rank's table columns;
-//   4. reduce:    the received rows are summed by key again (keys are disjoint across ranks);
-//   5. gather:    the reduced partitions travel to rank 0 column by column (grouped send /
-//                 recv), straight into the result table, in rank order.
+//   4. reduce:    the received rows are summed by key again (MergeReduce, sources in rank
+//                 order; keys are disjoint across ranks);
+//   5. output:    the reduced partitions travel to rank 0 column by column (grouped send /
+//                 recv), straight into the result table, in rank order -- or, when one process
+//                 drives every rank and wants host memory (bqg_merge_group_host), each rank
+//                 copies its partition straight into its slice of one pinned host result.
 // Only the row counts cross to the host (to size buffers).  librccl is loaded with dlopen on
 // first use, so libbqgpu itself loads where RCCL is absent; every entry here then fails with
 // a message instead.
 //
-// The merge is built from the library's own public entry points (groupby, push) plus the pack
-// kernels; this file adds the communicator and the exchange.  It runs any number of
+// The merge is built from the library's own public entry points (table create, push) plus the
+// pack and reduce kernels (k_misc.hip); this file adds the communicator and the exchange.  It runs any number of
 // local ranks from ONE host thread: bqg_merge drives one rank of a multi-process job (one
 // process per GPU), bqg_merge_group every rank of a process that owns several GPUs, with the
 // collective calls of all of them inside one ncclGroupStart / ncclGroupEnd.
@@ -269,35 +272,8 @@ bqg_table* concat_tables(bqg_ctx* c, const std::vector<bqg_table*>& parts, const
     off += n;
   }
   // no bqg_table_sync: the copies are ordered on the context's stream before anything that
-  // reads the table, and the regroup's planner computes the key statistics it needs
+  // reads the table
   return out.release();
-}
-
-// The client's re-group: sum of every non-key column by the first n_keys columns.
-bqg_table* regroup(bqg_ctx* c, bqg_table* t, int n_keys, int ncols) {
-  std::vector<int32_t> keys(std::max(1, n_keys));
-  for (int k = 0; k < n_keys; ++k) keys[k] = k;
-  std::vector<bqg_agg> aggs(std::max(1, ncols - n_keys));
-  for (int j = n_keys; j < ncols; ++j) aggs[j - n_keys] = bqg_agg{j, BQG_SUM};
-  bqg_query q{};
-  q.n_keys = n_keys;
-  q.key_cols = keys.data();
-  q.n_terms = 0;
-  q.terms = nullptr;
-  q.mask_col = -1;
-  q.n_aggs = ncols - n_keys;
-  q.aggs = aggs.data();
-  bqg_table* out = nullptr;
-  // the merge's re-groups run the query-specialised kernels whatever the table size (the
-  // context's jit_min_rows keeps small ad-hoc queries off the compiler; a merge's shape
-  // repeats, and its compiled kernels are cached)
-  // (a per-call override: the context's option, as bqg_get_option reports it, is untouched;
-  // the first merge of a schema pays the specialisation's compile, cached afterwards)
-  bqg_internal_jit_min_override(c, 0);
-  const int rc = bqg_groupby_table(c, t, &q, &out);
-  bqg_internal_jit_min_override(c, -1);
-  ck(c, rc);
-  return out;
 }
 
 struct Local {
@@ -518,23 +494,24 @@ void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& se
 // fills with its own partition (bqg_merge_group_host driving every rank: no gather)
 enum class MergeOut { kDeviceRoot, kHostRoot, kHostDirect };
 
-// the receive side's sum by key (MergeReduce, kernels.h) of a rank's received rows R (from
-// `sources` ranks, row blocks from_peer in rank order): launched on the rank's stream; the key
-// count lands in st->counts (read by the caller after a sync)
-void queue_reduce(Local& l, int n_keys, const std::vector<int32_t>& dts, const std::vector<int>& lg, int W,
-                  TableOwner& out) {
+// sum by key (MergeReduce, kernels.h) of the table `in` whose rows come from several sources
+// (row blocks [src_off[s], src_off[s + 1]), each unique by key) into `out` (capacity: every
+// row), launched on the rank's stream; the key count is copied to st->hcounts() (the caller
+// syncs, then lowers out's row count to it)
+void queue_reduce(Local& l, bqg_table* in, const std::vector<int64_t>& src_off, int n_keys,
+                  const std::vector<int32_t>& dts, const std::vector<int>& lg, TableOwner& out) {
   const int ncols = (int)dts.size();
-  const int64_t n = nrows_of(l.ctx, l.R.t);
+  const int64_t n = nrows_of(l.ctx, in);
   ck(l.ctx, bqg_table_create(l.ctx, n, ncols, dts.data(), &out.t));
   bqg::MergeReduce m{};
   m.keys.nkeys = n_keys;
   for (int k = 0; k < n_keys; ++k) {
-    m.keys.cols[k] = bqg::DevCol{(const unsigned char*)col_ptr(l.ctx, l.R.t, k), dts[k], lg[k]};
+    m.keys.cols[k] = bqg::DevCol{(const unsigned char*)col_ptr(l.ctx, in, k), dts[k], lg[k]};
     m.out_keys[k] = (unsigned char*)col_ptr(l.ctx, out.t, k);
   }
   m.nvals = ncols - n_keys;
   for (int j = 0; j < m.nvals; ++j) {
-    m.vals[j] = (const unsigned char*)col_ptr(l.ctx, l.R.t, n_keys + j);
+    m.vals[j] = (const unsigned char*)col_ptr(l.ctx, in, n_keys + j);
     m.vdt[j] = dts[n_keys + j];
     m.out_vals[j] = (unsigned char*)col_ptr(l.ctx, out.t, n_keys + j);
   }
@@ -555,10 +532,16 @@ void queue_reduce(Local& l, int n_keys, const std::vector<int32_t>& dts, const s
   m.groups = (unsigned long long*)cnt;                 // [0]: keys found
   m.overflow = (unsigned int*)(cnt + 1);               // [1]: probe overflow flag
   HIPCK(hipMemsetAsync(cnt + 1, 0, 8, l.stream));
-  std::vector<int64_t> off(W + 1, 0);
-  for (int s = 0; s < W; ++s) off[s + 1] = off[s] + l.from_peer[s];
-  bqg::launch_merge_reduce(m, off.data(), W, l.stream);
+  bqg::launch_merge_reduce(m, src_off.data(), (int)src_off.size() - 1, l.stream);
   HIPCK(hipGetLastError());
+  HIPCK(hipMemcpyAsync(l.st->hcounts(), cnt, 16, hipMemcpyDeviceToHost, l.stream));
+}
+
+// after queue_reduce and a sync of the rank's stream: the reduced table, its rows set
+void finish_reduce(Local& l, TableOwner& out) {
+  const int64_t* hc = (const int64_t*)l.st->hcounts();
+  if (hc[1] & 0xFFFFFFFFll) comm_fail(BQG_E_HIP, "merge reduce: hash table overflow");
+  ck(l.ctx, bqg_internal_table_set_rows(out.t, hc[0]));
 }
 
 void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t>& dts, int reduced, MergeOut mode,
@@ -643,23 +626,46 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     sync_all(ranks);
     *host_out = own.release();
   };
-  // 1-2. local reduce, then every row straight into its destination's packed block
+  // 1. local reduce: the rank's tables summed by key (one hash reduce over their row-
+  // concatenation, tables in order: the client's first-appearance order), unless the caller's
+  // one table is already reduced
+  {
+    std::vector<TableOwner> cat(ranks.size()), red(ranks.size());
+    for (size_t i = 0; i < ranks.size(); ++i) {
+      Local& l = ranks[i];
+      const double t0 = now_ms();
+      HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+      l.st->counts.ensure(sizeof(int64_t) * ((size_t)W * (W + 1) + 2));  // counts, reduce key count
+      std::vector<bqg_table*> parts;
+      for (bqg_table* t : l.tables)
+        if (nrows_of(l.ctx, t) > 0) parts.push_back(t);
+      if (parts.size() == 1 && reduced) {
+        l.Lv = parts[0];  // keys already unique (a one-pass groupby over the rank's shards)
+      } else if (!parts.empty()) {
+        std::vector<int64_t> off(1, 0);
+        for (bqg_table* t : parts) off.push_back(off.back() + nrows_of(l.ctx, t));
+        cat[i].t = concat_tables(l.ctx, parts, dts);
+        queue_reduce(l, cat[i].t, off, n_keys, dts, lg, red[i]);
+      }
+      if (timing) HIPCK(hipStreamSynchronize(l.stream));
+      l.st->phase_ms[0] += now_ms() - t0;
+    }
+    for (size_t i = 0; i < ranks.size(); ++i) {
+      if (!red[i].t) continue;
+      Local& l = ranks[i];
+      const double t0 = now_ms();
+      HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+      HIPCK(hipStreamSynchronize(l.stream));
+      finish_reduce(l, red[i]);
+      l.L.t = red[i].release();
+      l.Lv = l.L.t;
+      l.st->phase_ms[0] += now_ms() - t0;
+    }
+  }
+  // 2. every row straight into its destination's packed block
   for (Local& l : ranks) {
     const double t0 = now_ms();
     HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
-    std::vector<bqg_table*> parts;
-    for (bqg_table* t : l.tables)
-      if (nrows_of(l.ctx, t) > 0) parts.push_back(t);
-    if (!parts.empty()) {
-      if (reduced && parts.size() == 1) {
-        l.Lv = parts[0];  // keys already unique (a one-pass groupby over the rank's shards)
-      } else {
-        TableOwner cat;
-        cat.t = concat_tables(l.ctx, parts, dts);
-        l.L.t = regroup(l.ctx, cat.t, n_keys, ncols);
-        l.Lv = l.L.t;
-      }
-    }
     l.nl = l.Lv ? nrows_of(l.ctx, l.Lv) : 0;
     int64_t* cnt = (int64_t*)l.st->counts.ensure(sizeof(int64_t) * ((size_t)W * (W + 1) + 2));
     if (W == 1) {
@@ -744,8 +750,9 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       int sources = 0;
       for (int s = 0; s < W; ++s) sources += l.from_peer[s] > 0;
       if (sources > 1) {
-        queue_reduce(l, n_keys, dts, lg, W, red[i]);
-        HIPCK(hipMemcpyAsync(l.st->hcounts(), l.st->counts.p, 16, hipMemcpyDeviceToHost, l.stream));
+        std::vector<int64_t> off(W + 1, 0);
+        for (int s = 0; s < W; ++s) off[s + 1] = off[s] + l.from_peer[s];
+        queue_reduce(l, l.R.t, off, n_keys, dts, lg, red[i]);
       }
       if (timing) HIPCK(hipStreamSynchronize(l.stream));
       l.st->phase_ms[3] += now_ms() - t0;
@@ -758,9 +765,7 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       l.L.reset();  // sent (stream-ordered before any later use of its memory)
       l.Lv = nullptr;
       if (red[i].t) {
-        const int64_t* hc = (const int64_t*)l.st->hcounts();
-        if (hc[1] & 0xFFFFFFFFll) comm_fail(BQG_E_HIP, "merge reduce: hash table overflow");
-        ck(l.ctx, bqg_internal_table_set_rows(red[i].t, hc[0]));
+        finish_reduce(l, red[i]);
         l.R.reset();
         l.R.t = red[i].release();
       }

@@ -27,5 +27,3 @@ int bqg_internal_table_set_rows(bqg_table* t, int64_t n);
 // the context's message set)
 int bqg_internal_host_result(bqg_ctx* c, int64_t n, const std::vector<int32_t>& dts, std::vector<void*>& cols,
                              bqg_result** out);
-// per-call override of the jit_min_rows option (-1: none), not visible through bqg_get_option
-void bqg_internal_jit_min_override(bqg_ctx* c, int64_t rows);

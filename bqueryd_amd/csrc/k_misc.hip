@@ -855,8 +855,10 @@ __device__ __forceinline__ bool mred_same_keys(const PartitionCols& k, int64_t a
   return same;
 }
 
-// one source block [row0, row1): claim or find each row's slot, then store (new key) or add
-// (key of an earlier source) its values -- plain accesses, a key occurs once per source
+// one source block [row0, row1): claim or find each row's slot and add its values to the
+// slot's zero-initialised sums.  A source holds each key once (shard results, reduced
+// partitions), so a launch adds at most once per slot and the sums come out in source order
+// whatever the atomics' timing; a source that repeats a key is still summed correctly.
 __global__ __launch_bounds__(kBlock) void k_mred_insert(MergeReduce m) {
   for (int64_t row = m.row0 + (int64_t)blockIdx.x * kBlock + threadIdx.x; row < m.row1;
        row += (int64_t)gridDim.x * kBlock) {
@@ -864,7 +866,7 @@ __global__ __launch_bounds__(kBlock) void k_mred_insert(MergeReduce m) {
     const uint32_t hi = (uint32_t)(h >> 32);
     // the table position from a second mix: the rows of one rank share h mod nranks
     uint64_t pos = mix64(h ^ 0x9E3779B97F4A7C15ull) & m.mask;
-    bool fresh = false;
+    bool fresh = false;  // this row claimed the slot: it represents the key
     uint64_t i = 0;
     for (; i <= m.mask; ++i) {
       unsigned long long w = m.table[pos];
@@ -889,40 +891,55 @@ __global__ __launch_bounds__(kBlock) void k_mred_insert(MergeReduce m) {
       const int dt = m.vdt[j];
       const uint64_t v = mred_val(m.vals[j], dt, row);
       unsigned long long* a = m.acc + (size_t)j * (m.mask + 1) + pos;
-      if (fresh) *a = v;
-      else if (dtype_is_float(dt)) *a = as_u64(as_f64(*a) + as_f64(v));
-      else *a = *a + v;  // two's complement: wraps like bquery's typed sum at the output width
+      if (dtype_is_float(dt)) atomicAdd(reinterpret_cast<double*>(a), as_f64(v));
+      else atomicAdd(a, (unsigned long long)v);  // two's complement: wraps at the output width
     }
   }
 }
 
-// rank scan of the representative-row bitmap: exclusive popcount prefix per word inside
-// blocks of 1024 words, block totals
-__global__ __launch_bounds__(1024) void k_mred_word_scan(MergeReduce m, uint64_t nwords) {
+// Rank scan of a row bitmap (the merge reduce's representative rows, the byte encoder's first
+// rows): exclusive popcount prefix per word inside blocks of 1024 words, block totals, then an
+// exclusive scan of the block totals in one workgroup with the bit count in *total.
+__global__ __launch_bounds__(1024) void k_rank_word_scan(const unsigned int* bits, uint64_t nwords,
+                                                         unsigned int* word_prefix, unsigned int* block_sum) {
   const uint64_t w = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
-  const unsigned int c = w < nwords ? (unsigned int)__popc(m.rep_bits[w]) : 0u;
+  const unsigned int c = w < nwords ? (unsigned int)__popc(bits[w]) : 0u;
   unsigned int tot;
   const unsigned int e = block_excl_scan_1024(c, &tot);
-  if (w < nwords) m.word_prefix[w] = e;
-  if (threadIdx.x == 0) m.block_sum[blockIdx.x] = tot;
+  if (w < nwords) word_prefix[w] = e;
+  if (threadIdx.x == 0) block_sum[blockIdx.x] = tot;
 }
 
-// exclusive scan of the block totals (one workgroup, any count) and the key count
-__global__ __launch_bounds__(1024) void k_mred_block_scan(MergeReduce m, uint64_t nblocks) {
+__global__ __launch_bounds__(1024) void k_rank_block_scan(unsigned int* block_sum, uint64_t nblocks,
+                                                          unsigned long long* total) {
   __shared__ unsigned int carry;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
   for (uint64_t base = 0; base < nblocks; base += 1024) {
     const uint64_t i = base + threadIdx.x;
-    const unsigned int c = i < nblocks ? m.block_sum[i] : 0u;
+    const unsigned int c = i < nblocks ? block_sum[i] : 0u;
     unsigned int tot;
     const unsigned int e = block_excl_scan_1024(c, &tot);
-    if (i < nblocks) m.block_sum[i] = carry + e;
+    if (i < nblocks) block_sum[i] = carry + e;
     __syncthreads();
     if (threadIdx.x == 0) carry += tot;
     __syncthreads();
   }
-  if (threadIdx.x == 0) *m.groups = carry;
+  if (threadIdx.x == 0) *total = carry;
+}
+
+// number of set bits of the scanned bitmap before bit r
+__device__ __forceinline__ uint64_t bit_rank(const unsigned int* bits, const unsigned int* word_prefix,
+                                             const unsigned int* block_sum, uint32_t r) {
+  const uint32_t wi = r >> 5;
+  return (uint64_t)block_sum[wi >> 10] + word_prefix[wi] + (unsigned int)__popc(bits[wi] & ((1u << (r & 31)) - 1u));
+}
+
+static void launch_rank_scan(const unsigned int* bits, int64_t nrows, unsigned int* word_prefix, unsigned int* block_sum,
+                             unsigned long long* total, hipStream_t st) {
+  const uint64_t nwords = ((uint64_t)nrows + 31) / 32, nblocks = (nwords + 1023) / 1024;
+  if (nwords) hipLaunchKernelGGL(k_rank_word_scan, dim3((unsigned)nblocks), dim3(1024), 0, st, bits, nwords, word_prefix, block_sum);
+  hipLaunchKernelGGL(k_rank_block_scan, dim3(1), dim3(1024), 0, st, block_sum, nblocks, total);
 }
 
 // every occupied slot writes its output row at the rank of its representative row: keys as
@@ -933,9 +950,7 @@ __global__ __launch_bounds__(kBlock) void k_mred_emit(MergeReduce m) {
     const unsigned long long w = m.table[pos];
     if (w == kEmpty) continue;
     const uint32_t rep = (uint32_t)w;
-    const uint32_t wi = rep >> 5;
-    const uint64_t r = (uint64_t)m.block_sum[wi >> 10] + m.word_prefix[wi] +
-                       (unsigned int)__popc(m.rep_bits[wi] & ((1u << (rep & 31)) - 1u));
+    const uint64_t r = bit_rank(m.rep_bits, m.word_prefix, m.block_sum, rep);
     for (int k = 0; k < m.keys.nkeys; ++k) {
       const DevCol& c = m.keys.cols[k];
       switch (c.lg) {
@@ -956,8 +971,8 @@ __global__ __launch_bounds__(kBlock) void k_mred_emit(MergeReduce m) {
 void launch_merge_reduce(MergeReduce m, const int64_t* src_off, int nsrc, hipStream_t st) {
   const uint64_t cap = m.mask + 1;
   const uint64_t nwords = ((uint64_t)m.nrows + 31) / 32;
-  const uint64_t nblocks = (nwords + 1023) / 1024;
   (void)hipMemsetAsync(m.table, 0xFF, cap * 8, st);
+  (void)hipMemsetAsync(m.acc, 0, cap * 8 * (size_t)std::max(1, m.nvals), st);
   (void)hipMemsetAsync(m.rep_bits, 0, nwords * 4 + 4, st);
   for (int s = 0; s < nsrc; ++s) {
     m.row0 = src_off[s];
@@ -966,10 +981,95 @@ void launch_merge_reduce(MergeReduce m, const int64_t* src_off, int nsrc, hipStr
     const unsigned g = (unsigned)std::min<int64_t>((m.row1 - m.row0 + kBlock - 1) / kBlock, 2048);
     hipLaunchKernelGGL(k_mred_insert, dim3(g), dim3(kBlock), 0, st, m);
   }
-  if (nwords) hipLaunchKernelGGL(k_mred_word_scan, dim3((unsigned)nblocks), dim3(1024), 0, st, m, nwords);
-  hipLaunchKernelGGL(k_mred_block_scan, dim3(1), dim3(1024), 0, st, m, nblocks);
+  launch_rank_scan(m.rep_bits, m.nrows, m.word_prefix, m.block_sum, m.groups, st);
   const unsigned ge = (unsigned)std::min<uint64_t>((cap + kBlock - 1) / kBlock, 4096);
   hipLaunchKernelGGL(k_mred_emit, dim3(ge), dim3(kBlock), 0, st, m);
+}
+
+// ------------------------------------------------------------------------------------
+// Fixed-width byte strings (numpy 'S<n>' / 'U<n>', bqg_encode_bytes): dictionary codes in
+// first-appearance order.  A row's value is its `width` bytes (trailing zero bytes are
+// numpy's padding and take part like any other byte: equal strings have equal bytes).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t bytes_word(const unsigned char* p, int avail) {
+  uint64_t w = 0;
+  for (int b = 0; b < 8 && b < avail; ++b) w |= (uint64_t)p[b] << (8 * b);
+  return w;
+}
+
+__device__ __forceinline__ uint64_t bytes_hash(const unsigned char* p, int width) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)width;
+  for (int i = 0; i < width; i += 8) h = mix64(h ^ (bytes_word(p + i, width - i) + (uint64_t)i));
+  return h;
+}
+
+__device__ __forceinline__ bool bytes_equal(const unsigned char* a, const unsigned char* b, int width) {
+  for (int i = 0; i < width; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+__global__ __launch_bounds__(kBlock) void k_bytes_insert(BytesEncode e) {
+  for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < e.n; row += (int64_t)gridDim.x * kBlock) {
+    const unsigned char* mine = e.data + (size_t)row * e.width;
+    const uint64_t h = bytes_hash(mine, e.width);
+    const uint32_t hi = (uint32_t)(h >> 32);
+    uint64_t pos = h & e.mask;
+    uint64_t i = 0;
+    for (; i <= e.mask; ++i) {
+      unsigned long long w = e.table[pos];
+      if (w == kEmpty) {
+        const unsigned long long prev = atomicCAS(&e.table[pos], kEmpty, ((unsigned long long)hi << 32) | (uint32_t)row);
+        if (prev == kEmpty) break;
+        w = prev;
+      }
+      if ((uint32_t)(w >> 32) == hi && bytes_equal(e.data + (size_t)(uint32_t)w * e.width, mine, e.width)) break;
+      pos = (pos + 1) & e.mask;
+    }
+    if (i > e.mask) {
+      atomicOr(e.overflow, 1u);
+      continue;
+    }
+    e.row_slot[row] = (uint32_t)pos;
+    atomicMin(&e.first[pos], (uint32_t)row);
+  }
+}
+
+// the first row of every value, as a bit of the row bitmap
+__global__ __launch_bounds__(kBlock) void k_bytes_mark(BytesEncode e) {
+  const uint64_t cap = e.mask + 1;
+  for (uint64_t pos = (uint64_t)blockIdx.x * kBlock + threadIdx.x; pos < cap; pos += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t f = e.first[pos];
+    if (f != 0xFFFFFFFFu) atomicOr(&e.rep_bits[f >> 5], 1u << (f & 31));
+  }
+}
+
+// code = 1 + first-appearance rank (0 for the empty string: all zero bytes); first rows write
+// their value into the dictionary at their rank
+__global__ __launch_bounds__(kBlock) void k_bytes_codes(BytesEncode e) {
+  for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < e.n; row += (int64_t)gridDim.x * kBlock) {
+    const unsigned char* mine = e.data + (size_t)row * e.width;
+    const uint32_t f = e.first[e.row_slot[row]];
+    const uint64_t r = bit_rank(e.rep_bits, e.word_prefix, e.block_sum, f);
+    bool empty = true;
+    for (int b = 0; b < e.width; ++b) empty &= mine[b] == 0;
+    e.codes[row] = empty ? 0 : (int32_t)(r + 1);
+    if ((int64_t)f == row)
+      for (int b = 0; b < e.width; ++b) e.values[r * e.width + b] = mine[b];
+  }
+}
+
+void launch_bytes_encode(BytesEncode e, hipStream_t st) {
+  const uint64_t cap = e.mask + 1;
+  (void)hipMemsetAsync(e.table, 0xFF, cap * 8, st);
+  (void)hipMemsetAsync(e.first, 0xFF, cap * 4, st);
+  (void)hipMemsetAsync(e.rep_bits, 0, ((uint64_t)e.n + 31) / 32 * 4 + 4, st);
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((e.n + kBlock - 1) / kBlock, 4096));
+  hipLaunchKernelGGL(k_bytes_insert, dim3(g), dim3(kBlock), 0, st, e);
+  const unsigned gm = (unsigned)std::min<uint64_t>((cap + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL(k_bytes_mark, dim3(gm), dim3(kBlock), 0, st, e);
+  launch_rank_scan(e.rep_bits, e.n, e.word_prefix, e.block_sum, e.groups, st);
+  hipLaunchKernelGGL(k_bytes_codes, dim3(g), dim3(kBlock), 0, st, e);
 }
 
 // value runs: rows whose value differs from the previous row's (canonical bits: a float

@@ -265,14 +265,14 @@ struct MergePack {
 void merge_pack_grid(int64_t nrows, int32_t* nblocks, int64_t* rows_per_block);
 void launch_merge_pack(const MergePack& m, hipStream_t st);
 
-// cross-rank merge, receive side: the rows a rank received from every source rank (each
-// source's rows already unique by key) summed by key in one hash table -- no statistics, no
-// planner, no first-appearance sort.  Sources are inserted one launch each, in source order,
-// so every key's sums are added in source order (deterministic) with plain stores: within one
-// source a key occurs once, so no two rows of a launch touch one slot's accumulators.  The
-// table word is hash_hi32 << 32 | representative row (the key's first row, in the lowest
-// source holding it); keys compare in full at the representative row.  Output rows come in
-// representative-row order: first appearance in the received rows, as a re-group would give.
+// cross-rank merge: rows from several sources (the tables of one rank's shards, or the rows a
+// rank received from every source rank), each source's rows unique by key, summed by key in
+// one hash table -- no statistics, no planner, no first-appearance sort.  Sources are
+// inserted one launch each, in source order, so every key's sums are added in source order
+// (deterministic: a launch adds at most once per slot).  The table word is hash_hi32 << 32 |
+// representative row (the key's first row, in the lowest source holding it); keys compare in
+// full at the representative row.  Output rows come in representative-row order: first
+// appearance in the concatenated sources, the client's order for a rank's shard tables.
 constexpr int kMergeMaxVals = kMergeMaxCols;
 struct MergeReduce {
   PartitionCols keys;                         // key columns of the received table
@@ -301,6 +301,26 @@ inline uint64_t merge_reduce_cap(int64_t rows) {
 // every launch of the reduce on `st`: table init, one insert per non-empty source block
 // (src_off[0..nsrc]), rank scan, emit; `groups` receives the key count on the device
 void launch_merge_reduce(MergeReduce m, const int64_t* src_off, int nsrc, hipStream_t st);
+
+// fixed-width byte strings (numpy 'S<n>' / 'U<n>') -> INT32 dictionary codes: 1 + the value's
+// first-appearance rank, 0 for the empty string (bqg_encode_bytes)
+struct BytesEncode {
+  const unsigned char* data;  // [n][width] on the device
+  int64_t n;
+  int32_t width;
+  unsigned long long* table;  // [cap] kEmpty or hash_hi32 << 32 | a row holding the value
+  uint64_t mask;              // cap - 1
+  uint32_t* first;            // [cap] first row of each slot's value
+  uint32_t* row_slot;         // [n] each row's slot
+  unsigned int* rep_bits;     // [ceil(n / 32)] first rows
+  unsigned int* word_prefix;  // [ceil(n / 32)]
+  unsigned int* block_sum;    // [ceil(n / 32768)]
+  unsigned long long* groups; // out: distinct values
+  unsigned int* overflow;     // a probe ran past the table (cannot at load <= 1/2)
+  int32_t* codes;             // [n] out
+  unsigned char* values;      // [distinct][width] out, first-appearance order
+};
+void launch_bytes_encode(BytesEncode e, hipStream_t st);
 
 // std: per-slot means of the std columns (pass 1 totals -> pass 2 centers), on device
 struct StdCenters {

@@ -27,7 +27,7 @@ from collections import OrderedDict
 import numpy as np
 
 from . import bcolz_io
-from .engine import ShardTable, get_device
+from .engine import ShardTable, get_device, is_string
 from .terms import any_value_satisfies, parse_terms
 
 
@@ -165,8 +165,11 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
         for n in missing:
             self._table.add_column(n, self._dtypes[n])
             self._table.names.append(n)
-            if n in self._host:
-                self._table.push(n, self._host[n])
+            if n in self._host or is_string(self._dtypes[n]):
+                # string columns: decoded on the host, dictionary-encoded on the GPU
+                self._table.push(n, self._host_column(n))
+                if is_string(self._dtypes[n]) and self.rootdir:
+                    self._host.pop(n, None)
             else:
                 meta = bcolz_io.CArrayMeta(bcolz_io.ctable_column_dir(self.rootdir, n))
                 if meta.length != self._len:
@@ -197,7 +200,7 @@ class ctable:  # noqa: N801  (mirrors bquery's class name)
             vals = self._cached_values(col)
             if vals is None:
                 break
-            if not any_value_satisfies(vals.astype(self._dtypes[col]), code, value):
+            if not any_value_satisfies(np.asarray(vals).astype(self._dtypes[col]), code, value):
                 return False
         return True
 

@@ -100,10 +100,25 @@ def merge_phases(device):
 
 
 def _schema(groupby_cols, agg_list, dtypes):
+    """(column names, C dtype codes) of the merge: datetime64 keys travel as their int64 ticks;
+    string keys cannot merge on the device (each table's dictionary codes are its own)."""
     from . import _lib as L
+    from .engine import device_dtype, is_string
     names = list(groupby_cols) + [x[2] for x in agg_list]
-    codes = (ctypes.c_int32 * len(names))(*[L.DTYPE_CODE[np.dtype(dtypes[n])] for n in names])
+    for n in names:
+        if is_string(dtypes[n]):
+            raise NotImplementedError('device merge of a string column (%s): merge the host results' % n)
+    codes = (ctypes.c_int32 * len(names))(*[L.DTYPE_CODE[device_dtype(dtypes[n])] for n in names])
     return names, codes
+
+
+def _logical(cols, dtypes):
+    """datetime64 / timedelta64 columns back from their ticks."""
+    from .engine import is_time
+    for n in list(cols):
+        if is_time(dtypes[n]):
+            cols[n] = np.ascontiguousarray(cols[n]).view(dtypes[n])
+    return cols
 
 
 def merge_partials_device(local_tables, groupby_cols, agg_list, dtypes, comm, reduced=False):
@@ -126,7 +141,7 @@ def merge_partials_device(local_tables, groupby_cols, agg_list, dtypes, comm, re
                                      1 if reduced else 0, ctypes.byref(out)))
     if comm.rank != 0 or not out.value:
         return None
-    return _result_to_columns(dev, out, names)[0]
+    return _logical(_result_to_columns(dev, out, names)[0], dtypes)
 
 
 def merge_group_device(tables_per_rank, groupby_cols, agg_list, dtypes, group, reduced=False):
@@ -151,7 +166,7 @@ def merge_group_device(tables_per_rank, groupby_cols, agg_list, dtypes, group, r
     group.devices[0].check(L.lib().bqg_merge_group_host(w, ctxs, ntab, arr, len(groupby_cols), len(names), codes,
                                                         1 if reduced else 0, ctypes.byref(out)))
     LAST_MERGE.update(merge_ms=1e3 * (time.perf_counter() - t0))
-    return _result_to_columns(group.devices[0], out, names)[0]
+    return _logical(_result_to_columns(group.devices[0], out, names)[0], dtypes)
 
 
 def merge_group_device_table(tables_per_rank, groupby_cols, agg_list, dtypes, group, reduced=False):

@@ -14,7 +14,7 @@ from collections import OrderedDict
 import numpy as np
 
 from . import _lib as L
-from .terms import normalize, parse_agg_list, parse_terms
+from .terms import normalize, parse_agg_list, parse_terms, string_term, time_value
 
 
 class Device:
@@ -156,8 +156,54 @@ def _result_to_columns(dev, res_handle, names):
     return out, bool(view.filtered)
 
 
+def is_string(dt):
+    """numpy fixed-width bytes ('S<n>') / unicode ('U<n>'): dictionary codes on the device."""
+    return np.dtype(dt).kind in 'SU'
+
+
+def is_time(dt):
+    """numpy datetime64 / timedelta64: their int64 ticks on the device."""
+    return np.dtype(dt).kind in 'Mm'
+
+
+def device_dtype(dt):
+    """The dtype a logical column has in HBM: int32 dictionary codes for strings, int64 ticks
+    for datetime64 / timedelta64, the dtype itself otherwise."""
+    dt = np.dtype(dt)
+    if is_string(dt):
+        return np.dtype(np.int32)
+    if is_time(dt):
+        return np.dtype(np.int64)
+    return dt
+
+
+class StringDict:
+    """The dictionary of a string column (``bqg_encode_bytes``): ``values[code]`` -- code 0 is the
+    empty string, code r + 1 the value of first-appearance rank r (so a zero-initialised code
+    compares like bquery's zero-initialised string)."""
+
+    def __init__(self, dtype, ranked):
+        self.dtype = np.dtype(dtype)
+        empty = np.zeros(1, self.dtype)
+        self.values = np.concatenate([empty, np.asarray(ranked, self.dtype)])
+        self._index = None
+
+    def decode(self, codes):
+        return self.values[np.asarray(codes)]
+
+    def code_of(self, value):
+        if self._index is None:
+            self._index = {}
+            for c, v in enumerate(self.values.tolist()):
+                self._index.setdefault(v, c)
+        return self._index.get(value)
+
+
 class ShardTable:
-    """Device-resident columns of one shard."""
+    """Device-resident columns of one shard.  String columns ('S<n>' / 'U<n>') live in HBM as
+    INT32 dictionary codes (``bqg_encode_bytes``, on the GPU) with their dictionary on the host;
+    datetime64 / timedelta64 columns as their int64 ticks.  Keys, terms and results translate
+    at the boundary, so every kernel sees integer columns."""
 
     def __init__(self, columns, device=None, nrows=None):
         """``columns``: mapping name -> 1-D numpy array (all the same length); ``nrows`` is
@@ -170,9 +216,9 @@ class ShardTable:
         for a in arrays:
             if a.ndim != 1 or len(a) != n:
                 raise ValueError('all columns must be 1-D arrays of the same length')
-            if a.dtype not in L.DTYPE_CODE:
+            if device_dtype(a.dtype) not in L.DTYPE_CODE:
                 raise NotImplementedError('column dtype %s is not supported on the GPU' % a.dtype)
-        codes = (ctypes.c_int32 * max(1, len(arrays)))(*[L.DTYPE_CODE[a.dtype] for a in arrays])
+        codes = (ctypes.c_int32 * max(1, len(arrays)))(*[L.DTYPE_CODE[device_dtype(a.dtype)] for a in arrays])
         h = ctypes.c_void_p()
         self.dev.check(self._lib.bqg_table_create(self.dev.handle, n, len(arrays), codes,
                                                   ctypes.byref(h)))
@@ -182,13 +228,15 @@ class ShardTable:
         self.dtypes = OrderedDict((nm, a.dtype) for nm, a in zip(names, arrays))
         self._slot = {nm: i for i, nm in enumerate(names)}
         self._scratch = []
+        self._strings = {}
         for i, a in enumerate(arrays):
-            self.push(i, a)
+            self.push(names[i], a)
         self.sync()
 
     @classmethod
-    def _wrap(cls, handle, names, dtypes, device):
-        """A ShardTable around a table the library created (a device-resident result)."""
+    def _wrap(cls, handle, names, dtypes, device, strings=None):
+        """A ShardTable around a table the library created (a device-resident result);
+        ``strings``: the dictionaries of its string columns (codes of the table they came from)."""
         t = cls.__new__(cls)
         t.dev = device
         t._lib = L.lib()
@@ -200,6 +248,7 @@ class ShardTable:
         t.dtypes = OrderedDict((nm, np.dtype(dt)) for nm, dt in zip(names, dtypes))
         t._slot = {nm: i for i, nm in enumerate(names)}
         t._scratch = []
+        t._strings = dict(strings or {})
         return t
 
     @classmethod
@@ -217,6 +266,8 @@ class ShardTable:
         def dtype(p, n):
             return p.dtypes[n] if isinstance(p, ShardTable) else np.asarray(p[n]).dtype
 
+        if any(isinstance(p, ShardTable) and any(n in p._strings for n in names) for p in parts):
+            raise NotImplementedError('from_parts of device string columns: their dictionaries differ per table')
         total = sum(rows(p) for p in parts)
         t = cls(OrderedDict(), device=device, nrows=total)
         for n in names:
@@ -266,11 +317,41 @@ class ShardTable:
     def _touch(self):
         self.__dict__['_version'] = self.version + 1
 
+    def _logical(self, col):
+        s = self.slot(col)
+        for k, v in self._slot.items():
+            if v == s:
+                return k, self.dtypes[k]
+        raise KeyError(str(col))
+
     def push(self, col, array, row_offset=0):
         self._touch()
+        name, dt = self._logical(col)
         a = np.ascontiguousarray(array)
+        if is_string(dt):
+            return self._encode_strings(name, a.astype(dt, copy=False), row_offset)
+        if is_time(dt):
+            a = a.astype(dt, copy=False).view(np.int64)
         self.dev.check(self._lib.bqg_push_chunk(self.handle, self.slot(col), a.ctypes.data,
                                                 len(a), int(row_offset)))
+
+    def _encode_strings(self, name, a, row_offset):
+        """A whole string column -> INT32 codes in HBM + its dictionary (bqg_encode_bytes)."""
+        if row_offset != 0 or len(a) != self.nrows:
+            raise NotImplementedError('string columns are pushed whole')
+        a = np.ascontiguousarray(a)
+        width = a.dtype.itemsize
+        n_values = ctypes.c_int64()
+        cap = min(len(a), 1 << 16)
+        for _ in range(2):
+            values = np.empty(max(cap, 1), dtype=a.dtype)
+            rc = self._lib.bqg_encode_bytes(self.dev.handle, self.handle, self.slot(name), a.ctypes.data, width,
+                                            values.ctypes.data, len(values), ctypes.byref(n_values))
+            if rc == 0 or n_values.value <= len(values):
+                break
+            cap = n_values.value  # more distinct values than the first guess: once more, sized
+        self.dev.check(rc)
+        self._strings[name] = StringDict(a.dtype, values[:n_values.value])
 
     def push_device(self, col, dev_ptr, nrows, row_offset=0):
         """Device-to-device copy of ``nrows`` elements at ``dev_ptr`` into column ``col``."""
@@ -321,7 +402,7 @@ class ShardTable:
 
     def add_column(self, name, dtype):
         s = ctypes.c_int32()
-        self.dev.check(self._lib.bqg_table_add_column(self.handle, L.DTYPE_CODE[np.dtype(dtype)],
+        self.dev.check(self._lib.bqg_table_add_column(self.handle, L.DTYPE_CODE[device_dtype(dtype)],
                                                       ctypes.byref(s)))
         self._slot[name] = s.value
         self.dtypes[name] = np.dtype(dtype)
@@ -349,14 +430,19 @@ class ShardTable:
 
     def read(self, col):
         s = self.slot(col)
-        dt = self.dtypes[self.names[s]] if s < len(self.names) else None
-        if dt is None:
-            for k, v in self._slot.items():
-                if v == s:
-                    dt = self.dtypes[k]
-        out = np.empty(self.nrows, dtype=dt)
+        name, dt = self._logical(col)
+        out = np.empty(self.nrows, dtype=device_dtype(dt))
         self.dev.check(self._lib.bqg_table_read(self.handle, s, out.ctypes.data, self.nrows, 0))
-        return out
+        return self._to_logical(name, out)
+
+    def _to_logical(self, name, arr):
+        """Device values of column ``name`` (codes, ticks) as the column's own dtype."""
+        dt = self.dtypes.get(name)
+        if dt is not None and is_string(dt):
+            return self._strings[name].decode(arr)
+        if dt is not None and is_time(dt):
+            return np.ascontiguousarray(arr).view(dt)
+        return arr
 
     def stats(self, col):
         imin, imax = ctypes.c_int64(), ctypes.c_int64()
@@ -380,7 +466,14 @@ class ShardTable:
         arr = (L.Term * max(1, len(parsed)))()
         for i, (col, code, value) in enumerate(parsed):
             dt = self.dtypes[col]
-            op, ivals, fvals = normalize(dt, code, value)
+            if is_string(dt):
+                op, ivals, fvals = string_term(self._strings[col].values, code, value)
+                dt = np.dtype(np.int32)
+            elif is_time(dt):
+                op, ivals, fvals = normalize(np.int64, code, time_value(dt, code, value))
+                dt = np.dtype(np.int64)
+            else:
+                op, ivals, fvals = normalize(dt, code, value)
             if dt == np.uint64:
                 iv = np.array([v & 0xFFFFFFFFFFFFFFFF for v in ivals] or [0], np.uint64).view(np.int64)
             else:
@@ -443,7 +536,7 @@ class ShardTable:
         groupby_cols = list(groupby_cols)
         for c in groupby_cols:
             self.slot(c)
-        ops = parse_agg_list(self.dtypes, agg_list)
+        ops = self._parse_aggs(agg_list)
         names = groupby_cols + [o[1] for o in ops]
         if len(set(names)) != len(names):
             raise ValueError('duplicate output column names: %s' % names)
@@ -457,6 +550,13 @@ class ShardTable:
             self.__dict__['_last_plan_keep'] = keep  # the struct's arrays live until the next query
         return names, ops, q
 
+    def _parse_aggs(self, agg_list):
+        ops = parse_agg_list(self.dtypes, agg_list)
+        for in_col, out_col, op, dt in ops:
+            if op in ('sum', 'mean', 'std') and (is_string(self.dtypes[in_col]) or is_time(self.dtypes[in_col])):
+                raise NotImplementedError('%s of a %s column' % (op, self.dtypes[in_col]))
+        return ops
+
     def groupby(self, groupby_cols, agg_list, where_terms=None, mask=None):
         """bquery ``ctable.groupby`` semantics; returns (OrderedDict of columns, filtered)."""
         names, ops, q = self._plan(groupby_cols, agg_list, where_terms, mask)
@@ -464,6 +564,8 @@ class ShardTable:
         self.dev.check(self._lib.bqg_groupby(self.dev.handle, self.handle, ctypes.byref(q),
                                              ctypes.byref(res)))
         out, filtered = _result_to_columns(self.dev, res, names)
+        for k in list(groupby_cols):
+            out[k] = self._to_logical(k, out[k])
         for (in_col, out_col, op, dt) in ops:
             if out[out_col].dtype != dt:
                 out[out_col] = out[out_col].astype(dt)
@@ -474,7 +576,7 @@ class ShardTable:
         groupby_cols = list(groupby_cols)
         for c in groupby_cols:
             self.slot(c)
-        ops = parse_agg_list(self.dtypes, agg_list)
+        ops = self._parse_aggs(agg_list)
         names = groupby_cols + [o[1] for o in ops]
         if len(set(names)) != len(names):
             raise ValueError('duplicate output column names: %s' % names)
@@ -483,7 +585,7 @@ class ShardTable:
         h = ctypes.c_void_p()
         self.dev.check(self._lib.bqg_groupby_table(self.dev.handle, self.handle, ctypes.byref(q), ctypes.byref(h)))
         dts = [self.dtypes[c] for c in groupby_cols] + [o[3] for o in ops]
-        return ShardTable._wrap(h, names, dts, self.dev)
+        return ShardTable._wrap(h, names, dts, self.dev, {c: self._strings[c] for c in groupby_cols if c in self._strings})
 
     def select_rows_table(self, cols, where_terms=None, mask=None):
         """``select_rows`` whose result stays in HBM: a new ShardTable."""
@@ -494,7 +596,8 @@ class ShardTable:
         h = ctypes.c_void_p()
         self.dev.check(self._lib.bqg_select_rows_table(self.dev.handle, self.handle, ctypes.byref(q), len(cols),
                                                        sel.ctypes.data, ctypes.byref(h)))
-        return ShardTable._wrap(h, cols, [self.dtypes[c] for c in cols], self.dev)
+        return ShardTable._wrap(h, cols, [self.dtypes[c] for c in cols], self.dev,
+                                {c: self._strings[c] for c in cols if c in self._strings})
 
     def to_host(self, cols=None):
         """The table's columns as numpy arrays."""
@@ -506,7 +609,8 @@ class ShardTable:
         columns spanning at most 2^27 values through a lookup table, floats (khash identity),
         bools and wider spans through a hash of the canonical key bits."""
         s = self.slot(col)
-        dt = np.dtype(self.dtypes[col])
+        logical = np.dtype(self.dtypes[col])
+        dt = device_dtype(logical)
         cap = min(self.nrows, 1 << 22)
         if dt.kind in 'iu':
             st = self.stats(col)
@@ -523,7 +627,7 @@ class ShardTable:
                 break
             cap = n_values.value  # more distinct values than the first guess: once more, sized
         self.dev.check(rc)
-        return lab, values[:n_values.value]
+        return lab, self._to_logical(col, values[:n_values.value])
 
     def select_rows(self, cols, where_terms=None, mask=None):
         """aggregate=False: the passing rows of ``cols`` in row order."""
@@ -535,4 +639,6 @@ class ShardTable:
         self.dev.check(self._lib.bqg_select_rows(self.dev.handle, self.handle, ctypes.byref(q),
                                                  len(cols), sel.ctypes.data, ctypes.byref(res)))
         out, _ = _result_to_columns(self.dev, res, cols)
+        for c in cols:
+            out[c] = self._to_logical(c, out[c])
         return out

@@ -119,6 +119,67 @@ def normalize(dtype, code, value):
     raise NotImplementedError('where_terms on a column of dtype %s' % dtype)
 
 
+def coerce_string(dtype, v):
+    """A where-term value as an element of a string column of ``dtype``: bytes for 'S<n>' (a
+    str is encoded latin-1 -- the py2 str values of bqueryd's pickled params decode to latin-1
+    str, messages.py), str for 'U<n>'."""
+    if np.dtype(dtype).kind == 'S':
+        if isinstance(v, str):
+            return v.encode('latin-1')
+        return bytes(v) if isinstance(v, (bytes, bytearray, np.bytes_)) else v
+    if isinstance(v, (bytes, bytearray, np.bytes_)):
+        return bytes(v).decode('latin-1')
+    return v
+
+
+def string_mask(values, code, value):
+    """Which elements of the string array ``values`` satisfy the parsed term (bytes / str
+    comparisons, lexicographic; a value of another type never equals and never orders)."""
+    values = np.asarray(values)
+    dt = values.dtype
+    if code in (L.T_IN, L.T_NIN):
+        members = [coerce_string(dt, m) for m in value]
+        members = [m for m in members if isinstance(m, (bytes, str))]
+        # members keep their own width (a longer value must not truncate into a match)
+        hit = np.isin(values, np.asarray(members)) if members else np.zeros(len(values), bool)
+        return hit if code == L.T_IN else ~hit
+    v = coerce_string(dt, value)
+    if not isinstance(v, (bytes, str)):
+        return np.full(len(values), code == L.T_NE)
+    return {L.T_EQ: values == v, L.T_NE: values != v, L.T_GT: values > v, L.T_GE: values >= v,
+            L.T_LT: values < v, L.T_LE: values <= v}[code]
+
+
+def string_term(values_by_code, code, value):
+    """A term on a string column as an integer term on its dictionary codes (engine.StringDict:
+    ``values_by_code[c]`` is code c's string): the codes whose string satisfies the term, as
+    ``in`` (or ``nin`` of the rest, whichever list is shorter), folded to a constant when none
+    or all do."""
+    hit = string_mask(values_by_code, code, value)
+    codes = np.nonzero(hit)[0]
+    if len(codes) == 0:
+        return L.T_FALSE, [], []
+    if len(codes) == len(hit):
+        return L.T_TRUE, [], []
+    if len(codes) * 2 <= len(hit):
+        return L.T_IN, codes.tolist(), []
+    return L.T_NIN, np.nonzero(~hit)[0].tolist(), []
+
+
+def time_value(dtype, code, value):
+    """A where-term value on a datetime64 / timedelta64 column as the column's int64 ticks (an
+    in-list element by element); ints pass as ticks."""
+    dtype = np.dtype(dtype)
+
+    def one(v):
+        if isinstance(v, (int, np.integer)) and not isinstance(v, bool):
+            return int(v)
+        return int(np.asarray(v).astype(dtype).view(np.int64))
+    if code in (L.T_IN, L.T_NIN):
+        return set(one(v) for v in value)
+    return one(value)
+
+
 def parse_agg_list(dtypes, agg_list):
     """create_agg_ctable: -> [(in_col, out_col, op, out_dtype)].
 
@@ -152,6 +213,10 @@ def any_value_satisfies(values, code, value):
     unverified].  Same exact int / float rules as the row predicate (``normalize``); host
     logic over a handful of cached values, not a row scan."""
     values = np.asarray(values)
+    if values.dtype.kind in 'SU':
+        return bool(np.any(string_mask(values, code, value)))
+    if values.dtype.kind in 'Mm':
+        values, value = values.view(np.int64), time_value(values.dtype, code, value)
     op, ivals, fvals = normalize(values.dtype, code, value)
     if op == L.T_TRUE:
         return len(values) > 0

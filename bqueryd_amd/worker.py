@@ -35,7 +35,7 @@ import numpy as np
 
 from . import bcolz_io
 from .ctable import ctable
-from .engine import get_device
+from .engine import get_device, is_string
 
 
 def rm_file_or_dir(path, ignore_errors=True):
@@ -183,8 +183,32 @@ class CalcPath:
             shards[r].append(ct)
         t_open = time.perf_counter()
         names = list(groupby_col_list) + [x[2] for x in aggregation_list]
+        if any(is_string(ct.cols[c]) for cts in shards for ct in cts for c in groupby_col_list):
+            # string keys: every shard's dictionary codes are its own, so the shard results
+            # merge on the host values (the client's re-group, rpc.py:164-173, on the GPU)
+            from .rpc import merge_tables
+            per = []
+            for cts in shards:
+                for ct in cts:
+                    res = _shard_calc(ct, groupby_col_list, aggregation_list, where_terms_list, expand_filter_column,
+                                      True)
+                    if res is not None:
+                        per.append(res)
+            t_calc = time.perf_counter()
+            merged = merge_tables(per, groupby_col_list, aggregation_list, aggregate=True, device=self.device)
+            t_merge = time.perf_counter()
+            msg['data'] = '' if merged is None else bcolz_io.ctable_tar(
+                OrderedDict((n, np.asarray(merged[n])) for n in names), result_name())
+            msg['filenames'] = list(filenames)
+            self.last_stages = {'calc_s': t_calc - t_open, 'merge_s': t_merge - t_calc,
+                                'result_tar_s': time.perf_counter() - t_merge}
+            return msg
         dtypes = None
-        fused = dist.decomposable(aggregation_list) and not expand_filter_column
+        # one pass over a GPU's shard union for decomposable aggregations -- not over string
+        # columns, whose dictionary codes differ per shard (the union concatenates codes)
+        used = list(groupby_col_list) + [x[0] for x in aggregation_list] + [t[0] for t in (where_terms_list or [])]
+        fused = dist.decomposable(aggregation_list) and not expand_filter_column and not any(
+            is_string(ct.cols[c]) for cts in shards for ct in cts for c in used if c in ct.cols)
         reduced = fused
         for r, cts in enumerate(shards):
             if not cts:

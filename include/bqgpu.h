@@ -44,7 +44,8 @@ extern "C" {
 
 /* ABI history: 5 -- bqg_timing.narrow (exact 32-bit codes on the partitioned path);
  * 6 -- bqg_timing.narrow == 2 (packed entries) and the engine options (bqg_set_option);
- * 7 -- bqg_merge_host / bqg_merge_group_host (merged table straight to host memory). */
+ * 7 -- bqg_merge_host / bqg_merge_group_host (merged table straight to host memory),
+ *      bqg_encode_bytes (string columns as dictionary codes). */
 #define BQG_ABI_VERSION 7
 
 /* error codes */
@@ -264,6 +265,20 @@ int bqg_result_view_get(bqg_result* r, bqg_result_view* out);
 int bqg_hash_partition(bqg_ctx* ctx, bqg_table* t, int32_t n_keys, const int32_t* key_cols,
                        int32_t nparts, int32_t out_col, int64_t* counts);
 int bqg_result_free(bqg_result* r);
+
+/* ---------------- fixed-width byte / string columns ----------------
+ * bquery factorizes string key columns and compares them in where_terms [ext-bquery]; here a
+ * string column lives on the device as dictionary codes.  bqg_encode_bytes encodes t->nrows
+ * fixed-width values (`width` bytes each: numpy 'S<n>' bytes, or the UCS-4 bytes of 'U<n>';
+ * host or device memory) into the INT32 column `out_col`: code = 1 + the value's rank in order
+ * of first appearance, and 0 for the empty string (all zero bytes: numpy's padding), so a
+ * zero-initialised code compares like bquery's zero-initialised string.  values (NULL to
+ * skip; at most values_cap values of `width` bytes) receives the distinct values in order of
+ * first appearance, *n_values their count (BQG_E_INVALID when values_cap is too small).  On
+ * the GPU: a hash of each row's bytes into a table of representative rows with a full byte
+ * compare, the first row of each value, a rank scan of the first-row bitmap.  (ABI 7) */
+int bqg_encode_bytes(bqg_ctx* ctx, bqg_table* t, int32_t out_col, const void* bytes, int32_t width, void* values,
+                     int64_t values_cap, int64_t* n_values);
 
 /* ---------------- factor caches (bquery auto_cache, worker.py:291) ----------------
  * The <col>.factor / <col>.values carrays bquery writes next to a shard's columns the first

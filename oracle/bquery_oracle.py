@@ -99,7 +99,23 @@ def _exact_cmp(arr, code, value):
     if isinstance(value, bool):
         value = int(value)
     kind = arr.dtype.kind
-    if kind == 'b':
+    if kind in 'SU':
+        # string columns: bytes / str compared as numpy stores them (trailing NULs are padding;
+        # a py2 str value -- latin-1 after the worker's unpickling -- matches 'S' bytes)
+        if kind == 'S' and isinstance(value, str):
+            value = value.encode('latin-1')
+        if kind == 'U' and isinstance(value, bytes):
+            value = value.decode('latin-1')
+        if not isinstance(value, (bytes, str)):
+            return np.full(arr.shape, code == OP_NE)
+        v = value
+    elif kind in 'Mm':
+        # datetime64 / timedelta64: compared as the column's ticks (ints pass as ticks)
+        if isinstance(value, (int, np.integer)):
+            v = np.asarray(value, np.int64).view(arr.dtype)
+        else:
+            v = np.asarray(value).astype(arr.dtype)
+    elif kind == 'b':
         arr = arr.astype(np.int64)
         kind = 'i'
     if kind in 'iu':
@@ -135,7 +151,7 @@ def _exact_cmp(arr, code, value):
     elif kind == 'f':
         arr = arr.astype(np.float64)
         v = float(value)
-    else:
+    elif kind not in 'SUMm':
         raise NotImplementedError('where_terms on dtype %s' % arr.dtype)
     if code == OP_EQ:
         return arr == v
