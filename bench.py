@@ -364,7 +364,7 @@ def main(argv=None):
                     help='C5: one groupby per shard + local re-group instead of one pass over the rank\'s shards')
     ap.add_argument('--rows', type=int, default=None, help='override rows per shard')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--variant', default='exact', choices=['exact', 'raw'])
+    ap.add_argument('--variant', default='exact', choices=['exact', 'raw', 'wide'])
     ap.add_argument('--local-ranks', type=int, default=1,
                     help='C5: the full 80-shard workload over this many ranks as contexts on one GPU')
     args = ap.parse_args(argv)

@@ -307,7 +307,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -333,6 +333,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"distinct_slots", 0, 0, 1ll << 31},    // initial count_distinct set slots (0: from rows)
     {"part_pack", 1, 0, 1},                 // packed 4-byte partition entries when they fit
     {"scd_runs", 1, 0, 1},                  // fused distinct pass: 256-row steps for clustered keys
+    {"part_win", 0, 0, 4096},               // partitioned aggregate: tiles per window (0: auto; 64..4096)
 };
 
 static int opt_index(const char* name) {
@@ -345,6 +346,7 @@ static bool opt_valid(int i, int64_t v) {
   if (v < kOptDefs[i].lo || v > kOptDefs[i].hi) return false;
   if (i == kOptPartWbits) return v == 0 || v >= 6;
   if (i == kOptPartThreads) return v == 0 || v == 256 || v == 512 || v == 1024;
+  if (i == kOptPartWin) return v == 0 || v >= 64;
   return true;
 }
 
@@ -1149,6 +1151,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
           if (span16 > 0xFFFFull) L.pack = 0;
         }
       }
+      // launch shape: tile size, scatter grid, aggregate splits
       auto shape = [&]() {
         const bool nw = L.narrow != 0, pk = L.pack != 0;
         // scatter workgroup: the widest whose staged tile fits in LDS (option part_threads caps it)
@@ -1174,9 +1177,20 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, L.ntiles));
         L.rows_per_block = ((L.ntiles + L.blocks - 1) / L.blocks) * tr;
         L.blocks = (int)((N + L.rows_per_block - 1) / L.rows_per_block);
+        // aggregate window: the tile bounds of as many tiles as the LDS left beside the slot
+        // table holds (up to kAggWinMax, in 1024-tile steps; option part_win) -- fewer windows,
+        // fewer header-scan prologues; workgroups per CU stay what the slot table allows
+        {
+          const size_t table = part_agg_lds(L.wbits, nsum, pk);
+          const int per_cu_agg = std::max(1, (int)((160 * 1024) / part_agg_lds_launch(L.wbits, nsum, pk, kAggWin)));
+          const size_t budget = (160 * 1024) / per_cu_agg - 1024;  // static LDS of the scans
+          L.win = kAggWin;
+          while (L.win + 1024 <= kAggWinMax && table + 16 * (size_t)(L.win + 1024 + kAggK + 1) <= budget) L.win += 1024;
+          if (c->opt[kOptPartWin]) L.win = (int)std::min<int64_t>(kAggWinMax, c->opt[kOptPartWin]);
+        }
         // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
         // slot table allows one per CU)
-        const size_t agg_lds = part_agg_lds_launch(L.wbits, nsum, pk);
+        const size_t agg_lds = part_agg_lds_launch(L.wbits, nsum, pk, L.win);
         const int fit = std::max(1, (int)((160 * 1024) / agg_lds));
         L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, (c->cu * fit + L.nparts / 2) / L.nparts));
         if (c->opt[kOptPartSplits]) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, c->opt[kOptPartSplits]));
@@ -1187,9 +1201,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
           L.sbits = 40;
           L.pack_flush = 1ll << 23;
         }
-        return true;
       };
-      if (!shape()) shape();
+      shape();
       const bool nw = L.narrow != 0, pk = L.pack != 0;
       c->last.narrow = pk ? 2 : L.narrow;
       const int64_t tr = L.tile_rows;

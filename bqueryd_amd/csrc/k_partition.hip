@@ -153,10 +153,11 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   // F[j], global granule base B[j] (granule = B[j] + flattened position), E[j] (entry index in
   // the tile of a flattened granule's first entry = E[j] + 4 x position) and the segment's
   // entry range AB[j] = a | b << 16; K + 1 sentinels past the last tile.
+  const int WIN = L.win;  // <= kAggWinMax: the header loads below are 4 tiles per thread at most
   uint32_t* wF = reinterpret_cast<uint32_t*>(smem + part_agg_lds(L.wbits, nsum, PACK));
-  uint32_t* wB = wF + kAggWin + kAggK + 1;
-  uint32_t* wE = wB + kAggWin + kAggK + 1;
-  uint32_t* wAB = wE + kAggWin + kAggK + 1;
+  uint32_t* wB = wF + WIN + kAggK + 1;
+  uint32_t* wE = wB + WIN + kAggK + 1;
+  uint32_t* wAB = wE + WIN + kAggK + 1;
   const uint32_t TG = TR >> 2;  // granules per tile
   // one chunk of at most U x 64 consecutive granules of a wave's range, spanning at most K
   // tiles: per granule its 4 entries, its tile (global index; kNoRow past the chunk), the tile
@@ -195,14 +196,17 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   };
   const uint32_t gflush = (uint32_t)(L.pack_flush >> 2);  // granules between flushes
   for (int64_t w0 = t_lo; w0 < t_hi;) {
-    int nw = (int)min((int64_t)kAggWin, t_hi - w0);
-    // headers of the window's tiles (two per thread, contiguous for the scan)
-    uint32_t glen[2], ga[2], ab[2];
+    int nw = (int)min((int64_t)WIN, t_hi - w0);
+    // headers of the window's tiles (up to four per thread, contiguous for the scan; every
+    // load issued before the first is used)
+    constexpr int kHdr = kAggWinMax / 1024;
+    const int per = (nw + (int)blockDim.x - 1) / (int)blockDim.x;  // 1 .. kHdr, uniform
+    uint32_t glen[kHdr], ga[kHdr], ab[kHdr];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int j = 2 * tid + k;
+    for (int k = 0; k < kHdr; ++k) {
+      const int j = per * tid + k;
       glen[k] = ga[k] = ab[k] = 0;
-      if (j < nw) {
+      if (k < per && j < nw) {
         const uint16_t* th = L.hdr + (size_t)(w0 + j) * (size_t)(P + 1) + part;
         const uint32_t a = th[0], b = th[1];
         ga[k] = a >> 2;
@@ -210,18 +214,20 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
         ab[k] = a | (b << 16);
       }
     }
-    uint32_t tot;
-    const uint32_t ex0 = block_excl_scan_1024(glen[0] + glen[1], &tot);
+    uint32_t tot, mine = 0;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int j = 2 * tid + k;
-      const uint32_t fj = ex0 + (k ? glen[0] : 0u);
-      if (j < nw) {
+    for (int k = 0; k < kHdr; ++k) mine += glen[k];
+    uint32_t fj = block_excl_scan_1024(mine, &tot);
+#pragma unroll
+    for (int k = 0; k < kHdr; ++k) {
+      const int j = per * tid + k;
+      if (k < per && j < nw) {
         wF[j] = fj;
         wB[j] = (uint32_t)(w0 + j) * TG + ga[k] - fj;
         wE[j] = 4u * ga[k] - 4u * fj;
         wAB[j] = ab[k];
       }
+      fj += glen[k];
     }
     lds_barrier();
     if (PACK && tot > gflush) {
@@ -519,7 +525,7 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
     }
 #undef BQG_SCATTER
   }
-  const size_t agg_lds = part_agg_lds_launch(L.wbits, p.nsum, L.pack != 0);
+  const size_t agg_lds = part_agg_lds_launch(L.wbits, p.nsum, L.pack != 0, L.win);
   const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
   const unsigned cgrid = (unsigned)std::min<uint64_t>((p.nslots + 255) / 256, 4096);
   if (L.pack) {

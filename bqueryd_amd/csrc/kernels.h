@@ -211,6 +211,7 @@ struct PartLaunch {
   // splits > 1: [nparts][splits] split tables of partial_bytes each, added by k_part_combine
   unsigned char* partial;
   size_t partial_bytes;      // 2^wbits * (8 + 8 * nsum)
+  int win;                   // aggregate window: tiles whose bounds are staged in LDS at once
 };
 // LDS bytes of a scatter workgroup: the staged tile (values, meta), tile counts (two
 // buffers) / offsets and two sets of scan totals
@@ -222,12 +223,13 @@ inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1, boo
 __host__ __device__ inline size_t part_agg_lds(int wbits, int nsum, bool pack) {
   return ((size_t)1 << wbits) * (pack ? 12 : 8 + 8 * (size_t)nsum);
 }
-// the aggregate walks its split's tiles in windows of kAggWin tiles (four words of bounds per
-// tile in LDS); a chunk of entry granules spans at most kAggK tiles
-constexpr int kAggWin = 1024;
+// the aggregate walks its split's tiles in windows of PartLaunch::win tiles (four words of
+// bounds per tile in LDS, up to kAggWinMax); a chunk of entry granules spans at most kAggK tiles
+constexpr int kAggWin = 1024;     // the default window (option part_win = 0 and no room for more)
+constexpr int kAggWinMax = 4096;  // 1024 threads x 4 tiles of header loads
 constexpr int kAggK = 8;
-inline size_t part_agg_lds_launch(int wbits, int nsum, bool pack) {
-  return part_agg_lds(wbits, nsum, pack) + 4 * (size_t)(kAggWin + kAggK + 1) * 4;
+inline size_t part_agg_lds_launch(int wbits, int nsum, bool pack, int win = kAggWin) {
+  return part_agg_lds(wbits, nsum, pack) + 4 * (size_t)(win + kAggK + 1) * 4;
 }
 // fscatter: the query-specialised (JIT) scatter kernel, or nullptr for the precompiled one
 // ffirst: the query-specialised (JIT) first-row pass of packed entries, or nullptr

@@ -246,19 +246,33 @@ __device__ __forceinline__ void part_first_rows_body(const ScanParams& p, const 
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       load_rows4_clamped<NC>(p, base + ((int64_t)threadIdx.x + k * kFirstRowsBlock) * kRowsPerThread, end, raw[k], need, base);
+    // every row's slot first, then all 16 tag loads (independent: issued together), then the
+    // atomics of the matching rows -- a tag load per row waited for one at a time (behind the
+    // previous row's atomic) made the pass latency-bound
+    uint32_t slot[4][4], pass[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int64_t row0 = base + ((int64_t)threadIdx.x + k * kFirstRowsBlock) * kRowsPerThread;
-      if (row0 >= end) continue;
       uint64_t v[NC][4], code[4];
       decode_all<NC, 4>(p, raw[k], v);
-      uint32_t pass = vals_pass<NC, 4>(p, row0, v);
       const int64_t rem = end - row0;
-      pass &= rem >= 4 ? 0xFu : ((1u << rem) - 1u);
+      pass[k] = rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
+      pass[k] &= vals_pass<NC, 4, false>(p, row0, v);
       vals_code<NC, 4>(p, v, code);
 #pragma unroll
+      for (int r = 0; r < 4; ++r) slot[k][r] = ((pass[k] >> r) & 1u) ? (uint32_t)code[r] : 0u;
+    }
+    unsigned char tg[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tg[k][r] = L.first_tag[slot[k][r]];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t row0 = base + ((int64_t)threadIdx.x + k * kFirstRowsBlock) * kRowsPerThread;
+#pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (((pass >> r) & 1u) && L.first_tag[code[r]] == tag) atomicMin(&sa.fst[code[r]], (uint32_t)(row0 + r));
+        if (((pass[k] >> r) & 1u) && tg[k][r] == tag) atomicMin(&sa.fst[slot[k][r]], (uint32_t)(row0 + r));
     }
   }
 }

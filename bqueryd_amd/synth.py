@@ -6,7 +6,9 @@ the same data as in the full shard.
 Float value columns come in two variants:
 * ``exact`` -- quantised to multiples of 2**-6, so every partial sum is exact in float64 and
   GPU/CPU sums agree bit for bit in any order;
-* ``raw`` -- rounded to cents (tolerance tests).
+* ``raw`` -- rounded to cents (tolerance tests);
+* ``wide`` -- fare_amount with refunds and outliers (cents spanning ~2 M codes: the 8-byte
+  partition entries instead of the packed 4-byte ones); other columns as ``raw``.
 """
 from __future__ import annotations
 
@@ -18,7 +20,11 @@ PAYMENT_W = np.array([0.55, 0.30, 0.06, 0.04, 0.02, 0.01, 0.006, 0.002, 0.001, 0
 PASSENGER_W = np.array([0.002, 0.70, 0.14, 0.04, 0.02, 0.05, 0.045, 0.001, 0.001, 0.001])
 
 COLUMNS = ('payment_type', 'vendor_id', 'pu_location_id', 'pickup_location', 'passenger_count',
-           'fare_amount', 'trip_distance')
+           'fare_amount', 'trip_distance', 'store_and_fwd_flag', 'vendor_name', 'pickup_datetime')
+# the taxi frame's non-numeric columns (tests/test_simple_rpc.py:22-26 builds its shards from the
+# full CSV with parse_dates): a one-byte flag ('N' / 'Y', a few empty), a unicode vendor name
+# and the pickup time (datetime64[ns], January 2016)
+STRING_COLUMNS = ('store_and_fwd_flag', 'vendor_name')
 
 
 def _choice(rng, weights, n, offset=0):
@@ -51,7 +57,21 @@ def _draw(name, rng, n, variant):
         return rng.integers(0, 500000, n, dtype=np.int32)
     if name == 'passenger_count':
         return _choice(rng, PASSENGER_W, n)
+    if name == 'store_and_fwd_flag':
+        return np.array([b'N', b'Y', b''], dtype='S1')[_choice(rng, np.array([0.989, 0.01, 0.001]), n)]
+    if name == 'vendor_name':
+        return np.array(['CMT', 'VTS', 'DDS', 'VeriFone'], dtype='U8')[_choice(rng, np.array([0.45, 0.5, 0.03, 0.02]), n)]
+    if name == 'pickup_datetime':
+        t0 = np.datetime64('2016-01-01T00:00:00', 'ns').astype(np.int64)
+        ticks = np.sort(rng.integers(0, 31 * 86400, n)).astype(np.int64) * 1_000_000_000
+        return (t0 + ticks).view('M8[ns]')
     if name == 'fare_amount':
+        if variant == 'wide':
+            # a real fare column's tails: refunds (negative) and outliers in the thousands, in
+            # cents -- ~2 M distinct codes, too wide for the packed 16-bit partition entries
+            v = rng.lognormal(2.3, 0.6, n)
+            v = np.where(rng.random(n) < 0.01, v * rng.uniform(-5.0, 400.0, n), v)
+            return np.round(np.clip(v, -1000.0, 10000.0), 2)
         v = np.clip(rng.lognormal(2.3, 0.6, n), 2.5, 500.0)
     else:  # trip_distance
         v = np.clip(rng.lognormal(0.6, 0.8, n), 0.0, 100.0)

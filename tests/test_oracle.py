@@ -279,3 +279,26 @@ def test_golden_fixtures_against_pandas(name):
         spec.append((a[0], method, a[2]))
     ref = _pd_groupby(pd.DataFrame(cols)[mask], q['groupby'], spec)
     _cmp(out, ref, rtol=1e-12)
+
+
+def test_pandas_string_and_datetime_semantics():
+    """The restatement's string / datetime rules against pandas (the reference's test oracle):
+    first-appearance groups of string and datetime keys, string where-terms (== / != / in /
+    ordering, a py2 str value matching 'S' bytes), and count / nunique of string columns."""
+    cols = synth.taxi_shard(20_000, config_id=2, columns=('payment_type', 'store_and_fwd_flag', 'vendor_name',
+                                                          'pickup_datetime', 'fare_amount'))
+    df = pd.DataFrame(cols)
+    for key in ('store_and_fwd_flag', 'vendor_name', 'pickup_datetime'):
+        got = bo.groupby(cols, [key], [['fare_amount', 'sum', 'fs'], ['vendor_name', 'count_distinct', 'vcd']])
+        ref = df.groupby(key, sort=False).agg(fs=('fare_amount', 'sum'), vcd=('vendor_name', 'nunique')).reset_index()
+        np.testing.assert_array_equal(got[key], ref[key].values.astype(cols[key].dtype))
+        np.testing.assert_allclose(got['fs'], ref['fs'].values, rtol=1e-12)
+        np.testing.assert_array_equal(got['vcd'], ref['vcd'].values)
+    for terms, ref_mask in [
+        ([('store_and_fwd_flag', '==', 'Y')], df['store_and_fwd_flag'] == b'Y'),
+        ([('store_and_fwd_flag', 'nin', ['N', 'Y'])], ~df['store_and_fwd_flag'].isin([b'N', b'Y'])),
+        ([('vendor_name', '>', 'CMT')], df['vendor_name'] > 'CMT'),
+        ([('vendor_name', 'in', ['DDS', 'VTS'])], df['vendor_name'].isin(['DDS', 'VTS'])),
+        ([('pickup_datetime', '<', np.datetime64('2016-01-10'))], df['pickup_datetime'] < pd.Timestamp('2016-01-10')),
+    ]:
+        np.testing.assert_array_equal(bo.where_terms(cols, terms), ref_mask.values)

@@ -508,6 +508,7 @@ int main(int argc, char** argv) {
   L.rows_per_block = ((L.ntiles + L.blocks - 1) / L.blocks) * 4096;
   L.blocks = (int)((n + L.rows_per_block - 1) / L.rows_per_block);
   L.splits = 2;
+  L.win = kAggWin;
   L.capacity = (uint64_t)L.ntiles * 4096;
   CK(hipMalloc(&L.hdr, (size_t)L.ntiles * (L.nparts + 1) * 2 + 256));
   CK(hipMalloc(&L.meta, L.capacity * 4 + 256));
