@@ -25,6 +25,7 @@ import ctypes.util
 import functools
 import json
 import os
+import threading
 import struct
 from collections import OrderedDict
 from concurrent.futures import ThreadPoolExecutor
@@ -91,15 +92,32 @@ def _chunklen_for(itemsize, expectedlen):
 # ------------------------------------------------------------------------------------------
 # blosc frames
 # ------------------------------------------------------------------------------------------
+_TLS = threading.local()
+_ARENA_KEEP_BYTES = 256 << 20  # result arenas up to this size stay allocated between results
+
+
 def compress_chunk(arr, clevel=5, shuffle=1, cname='lz4', nthreads=1):
     arr = np.ascontiguousarray(arr)
     nbytes = arr.nbytes
-    dest = ctypes.create_string_buffer(nbytes + BLOSC_MAX_OVERHEAD)
-    n = blosc().blosc_compress_ctx(clevel, shuffle, arr.dtype.itemsize, nbytes, arr.ctypes.data, dest,
+    # a per-thread destination reused across calls and one copy of the compressed bytes out: a
+    # fresh chunk-sized buffer per call (mmap, page faults, munmap) serialised the compression
+    # pool's threads on the process's memory map
+    dest = getattr(_TLS, 'dest', None)
+    if dest is None or len(dest) < nbytes + BLOSC_MAX_OVERHEAD:
+        dest = _TLS.dest = np.empty(max(nbytes + BLOSC_MAX_OVERHEAD, 1 << 20), np.uint8)
+    n = compress_into(arr, dest, clevel, shuffle, cname, nthreads)
+    return dest[:n].tobytes()
+
+
+def compress_into(arr, dest, clevel=5, shuffle=1, cname='lz4', nthreads=1):
+    """Compress the contiguous array ``arr`` into the uint8 array ``dest`` (at least
+    arr.nbytes + BLOSC_MAX_OVERHEAD long); returns the frame's length."""
+    nbytes = arr.nbytes
+    n = blosc().blosc_compress_ctx(clevel, shuffle, arr.dtype.itemsize, nbytes, arr.ctypes.data, dest.ctypes.data,
                                    nbytes + BLOSC_MAX_OVERHEAD, cname.encode('ascii'), 0, nthreads)
     if n <= 0:
         raise RuntimeError('blosc compression failed (%d)' % n)
-    return dest.raw[:n]
+    return n
 
 
 def decompress_into(frame, out_view):
@@ -190,9 +208,9 @@ def _pool():
     return _POOL
 
 
-def carray_files(arr, chunklen=None, clevel=5, shuffle=1, cname='lz4', frames=None):
+def carray_files(arr, chunklen=None, clevel=5, shuffle=1, cname='lz4', frames=None, parts=False):
     """The files of a carray directory: [(path relative to the carray rootdir, bytes)].
-    ``frames``: the column's compressed chunks when the caller already has them."""
+    ``frames``: the column's compressed chunks (bytes-like) when the caller already has them."""
     arr = np.ascontiguousarray(arr)
     if arr.dtype.kind not in _WRITABLE_KINDS:
         raise NotImplementedError('bcolz writer: dtype %s' % arr.dtype)
@@ -206,7 +224,8 @@ def carray_files(arr, chunklen=None, clevel=5, shuffle=1, cname='lz4', frames=No
     files = []
     cbytes = 0
     for i, frame in enumerate(frames):
-        files.append(('data/__%d.blp' % i, bloscpack_header(1) + frame))
+        # parts=True: the file as (header, frame) -- the caller writes both without joining them
+        files.append(('data/__%d.blp' % i, (bloscpack_header(1), frame) if parts else bloscpack_header(1) + frame))
         cbytes += len(frame) + BLOSCPACK_HEADER
     files.append(('meta/storage', _storage_json(arr.dtype, clevel, shuffle, cname, int(chunklen), int(max(n, 1)))))
     files.append(('meta/sizes', _json_bytes({'shape': [int(n)], 'nbytes': int(arr.nbytes), 'cbytes': int(cbytes)})))
@@ -344,10 +363,12 @@ def ctable_tar(columns, arcname, chunklen=None, cname='lz4'):
     out = []
 
     def member(name, data):
-        out.append(_tar_header(name, len(data), 0o644, now, False))
-        out.append(data)
-        if len(data) % 512:
-            out.append(bytes(512 - len(data) % 512))
+        parts = data if isinstance(data, tuple) else (data,)
+        size = sum(len(d) for d in parts)
+        out.append(_tar_header(name, size, 0o644, now, False))
+        out.extend(parts)
+        if size % 512:
+            out.append(bytes(512 - size % 512))
 
     def directory(name):
         out.append(_tar_header(name + '/', 0, 0o755, now, True))
@@ -362,21 +383,38 @@ def ctable_tar(columns, arcname, chunklen=None, cname='lz4'):
     jobs = [(n, lo) for n in names for lo in range(0, len(arrays[n]), clen[n])]
     total = sum(a.nbytes for a in arrays.values())
 
-    def comp(job):
-        n, lo = job
-        return compress_chunk(arrays[n][lo:lo + clen[n]], 5, 1, cname)
+    # every frame compressed straight into one arena, kept per calling thread and reused (per-
+    # frame buffers cost each pool thread an mmap / munmap pair and page faults on a fresh
+    # buffer, which serialise on the process's memory map) and handed to the tar as views of it
+    # -- the join below copies them out before the arena is used again
+    offs, o = [], 0
+    for n, lo in jobs:
+        offs.append(o)
+        o += min(clen[n], len(arrays[n]) - lo) * arrays[n].dtype.itemsize + BLOSC_MAX_OVERHEAD
+    arena = getattr(_TLS, 'arena', None)
+    if arena is None or len(arena) < o:
+        arena = np.empty(max(o, 1 << 20), np.uint8)
+        if o <= _ARENA_KEEP_BYTES:
+            _TLS.arena = arena
+    view = memoryview(arena)
 
-    done = list(_pool().map(comp, jobs)) if total >= _PARALLEL_MIN_BYTES and len(jobs) > 1 else [comp(j) for j in jobs]
+    def comp(i):
+        n, lo = jobs[i]
+        a = arrays[n][lo:lo + clen[n]]
+        return compress_into(a, arena[offs[i]:offs[i] + a.nbytes + BLOSC_MAX_OVERHEAD], 5, 1, cname)
+
+    idx = range(len(jobs))
+    done = list(_pool().map(comp, idx)) if total >= _PARALLEL_MIN_BYTES and len(jobs) > 1 else [comp(i) for i in idx]
     frames = {n: [] for n in names}
-    for (n, _), f in zip(jobs, done):
-        frames[n].append(f)
+    for i, ((n, _), f) in enumerate(zip(jobs, done)):
+        frames[n].append(view[offs[i]:offs[i] + f])
     root = {ATTRS: _json_bytes({}), ROOTDIRS: _json_bytes({'names': names, 'dirs': {n: n for n in names}})}
     directory(arcname)
     for entry in sorted(list(root) + names):
         if entry in root and entry not in columns:
             member(arcname + '/' + entry, root[entry])
             continue
-        files = dict(carray_files(arrays[entry], chunklen=clen[entry], cname=cname, frames=frames[entry]))
+        files = dict(carray_files(arrays[entry], chunklen=clen[entry], cname=cname, frames=frames[entry], parts=True))
         cdir = arcname + '/' + entry
         directory(cdir)
         member(cdir + '/' + ATTRS, files.pop(ATTRS))

@@ -1186,7 +1186,11 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
           const size_t budget = (160 * 1024) / per_cu_agg - 1024;  // static LDS of the scans
           L.win = kAggWin;
           while (L.win + 1024 <= kAggWinMax && table + 16 * (size_t)(L.win + 1024 + kAggK + 1) <= budget) L.win += 1024;
-          if (c->opt[kOptPartWin]) L.win = (int)std::min<int64_t>(kAggWinMax, c->opt[kOptPartWin]);
+          if (c->opt[kOptPartWin]) {
+            // as asked, but no wider than the LDS beside the slot table holds
+            L.win = (int)std::min<int64_t>(kAggWinMax, c->opt[kOptPartWin]);
+            while (L.win > 64 && table + 16 * (size_t)(L.win + kAggK + 1) > (160 - 1) * 1024) L.win -= 64;
+          }
         }
         // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
         // slot table allows one per CU)

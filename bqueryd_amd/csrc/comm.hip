@@ -499,7 +499,7 @@ enum class MergeOut { kDeviceRoot, kHostRoot, kHostDirect };
 // row), launched on the rank's stream; the key count is copied to st->hcounts() (the caller
 // syncs, then lowers out's row count to it)
 void queue_reduce(Local& l, bqg_table* in, const std::vector<int64_t>& src_off, int n_keys,
-                  const std::vector<int32_t>& dts, const std::vector<int>& lg, TableOwner& out) {
+                  const std::vector<int32_t>& dts, const std::vector<int>& lg, TableOwner& out, bool unique_sources) {
   const int ncols = (int)dts.size();
   const int64_t n = nrows_of(l.ctx, in);
   ck(l.ctx, bqg_table_create(l.ctx, n, ncols, dts.data(), &out.t));
@@ -516,6 +516,7 @@ void queue_reduce(Local& l, bqg_table* in, const std::vector<int64_t>& src_off, 
     m.out_vals[j] = (unsigned char*)col_ptr(l.ctx, out.t, n_keys + j);
   }
   m.nrows = n;
+  m.unique_sources = unique_sources ? 1 : 0;
   const uint64_t cap = bqg::merge_reduce_cap(n);
   m.mask = cap - 1;
   const uint64_t nwords = ((uint64_t)n + 31) / 32, nblocks = (nwords + 1023) / 1024;
@@ -645,7 +646,8 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
         std::vector<int64_t> off(1, 0);
         for (bqg_table* t : parts) off.push_back(off.back() + nrows_of(l.ctx, t));
         cat[i].t = concat_tables(l.ctx, parts, dts);
-        queue_reduce(l, cat[i].t, off, n_keys, dts, lg, red[i]);
+        // a rank's tables (per-shard results) may repeat a key: atomic sums
+        queue_reduce(l, cat[i].t, off, n_keys, dts, lg, red[i], false);
       }
       if (timing) HIPCK(hipStreamSynchronize(l.stream));
       l.st->phase_ms[0] += now_ms() - t0;
@@ -752,7 +754,8 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       if (sources > 1) {
         std::vector<int64_t> off(W + 1, 0);
         for (int s = 0; s < W; ++s) off[s + 1] = off[s] + l.from_peer[s];
-        queue_reduce(l, l.R.t, off, n_keys, dts, lg, red[i]);
+        // every source sent a block of its reduced table: each key once per source
+        queue_reduce(l, l.R.t, off, n_keys, dts, lg, red[i], true);
       }
       if (timing) HIPCK(hipStreamSynchronize(l.stream));
       l.st->phase_ms[3] += now_ms() - t0;

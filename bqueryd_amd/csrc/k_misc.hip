@@ -856,9 +856,10 @@ __device__ __forceinline__ bool mred_same_keys(const PartitionCols& k, int64_t a
 }
 
 // one source block [row0, row1): claim or find each row's slot and add its values to the
-// slot's zero-initialised sums.  A source holds each key once (shard results, reduced
-// partitions), so a launch adds at most once per slot and the sums come out in source order
-// whatever the atomics' timing; a source that repeats a key is still summed correctly.
+// slot's sums -- atomics on zero-initialised sums for tables that may repeat a key (a rank's
+// input tables: a launch adds at most once per slot when they do not, so the sums come out in
+// source order whatever the atomics' timing), plain stores and adds for sources known to hold
+// each key once (the reduced partitions a rank receives).
 __global__ __launch_bounds__(kBlock) void k_mred_insert(MergeReduce m) {
   for (int64_t row = m.row0 + (int64_t)blockIdx.x * kBlock + threadIdx.x; row < m.row1;
        row += (int64_t)gridDim.x * kBlock) {
@@ -891,8 +892,16 @@ __global__ __launch_bounds__(kBlock) void k_mred_insert(MergeReduce m) {
       const int dt = m.vdt[j];
       const uint64_t v = mred_val(m.vals[j], dt, row);
       unsigned long long* a = m.acc + (size_t)j * (m.mask + 1) + pos;
-      if (dtype_is_float(dt)) atomicAdd(reinterpret_cast<double*>(a), as_f64(v));
-      else atomicAdd(a, (unsigned long long)v);  // two's complement: wraps at the output width
+      if (m.unique_sources) {
+        // no other row of this launch has this key: the first source stores, later ones add
+        if (fresh) *a = v;
+        else if (dtype_is_float(dt)) *a = as_u64(as_f64(*a) + as_f64(v));
+        else *a += v;  // two's complement: wraps at the output width
+      } else if (dtype_is_float(dt)) {
+        atomicAdd(reinterpret_cast<double*>(a), as_f64(v));
+      } else {
+        atomicAdd(a, (unsigned long long)v);
+      }
     }
   }
 }
@@ -972,7 +981,7 @@ void launch_merge_reduce(MergeReduce m, const int64_t* src_off, int nsrc, hipStr
   const uint64_t cap = m.mask + 1;
   const uint64_t nwords = ((uint64_t)m.nrows + 31) / 32;
   (void)hipMemsetAsync(m.table, 0xFF, cap * 8, st);
-  (void)hipMemsetAsync(m.acc, 0, cap * 8 * (size_t)std::max(1, m.nvals), st);
+  if (!m.unique_sources) (void)hipMemsetAsync(m.acc, 0, cap * 8 * (size_t)std::max(1, m.nvals), st);
   (void)hipMemsetAsync(m.rep_bits, 0, nwords * 4 + 4, st);
   for (int s = 0; s < nsrc; ++s) {
     m.row0 = src_off[s];

@@ -290,6 +290,9 @@ struct MergeReduce {
   unsigned int* word_prefix;                  // [ceil(nrows / 32)] rank-scan scratch
   unsigned int* block_sum;                    // [ceil(nrows / 32768)] rank-scan scratch
   unsigned int* overflow;                     // a probe ran past the table (cannot at load <= 1/2)
+  int32_t unique_sources;                     // 1: every source holds each key at most once
+                                              // (reduced partitions): plain stores / adds, no
+                                              // zero-initialised sums
   unsigned long long* groups;                 // out: keys found
   unsigned char* out_keys[kMaxKeys];          // out columns, capacity nrows
   unsigned char* out_vals[kMergeMaxVals];

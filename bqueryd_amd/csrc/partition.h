@@ -126,8 +126,11 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
     // the tile histogram alternates between two buffers: the one this tile zeroes at its end
     // is next counted into two tiles later, past the next tile's barriers
     uint32_t* hist = hist2 + parity * P;
+    // PACK keeps one 32-bit staged word and one part|rank word per row across the tile's
+    // barriers (the summed value is packed right after the decode); the wide layouts keep
+    // the values themselves
     uint32_t pass[K], part[K][4], rank[K][4], low[K][4];
-    uint64_t sv[NS][K][4];
+    uint64_t sv[PACK ? 1 : NS][K][4];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int64_t row0 = base + k * CH + (int64_t)tid * kRowsPerThread;
@@ -142,6 +145,10 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
       for (int r = 0; r < 4; ++r) {
         part[k][r] = (uint32_t)(code[r] >> L.wbits);
         low[k][r] = (uint32_t)(code[r] & lowmask);
+        if (PACK) {
+          low[k][r] |= nsum ? part_code16(p, L, v[0][r]) : 0u;
+          continue;
+        }
 #pragma unroll
         for (int s = 0; s < NS; ++s) sv[s][k][r] = v[s][r];
       }
@@ -149,7 +156,11 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
 #pragma unroll
     for (int k = 0; k < K; ++k)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) rank[k][r] = (pass[k] & (1u << r)) ? atomicAdd(&hist[part[k][r]], 1u) : 0u;
+      for (int r = 0; r < 4; ++r) {
+        rank[k][r] = (pass[k] & (1u << r)) ? atomicAdd(&hist[part[k][r]], 1u) : 0u;
+        // partitions < 2^16 and tile ranks < 2^16 (TR <= 16384): one word
+        if (PACK) part[k][r] = (part[k][r] << 16) | rank[k][r];
+      }
     lds_barrier();
     // tile offsets: exclusive scan of the tile histogram, also the tile's header
     uint32_t local = 0;
@@ -171,11 +182,11 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if (!(pass[k] & (1u << r))) continue;
-        const uint32_t pos = toff[part[k][r]] + rank[k][r];
         if (PACK) {
-          smeta[pos] = (nsum ? part_code16(p, L, sv[0][k][r]) : 0u) | low[k][r];
+          smeta[toff[part[k][r] >> 16] + (part[k][r] & 0xFFFFu)] = low[k][r];
           continue;
         }
+        const uint32_t pos = toff[part[k][r]] + rank[k][r];
         smeta[pos] = ((rit0 + r) << L.wbits) | low[k][r];
 #pragma unroll
         for (int s = 0; s < NS; ++s)

@@ -135,18 +135,22 @@ def test_tar_of_tars_and_concat_merge(tmp_path):
     assert rpc.merge_tables([], ['k'], [], aggregate=True) is None
 
 
-@pytest.mark.parametrize('nrows', [0, 1, 70_000])
-def test_ctable_tar_matches_tar_of_written_ctable(tmp_path, nrows):
+@pytest.mark.parametrize('nrows', [0, 1, 70_000, 600_000])
+def test_ctable_tar_matches_tar_of_written_ctable(tmp_path, nrows, monkeypatch):
     """The in-memory result tar has the members, order and contents of tarfile.add over the
     ctable directory write_ctable creates (worker.py:335-346) -- also for a zero-row result,
-    whose columns have no chunk file but keep their data/ and meta/ directories."""
+    whose columns have no chunk file but keep their data/ and meta/ directories; 600 K rows
+    take the compression pool (several chunks per column, frames in one reused arena)."""
     rng = np.random.default_rng(nrows)
     cols = OrderedDict(k=rng.integers(0, 9, nrows).astype(np.int32), s=rng.normal(size=nrows),
                        n=np.arange(nrows, dtype=np.int64))
     d = str(tmp_path / 'result_abcdefgh')
     bcolz_io.write_ctable(d, cols)
     ref = worker.tar_directory(d)
+    import time as _time
+    monkeypatch.setattr(_time, 'time', lambda: 1_700_000_000.25)
     got = bcolz_io.ctable_tar(cols, 'result_abcdefgh')
+    assert bcolz_io.ctable_tar(cols, 'result_abcdefgh') == got  # the reused arena
     with tarfile.open(fileobj=io.BytesIO(ref)) as a, tarfile.open(fileobj=io.BytesIO(got)) as b:
         ma, mb = a.getmembers(), b.getmembers()
         assert [(m.name, m.isdir()) for m in ma] == [(m.name, m.isdir()) for m in mb]
