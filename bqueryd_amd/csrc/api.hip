@@ -1097,6 +1097,19 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   } else {
     // the partitioned aggregate writes every slot itself (no initialisation pass)
     if (pl.mode != kPartitioned) launch_init_slots(sa, nsum, S, st);
+    if (pl.mode != kPartitioned && c->opt[kOptPartNarrow] != 0) {
+      // atomic modes: float sums of exactly codable columns accumulate integer codes (the
+      // same column statistics as the partitioned narrow entries) -- bit-reproducible sums
+      for (int q = 0; q < nsum; ++q) {
+        if (!pl.p.sum_is_float[q] || pl.p.sum_centered[q]) continue;
+        compute_stats(t, pl.tcol[q]);
+        const ColStats& cs = t->cols[pl.tcol[q]].stats;
+        if (!cs.enc) continue;
+        pl.p.sum_enc[q] = cs.enc;
+        pl.p.sum_mul[q] = cs.enc == 1 ? std::ldexp(1.0, cs.enc_k) : 100.0;
+        e.sum_dec[q] = pl.p.sum_mul[q];
+      }
+    }
     HIPCHECK(hipMemsetAsync(sa.hash_fill, 0, 8, st));
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
     if (pl.mode == kShared) {
@@ -1264,7 +1277,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       const int v = pl.std_cols[i];
       const int dt = t->cols[pl.tcol[v]].dtype;
       sc.state[i] = v;
-      sc.conv[i] = dtype_is_float(dt) ? 0 : dt == BQG_U64 ? 2 : 1;
+      sc.conv[i] = pl.p.sum_enc[v] ? 3 : dtype_is_float(dt) ? 0 : dt == BQG_U64 ? 2 : 1;
+      sc.dec[i] = pl.p.sum_mul[v];
     }
     launch_std_centers(sa.cnt, sa.acc, sc, S, centers, st);
     HIPCHECK(hipGetLastError());
@@ -1286,6 +1300,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       q2.sum_is_float[i] = 1;
       q2.sum_conv[i] = pl.p.sum_conv[pl.std_cols[i]];
       q2.sum_centered[i] = 1;
+      q2.sum_enc[i] = 0;
       q2.centers[i] = centers + (size_t)i * S;
     }
     SlotArrays sa2 = sa;

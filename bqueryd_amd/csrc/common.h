@@ -82,6 +82,12 @@ struct ScanParams {
   int32_t sum_conv[kMaxSums];          // input: 0 float bits, 1 signed int, 2 uint64
   int32_t sum_centered[kMaxSums];      // accumulate (v - center[slot])^2 (std pass 2)
   const double* centers[kMaxSums];
+  // shared / global modes: a float sum whose column has an exact 32-bit integer code for every
+  // value (column statistics) accumulates the codes as int64 -- 1 dyadic, code = v * sum_mul;
+  // 2 cents, code = rint(v * sum_mul); 0 = float64 arrival-order sum.  Integer atomics make the
+  // sum independent of the arrival order (bit-reproducible); EmitParams::sum_dec scales it back.
+  int32_t sum_enc[kMaxSums];
+  double sum_mul[kMaxSums];
 };
 
 // Per-slot aggregation state in device memory (global modes, and the target of the

@@ -441,14 +441,16 @@ __device__ __forceinline__ void emit_slot(const EmitParams& e, uint64_t slot, ui
     } else {
       switch (c.op) {
         case BQG_SUM: {
-          const unsigned long long a = t.acc[c.state];
+          unsigned long long a = t.acc[c.state];
+          if (c.in_float && e.sum_dec[c.state] != 0.0) a = as_u64((double)(long long)a / e.sum_dec[c.state]);
           if (c.in_float) bits = (c.out_dtype == BQG_F32) ? (uint64_t)__float_as_uint((float)as_f64(a)) : a;
           else bits = a;  // wrap-around to the output width happens in store_elem
         } break;
         case BQG_COUNT: bits = t.cnt; break;
         case BQG_MEAN: {
           const unsigned long long a = t.acc[c.state];
-          const double s = c.in_float ? as_f64(a) : (c.in_dtype == BQG_U64 ? (double)(uint64_t)a : (double)(long long)a);
+          const double s = c.in_float ? (e.sum_dec[c.state] != 0.0 ? (double)(long long)a / e.sum_dec[c.state] : as_f64(a))
+                                      : (c.in_dtype == BQG_U64 ? (double)(uint64_t)a : (double)(long long)a);
           bits = as_u64(s / (double)t.cnt);
         } break;
         case BQG_STD: {

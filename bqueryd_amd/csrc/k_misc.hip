@@ -804,7 +804,10 @@ __global__ __launch_bounds__(kBlock) void k_std_centers(const unsigned long long
     const int k = (int)(i / nslots);
     const uint64_t s = i - (uint64_t)k * nslots;
     const unsigned long long a = acc[(size_t)sc.state[k] * nslots + s];
-    const double sum = sc.conv[k] == 0 ? as_f64(a) : sc.conv[k] == 2 ? (double)a : (double)(long long)a;
+    const double sum = sc.conv[k] == 0   ? as_f64(a)
+                       : sc.conv[k] == 2 ? (double)a
+                       : sc.conv[k] == 3 ? (double)(long long)a / sc.dec[k]
+                                         : (double)(long long)a;
     const unsigned long long c = cnt[s];
     centers[i] = c ? sum / (double)c : 0.0;
   }

@@ -7,6 +7,12 @@
 
 namespace bqg {
 
+// the exact integer code of a summed float value (ScanParams::sum_enc)
+__device__ __forceinline__ long long sum_code(const ScanParams& p, int q, uint64_t v) {
+  const double d = value_f64(v, p.sum_conv[q]) * p.sum_mul[q];
+  return (long long)(p.sum_enc[q] == 1 ? d : rint(d));
+}
+
 // SHARED mode: one LDS table per workgroup updated with LDS atomics (ds_add_u32/ds_min_u32/
 // ds_add_f64/ds_add_u64), flushed to the per-slot HBM arrays with device-scope atomics.
 // Used for mid-size dense slot spaces (e.g. config C4's 265 pickup locations).
@@ -49,7 +55,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
 #pragma unroll
         for (int q = 0; q < (NC < kMaxSums ? NC : kMaxSums); ++q) {
           if (q < nsum) {
-            if (p.sum_is_float[q]) {
+            if (p.sum_is_float[q] && p.sum_enc[q]) {
+              atomicAdd(&acc[(size_t)q * S + s], (unsigned long long)sum_code(p, q, v[q][r]));
+            } else if (p.sum_is_float[q]) {
               double x = value_f64(v[q][r], p.sum_conv[q]);
               if (p.sum_centered[q]) {
                 const double d = x - p.centers[q][s];
@@ -72,7 +80,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
     atomicMin(&sa.fst[s], fst[s]);
     for (int q = 0; q < nsum; ++q) {
       const unsigned long long a = acc[(size_t)q * S + s];
-      if (p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)q * p.nslots + s]), as_f64(a));
+      if (p.sum_is_float[q] && !p.sum_enc[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)q * p.nslots + s]), as_f64(a));
       else atomicAdd(&sa.acc[(size_t)q * p.nslots + s], a);
     }
   }
@@ -112,7 +120,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_global(ScanParams p, SlotArr
 #pragma unroll
         for (int q = 0; q < (NC < kMaxSums ? NC : kMaxSums); ++q) {
           if (q < nsum) {
-            if (p.sum_is_float[q]) {
+            if (p.sum_is_float[q] && p.sum_enc[q]) {
+              atomicAdd(&sa.acc[(size_t)q * p.nslots + s], (unsigned long long)sum_code(p, q, v[q][r]));
+            } else if (p.sum_is_float[q]) {
               double x = value_f64(v[q][r], p.sum_conv[q]);
               if (p.sum_centered[q]) {
                 const double d = x - p.centers[q][s];

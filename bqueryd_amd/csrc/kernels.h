@@ -30,6 +30,7 @@ struct EmitParams {
   const unsigned long long* cd[kMaxAggs];        // count_distinct per slot
   const unsigned long long* scd_changes[kMaxAggs];
   const unsigned long long* scd_first[kMaxAggs]; // first value bits per slot
+  double sum_dec[kMaxSums];  // != 0: sum state q holds int64 codes, value = code / sum_dec[q]
 };
 
 // Private-LDS mode (small dense slot spaces): the scan writes per-workgroup partials, the
@@ -331,7 +332,8 @@ void launch_bytes_encode(BytesEncode e, hipStream_t st);
 struct StdCenters {
   int32_t n;                // std columns
   int32_t state[kMaxSums];  // their sum-state index in SlotArrays::acc
-  int32_t conv[kMaxSums];   // 0 float bits, 1 signed integer, 2 unsigned integer
+  int32_t conv[kMaxSums];   // 0 float bits, 1 signed integer, 2 unsigned integer, 3 int64 codes / dec
+  double dec[kMaxSums];
 };
 void launch_std_centers(const unsigned long long* cnt, const unsigned long long* acc, const StdCenters& sc,
                         uint64_t nslots, double* centers, hipStream_t st);

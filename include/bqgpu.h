@@ -159,7 +159,9 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *   part_threads   0  scatter workgroup size (0: auto)                 0 | 256 | 512 | 1024
  *   part_per_cu    0  scatter workgroups per CU (0: auto)              0..8
  *   part_splits    0  aggregate workgroups per partition (0: auto)
- *   part_narrow    1  exact 32-bit value codes in partition entries     0 | 1
+ *   part_narrow    1  exact 32-bit value codes of float sums: partition     0 | 1
+ *                     entries, and integer (order-independent) sums in the
+ *                     shared / global atomic modes
  *   fused_scd      1  one fused pass for count / distinct queries       0 | 1
  *   scd_compact    1  ... with 32-bit value codes when they fit         0 | 1
  *   scd_pack16     1  ... first value and first row in one LDS word     0 | 1

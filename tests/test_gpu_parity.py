@@ -750,3 +750,68 @@ def test_engine_options_validate(gpu_device):
         gpu_device.set_option('part_wbits', 3)
     gpu_device.reset_options()
     assert gpu_device.get_option('jit') in (0, 1) and gpu_device.get_option('part_narrow') == 1
+
+
+def _code_sums(keys_codes, ngroups, codes):
+    out = np.zeros(ngroups, np.int64)
+    np.add.at(out, keys_codes, codes)
+    return out
+
+
+@pytest.mark.parametrize('mode', ['shared', 'global_dense', 'hash'])
+@pytest.mark.parametrize('values', ['cents', 'dyadic', 'raw'])
+def test_atomic_mode_float_sums_reproducible(mode, values, oracle_c, engine_options):
+    """The shared / global / hashed atomic modes add a float column with an exact 32-bit code
+    per value (cents, dyadic) as int64 codes: the sums are the same bits on every run and equal
+    the exact code sum scaled back once (one correctly rounded division per group); means
+    follow.  Arbitrary doubles (raw) keep the float64 arrival-order sum: within tolerance of
+    the row-order oracle, not bit-reproducible.  bquery sums in row order
+    (/root/reference/bqueryd/worker.py:313 via bquery's groupby) -- within tolerance of it."""
+    rng = np.random.default_rng(11)
+    n = 1_500_000
+    if mode == 'shared':
+        ng = 1000
+        k = rng.integers(0, ng, n).astype(np.int32)
+    elif mode == 'global_dense':
+        engine_options(partition=0)
+        ng = 200_000
+        k = rng.integers(0, ng, n).astype(np.int32)
+    else:
+        pool = np.unique(rng.integers(-2**40, 2**40, 30_000))
+        ng = len(pool)
+        k = pool[rng.integers(0, ng, n)]
+    if values == 'cents':
+        codes = rng.integers(-500_000, 5_000_000, n)
+        v, mul = codes / 100.0, 100.0
+    elif values == 'dyadic':
+        codes = rng.integers(-2**20, 2**24, n)
+        v, mul = np.ldexp(codes.astype(np.float64), -6), 64.0
+    else:
+        v, mul = rng.normal(size=n) * 1e3, None
+    cols = OrderedDict(k=k, v=v)
+    aggs = [['v', 'sum', 's'], ['v', 'mean', 'm'], ['v', 'count', 'n']]
+    runs = []
+    t = ShardTable(cols)
+    try:
+        for _ in range(3):
+            got, _ = t.groupby(['k'], aggs)
+            runs.append(got)
+            info = t.dev.last_timing()
+    finally:
+        t.close()
+    assert info['mode'] == {'shared': 1, 'global_dense': 2, 'hash': 3}[mode], info
+    ref = oracle_c.groupby(cols, ['k'], aggs, None)
+    assert_tables_equal(runs[0], ref)
+    if mul is None:
+        return
+    for r in runs[1:]:
+        assert_tables_equal(r, runs[0], exact_float_sums=True)
+    # the exact code sum per group, scaled back once
+    gk = runs[0]['k']
+    if mode == 'hash':
+        idx = np.searchsorted(pool, k)
+        exp = _code_sums(idx, ng, codes)[np.searchsorted(pool, gk)]
+    else:
+        exp = _code_sums(k, ng, codes)[gk]
+    np.testing.assert_array_equal(runs[0]['s'], exp.astype(np.float64) / mul)
+    np.testing.assert_array_equal(runs[0]['m'], (exp.astype(np.float64) / mul) / runs[0]['n'].astype(np.float64))
