@@ -138,6 +138,10 @@ struct ColStats {
   // codes): 1 = dyadic, code = v * 2^enc_k; 2 = cents, code = rint(v * 100); 0 = none
   int enc = 0;
   int enc_k = 0;
+  // the same codes where the sum of every row's |code| stays below 2^63 (int64 sums that
+  // cannot overflow; the atomic modes and the wide partitioned entries): a superset of enc
+  int enc64 = 0;
+  int enc64_k = 0;
   int64_t runs = -1;  // value runs (rows differing from the row before + 1), -1 = not measured
 };
 
@@ -417,7 +421,7 @@ int guard(bqg_ctx* ctx, F&& f) {
 // statistics
 // ------------------------------------------------------------------------------------
 // the k_stats result words of one column -> its ColStats (min / max / NaN / exact codes)
-void finish_stats(Column& k, const unsigned long long* r) {
+void finish_stats(Column& k, const unsigned long long* r, int64_t nrows) {
   const unsigned long long mn = r[0], mx = r[1], lsb = r[3], enc = r[4];
   k.stats.has_nan = r[2] != 0;
   k.stats.empty = mn > mx;
@@ -441,6 +445,17 @@ void finish_stats(Column& k, const unsigned long long* r) {
           k.stats.enc_k = kk;
         } else if (!(enc & 2ull) && maxabs * 100.0 < 2147483647.0) {
           k.stats.enc = 2;
+        }
+        const double rows = (double)std::max<int64_t>(nrows, 1);
+        if (!(enc & 1ull) && kk <= 1000 && std::ldexp(maxabs, kk) * rows < 9.2e18) {
+          k.stats.enc64 = 1;
+          k.stats.enc64_k = kk;
+        } else if (!(enc & 2ull) && maxabs * 100.0 * rows < 9.2e18) {
+          k.stats.enc64 = 2;
+        }
+        if (k.stats.enc) {  // the 32-bit code's kind wins (same kind, same scale)
+          k.stats.enc64 = k.stats.enc;
+          k.stats.enc64_k = k.stats.enc_k;
         }
       }
     } else if (k.dtype == BQG_U64) {
@@ -483,7 +498,7 @@ void compute_stats_many(bqg_table* t, const std::vector<int>& cols) {
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipMemcpyAsync(h + 8 * n, d, n * sizeof(init), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
-  for (size_t i = 0; i < n; ++i) finish_stats(t->cols[todo[i]], h + 8 * n + 8 * i);
+  for (size_t i = 0; i < n; ++i) finish_stats(t->cols[todo[i]], h + 8 * n + 8 * i, t->nrows);
 }
 
 void compute_stats(bqg_table* t, int col) {
@@ -1104,9 +1119,9 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         if (!pl.p.sum_is_float[q] || pl.p.sum_centered[q]) continue;
         compute_stats(t, pl.tcol[q]);
         const ColStats& cs = t->cols[pl.tcol[q]].stats;
-        if (!cs.enc) continue;
-        pl.p.sum_enc[q] = cs.enc;
-        pl.p.sum_mul[q] = cs.enc == 1 ? std::ldexp(1.0, cs.enc_k) : 100.0;
+        if (!cs.enc64) continue;
+        pl.p.sum_enc[q] = cs.enc64;
+        pl.p.sum_mul[q] = cs.enc64 == 1 ? std::ldexp(1.0, cs.enc64_k) : 100.0;
         e.sum_dec[q] = pl.p.sum_mul[q];
       }
     }
@@ -1140,6 +1155,17 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
                      (cs.empty || (uint64_t)cs.imax - (uint64_t)cs.imin <= 0xFFFFFFFFull);
           L.enc_kind[q] = 3;
           L.enc_off[q] = cs.empty ? 0 : cs.imin;
+        }
+      }
+      if (!L.narrow && c->opt[kOptPartNarrow] != 0) {
+        // wide entries: float sums of int64-codable columns add codes (deterministic)
+        for (int q = 0; q < nsum; ++q) {
+          if (!pl.p.sum_is_float[q] || pl.p.sum_centered[q]) continue;
+          compute_stats(t, pl.tcol[q]);
+          const ColStats& cs = t->cols[pl.tcol[q]].stats;
+          if (!cs.enc64) continue;
+          pl.p.sum_enc[q] = cs.enc64;
+          pl.p.sum_mul[q] = cs.enc64 == 1 ? std::ldexp(1.0, cs.enc64_k) : 100.0;
         }
       }
       // packed 4-byte entries (option part_pack): no summed column, or one narrow-coded

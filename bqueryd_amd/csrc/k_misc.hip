@@ -122,19 +122,14 @@ __global__ void k_setbits(const uint32_t* list_fst, unsigned int n, unsigned int
 
 __global__ __launch_bounds__(1024) void k_word_scan(const unsigned int* bitmap, uint64_t nwords,
                                                     unsigned int* word_prefix, unsigned int* block_sum) {
-  __shared__ unsigned int sh[1024];
+  // the block scan of wave scans (one barrier; a 20-barrier LDS ladder took 17 us for the
+  // 3 M words of a 100 M-row bitmap)
   const uint64_t w = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
   const unsigned int c = w < nwords ? (unsigned int)__popc(bitmap[w]) : 0u;
-  sh[threadIdx.x] = c;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const unsigned int t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
-    __syncthreads();
-    sh[threadIdx.x] += t;
-    __syncthreads();
-  }
-  if (w < nwords) word_prefix[w] = sh[threadIdx.x] - c;
-  if (threadIdx.x == 1023) block_sum[blockIdx.x] = sh[1023];
+  unsigned int tot;
+  const unsigned int e = block_excl_scan_1024(c, &tot);
+  if (w < nwords) word_prefix[w] = e;
+  if (threadIdx.x == 0) block_sum[blockIdx.x] = tot;
 }
 
 __global__ __launch_bounds__(1024) void k_block_scan(unsigned int* block_sum, uint64_t nblocks) {
@@ -336,7 +331,8 @@ __device__ __forceinline__ unsigned long long ord_key_f(double d) {
 // out[3]: min over non-zero values of (exponent of the lowest set mantissa bit + 4096), so
 // every value is an integer multiple of 2^(out[3] - 4096); out[4]: bit 0 -- some value is
 // subnormal or infinite (no dyadic code), bit 1 -- some value is not a whole number of
-// hundredths (rint(v * 100) / 100 != v: no cents code).
+// hundredths (rint(v * 100) / 100 != v, or |v * 100| > 2^53: no cents code).  The code's
+// width bounds (32-bit codes, or int64 sums that cannot overflow) are the host's.
 __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsigned long long* partial) {
   unsigned long long mn = ~0ull, mx = 0ull, nan = 0ull, lsb = ~0ull, enc = 0ull;
   const bool isf = dtype_is_float(c.dtype);
@@ -365,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsig
           lsb = min(lsb, (unsigned long long)((int)ex - 1075 + __builtin_ctzll(m) + 4096));
         }
         const double n = rint(d * 100.0);
-        if (n / 100.0 != d || fabs(n) > 2147483647.0) enc |= 2ull;
+        if (n / 100.0 != d || fabs(n) > 9007199254740992.0) enc |= 2ull;
       } else if (u64) {
         k = (unsigned long long)chunk_i64(ch, c.dtype, r);
       } else {

@@ -47,6 +47,12 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartL
 // slot's first tile, and the combine leaves first rows to k_part_first_rows.
 // One split's record of a slot: count, first row (PACK: first tile), sums (PACK: 64-bit count
 // c64 and the code16 sum a[0]).
+// the exact int64 code of a summed float value of a wide entry (ScanParams::sum_enc)
+__device__ __forceinline__ long long part_sum_code(const ScanParams& p, int q, uint64_t v) {
+  const double d = value_f64(v, p.sum_conv[q]) * p.sum_mul[q];
+  return (long long)(p.sum_enc[q] == 1 ? d : rint(d));
+}
+
 template <int NV>
 struct PartRec {
   unsigned long long a[NV];
@@ -100,7 +106,7 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
     f = r.f < f ? r.f : f;
 #pragma unroll
     for (int q = 0; q < nsum; ++q) {
-      if (!NARROW && p.sum_is_float[q]) a[q] = as_u64(as_f64(a[q]) + as_f64(r.a[q]));
+      if (!NARROW && p.sum_is_float[q] && !p.sum_enc[q]) a[q] = as_u64(as_f64(a[q]) + as_f64(r.a[q]));
       else a[q] += r.a[q];
     }
   }
@@ -113,6 +119,8 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
     if (NARROW) {
       if (L.enc_kind[q] == 3) a[q] += (unsigned long long)c * (unsigned long long)L.enc_off[q];
       else a[q] = as_u64((double)(long long)a[q] / L.enc_mul[q]);
+    } else if (p.sum_is_float[q] && p.sum_enc[q]) {
+      a[q] = as_u64((double)(long long)a[q] / p.sum_mul[q]);
     }
     sa.acc[(size_t)q * p.nslots + gs] = a[q];
   }
@@ -347,7 +355,10 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
           atomicMin(&fst[sl], row);
 #pragma unroll
           for (int q = 0; q < nsum; ++q) {
-            if (!NARROW && p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][e][q], p.sum_conv[q]));
+            // wide entries of an int64-codable float column (ScanParams::sum_enc): integer
+            // code sums, the same whatever order the entries arrive in
+            if (!NARROW && p.sum_is_float[q] && p.sum_enc[q]) atomicAdd(&acc[(size_t)q * W + sl], (unsigned long long)part_sum_code(p, q, en.v[u][e][q]));
+            else if (!NARROW && p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][e][q], p.sum_conv[q]));
             else atomicAdd(&acc[(size_t)q * W + sl], en.v[u][e][q]);
           }
         }

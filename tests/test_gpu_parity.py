@@ -758,19 +758,23 @@ def _code_sums(keys_codes, ngroups, codes):
     return out
 
 
-@pytest.mark.parametrize('mode', ['shared', 'global_dense', 'hash'])
-@pytest.mark.parametrize('values', ['cents', 'dyadic', 'raw'])
+@pytest.mark.parametrize('mode', ['shared', 'global_dense', 'hash', 'partitioned'])
+@pytest.mark.parametrize('values', ['cents', 'dyadic', 'cents_big', 'dyadic_big', 'raw'])
 def test_atomic_mode_float_sums_reproducible(mode, values, oracle_c, engine_options):
-    """The shared / global / hashed atomic modes add a float column with an exact 32-bit code
-    per value (cents, dyadic) as int64 codes: the sums are the same bits on every run and equal
-    the exact code sum scaled back once (one correctly rounded division per group); means
-    follow.  Arbitrary doubles (raw) keep the float64 arrival-order sum: within tolerance of
-    the row-order oracle, not bit-reproducible.  bquery sums in row order
+    """The shared / global / hashed atomic modes and the partitioned path's wide entries add
+    a float column with an exact integer code per value (cents, dyadic; _big: codes beyond
+    32 bits whose int64 sums cannot overflow) as int64 codes: the sums are the same bits on
+    every run and equal the exact code sum scaled back once (one correctly rounded division per
+    group); means follow.  Arbitrary doubles (raw) keep the float64 arrival-order sum: within
+    tolerance of the row-order oracle, not bit-reproducible.  bquery sums in row order
     (/root/reference/bqueryd/worker.py:313 via bquery's groupby) -- within tolerance of it."""
     rng = np.random.default_rng(11)
     n = 1_500_000
     if mode == 'shared':
         ng = 1000
+        k = rng.integers(0, ng, n).astype(np.int32)
+    elif mode == 'partitioned':
+        ng = 300_000
         k = rng.integers(0, ng, n).astype(np.int32)
     elif mode == 'global_dense':
         engine_options(partition=0)
@@ -786,6 +790,12 @@ def test_atomic_mode_float_sums_reproducible(mode, values, oracle_c, engine_opti
     elif values == 'dyadic':
         codes = rng.integers(-2**20, 2**24, n)
         v, mul = np.ldexp(codes.astype(np.float64), -6), 64.0
+    elif values == 'cents_big':
+        codes = rng.integers(-10**11, 10**12, n)
+        v, mul = codes / 100.0, 100.0
+    elif values == 'dyadic_big':
+        codes = rng.integers(-2**40, 2**41, n)
+        v, mul = np.ldexp(codes.astype(np.float64), -6), 64.0
     else:
         v, mul = rng.normal(size=n) * 1e3, None
     cols = OrderedDict(k=k, v=v)
@@ -799,7 +809,7 @@ def test_atomic_mode_float_sums_reproducible(mode, values, oracle_c, engine_opti
             info = t.dev.last_timing()
     finally:
         t.close()
-    assert info['mode'] == {'shared': 1, 'global_dense': 2, 'hash': 3}[mode], info
+    assert info['mode'] == {'shared': 1, 'global_dense': 2, 'hash': 3, 'partitioned': 4}[mode], info
     ref = oracle_c.groupby(cols, ['k'], aggs, None)
     assert_tables_equal(runs[0], ref)
     if mul is None:

@@ -12,7 +12,7 @@
 //      the last value -- two random LDS accesses per slot instead of three per row.
 // Rows: C4's shape (265 pickup locations, passenger_count values 0..9), random order; one wave
 // per 64 Ki-row chunk, 20-byte-per-slot wave state as in the compact library kernel.
-// build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/micro/scd_match_micro.hip -o build/scd_match_micro
+// build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/micro/scd_match_micro.hip -o tools/micro/bin/scd_match_micro
 // run:   scd_match_micro [rows] [reps]
 #include <hip/hip_runtime.h>
 
