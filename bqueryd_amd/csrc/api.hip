@@ -616,14 +616,26 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     if (g.op == BQG_SUM || g.op == BQG_MEAN || g.op == BQG_STD) {
       const int dt = t->cols[g.col].dtype;
       if (dt == BQG_BOOL) fail(BQG_E_UNSUPPORTED, "sum/mean/std of a bool column");
+      // mean / std of a 64-bit integer column whose sum can leave the 64-bit accumulator: a
+      // float64 sum state of its own (bquery's incremental mean runs in float64 and never
+      // wraps; the sum keeps its wrapping integer state)
+      bool fview = false;
+      if ((g.op == BQG_MEAN || g.op == BQG_STD) && (dt == BQG_I64 || dt == BQG_U64)) {
+        compute_stats(t, g.col);
+        const ColStats& cs = t->cols[g.col].stats;
+        const double rows = (double)std::max<int64_t>(t->nrows, 1);
+        const double mx = dt == BQG_U64 ? (double)(uint64_t)cs.imax
+                                        : std::max(std::fabs((double)cs.imin), std::fabs((double)cs.imax));
+        fview = !cs.empty && mx * rows >= (dt == BQG_U64 ? 1.8e19 : 9.2e18);
+      }
       int st = -1;
       for (int s = 0; s < (int)pl.tcol.size(); ++s)
-        if (pl.tcol[s] == g.col) st = s;
+        if (pl.tcol[s] == g.col && (pl.p.sum_is_float[s] != 0) == (dtype_is_float(dt) || fview)) st = s;
       if (st < 0) {
         if ((int)pl.tcol.size() >= kMaxSums) fail(BQG_E_UNSUPPORTED, "more than %d summed columns", kMaxSums);
         pl.tcol.push_back(g.col);
         st = (int)pl.tcol.size() - 1;
-        pl.p.sum_is_float[st] = dtype_is_float(dt);
+        pl.p.sum_is_float[st] = dtype_is_float(dt) || fview;
         pl.p.sum_conv[st] = dtype_is_float(dt) ? 0 : (dt == BQG_U64 ? 2 : 1);
         pl.p.sum_centered[st] = 0;
         pl.p.centers[st] = nullptr;
@@ -823,6 +835,8 @@ void build_emit(bqg_table* t, const bqg_query* q, const Plan& pl, EmitParams& e,
     ec.in_dtype = in_dt;
     ec.in_float = dtype_is_float(in_dt);
     ec.out_dtype = agg_out_dtype(g.op, in_dt);
+    // a mean over an integer column's float64 sum state (plan_query: 64-bit sums that can wrap)
+    if (g.op == BQG_MEAN) ec.in_float = pl.p.sum_is_float[pl.agg_state[a]];
     if (g.op == BQG_SUM || g.op == BQG_MEAN) ec.state = pl.agg_state[a];
     else if (g.op == BQG_STD) {
       int idx = 0;
@@ -1303,8 +1317,11 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       const int v = pl.std_cols[i];
       const int dt = t->cols[pl.tcol[v]].dtype;
       sc.state[i] = v;
-      sc.conv[i] = pl.p.sum_enc[v] ? 3 : dtype_is_float(dt) ? 0 : dt == BQG_U64 ? 2 : 1;
-      sc.dec[i] = pl.p.sum_mul[v];
+      // the pass-1 accumulator: int64 codes (atomic modes, e.sum_dec), float64 bits (float
+      // columns, float64 sum states of integer columns, the partitioned path's finished
+      // codes) or an integer sum
+      sc.conv[i] = e.sum_dec[v] != 0.0 ? 3 : pl.p.sum_is_float[v] ? 0 : dt == BQG_U64 ? 2 : 1;
+      sc.dec[i] = e.sum_dec[v];
     }
     launch_std_centers(sa.cnt, sa.acc, sc, S, centers, st);
     HIPCHECK(hipGetLastError());

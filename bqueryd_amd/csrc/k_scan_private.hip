@@ -16,53 +16,63 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_private(ScanParams p, Privat
 
 __device__ void private_finish_body(const FinishParams& f, const SlotArrays& sa, const EmitParams& e, int tid);
 
-// One workgroup per (component, slot): sums / mins that slot's per-workgroup partials in a
-// fixed order (coalesced reads, fixed LDS tree: bitwise deterministic).  The last workgroup
-// to finish (device-scope counter) runs the finish step, so a query is one launch after the
-// scan.
-__global__ __launch_bounds__(kBlock) void k_private_reduce(FinishParams f, SlotArrays sa, EmitParams e) {
-  __shared__ unsigned long long red[kBlock];
-  const int pair = blockIdx.x, tid = threadIdx.x;
+// ONE workgroup: every (component, slot) pair's per-workgroup partials are reduced by one wave
+// (lane-strided reads in a fixed order, then a fixed shuffle tree: bitwise deterministic) into
+// LDS, and wave 0 runs the finish step -- no grid of reduce workgroups, no device-scope
+// "last workgroup" counter and fences between them (the two-level version took ~11 us of C2's
+// ~0.29 ms step).
+constexpr int kPrivReduceThreads = 1024;
+__global__ __launch_bounds__(kPrivReduceThreads) void k_private_reduce(FinishParams f, SlotArrays sa, EmitParams e) {
+  __shared__ unsigned long long tot[(2 + kMaxSums) * kMaxPrivateSlots];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = kPrivReduceThreads / 64;
   const int S = f.nslots, nb = f.blocks;
-  const int comp = pair / S;
-  const bool isf = comp >= 2 && f.sum_is_float[comp - 2];
-  const unsigned long long* src = f.partials + (size_t)pair * nb;
-  unsigned long long v;
-  if (comp == 1) {
-    uint32_t m = kNoRow;
-    for (int b = tid; b < nb; b += kBlock) m = min(m, (uint32_t)src[b]);
-    v = m;
-  } else if (isf) {
-    double x = 0.0;
-    for (int b = tid; b < nb; b += kBlock) x += as_f64(src[b]);
-    v = as_u64(x);
-  } else {
-    unsigned long long x = 0;
-    for (int b = tid; b < nb; b += kBlock) x += src[b];
-    v = x;
-  }
-  red[tid] = v;
-  __syncthreads();
-  for (int w = kBlock / 2; w >= 1; w >>= 1) {
-    if (tid < w) {
-      const unsigned long long o = red[tid + w];
-      if (comp == 1) red[tid] = min(red[tid], o);
-      else if (isf) red[tid] = as_u64(as_f64(red[tid]) + as_f64(o));
-      else red[tid] = red[tid] + o;
+  const int P = (2 + f.nsum) * S;
+  for (int pair = wave; pair < P; pair += nwaves) {
+    const int comp = pair / S;
+    const bool isf = comp >= 2 && f.sum_is_float[comp - 2];
+    const unsigned long long* src = f.partials + (size_t)pair * nb;
+    // the lane's partials, 16 loads issued together per round (nb <= 1024 at 4 workgroups per
+    // CU: one round), then combined in order
+    unsigned long long acc = comp == 1 ? (unsigned long long)kNoRow : 0ull;
+    for (int b0 = 0; b0 < nb; b0 += 64 * 16) {
+      unsigned long long x[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int b = b0 + i * 64 + lane;
+        x[i] = b < nb ? src[b] : (comp == 1 ? (unsigned long long)kNoRow : 0ull);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (comp == 1) acc = min(acc, x[i]);
+        else if (isf) acc = as_u64(as_f64(acc) + as_f64(x[i]));
+        else acc += x[i];
+      }
     }
-    __syncthreads();
-  }
-  __shared__ bool last;
-  if (tid == 0) {
-    f.totals[pair] = red[0];
-    __threadfence();  // release the total before counting this workgroup done
-    last = atomicAdd(f.done, 1u) == gridDim.x - 1;
+    unsigned long long v;
+    if (comp == 1) {
+      uint32_t m = (uint32_t)acc;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
+      v = m;
+    } else if (isf) {
+      double x = as_f64(acc);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+      v = as_u64(x);
+    } else {
+      unsigned long long x = acc;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) x += (unsigned long long)__shfl_xor((long long)x, o, 64);
+      v = x;
+    }
+    if (lane == 0) tot[pair] = v;
   }
   __syncthreads();
-  if (!last) return;
-  __threadfence();  // acquire every workgroup's total
-  if (tid < 64) private_finish_body(f, sa, e, tid);
-  if (tid == 0) *f.done = 0u;  // ready for the next launch (stream order)
+  if (tid < 64) {
+    FinishParams g = f;
+    g.totals = tot;  // the finish step reads the totals from LDS
+    private_finish_body(g, sa, e, tid);
+  }
 }
 
 // Emits the groups in first-appearance order (S is small: rank by counting), or stores the
@@ -116,7 +126,7 @@ void launch_scan_private(const ScanParams& p, const PrivateLaunch& l, hipStream_
 }
 
 void launch_private_finish(const FinishParams& f, const SlotArrays& s, const EmitParams& e, hipStream_t st) {
-  hipLaunchKernelGGL(k_private_reduce, dim3((2 + f.nsum) * f.nslots), dim3(kBlock), 0, st, f, s, e);
+  hipLaunchKernelGGL(k_private_reduce, dim3(1), dim3(kPrivReduceThreads), 0, st, f, s, e);
 }
 
 }  // namespace bqg

@@ -825,3 +825,38 @@ def test_atomic_mode_float_sums_reproducible(mode, values, oracle_c, engine_opti
         exp = _code_sums(k, ng, codes)[gk]
     np.testing.assert_array_equal(runs[0]['s'], exp.astype(np.float64) / mul)
     np.testing.assert_array_equal(runs[0]['m'], (exp.astype(np.float64) / mul) / runs[0]['n'].astype(np.float64))
+
+
+@pytest.mark.parametrize('mode', ['private', 'shared', 'global_dense', 'partitioned', 'hash'])
+def test_moments_of_wrapping_int64_and_coded_columns(mode, oracle_c, engine_options):
+    """mean / std next to sum: of an int64 column whose sum wraps the 64-bit accumulator
+    (bquery's typed sum wraps, its float64 incremental mean and std do not: the mean / std
+    take a float64 sum state of their own), and of a cents column (integer-coded sums in the
+    atomic modes and the wide partitioned entries: the std centres decode the codes exactly
+    once).  Sums bit-exact (the integer one modulo 2^64), moments within 1e-12."""
+    rng = np.random.default_rng(21)
+    n = 200_000
+    if mode == 'private':
+        k = rng.integers(0, 6, n).astype(np.int32)
+    elif mode == 'shared':
+        k = rng.integers(0, 900, n).astype(np.int32)
+    elif mode == 'global_dense':
+        engine_options(partition=0)
+        k = rng.integers(0, 150_000, n).astype(np.int32)
+    elif mode == 'partitioned':
+        k = rng.integers(0, 150_000, n).astype(np.int32)
+    else:
+        k = rng.integers(-2**40, 2**40, 5_000)[rng.integers(0, 5_000, n)]
+    cols = OrderedDict(k=k, big=rng.integers(2**61, 2**62, n).astype(np.int64),
+                       c=rng.integers(-10**11, 10**11, n) / 100.0)
+    aggs = [['big', 'sum', 'bs'], ['big', 'mean', 'bm'], ['big', 'std', 'bsd'],
+            ['c', 'sum', 'cs'], ['c', 'mean', 'cm'], ['c', 'std', 'csd'], ['c', 'count', 'n']]
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(['k'], aggs)
+        info = t.dev.last_timing()
+    finally:
+        t.close()
+    assert info['mode'] == {'private': 0, 'shared': 1, 'global_dense': 2, 'hash': 3, 'partitioned': 4}[mode], info
+    ref = bo.groupby(cols, ['k'], aggs)
+    assert_tables_equal(got, ref, exact_cols={'bs'})
