@@ -156,13 +156,26 @@ def _case(seed):
 
 
 @pytest.mark.parametrize('seed', range(N_CASES))
-def test_random_queries_match_the_oracle(seed):
+def test_random_queries_match_the_oracle(seed, engine_options):
+    """A third of the cases run the run-time specialised (hiprtc) kernels at these small
+    sizes (option jit_min_rows=0); cases with terms also run bquery's expand_filter_column
+    (worker.py:306-307: the mask widened to whole runs of a key column)."""
     cols, keys, aggs, terms, raw_rows = _case(seed)
+    if seed % 3 == 1:
+        engine_options(jit_min_rows=0)
     ref = bo.handle_work(cols, keys, aggs, terms)
     t = ShardTable(cols)
     try:
         got, _ = t.groupby(keys, aggs, where_terms=terms)
         assert_tables_equal(got, ref)
+        if terms and len(cols[keys[0]]):
+            basket = keys[int(seed) % len(keys)]
+            if cols[basket].dtype.kind in 'iub':
+                m, _ = t.where(terms)
+                e = t.expand_subgroups(basket, m)
+                got_e, _ = t.groupby(keys, aggs, mask=e)
+                ref_e = bo.handle_work(cols, keys, aggs, terms, expand_filter_column=basket)
+                assert_tables_equal(got_e, ref_e)
         if raw_rows:
             sel = list(keys) + [a[0] for a in aggs if a[0] not in keys]
             sel = list(OrderedDict.fromkeys(sel))
@@ -249,3 +262,80 @@ def test_random_merges_match_the_client_merge(seed):
         return
     got = OrderedDict((k, np.asarray(merged[k])) for k in ref)
     assert_tables_equal(sort_by_keys(got, keys), sort_by_keys(ref, keys))
+
+
+N_WORKER_CASES = 10
+WORKER_KEY_KINDS = ['i4', 'u2', 'f8', 'S3', 'U2', 'M8', 'i8w']
+
+
+@pytest.mark.parametrize('seed', range(N_WORKER_CASES))
+def test_random_worker_messages_match_the_reference_path(seed, tmp_path):
+    """The whole drop-in path on random bcolz shards: 1-4 shard files (string, datetime and
+    numeric columns) written by bcolz_io, one CalcPath.handle_work per file (worker.py:269-348:
+    ctable open, factor caches, where terms, groupby, result ctable + tar) and, for
+    aggregate=True, one node-level message over all of them; the controller's tar of tars and
+    the client's uncompress_groupby_to_df (rpc.py:134-179) -- against the reference client
+    merge of the oracle's per-shard results (sorted by the keys: the reference's own order is
+    the glob order, rpc.py:151)."""
+    import os
+    from bqueryd_amd import bcolz_io, messages, rpc
+    from bqueryd_amd.worker import CalcPath
+    from tests.helpers import sort_by_keys
+    rng = np.random.default_rng(9000 + seed)
+    n_files = int(rng.integers(1, 5))
+    nkeys = int(rng.integers(1, 3))
+    key_kinds = [WORKER_KEY_KINDS[i] for i in rng.choice(len(WORKER_KEY_KINDS), nkeys, replace=False)]
+    val_kinds = [VALUE_KINDS[i] for i in rng.choice(len(VALUE_KINDS), 2, replace=False)]
+    files, shards = [], []
+    for f in range(n_files):
+        n = [1, 700, 9_000, 20_001][int(rng.integers(0, 4))]
+        cols = OrderedDict()
+        for i, k in enumerate(key_kinds):
+            cols['k%d_%s' % (i, k)] = _key_column(rng, k, n)
+        for i, k in enumerate(val_kinds):
+            cols['v%d_%s' % (i, k)] = _value_column(rng, k, n)
+        fn = 'shard-%d.bcolzs' % f
+        bcolz_io.write_ctable(os.path.join(str(tmp_path), fn), cols)
+        files.append(fn)
+        shards.append(cols)
+    keys = list(shards[0])[:nkeys]
+    aggs = []
+    for j in range(int(rng.integers(1, 4))):
+        vi = int(rng.integers(0, 2))
+        name, kind = 'v%d_%s' % (vi, val_kinds[vi]), val_kinds[vi]
+        ops = ['count'] + (['sum'] if kind in SUMMABLE else []) + (['mean'] if kind in MOMENTS else []) + \
+              (['count_distinct'] if kind in DISTINCTABLE else [])
+        aggs.append([name, ops[int(rng.integers(0, len(ops)))], 'o%d' % j])
+    terms = []
+    if rng.random() < 0.5 and len(shards[0][keys[0]]):
+        terms.append(_term(rng, keys[0], shards[0][keys[0]]))
+    aggregate = bool(rng.random() < 0.7)
+
+    def msg(fn):
+        m = messages.CalcMessage({'payload': 'groupby', 'token': 'ab' * 8, 'filename': fn if isinstance(fn, str) else fn[0]})
+        m.set_args_kwargs([fn, keys, aggs, terms], {'aggregate': aggregate})
+        return m
+
+    def as_cols(df, like):
+        return OrderedDict((c, np.asarray(df[c].values.tolist(), dtype=like[c].dtype) if like[c].dtype.kind in 'SU'
+                            else np.asarray(df[c].values).astype(like[c].dtype)) for c in df.columns)
+
+    calc = CalcPath(str(tmp_path))
+    per = [bo.handle_work(s, keys, aggs, terms, aggregate=aggregate) for s in shards]
+    ref = bo.client_merge(per, keys, aggs, aggregate=aggregate)
+    replies = OrderedDict((fn, calc.handle_work(msg(fn))['data']) for fn in files)
+    df = rpc.uncompress_groupby_to_df(rpc.tar_of_tars(replies), keys, aggs, terms, aggregate=aggregate)
+    if ref is None or len(next(iter(ref.values()))) == 0:
+        assert len(df) == 0
+        return
+    got = as_cols(df, ref)
+    if aggregate:
+        assert_tables_equal(sort_by_keys(got, keys), sort_by_keys(ref, keys))
+    else:
+        # raw rows: the per-file results concatenated in file order
+        assert_tables_equal(got, ref, exact_float_sums=True)
+    if aggregate and n_files > 1:
+        node = calc.handle_work(msg(list(files)))
+        df_n = rpc.uncompress_groupby_to_df(rpc.tar_of_tars({files[0]: node['data']}), keys, aggs, terms,
+                                            aggregate=True)
+        assert_tables_equal(sort_by_keys(as_cols(df_n, ref), keys), sort_by_keys(ref, keys))
