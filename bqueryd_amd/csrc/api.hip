@@ -809,6 +809,21 @@ int agg_out_dtype(int op, int in_dt) {
   return in_dt;
 }
 
+// Float sum states whose column has an exact int64 code for every value (ColStats::enc64) and
+// is not centred: ScanParams::sum_enc / sum_mul for the kernels, and (atomic modes, whose
+// accumulators keep the codes to the emit) EmitParams::sum_dec
+void set_sum_codes(bqg_table* t, Plan& pl, EmitParams* e) {
+  for (int q = 0; q < pl.nsum; ++q) {
+    if (!pl.p.sum_is_float[q] || pl.p.sum_centered[q]) continue;
+    compute_stats(t, pl.tcol[q]);
+    const ColStats& cs = t->cols[pl.tcol[q]].stats;
+    if (!cs.enc64) continue;
+    pl.p.sum_enc[q] = cs.enc64;
+    pl.p.sum_mul[q] = cs.enc64 == 1 ? std::ldexp(1.0, cs.enc64_k) : 100.0;
+    if (e) e->sum_dec[q] = pl.p.sum_mul[q];
+  }
+}
+
 void build_emit(bqg_table* t, const bqg_query* q, const Plan& pl, EmitParams& e, std::vector<int>& out_dt) {
   memset(&e, 0, sizeof(e));
   e.nkeys = q->n_keys;
@@ -1126,19 +1141,10 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   } else {
     // the partitioned aggregate writes every slot itself (no initialisation pass)
     if (pl.mode != kPartitioned) launch_init_slots(sa, nsum, S, st);
-    if (pl.mode != kPartitioned && c->opt[kOptPartNarrow] != 0) {
-      // atomic modes: float sums of exactly codable columns accumulate integer codes (the
-      // same column statistics as the partitioned narrow entries) -- bit-reproducible sums
-      for (int q = 0; q < nsum; ++q) {
-        if (!pl.p.sum_is_float[q] || pl.p.sum_centered[q]) continue;
-        compute_stats(t, pl.tcol[q]);
-        const ColStats& cs = t->cols[pl.tcol[q]].stats;
-        if (!cs.enc64) continue;
-        pl.p.sum_enc[q] = cs.enc64;
-        pl.p.sum_mul[q] = cs.enc64 == 1 ? std::ldexp(1.0, cs.enc64_k) : 100.0;
-        e.sum_dec[q] = pl.p.sum_mul[q];
-      }
-    }
+    // atomic modes: float sums of exactly codable columns accumulate integer codes (the same
+    // column statistics as the partitioned narrow entries) -- bit-reproducible sums; the emit
+    // scales them back
+    if (pl.mode != kPartitioned && c->opt[kOptPartNarrow] != 0) set_sum_codes(t, pl, &e);
     HIPCHECK(hipMemsetAsync(sa.hash_fill, 0, 8, st));
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
     if (pl.mode == kShared) {
@@ -1171,17 +1177,9 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
           L.enc_off[q] = cs.empty ? 0 : cs.imin;
         }
       }
-      if (!L.narrow && c->opt[kOptPartNarrow] != 0) {
-        // wide entries: float sums of int64-codable columns add codes (deterministic)
-        for (int q = 0; q < nsum; ++q) {
-          if (!pl.p.sum_is_float[q] || pl.p.sum_centered[q]) continue;
-          compute_stats(t, pl.tcol[q]);
-          const ColStats& cs = t->cols[pl.tcol[q]].stats;
-          if (!cs.enc64) continue;
-          pl.p.sum_enc[q] = cs.enc64;
-          pl.p.sum_mul[q] = cs.enc64 == 1 ? std::ldexp(1.0, cs.enc64_k) : 100.0;
-        }
-      }
+      // wide entries: float sums of int64-codable columns add codes (deterministic); the
+      // combine scales them back
+      if (!L.narrow && c->opt[kOptPartNarrow] != 0) set_sum_codes(t, pl, nullptr);
       // packed 4-byte entries (option part_pack): no summed column, or one narrow-coded
       // column whose codes span at most 2^16 values -- {code16, slot_low} per entry
       L.pack = 0;
