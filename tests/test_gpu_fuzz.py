@@ -339,3 +339,60 @@ def test_random_worker_messages_match_the_reference_path(seed, tmp_path):
         df_n = rpc.uncompress_groupby_to_df(rpc.tar_of_tars({files[0]: node['data']}), keys, aggs, terms,
                                             aggregate=True)
         assert_tables_equal(sort_by_keys(as_cols(df_n, ref), keys), sort_by_keys(ref, keys))
+
+
+N_LARGE_CASES = 8
+
+
+def _large_key(rng, kind, n):
+    if kind == 'dense_i4':  # 100 K - 1.5 M groups alone: the partitioned path
+        return rng.integers(0, int(rng.integers(100_000, 1_500_000)), n).astype(np.int32)
+    if kind == 'pair_u2':
+        return rng.integers(0, 700, n).astype(np.uint16)
+    if kind == 'pair_i1':
+        return rng.integers(-100, 100, n).astype(np.int8)
+    if kind == 'wide_i8':
+        return rng.integers(-2**50, 2**50, 200_000)[rng.integers(0, 200_000, n)].astype(np.int64)
+    if kind == 'sorted_i4':  # clustered keys: every tile holds some group's first row
+        return np.sort(rng.integers(0, 300_000, n)).astype(np.int32)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize('seed', range(N_LARGE_CASES))
+def test_random_large_queries_match_the_c_oracle(seed, oracle_c, engine_options):
+    """Random queries at 4.5 M rows -- past the hiprtc threshold, so the run-time specialised
+    kernels run -- with 10^5-10^6 groups (the partitioned tile-scatter path, dense or packed
+    entries by the value column's codes; sorted keys; hashed wide keys), random numeric value
+    dtypes and terms, against the C restatement (oracle/cbquery.c)."""
+    rng = np.random.default_rng(7000 + seed)
+    n = 4_500_000
+    layouts = [['dense_i4'], ['pair_u2', 'pair_i1'], ['wide_i8'], ['sorted_i4'], ['pair_i1', 'dense_i4']]
+    kinds = layouts[seed % len(layouts)]
+    cols = OrderedDict(('k%d' % i, _large_key(rng, k, n)) for i, k in enumerate(kinds))
+    val_kinds = [('cents', 'i4'), ('small', 'i8'), ('raw', 'cents'), ('i4', 'f4'), ('cents', 'small'),
+                 ('u4', 'raw'), ('cents', 'i8'), ('i8', 'raw')][seed % 8]
+    for i, k in enumerate(val_kinds):
+        cols['v%d' % i] = _value_column(rng, k, n)
+    keys = list(cols)[:len(kinds)]
+    aggs = []
+    for j in range(int(rng.integers(1, 4))):
+        vi = int(rng.integers(0, 2))
+        kind = val_kinds[vi]
+        ops = ['count'] + (['sum', 'mean'] if kind in SUMMABLE else []) + \
+              (['count_distinct', 'sorted_count_distinct'] if kind in DISTINCTABLE else [])
+        aggs.append(['v%d' % vi, ops[int(rng.integers(0, len(ops)))], 'o%d' % j])
+    terms = []
+    if rng.random() < 0.5:
+        name = ['v0', 'v1'][int(rng.integers(0, 2))]
+        if cols[name].dtype.kind in 'iu':
+            op = ['>', '<=', '!=', 'in'][int(rng.integers(0, 4))]
+            terms.append((name, op, [int(x) for x in cols[name][:3]] if op == 'in' else int(cols[name][0])))
+        else:
+            terms.append((name, ['>', '<='][int(rng.integers(0, 2))], float(np.median(cols[name][:1000]))))
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(keys, aggs, where_terms=terms)
+    finally:
+        t.close()
+    ref = oracle_c.groupby(cols, keys, aggs, oracle_c.where_terms(cols, terms) if terms else None)
+    assert_tables_equal(got, ref)
