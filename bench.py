@@ -526,6 +526,11 @@ def main(argv=None):
             'engine_mode': MODES[mode or 0],
             # partitioned mode: summed values carried as exact 32-bit integer codes
             **({'narrow_entries': bool(timings[-1].get('narrow'))} if timings and mode == 4 else {}),
+            # private mode: the scan reads the columns' compact resident copies
+            **({'resident_columns': 'compact copies: integer columns as offsets from their minimum in the '
+                                    'fewest bytes holding their range, float64 columns that are only summed as '
+                                    'their exact int32 codes (%d B per row read)' % round(bytes_per_launch / max(rows, 1))}
+               if mode == 0 and dev.get_option('compact') else {}),
             **cfg_extra,
         },
         'roofline': {

@@ -145,11 +145,27 @@ struct ColStats {
   int64_t runs = -1;  // value runs (rows differing from the row before + 1), -1 = not measured
 };
 
+// A compact resident copy of a column for the HBM-bound scans: an integer column as its
+// offset from the minimum in the fewest of 1 / 2 / 4 bytes that hold its range, a float64
+// column as its exact int32 codes (ColStats::enc).  Built on first use by a scan that can read
+// it, rebuilt when the column's statistics are (its data changed); every other path reads the
+// column itself.
+struct Shadow {
+  unsigned char* dev = nullptr;
+  size_t bytes = 0;
+  bool valid = false;
+  int dtype = 0;    // stored type
+  int enc = 0;      // 1: integer offset (DevCol::enc), 2: float64 as int32 codes
+  int64_t off = 0;  // enc 1
+  double mul = 0;   // enc 2: code = v * mul (value = code / mul)
+};
+
 struct Column {
   int dtype = 0;
   unsigned char* dev = nullptr;
   size_t bytes = 0;
   ColStats stats;
+  Shadow shadow;
 };
 
 struct bqg_table {
@@ -311,7 +327,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -338,6 +354,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"part_pack", 1, 0, 1},                 // packed 4-byte partition entries when they fit
     {"scd_runs", 1, 0, 1},                  // fused distinct pass: 256-row steps for clustered keys
     {"part_win", 0, 0, 4096},               // partitioned aggregate: tiles per window (0: auto; 64..4096)
+    {"compact", 1, 0, 1},                   // private scan reads compact resident copies of its columns
 };
 
 static int opt_index(const char* name) {
@@ -492,6 +509,7 @@ void compute_stats_many(bqg_table* t, const std::vector<int>& cols) {
   for (size_t i = 0; i < n; ++i) {
     Column& k = t->cols[todo[i]];
     k.stats.runs = -1;  // measured again on demand (column_runs)
+    k.shadow.valid = false;  // the data changed: the compact copy is rebuilt on demand
     DevCol dc{k.dev, k.dtype, dtype_lg(k.dtype)};
     if (t->nrows > 0) launch_stats(dc, t->nrows, d + 8 * i, d + 8 * n, c->stream);
   }
@@ -540,6 +558,7 @@ struct Plan {
   int wbits = 12;
   bool has_filter = false;
   int64_t alg_bytes = 0;
+  bool dummy_col = false;      // the one scan column of a plan that reads none (not in alg_bytes)
 };
 
 int scan_col(Plan& pl, int tc) {
@@ -721,6 +740,7 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     const int tc = q->n_aggs > 0 ? q->aggs[0].col : 0;
     scan_col(pl, tc);
     pl.p.ncols = 1;
+    pl.dummy_col = true;
     const Column& col = t->cols[tc];
     pl.p.cols[0] = DevCol{col.dev, col.dtype, dtype_lg(col.dtype)};
   }
@@ -807,6 +827,54 @@ int agg_out_dtype(int op, int in_dt) {
   if (op == BQG_COUNT || op == BQG_COUNT_DISTINCT || op == BQG_SORTED_COUNT_DISTINCT) return BQG_I64;
   if (op == BQG_MEAN || op == BQG_STD) return BQG_F64;
   return in_dt;
+}
+
+// The compact copy of table column `tc` (Column::shadow), built if needed: kind 1 for an
+// integer column whose range fits fewer bytes, kind 2 for a float64 column with exact int32
+// codes; returns false when the column has none of the wanted kind.
+bool ensure_shadow(bqg_ctx* c, bqg_table* t, int tc, int kind) {
+  Column& col = t->cols[tc];
+  compute_stats(t, tc);
+  const ColStats& cs = col.stats;
+  Shadow& sh = col.shadow;
+  int dtype = 0, enc = 0;
+  int64_t off = 0;
+  double mul = 0;
+  if (kind == 1) {
+    if (dtype_is_float(col.dtype) || col.dtype == BQG_BOOL || col.dtype == BQG_U64 || cs.empty) return false;
+    const uint64_t range = (uint64_t)cs.imax - (uint64_t)cs.imin;
+    const int lg = range < 0x100ull ? 0 : range < 0x10000ull ? 1 : range < 0x100000000ull ? 2 : 3;
+    if (lg >= dtype_lg(col.dtype)) return false;  // no narrower
+    dtype = lg == 0 ? BQG_U8 : lg == 1 ? BQG_U16 : BQG_U32;
+    enc = 1;
+    off = cs.imin;
+  } else {
+    if (col.dtype != BQG_F64 || !cs.enc) return false;
+    dtype = BQG_I32;
+    enc = 2;
+    mul = cs.enc == 1 ? std::ldexp(1.0, cs.enc_k) : 100.0;
+  }
+  if (sh.valid && sh.dtype == dtype && sh.enc == enc && sh.off == off && sh.mul == mul) return true;
+  const size_t need = column_bytes(t->nrows, dtype);
+  if (sh.bytes < need) {
+    c->colpool.put(sh.dev, sh.bytes);
+    size_t cap = 0;
+    sh.dev = (unsigned char*)c->colpool.get(need, &cap);
+    sh.bytes = sh.dev ? cap : 0;
+    if (!sh.dev) return false;  // no room: the scan reads the column itself
+  }
+  // zero padding past the last row (the scans' vector loads read it), then the rows
+  const size_t used = (size_t)t->nrows * dtype_size(dtype);
+  HIPCHECK(hipMemsetAsync(sh.dev + used, 0, sh.bytes - used, c->stream));
+  if (enc == 1) launch_shadow_int(DevCol{col.dev, col.dtype, dtype_lg(col.dtype)}, t->nrows, off, sh.dev, dtype_lg(dtype), c->stream);
+  else launch_shadow_code((const double*)col.dev, t->nrows, cs.enc, mul, (int32_t*)sh.dev, c->stream);
+  HIPCHECK(hipGetLastError());
+  sh.valid = true;
+  sh.dtype = dtype;
+  sh.enc = enc;
+  sh.off = off;
+  sh.mul = mul;
+  return true;
 }
 
 // Float sum states whose column has an exact int64 code for every value (ColStats::enc64) and
@@ -1054,11 +1122,37 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     L.blocks = scan_blocks(c, N, per_cu);
     L.lds_bytes = lds;
     L.partials = (unsigned long long*)c->partials.ensure((size_t)(2 + nsum) * L.blocks * S * 8);
+    // the scan's columns as their compact resident copies where they have one (option
+    // compact): integer keys / terms / sums as narrow offsets (the decode restores the
+    // canonical value), float64 columns that are only summed as their exact int32 codes,
+    // summed as integers and scaled back once at emit -- fewer HBM bytes for the same rows
+    ScanParams sp = pl.p;
+    if (c->opt[kOptCompact]) {
+      for (int i = 0; i < sp.ncols; ++i) {
+        const int tc = pl.tcol[i];
+        Column& col = t->cols[tc];
+        bool other = i == sp.mask_col;  // used as anything but a plain sum state
+        for (int k = 0; k < sp.nkeys; ++k) other |= sp.keys[k].col == i;
+        for (int k = 0; k < sp.nterms; ++k) other |= sp.terms[k].col == i;
+        const bool sum_only = i < nsum && !other &&
+                              std::find(pl.std_cols.begin(), pl.std_cols.end(), i) == pl.std_cols.end();
+        if (ensure_shadow(c, t, tc, 1)) {
+          sp.cols[i] = DevCol{col.shadow.dev, col.shadow.dtype, dtype_lg(col.shadow.dtype), 1, 0, col.shadow.off};
+        } else if (sum_only && ensure_shadow(c, t, tc, 2)) {
+          sp.cols[i] = DevCol{col.shadow.dev, BQG_I32, 2};
+          sp.sum_is_float[i] = 0;
+          sp.sum_conv[i] = 1;
+          e.sum_dec[i] = col.shadow.mul;
+        }
+        // algorithmic bytes: what the scan reads of this column
+        if (!pl.dummy_col) pl.alg_bytes -= ((int64_t)dtype_size(col.dtype) - ((int64_t)1 << sp.cols[i].lg)) * N;
+      }
+    }
     FinishParams F{};
     F.nslots = (int)S;
     F.blocks = L.blocks;
     F.nsum = nsum;
-    for (int i = 0; i < kMaxSums; ++i) F.sum_is_float[i] = pl.p.sum_is_float[i];
+    for (int i = 0; i < kMaxSums; ++i) F.sum_is_float[i] = sp.sum_is_float[i];
     F.partials = L.partials;
     F.out_hdr = (unsigned long long*)c->hdr.ensure(64);
     F.totals = (unsigned long long*)c->counter.ensure((size_t)(2 + kMaxSums) * kMaxPrivateSlots * 8);
@@ -1081,19 +1175,19 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     }
     hipFunction_t jfn = nullptr;
     if (c->opt[kOptJit] && N >= c->jit_min_rows()) {
-      std::string spec = jit_spec(pl.p);
+      std::string spec = jit_spec(sp);
       // tiles in flight per workgroup (profiling option; default in scan_private.h)
       if (c->opt[kOptPrivAhead]) spec += std::string("#define BQ_PRIV_AHEAD ") + std::to_string(c->opt[kOptPrivAhead]) + "\n";
       jfn = jit_function("bq_jit_scan_private", spec);
     }
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
     if (jfn) {
-      void* args[] = {(void*)&pl.p, (void*)&L};
+      void* args[] = {(void*)&sp, (void*)&L};
       HIPCHECK(hipModuleLaunchKernel(jfn, (unsigned)L.blocks, 1, 1, kBlock, 1, 1, (unsigned)L.lds_bytes, st, args,
                                      nullptr));
       c->last.specialized = 1;
     } else {
-      launch_scan_private(pl.p, L, st);
+      launch_scan_private(sp, L, st);
     }
     HIPCHECK(hipGetLastError());
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));
@@ -1960,7 +2054,10 @@ int bqg_table_destroy(bqg_table* t) {
   if (!t) return BQG_OK;
   int rc = guard(t->ctx, [&] {
     HIPCHECK(hipStreamSynchronize(t->ctx->stream));
-    for (Column& col : t->cols) t->ctx->colpool.put(col.dev, col.bytes);
+    for (Column& col : t->cols) {
+      t->ctx->colpool.put(col.dev, col.bytes);
+      t->ctx->colpool.put(col.shadow.dev, col.shadow.bytes);
+    }
   });
   delete t;
   return rc;

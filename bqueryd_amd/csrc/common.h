@@ -43,8 +43,15 @@ __host__ __device__ inline bool dtype_is_unsigned(int dt) {
 // ------------------------------------------------------------------------------------
 struct DevCol {
   const unsigned char* ptr;
-  int32_t dtype;
+  int32_t dtype;  // the STORED element type (a compact copy's narrow type, see enc)
   int32_t lg;
+  // compact resident copy (api.hip Column::shadow): enc 1 -- an integer column stored as an
+  // unsigned offset from `off` in fewer bytes; the decode adds `off` back, so every consumer
+  // sees the column's canonical int64 value.  (A float64 column stored as its exact int32
+  // codes carries enc 0: its canonical value IS the code, and only code-aware sum states read it.)
+  int32_t enc;
+  int32_t pad_;
+  int64_t off;
 };
 
 struct DevTerm {

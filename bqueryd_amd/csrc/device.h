@@ -167,7 +167,13 @@ __device__ __forceinline__ double value_f64(uint64_t v, int conv) {
 template <int NC, int R>
 __device__ __forceinline__ void decode_all(const ScanParams& p, const Chunk (&raw)[NC], uint64_t (&v)[NC][R]) {
 #pragma unroll
-  for (int c = 0; c < NC; ++c) decode<R>(raw[c], p.cols[c].dtype, v[c]);
+  for (int c = 0; c < NC; ++c) {
+    decode<R>(raw[c], p.cols[c].dtype, v[c]);
+    if (p.cols[c].enc == 1) {  // compact copy: offset back to the canonical value
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[c][r] += (uint64_t)p.cols[c].off;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------

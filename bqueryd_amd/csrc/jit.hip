@@ -150,7 +150,8 @@ std::string jit_spec(const ScanParams& p) {
   s << "#define BQ_NC " << p.ncols << "\n#define BQ_SPEC ";
   s << "p.ncols=" << p.ncols << ";";
   for (int c = 0; c < p.ncols; ++c)
-    s << "p.cols[" << c << "].dtype=" << p.cols[c].dtype << ";p.cols[" << c << "].lg=" << p.cols[c].lg << ";";
+    s << "p.cols[" << c << "].dtype=" << p.cols[c].dtype << ";p.cols[" << c << "].lg=" << p.cols[c].lg
+      << ";p.cols[" << c << "].enc=" << p.cols[c].enc << ";";
   s << "p.nterms=" << p.nterms << ";";
   for (int t = 0; t < p.nterms; ++t) {
     const DevTerm& tm = p.terms[t];

@@ -790,6 +790,47 @@ __global__ __launch_bounds__(kBlock) void k_mpack_scatter(MergePack m) {
   }
 }
 
+// Compact resident copies (Column::shadow).  Integer source: its canonical value minus `off`,
+// stored in 1 / 2 / 4 bytes; float64 source: the exact int32 code of every value (the column
+// statistics guarantee one exists and the decode divides it back exactly).
+__global__ __launch_bounds__(kBlock) void k_shadow_int(DevCol src, int64_t n, int64_t off, void* dst, int dst_lg) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    int64_t v;
+    switch (src.dtype) {
+      case BQG_I8: v = reinterpret_cast<const int8_t*>(src.ptr)[i]; break;
+      case BQG_I16: v = reinterpret_cast<const int16_t*>(src.ptr)[i]; break;
+      case BQG_I32: v = reinterpret_cast<const int32_t*>(src.ptr)[i]; break;
+      case BQG_U8: v = reinterpret_cast<const uint8_t*>(src.ptr)[i]; break;
+      case BQG_U16: v = reinterpret_cast<const uint16_t*>(src.ptr)[i]; break;
+      case BQG_U32: v = reinterpret_cast<const uint32_t*>(src.ptr)[i]; break;
+      default: v = reinterpret_cast<const int64_t*>(src.ptr)[i]; break;
+    }
+    const uint64_t u = (uint64_t)(v - off);
+    if (dst_lg == 0) reinterpret_cast<uint8_t*>(dst)[i] = (uint8_t)u;
+    else if (dst_lg == 1) reinterpret_cast<uint16_t*>(dst)[i] = (uint16_t)u;
+    else reinterpret_cast<uint32_t*>(dst)[i] = (uint32_t)u;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_shadow_code(const double* src, int64_t n, int kind, double mul, int32_t* dst) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const double d = src[i] * mul;
+    dst[i] = (int32_t)(kind == 1 ? d : rint(d));
+  }
+}
+
+void launch_shadow_int(const DevCol& src, int64_t nrows, int64_t off, void* dst, int dst_lg, hipStream_t st) {
+  if (nrows <= 0) return;
+  const unsigned g = (unsigned)std::min<int64_t>((nrows + kBlock - 1) / kBlock, 8192);
+  hipLaunchKernelGGL(k_shadow_int, dim3(g), dim3(kBlock), 0, st, src, nrows, off, dst, dst_lg);
+}
+
+void launch_shadow_code(const double* src, int64_t nrows, int kind, double mul, int32_t* dst, hipStream_t st) {
+  if (nrows <= 0) return;
+  const unsigned g = (unsigned)std::min<int64_t>((nrows + kBlock - 1) / kBlock, 8192);
+  hipLaunchKernelGGL(k_shadow_code, dim3(g), dim3(kBlock), 0, st, src, nrows, kind, mul, dst);
+}
+
 // std pass 2 centers: the mean of every slot of every std column, from pass 1's count and sum
 // (conv: 0 float bits, 1 signed, 2 unsigned integer sum), written where pass 2 reads them --
 // no host round trip between the passes

@@ -335,6 +335,11 @@ struct StdCenters {
   int32_t conv[kMaxSums];   // 0 float bits, 1 signed integer, 2 unsigned integer, 3 int64 codes / dec
   double dec[kMaxSums];
 };
+// compact resident copies (api.hip Column::shadow): an integer column as (v - off) in 1, 2 or 4
+// bytes (dst_lg), a float64 column as its exact int32 codes (kind 1 dyadic v * mul, 2 cents
+// rint(v * mul))
+void launch_shadow_int(const DevCol& src, int64_t nrows, int64_t off, void* dst, int dst_lg, hipStream_t st);
+void launch_shadow_code(const double* src, int64_t nrows, int kind, double mul, int32_t* dst, hipStream_t st);
 void launch_std_centers(const unsigned long long* cnt, const unsigned long long* acc, const StdCenters& sc,
                         uint64_t nslots, double* centers, hipStream_t st);
 
