@@ -27,45 +27,62 @@ __global__ __launch_bounds__(kPrivReduceThreads) void k_private_reduce(FinishPar
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = kPrivReduceThreads / 64;
   const int S = f.nslots, nb = f.blocks;
   const int P = (2 + f.nsum) * S;
-  for (int pair = wave; pair < P; pair += nwaves) {
-    const int comp = pair / S;
-    const bool isf = comp >= 2 && f.sum_is_float[comp - 2];
-    const unsigned long long* src = f.partials + (size_t)pair * nb;
-    // the lane's partials, 16 loads issued together per round (nb <= 1024 at 4 workgroups per
-    // CU: one round), then combined in order
-    unsigned long long acc = comp == 1 ? (unsigned long long)kNoRow : 0ull;
+  // every wave takes its pairs two at a time (pair, pair + 16): the loads of both issued together
+  // -- one memory round trip per two pairs (C2: 30 pairs, one round)
+  for (int pair0 = wave; pair0 < P; pair0 += 2 * nwaves) {
+    unsigned long long acc[2];
+    int comps[2];
+    bool isfs[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pair = pair0 + h * nwaves;
+      comps[h] = pair < P ? pair / S : 0;
+      isfs[h] = pair < P && comps[h] >= 2 && f.sum_is_float[comps[h] - 2];
+      acc[h] = comps[h] == 1 ? (unsigned long long)kNoRow : 0ull;
+    }
     for (int b0 = 0; b0 < nb; b0 += 64 * 16) {
-      unsigned long long x[16];
+      unsigned long long x[2][16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int b = b0 + i * 64 + lane;
-        x[i] = b < nb ? src[b] : (comp == 1 ? (unsigned long long)kNoRow : 0ull);
+      for (int h = 0; h < 2; ++h) {
+        const int pair = pair0 + h * nwaves;
+        const unsigned long long* src = f.partials + (size_t)(pair < P ? pair : 0) * nb;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int b = b0 + i * 64 + lane;
+          x[h][i] = (pair < P && b < nb) ? src[b] : (comps[h] == 1 ? (unsigned long long)kNoRow : 0ull);
+        }
       }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (comp == 1) acc = min(acc, x[i]);
-        else if (isf) acc = as_u64(as_f64(acc) + as_f64(x[i]));
-        else acc += x[i];
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (comps[h] == 1) acc[h] = min(acc[h], x[h][i]);
+          else if (isfs[h]) acc[h] = as_u64(as_f64(acc[h]) + as_f64(x[h][i]));
+          else acc[h] += x[h][i];
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pair = pair0 + h * nwaves;
+      unsigned long long v;
+      if (comps[h] == 1) {
+        uint32_t m = (uint32_t)acc[h];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
+        v = m;
+      } else if (isfs[h]) {
+        double xx = as_f64(acc[h]);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) xx += __shfl_xor(xx, o, 64);
+        v = as_u64(xx);
+      } else {
+        unsigned long long xx = acc[h];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) xx += (unsigned long long)__shfl_xor((long long)xx, o, 64);
+        v = xx;
       }
+      if (lane == 0 && pair < P) tot[pair] = v;
     }
-    unsigned long long v;
-    if (comp == 1) {
-      uint32_t m = (uint32_t)acc;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
-      v = m;
-    } else if (isf) {
-      double x = as_f64(acc);
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-      v = as_u64(x);
-    } else {
-      unsigned long long x = acc;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) x += (unsigned long long)__shfl_xor((long long)x, o, 64);
-      v = x;
-    }
-    if (lane == 0) tot[pair] = v;
   }
   __syncthreads();
   if (tid < 64) {
