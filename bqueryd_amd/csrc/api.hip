@@ -354,7 +354,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"part_pack", 1, 0, 1},                 // packed 4-byte partition entries when they fit
     {"scd_runs", 1, 0, 1},                  // fused distinct pass: 256-row steps for clustered keys
     {"part_win", 0, 0, 4096},               // partitioned aggregate: tiles per window (0: auto; 64..4096)
-    {"compact", 1, 0, 1},                   // private scan reads compact resident copies of its columns
+    {"compact", 1, 0, 1},                   // private / shared / dense global scans read compact column copies
 };
 
 static int opt_index(const char* name) {
@@ -877,6 +877,38 @@ bool ensure_shadow(bqg_ctx* c, bqg_table* t, int tc, int kind) {
   return true;
 }
 
+// The scan parameters with the columns' compact resident copies where they have one (option
+// compact; private, shared and dense global scans): integer keys / terms / sums as narrow
+// offsets (the decode restores the canonical value), float64 columns that are only summed as
+// their exact int32 codes, summed as integers and scaled back once at emit (EmitParams::
+// sum_dec) -- fewer HBM bytes for the same rows.  pl.alg_bytes follows the bytes read.
+ScanParams compact_scan(bqg_ctx* c, bqg_table* t, Plan& pl, EmitParams& e) {
+  ScanParams sp = pl.p;
+  if (!c->opt[kOptCompact] || pl.p.hash) return sp;
+  const int64_t N = t->nrows;
+  for (int i = 0; i < sp.ncols; ++i) {
+    const int tc = pl.tcol[i];
+    Column& col = t->cols[tc];
+    bool other = i == sp.mask_col;  // used as anything but a plain sum state
+    for (int k = 0; k < sp.nkeys; ++k) other |= sp.keys[k].col == i;
+    for (int k = 0; k < sp.nterms; ++k) other |= sp.terms[k].col == i;
+    const bool sum_only = i < pl.nsum && !other &&
+                          std::find(pl.std_cols.begin(), pl.std_cols.end(), i) == pl.std_cols.end();
+    if (ensure_shadow(c, t, tc, 1)) {
+      sp.cols[i] = DevCol{col.shadow.dev, col.shadow.dtype, dtype_lg(col.shadow.dtype), 1, 0, col.shadow.off};
+    } else if (sum_only && ensure_shadow(c, t, tc, 2)) {
+      sp.cols[i] = DevCol{col.shadow.dev, BQG_I32, 2};
+      sp.sum_is_float[i] = 0;
+      sp.sum_conv[i] = 1;
+      sp.sum_enc[i] = 0;
+      e.sum_dec[i] = col.shadow.mul;
+    }
+    // algorithmic bytes: what the scan reads of this column
+    if (!pl.dummy_col) pl.alg_bytes -= ((int64_t)dtype_size(col.dtype) - ((int64_t)1 << sp.cols[i].lg)) * N;
+  }
+  return sp;
+}
+
 // Float sum states whose column has an exact int64 code for every value (ColStats::enc64) and
 // is not centred: ScanParams::sum_enc / sum_mul for the kernels, and (atomic modes, whose
 // accumulators keep the codes to the emit) EmitParams::sum_dec
@@ -1126,28 +1158,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     // compact): integer keys / terms / sums as narrow offsets (the decode restores the
     // canonical value), float64 columns that are only summed as their exact int32 codes,
     // summed as integers and scaled back once at emit -- fewer HBM bytes for the same rows
-    ScanParams sp = pl.p;
-    if (c->opt[kOptCompact]) {
-      for (int i = 0; i < sp.ncols; ++i) {
-        const int tc = pl.tcol[i];
-        Column& col = t->cols[tc];
-        bool other = i == sp.mask_col;  // used as anything but a plain sum state
-        for (int k = 0; k < sp.nkeys; ++k) other |= sp.keys[k].col == i;
-        for (int k = 0; k < sp.nterms; ++k) other |= sp.terms[k].col == i;
-        const bool sum_only = i < nsum && !other &&
-                              std::find(pl.std_cols.begin(), pl.std_cols.end(), i) == pl.std_cols.end();
-        if (ensure_shadow(c, t, tc, 1)) {
-          sp.cols[i] = DevCol{col.shadow.dev, col.shadow.dtype, dtype_lg(col.shadow.dtype), 1, 0, col.shadow.off};
-        } else if (sum_only && ensure_shadow(c, t, tc, 2)) {
-          sp.cols[i] = DevCol{col.shadow.dev, BQG_I32, 2};
-          sp.sum_is_float[i] = 0;
-          sp.sum_conv[i] = 1;
-          e.sum_dec[i] = col.shadow.mul;
-        }
-        // algorithmic bytes: what the scan reads of this column
-        if (!pl.dummy_col) pl.alg_bytes -= ((int64_t)dtype_size(col.dtype) - ((int64_t)1 << sp.cols[i].lg)) * N;
-      }
-    }
+    ScanParams sp = compact_scan(c, t, pl, e);
     FinishParams F{};
     F.nslots = (int)S;
     F.blocks = L.blocks;
@@ -1240,11 +1251,14 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     // scales them back
     if (pl.mode != kPartitioned && c->opt[kOptPartNarrow] != 0) set_sum_codes(t, pl, &e);
     HIPCHECK(hipMemsetAsync(sa.hash_fill, 0, 8, st));
+    // shared / dense global scans read the columns' compact copies (after set_sum_codes: a
+    // code-copy column's state sums the codes as integers)
+    ScanParams sp = pl.mode == kPartitioned ? pl.p : compact_scan(c, t, pl, e);
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
     if (pl.mode == kShared) {
       const size_t lds = (size_t)S * (8 + 8 * (size_t)nsum);
       int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
-      launch_scan_shared(pl.p, sa, scan_blocks(c, N, std::max(per_cu, 1)), lds, st);
+      launch_scan_shared(sp, sa, scan_blocks(c, N, std::max(per_cu, 1)), lds, st);
     } else if (pl.mode == kPartitioned) {
       PartLaunch L{};
       L.wbits = pl.wbits;
@@ -1386,7 +1400,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       }
       launch_partitioned(pl.p, sa, L, st, fs, ff);
     } else {
-      launch_scan_global(pl.p, sa, scan_blocks(c, N, 8), st);
+      launch_scan_global(sp, sa, scan_blocks(c, N, 8), st);
     }
     HIPCHECK(hipGetLastError());
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));

@@ -173,9 +173,10 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *   part_pack      1  packed 4-byte partition entries when they fit    0 | 1
  *   scd_runs       1  fused distinct pass in 256-row steps for clustered keys  0 | 1
  *   part_win       0  partitioned aggregate: tiles of bounds per LDS window   0 (auto) | 64..4096
- *   compact        1  private scan reads compact resident copies of its     0 | 1
- *                     columns (narrow integer offsets, exact int32 codes of
- *                     float64 columns that are only summed)
+ *   compact        1  private / shared / dense global scans read compact  0 | 1
+ *                     resident copies of their columns (narrow integer
+ *                     offsets, exact int32 codes of float64 columns that
+ *                     are only summed)
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);

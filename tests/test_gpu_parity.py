@@ -860,3 +860,53 @@ def test_moments_of_wrapping_int64_and_coded_columns(mode, oracle_c, engine_opti
     assert info['mode'] == {'private': 0, 'shared': 1, 'global_dense': 2, 'hash': 3, 'partitioned': 4}[mode], info
     ref = bo.groupby(cols, ['k'], aggs)
     assert_tables_equal(got, ref, exact_cols={'bs'})
+
+
+@pytest.mark.parametrize('mode', ['private', 'shared', 'global_dense'])
+def test_compact_resident_copies(mode, oracle_c, engine_options):
+    """Compact resident copies (option compact): narrow integer offsets for keys / terms /
+    integer sums (negative minima, every width), exact int32 codes for a float64 column that is
+    only summed (cents and dyadic) -- the same answers as the full-width scan and the oracle,
+    fewer algorithmic bytes; a pushed column rebuilds its copy (the next query sees the new
+    values); a float column in a term keeps its full width."""
+    rng = np.random.default_rng(31)
+    n = 300_000
+    if mode == 'private':
+        k = rng.integers(-5, 3, n).astype(np.int64)              # 8 values of an int64 key
+    elif mode == 'shared':
+        k = rng.integers(-400, 500, n).astype(np.int32)
+    else:
+        engine_options(partition=0)
+        k = rng.integers(-70_000, 60_000, n).astype(np.int32)
+    cols = OrderedDict(k=k, t=rng.integers(-30_000, 30_000, n).astype(np.int32),
+                       i=rng.integers(-2**40, -2**40 + 200, n).astype(np.int64),
+                       c=rng.integers(-50_000, 90_000, n) / 100.0,
+                       d=np.ldexp(rng.integers(-2**20, 2**20, n).astype(np.float64), -5))
+    aggs = [['c', 'sum', 'cs'], ['c', 'mean', 'cm'], ['d', 'sum', 'ds'], ['i', 'sum', 'is'], ['i', 'count', 'n']]
+    terms = [('t', '>=', -12_345)]
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(['k'], aggs, where_terms=terms)
+        info = t.dev.last_timing()
+        with t.dev.options(compact=0):
+            full, _ = t.groupby(['k'], aggs, where_terms=terms)
+            finfo = t.dev.last_timing()
+        assert info['mode'] == finfo['mode'] == {'private': 0, 'shared': 1, 'global_dense': 2}[mode], (info, finfo)
+        # k: 1 B / 2 B / 4 B offsets (from 8 / 4 / 4), t 2 B (from 4), i 1 B (from 8), c / d 4 B (from 8)
+        assert info['bytes'] < finfo['bytes'], (info['bytes'], finfo['bytes'])
+        ref = oracle_c.groupby(cols, ['k'], aggs, oracle_c.where_terms(cols, terms))
+        assert_tables_equal(got, ref, exact_cols={'ds', 'is'})
+        assert_tables_equal(full, ref, exact_cols={'ds', 'is'})
+        # new values in a column: its copy is rebuilt
+        cols['t'] = rng.integers(-100, 100_000, n).astype(np.int32)
+        t.push('t', cols['t'])
+        t.sync()
+        got2, _ = t.groupby(['k'], aggs, where_terms=terms)
+        ref2 = oracle_c.groupby(cols, ['k'], aggs, oracle_c.where_terms(cols, terms))
+        assert_tables_equal(got2, ref2, exact_cols={'ds', 'is'})
+        # a float column in a term is read at full width (its value, not its code, compares)
+        got3, _ = t.groupby(['k'], [['c', 'sum', 'cs']], where_terms=[('c', '>', 12.34)])
+        ref3 = oracle_c.groupby(cols, ['k'], [['c', 'sum', 'cs']], oracle_c.where_terms(cols, [('c', '>', 12.34)]))
+        assert_tables_equal(got3, ref3)
+    finally:
+        t.close()
