@@ -147,7 +147,8 @@ struct ColStats {
 
 // A compact resident copy of a column for the HBM-bound scans: an integer column as its
 // offset from the minimum in the fewest of 1 / 2 / 4 bytes that hold its range, a float64
-// column as its exact int32 codes (ColStats::enc).  Built on first use by a scan that can read
+// column as its exact integer codes (ColStats::enc) -- as offsets from the smallest code in 1
+// or 2 bytes when the codes span fewer than 2^16, else as int32 codes.  Built on first use by a scan that can read
 // it, rebuilt when the column's statistics are (its data changed); every other path reads the
 // column itself.
 struct Shadow {
@@ -155,8 +156,8 @@ struct Shadow {
   size_t bytes = 0;
   bool valid = false;
   int dtype = 0;    // stored type
-  int enc = 0;      // 1: integer offset (DevCol::enc), 2: float64 as int32 codes
-  int64_t off = 0;  // enc 1
+  int enc = 0;      // 1: integer offset (DevCol::enc), 2: float64 as integer codes
+  int64_t off = 0;  // stored = value - off (enc 1), code - off (enc 2 with a 1 / 2-byte type)
   double mul = 0;   // enc 2: code = v * mul (value = code / mul)
 };
 
@@ -354,7 +355,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"part_pack", 1, 0, 1},                 // packed 4-byte partition entries when they fit
     {"scd_runs", 1, 0, 1},                  // fused distinct pass: 256-row steps for clustered keys
     {"part_win", 0, 0, 4096},               // partitioned aggregate: tiles per window (0: auto; 64..4096)
-    {"compact", 1, 0, 1},                   // private / shared / dense global scans read compact column copies
+    {"compact", 1, 0, 2},                   // private / shared / dense global scans read compact column copies
 };
 
 static int opt_index(const char* name) {
@@ -401,7 +402,7 @@ struct bqg_ctx {
   // (device-to-device copies of the output columns) instead of a host result
   bqg_table** dev_target = nullptr;
   // timing
-  bool timing = false;
+  int timing = 0;  // 1: query window and scan window events, 2: the scan window only
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bqg_timing last{};
 };
@@ -849,10 +850,16 @@ bool ensure_shadow(bqg_ctx* c, bqg_table* t, int tc, int kind) {
     enc = 1;
     off = cs.imin;
   } else {
-    if (col.dtype != BQG_F64 || !cs.enc) return false;
-    dtype = BQG_I32;
+    if (col.dtype != BQG_F64 || !cs.enc || cs.empty) return false;
     enc = 2;
     mul = cs.enc == 1 ? std::ldexp(1.0, cs.enc_k) : 100.0;
+    // the codes' range (exact products for dyadic codes, rint is monotonic for cents)
+    const int64_t cmin = (int64_t)(cs.enc == 1 ? cs.fmin * mul : std::rint(cs.fmin * mul));
+    const int64_t cmax = (int64_t)(cs.enc == 1 ? cs.fmax * mul : std::rint(cs.fmax * mul));
+    const uint64_t span = (uint64_t)cmax - (uint64_t)cmin;
+    dtype = span < 0x100ull ? BQG_U8 : span < 0x10000ull ? BQG_U16 : BQG_I32;
+    if (c->opt[kOptCompact] == 2) dtype = BQG_I32;  // option compact=2: int32 codes only
+    off = dtype == BQG_I32 ? 0 : cmin;
   }
   if (sh.valid && sh.dtype == dtype && sh.enc == enc && sh.off == off && sh.mul == mul) return true;
   const size_t need = column_bytes(t->nrows, dtype);
@@ -867,7 +874,7 @@ bool ensure_shadow(bqg_ctx* c, bqg_table* t, int tc, int kind) {
   const size_t used = (size_t)t->nrows * dtype_size(dtype);
   HIPCHECK(hipMemsetAsync(sh.dev + used, 0, sh.bytes - used, c->stream));
   if (enc == 1) launch_shadow_int(DevCol{col.dev, col.dtype, dtype_lg(col.dtype)}, t->nrows, off, sh.dev, dtype_lg(dtype), c->stream);
-  else launch_shadow_code((const double*)col.dev, t->nrows, cs.enc, mul, (int32_t*)sh.dev, c->stream);
+  else launch_shadow_code((const double*)col.dev, t->nrows, cs.enc, mul, off, sh.dev, dtype_lg(dtype), c->stream);
   HIPCHECK(hipGetLastError());
   sh.valid = true;
   sh.dtype = dtype;
@@ -897,7 +904,9 @@ ScanParams compact_scan(bqg_ctx* c, bqg_table* t, Plan& pl, EmitParams& e) {
     if (ensure_shadow(c, t, tc, 1)) {
       sp.cols[i] = DevCol{col.shadow.dev, col.shadow.dtype, dtype_lg(col.shadow.dtype), 1, 0, col.shadow.off};
     } else if (sum_only && ensure_shadow(c, t, tc, 2)) {
-      sp.cols[i] = DevCol{col.shadow.dev, BQG_I32, 2};
+      // int32 codes as they are; 1 / 2-byte codes as offsets (the decode adds the smallest back)
+      const Shadow& sh = col.shadow;
+      sp.cols[i] = DevCol{sh.dev, sh.dtype, dtype_lg(sh.dtype), sh.dtype == BQG_I32 ? 0 : 1, 0, sh.off};
       sp.sum_is_float[i] = 0;
       sp.sum_conv[i] = 1;
       sp.sum_enc[i] = 0;
@@ -905,6 +914,26 @@ ScanParams compact_scan(bqg_ctx* c, bqg_table* t, Plan& pl, EmitParams& e) {
     }
     // algorithmic bytes: what the scan reads of this column
     if (!pl.dummy_col) pl.alg_bytes -= ((int64_t)dtype_size(col.dtype) - ((int64_t)1 << sp.cols[i].lg)) * N;
+    // a key / term column that is not summed works in its copy's own domain (stored = value
+    // - off): key minima and scalar term constants shift by -off instead of every row adding
+    // off back (an `in` / `nin` list keeps the decode offset; its values stay canonical)
+    if (sp.cols[i].enc != 1 || i < pl.nsum) continue;
+    bool list = false;
+    for (int k = 0; k < sp.nterms; ++k)
+      list |= sp.terms[k].col == i && (sp.terms[k].op == BQG_T_IN || sp.terms[k].op == BQG_T_NIN);
+    if (list) continue;
+    const int64_t off = sp.cols[i].off;
+    for (int k = 0; k < sp.nkeys; ++k)
+      if (sp.keys[k].col == i) sp.keys[k].min = (int64_t)((uint64_t)sp.keys[k].min - (uint64_t)off);
+    for (int k = 0; k < sp.nterms; ++k) {
+      DevTerm& tm = sp.terms[k];
+      if (tm.col != i || tm.op < BQG_T_EQ || tm.op > BQG_T_LE) continue;
+      // stored values lie in [0, 2^32): a constant clamped into int64 compares the same
+      const __int128 v = (__int128)tm.iv0 - off;
+      tm.iv0 = v < (__int128)INT64_MIN ? INT64_MIN : v > (__int128)INT64_MAX ? INT64_MAX : (int64_t)v;
+    }
+    sp.cols[i].enc = 0;
+    sp.cols[i].off = 0;
   }
   return sp;
 }
@@ -1120,7 +1149,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
 
   // output columns (device), capacity S rows (private) or G rows (generic, sized later)
   hipStream_t st = c->stream;
-  if (c->timing) HIPCHECK(hipEventRecord(c->ev[0], st));
+  if (c->timing == 1) HIPCHECK(hipEventRecord(c->ev[0], st));
 
   // count / distinct-only queries on a small dense slot space: one fused pass
   // (k_scd_fused) produces rows, first rows, sorted_count_distinct and one count_distinct
@@ -1186,10 +1215,10 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     }
     hipFunction_t jfn = nullptr;
     if (c->opt[kOptJit] && N >= c->jit_min_rows()) {
-      std::string spec = jit_spec(sp);
       // tiles in flight per workgroup (profiling option; default in scan_private.h)
-      if (c->opt[kOptPrivAhead]) spec += std::string("#define BQ_PRIV_AHEAD ") + std::to_string(c->opt[kOptPrivAhead]) + "\n";
-      jfn = jit_function("bq_jit_scan_private", spec);
+      std::string extra;
+      if (c->opt[kOptPrivAhead]) extra = std::string("#define BQ_PRIV_AHEAD ") + std::to_string(c->opt[kOptPrivAhead]) + "\n";
+      jfn = jit_function_for("bq_jit_scan_private", sp, extra);
     }
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
     if (jfn) {
@@ -1207,7 +1236,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     if (!need_generic && c->dev_target) {
       unsigned long long* hh = (unsigned long long*)c->hhdr.ensure(64);
       HIPCHECK(hipMemcpyAsync(hh, F.out_hdr, 16, hipMemcpyDeviceToHost, st));
-      if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
+      if (c->timing == 1) HIPCHECK(hipEventRecord(c->ev[3], st));
       HIPCHECK(hipStreamSynchronize(st));
       std::vector<const void*> src;
       for (int j = 0; j < e.ncols; ++j) src.push_back(e.cols[j].out);
@@ -1217,15 +1246,18 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
         c->last.scan_ms = ms;
         c->last.scan_launches = 1;
-        HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
-        c->last.total_ms = ms;
+        c->last.total_ms = NAN;
+        if (c->timing == 1) {
+          HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+          c->last.total_ms = ms;
+        }
       }
       c->last.bytes = pl.alg_bytes + (int64_t)hh[0] * (int64_t)e.ncols * 8;
       return;
     }
     if (!need_generic) {
       unsigned char* h = (unsigned char*)hblk.b.p;
-      if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
+      if (c->timing == 1) HIPCHECK(hipEventRecord(c->ev[3], st));
       HIPCHECK(hipStreamSynchronize(st));
       const unsigned long long G = ((unsigned long long*)h)[0], total = ((unsigned long long*)h)[1];
       std::vector<size_t> offs;
@@ -1236,8 +1268,11 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
         c->last.scan_ms = ms;
         c->last.scan_launches = 1;
-        HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
-        c->last.total_ms = ms;
+        c->last.total_ms = NAN;
+        if (c->timing == 1) {
+          HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+          c->last.total_ms = ms;
+        }
       }
       c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
       *out = r;
@@ -1391,11 +1426,10 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       }
       hipFunction_t fs = nullptr, ff = nullptr;
       if (c->opt[kOptJit] && N >= c->jit_min_rows()) {
-        const std::string spec = jit_spec(pl.p) + "#define BQ_PART_K " + std::to_string(L.k) +
-                                 "\n#define BQ_PART_NARROW " + std::to_string(L.narrow) +
-                                 "\n#define BQ_PART_PACK " + std::to_string(L.pack) + "\n";
-        fs = jit_function("bq_jit_part_scatter", spec);
-        if (pk) ff = jit_function("bq_jit_part_first_rows", spec);
+        const std::string extra = "#define BQ_PART_K " + std::to_string(L.k) + "\n#define BQ_PART_NARROW " +
+                                  std::to_string(L.narrow) + "\n#define BQ_PART_PACK " + std::to_string(L.pack) + "\n";
+        fs = jit_function_for("bq_jit_part_scatter", pl.p, extra);
+        if (pk) ff = jit_function_for("bq_jit_part_first_rows", pl.p, extra);
         c->last.specialized = fs ? 1 : 0;
       }
       launch_partitioned(pl.p, sa, L, st, fs, ff);
@@ -1682,10 +1716,11 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         const int nc = pc.p.ncols;
         const int vc = d.vcol >= 0 && d.vcol < nc ? d.vcol : 0;
         const int cc = d.cd.vcol >= 0 && d.cd.vcol < nc ? d.cd.vcol : 0;
-        std::string spec = jit_spec(pc.p) + "#define BQ_SCD_CD " + std::to_string(cd_mode) + "\n#define BQ_SCD_VC " +
-                           std::to_string(vc) + "\n#define BQ_SCD_CC " + std::to_string(cc) + "\n#define BQ_SCD_P16 " +
-                           std::to_string(d.pack16) + "\n";
-        sfn = jit_function(d.runs ? "bq_jit_scd_runs32" : d.compact ? "bq_jit_scd_fused32" : "bq_jit_scd_fused", spec);
+        const std::string extra = "#define BQ_SCD_CD " + std::to_string(cd_mode) + "\n#define BQ_SCD_VC " +
+                                  std::to_string(vc) + "\n#define BQ_SCD_CC " + std::to_string(cc) +
+                                  "\n#define BQ_SCD_P16 " + std::to_string(d.pack16) + "\n";
+        sfn = jit_function_for(d.runs ? "bq_jit_scd_runs32" : d.compact ? "bq_jit_scd_fused32" : "bq_jit_scd_fused",
+                               pc.p, extra);
         c->last.specialized = sfn ? 1 : 0;
       }
       if (fused && c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
@@ -1721,7 +1756,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     } else {
       hh = (const unsigned long long*)blk.b.p;
     }
-    if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
+    if (c->timing == 1) HIPCHECK(hipEventRecord(c->ev[3], st));
     HIPCHECK(hipStreamSynchronize(st));
     const int64_t G = (int64_t)hh[0];
     const int filtered = pl.has_filter && (int64_t)hh[1] < N;
@@ -1729,8 +1764,11 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       float ms = 0;
       HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
       c->last.scan_ms = ms;
-      HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
-      c->last.total_ms = ms;
+      c->last.total_ms = NAN;
+      if (c->timing == 1) {
+        HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+        c->last.total_ms = ms;
+      }
     }
     c->last.bytes = pl.alg_bytes + G * (int64_t)e.ncols * 8;
     if (G == 0) {
@@ -1796,7 +1834,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   }
   HIPCHECK(hipGetLastError());
   if (c->dev_target) {
-    if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
+    if (c->timing == 1) HIPCHECK(hipEventRecord(c->ev[3], st));
     std::vector<const void*> src;
     for (int j = 0; j < e.ncols; ++j) src.push_back(e.cols[j].out);
     table_from_device(c, out_dt, src, (int64_t)G);
@@ -1804,8 +1842,11 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       float ms = 0;
       HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
       c->last.scan_ms = ms;
-      HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
-      c->last.total_ms = ms;
+      c->last.total_ms = NAN;
+      if (c->timing == 1) {
+        HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+        c->last.total_ms = ms;
+      }
     }
     c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
     return;
@@ -1813,7 +1854,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   BlockGuard blk;
   blk.reset(c->pool, c->pool_get(obytes + 64));
   HIPCHECK(hipMemcpyAsync(blk.b.p, ob, obytes, hipMemcpyDeviceToHost, st));
-  if (c->timing) HIPCHECK(hipEventRecord(c->ev[3], st));
+  if (c->timing == 1) HIPCHECK(hipEventRecord(c->ev[3], st));
   HIPCHECK(hipStreamSynchronize(st));
   std::vector<size_t> offs;
   {
@@ -1828,8 +1869,11 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     float ms = 0;
     HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
     c->last.scan_ms = ms;
-    HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
-    c->last.total_ms = ms;
+    c->last.total_ms = NAN;
+    if (c->timing == 1) {
+      HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+      c->last.total_ms = ms;
+    }
   }
   c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
   *out = r;
@@ -1861,7 +1905,7 @@ void run_groupby_grow(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result**
 
 int bqg_internal_device(bqg_ctx* c) { return c->device; }
 hipStream_t bqg_internal_stream(bqg_ctx* c) { return c->stream; }
-bool bqg_internal_timing(bqg_ctx* c) { return c->timing; }
+bool bqg_internal_timing(bqg_ctx* c) { return c->timing != 0; }
 void bqg_internal_set_error(bqg_ctx* c, const std::string& msg) {
   if (c) c->err = msg;
   g_err = msg;
@@ -2033,7 +2077,7 @@ int bqg_synchronize(bqg_ctx* c) {
 }
 
 int bqg_enable_timing(bqg_ctx* c, int on) {
-  return guard(c, [&] { c->timing = on != 0; });
+  return guard(c, [&] { c->timing = on == 2 ? 2 : (on != 0 ? 1 : 0); });
 }
 
 int bqg_last_timing(bqg_ctx* c, bqg_timing* out) {

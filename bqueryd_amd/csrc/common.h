@@ -130,8 +130,26 @@ __device__ __forceinline__ uint4 load_stream16(const unsigned char* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ void load_chunk(Chunk& c, const DevCol& col, int64_t row0) {
   const int64_t off = row0 << col.lg;
+#ifdef BQ_NC
+  // query-specialised build: the width is a constant, so a 1- / 2-byte column loads exactly
+  // its lane's 4 rows (one dword / dwordx2 at the 4-row-aligned row0; the wave's loads stay
+  // contiguous) -- no 16-byte block to pick the lane's word out of at decode
+  if (col.lg == 0) {
+    c.a = make_uint4(__builtin_nontemporal_load(reinterpret_cast<const unsigned int*>(col.ptr + off)), 0u, 0u, 0u);
+    c.sh = 0;
+    return;
+  }
+  if (col.lg == 1) {
+    const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(col.ptr + off));
+    c.a = make_uint4(v.x, v.y, 0u, 0u);
+    c.sh = 0;
+    return;
+  }
+#endif
   const unsigned char* p = col.ptr + (off & ~int64_t(15));
   c.a = load_stream16(p);
   if (col.lg == 3) c.b = load_stream16(p + 16);

@@ -20,4 +20,8 @@ std::string jit_spec(const ScanParams& p);
 // all is the caller's choice (context options "jit" / "jit_min_rows", api.hip)
 hipFunction_t jit_function(const char* kernel, const std::string& spec);
 
+// jit_function(kernel, jit_spec(p) + extra), looked up first by the binary image of p's
+// specialised fields (the per-query path: no prologue text is built for a known shape)
+hipFunction_t jit_function_for(const char* kernel, const ScanParams& p, const std::string& extra = std::string());
+
 }  // namespace bqg

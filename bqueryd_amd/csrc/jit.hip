@@ -13,6 +13,7 @@
 #include <map>
 #include <mutex>
 #include <sstream>
+#include <unordered_map>
 #include <vector>
 
 #include "jit_src.inc"
@@ -99,6 +100,9 @@ struct JitState {
   Rtc* rtc = nullptr;
   bool tried = false;
   std::map<std::string, hipFunction_t> fns;  // device:kernel:hash -> function (nullptr = failed)
+  // per-query front cache (jit_function_for): binary shape key -> function, so a repeated query
+  // shape costs one hash lookup instead of formatting and hashing its prologue
+  std::unordered_map<std::string, hipFunction_t> by_shape;
 
   bool compile(const std::string& src, std::vector<char>& code) {
     if (!tried) {
@@ -145,32 +149,87 @@ JitState& state() {
 
 }  // namespace
 
+namespace {
+
+// Every ScanParams field the specialisation reads, in prologue order: f(array, index, field,
+// value, suffix) -- "p.cols[0].dtype=3;" is ("p.cols", 0, "dtype", 3, ""), "p.ncols=2;" is
+// ("p", -1, "ncols", 2, ""), "p.sum_conv[1]=0;" is ("p.sum_conv", 1, nullptr, 0, "").  The
+// prologue text and the per-query cache key below are both built from this one list.
+template <class F>
+void spec_fields(const ScanParams& p, F&& f) {
+  f("p", -1, "ncols", p.ncols, "");
+  for (int c = 0; c < p.ncols; ++c) {
+    f("p.cols", c, "dtype", p.cols[c].dtype, "");
+    f("p.cols", c, "lg", p.cols[c].lg, "");
+    f("p.cols", c, "enc", p.cols[c].enc, "");
+  }
+  f("p", -1, "nterms", p.nterms, "");
+  for (int t = 0; t < p.nterms; ++t) {
+    const DevTerm& tm = p.terms[t];
+    f("p.terms", t, "col", tm.col, "");
+    f("p.terms", t, "op", tm.op, "");
+    f("p.terms", t, "is_float", tm.is_float, "");
+    if ((tm.op == BQG_T_IN || tm.op == BQG_T_NIN) && tm.nvals <= 8) f("p.terms", t, "nvals", tm.nvals, "");
+  }
+  f("p", -1, "nkeys", p.nkeys, "");
+  for (int k = 0; k < p.nkeys; ++k) {
+    const DevKey& key = p.keys[k];
+    f("p.keys", k, "col", key.col, "");
+    f("p.keys", k, "is_float", key.is_float, "");
+    if (key.stride == 1) f("p.keys", k, "stride", 1, "ull");
+  }
+  f("p", -1, "nsum", p.nsum, "");
+  for (int i = 0; i < p.nsum && i < kMaxSums; ++i) {
+    f("p.sum_is_float", i, nullptr, p.sum_is_float[i], "");
+    f("p.sum_conv", i, nullptr, p.sum_conv[i], "");
+    f("p.sum_centered", i, nullptr, p.sum_centered[i], "");
+  }
+  f("p", -1, "mask_col", p.mask_col, "");
+  f("p", -1, "hash", p.hash, "");
+}
+
+}  // namespace
+
 std::string jit_spec(const ScanParams& p) {
   std::ostringstream s;
   s << "#define BQ_NC " << p.ncols << "\n#define BQ_SPEC ";
-  s << "p.ncols=" << p.ncols << ";";
-  for (int c = 0; c < p.ncols; ++c)
-    s << "p.cols[" << c << "].dtype=" << p.cols[c].dtype << ";p.cols[" << c << "].lg=" << p.cols[c].lg
-      << ";p.cols[" << c << "].enc=" << p.cols[c].enc << ";";
-  s << "p.nterms=" << p.nterms << ";";
-  for (int t = 0; t < p.nterms; ++t) {
-    const DevTerm& tm = p.terms[t];
-    s << "p.terms[" << t << "].col=" << tm.col << ";p.terms[" << t << "].op=" << tm.op << ";p.terms[" << t
-      << "].is_float=" << tm.is_float << ";";
-    if ((tm.op == BQG_T_IN || tm.op == BQG_T_NIN) && tm.nvals <= 8) s << "p.terms[" << t << "].nvals=" << tm.nvals << ";";
-  }
-  s << "p.nkeys=" << p.nkeys << ";";
-  for (int k = 0; k < p.nkeys; ++k) {
-    const DevKey& key = p.keys[k];
-    s << "p.keys[" << k << "].col=" << key.col << ";p.keys[" << k << "].is_float=" << key.is_float << ";";
-    if (key.stride == 1) s << "p.keys[" << k << "].stride=1ull;";
-  }
-  s << "p.nsum=" << p.nsum << ";";
-  for (int i = 0; i < p.nsum && i < kMaxSums; ++i)
-    s << "p.sum_is_float[" << i << "]=" << p.sum_is_float[i] << ";p.sum_conv[" << i << "]=" << p.sum_conv[i]
-      << ";p.sum_centered[" << i << "]=" << p.sum_centered[i] << ";";
-  s << "p.mask_col=" << p.mask_col << ";p.hash=" << p.hash << ";\n";
+  spec_fields(p, [&](const char* arr, int idx, const char* field, long long v, const char* sfx) {
+    s << arr;
+    if (idx >= 0) s << "[" << idx << "]";
+    if (field) s << "." << field;
+    s << "=" << v << sfx << ";";
+  });
+  s << "\n";
   return s.str();
+}
+
+hipFunction_t jit_function_for(const char* kernel, const ScanParams& p, const std::string& extra) {
+  // the key: device, kernel, extra defines, then (field, value) for every specialised field --
+  // the field names' addresses mark which conditional fields are present
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::string key;
+  key.reserve(512 + extra.size());
+  key.append((const char*)&dev, sizeof(dev));
+  key.append(kernel);
+  key.push_back('\0');
+  key.append(extra);
+  key.push_back('\0');
+  spec_fields(p, [&](const char* arr, int, const char* field, long long v, const char*) {
+    const void* tag[2] = {arr, field};
+    key.append((const char*)tag, sizeof(tag));
+    key.append((const char*)&v, sizeof(v));
+  });
+  JitState& js = state();
+  {
+    std::lock_guard<std::mutex> lk(js.mu);
+    auto it = js.by_shape.find(key);
+    if (it != js.by_shape.end()) return it->second;
+  }
+  hipFunction_t fn = jit_function(kernel, jit_spec(p) + extra);
+  std::lock_guard<std::mutex> lk(js.mu);
+  js.by_shape.emplace(std::move(key), fn);
+  return fn;
 }
 
 hipFunction_t jit_function(const char* kernel, const std::string& spec) {

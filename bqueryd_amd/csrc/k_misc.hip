@@ -289,8 +289,8 @@ __global__ __launch_bounds__(1024) void k_emit_small(EmitParams e, SlotArrays sa
     }
     unsigned int rank = 0;
     for (unsigned int j = 0; j < G; ++j) rank += kf[j] < f ? 1u : 0u;
+    // (outputs in pinned host memory are read after hipStreamSynchronize: no system fence)
     if (threadIdx.x < G) emit_one(s, rank);
-    __threadfence_system();  // outputs may live in device-mapped host memory
     return;
   }
   unsigned int m = 1;
@@ -314,7 +314,6 @@ __global__ __launch_bounds__(1024) void k_emit_small(EmitParams e, SlotArrays sa
     }
   }
   for (unsigned int i = threadIdx.x; i < G; i += blockDim.x) emit_one(ks[i], i);
-  __threadfence_system();
 }
 
 // ------------------------------------------------------------------------------------
@@ -812,10 +811,15 @@ __global__ __launch_bounds__(kBlock) void k_shadow_int(DevCol src, int64_t n, in
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_shadow_code(const double* src, int64_t n, int kind, double mul, int32_t* dst) {
+__global__ __launch_bounds__(kBlock) void k_shadow_code(const double* src, int64_t n, int kind, double mul, int64_t off,
+                                                       void* dst, int dst_lg) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
     const double d = src[i] * mul;
-    dst[i] = (int32_t)(kind == 1 ? d : rint(d));
+    const int64_t code = (int64_t)(kind == 1 ? d : rint(d));
+    const uint64_t u = (uint64_t)(code - off);
+    if (dst_lg == 0) reinterpret_cast<uint8_t*>(dst)[i] = (uint8_t)u;
+    else if (dst_lg == 1) reinterpret_cast<uint16_t*>(dst)[i] = (uint16_t)u;
+    else reinterpret_cast<int32_t*>(dst)[i] = (int32_t)code;
   }
 }
 
@@ -825,10 +829,11 @@ void launch_shadow_int(const DevCol& src, int64_t nrows, int64_t off, void* dst,
   hipLaunchKernelGGL(k_shadow_int, dim3(g), dim3(kBlock), 0, st, src, nrows, off, dst, dst_lg);
 }
 
-void launch_shadow_code(const double* src, int64_t nrows, int kind, double mul, int32_t* dst, hipStream_t st) {
+void launch_shadow_code(const double* src, int64_t nrows, int kind, double mul, int64_t off, void* dst, int dst_lg,
+                        hipStream_t st) {
   if (nrows <= 0) return;
   const unsigned g = (unsigned)std::min<int64_t>((nrows + kBlock - 1) / kBlock, 8192);
-  hipLaunchKernelGGL(k_shadow_code, dim3(g), dim3(kBlock), 0, st, src, nrows, kind, mul, dst);
+  hipLaunchKernelGGL(k_shadow_code, dim3(g), dim3(kBlock), 0, st, src, nrows, kind, mul, off, dst, dst_lg);
 }
 
 // std pass 2 centers: the mean of every slot of every std column, from pass 1's count and sum

@@ -336,10 +336,11 @@ struct StdCenters {
   double dec[kMaxSums];
 };
 // compact resident copies (api.hip Column::shadow): an integer column as (v - off) in 1, 2 or 4
-// bytes (dst_lg), a float64 column as its exact int32 codes (kind 1 dyadic v * mul, 2 cents
-// rint(v * mul))
+// bytes (dst_lg), a float64 column as its exact integer codes (kind 1 dyadic v * mul, 2 cents
+// rint(v * mul)): code - off in 1 / 2 bytes (dst_lg 0 / 1), or the int32 code (dst_lg 2)
 void launch_shadow_int(const DevCol& src, int64_t nrows, int64_t off, void* dst, int dst_lg, hipStream_t st);
-void launch_shadow_code(const double* src, int64_t nrows, int kind, double mul, int32_t* dst, hipStream_t st);
+void launch_shadow_code(const double* src, int64_t nrows, int kind, double mul, int64_t off, void* dst, int dst_lg,
+                        hipStream_t st);
 void launch_std_centers(const unsigned long long* cnt, const unsigned long long* acc, const StdCenters& sc,
                         uint64_t nslots, double* centers, hipStream_t st);
 

@@ -55,16 +55,27 @@ __device__ __forceinline__ void scan_private_body(const ScanParams& p, const Pri
     decode_all<NC, 4>(p, ring[a], v);
     const int64_t next = tile + kPrivAhead * grid;
     load_rows4<NC>(p, (next < ntiles ? next : tile) * kTileRows + lane_row, ring[a]);
-    const uint32_t pass = vals_pass<NC, 4>(p, row0, v);
+    // the row bound only on the last tile (wave-uniform branch): full tiles skip its 64-bit
+    // compares
+    uint32_t pass = 0xFu;
+    if (tile == ntiles - 1) {
+      const int64_t rem = p.nrows - row0;
+      pass = rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
+    }
+    pass &= vals_pass<NC, 4, false>(p, row0, v);
     uint64_t code[4];
     vals_code<NC, 4>(p, v, code);
+    // count, first row and integer sums as LDS atomics whose results are unused (ds_add /
+    // ds_min without return): the slot rows are lane-private, so nothing contends, and no row
+    // waits for a read of the row before it (a read-modify-write chain per row stalled the
+    // wave on two LDS round trips).  Rows are visited in increasing order, so min = first.
+    // Float sums keep the ordered read-modify-write (row-order float64 additions per lane).
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (pass & (1u << r)) {
         const int idx = (int)code[r] * kBlock + tid;
-        const uint32_t c0 = cnt[idx];
-        if (c0 == 0) fst[idx] = (uint32_t)(row0 + r);
-        cnt[idx] = c0 + 1;
+        atomicMin(&fst[idx], (uint32_t)(row0 + r));
+        atomicAdd(&cnt[idx], 1u);
 #pragma unroll
         for (int s = 0; s < (NC < kMaxSums ? NC : kMaxSums); ++s) {
           if (s < nsum) {
@@ -77,7 +88,7 @@ __device__ __forceinline__ void scan_private_body(const ScanParams& p, const Pri
               }
               *a = as_u64(as_f64(*a) + x);
             } else {
-              *a += v[s][r];
+              atomicAdd(a, (unsigned long long)v[s][r]);
             }
           }
         }

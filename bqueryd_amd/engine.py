@@ -47,8 +47,10 @@ class Device:
     def synchronize(self):
         self.check(self._lib.bqg_synchronize(self.handle))
 
-    def enable_timing(self, on=True):
-        self.check(self._lib.bqg_enable_timing(self.handle, 1 if on else 0))
+    def enable_timing(self, on=True, scan_only=False):
+        """HIP-event timing of each query (``last_timing``): the scan kernels and the whole
+        query, or with ``scan_only`` the scan kernels alone (``total_ms`` NaN)."""
+        self.check(self._lib.bqg_enable_timing(self.handle, (2 if scan_only else 1) if on else 0))
 
     def last_timing(self):
         t = L.Timing()
@@ -95,14 +97,25 @@ class _Unfreezable(Exception):
     pass
 
 
+_FREEZE_SCALARS = (bytes, bool, int, float, type(None))
+
+
 def _freeze(x):
-    """Hashable, type-exact image of a query argument (plan-cache key)."""
-    if isinstance(x, (list, tuple)):
-        return (type(x).__name__,) + tuple(_freeze(v) for v in x)
-    if isinstance(x, (set, frozenset)):
-        return ('set', frozenset(_freeze(v) for v in x))
-    if isinstance(x, (str, bytes, bool, int, float, type(None), np.generic)):
-        return (type(x), x)
+    """Hashable, type-exact image of a query argument (plan-cache key).  Exact-type checks
+    first (this runs on every query): a plain str stands for itself, a list / tuple is a tuple
+    tagged with which of the two it was; subclasses other than str / numpy scalars are not
+    cached."""
+    t = type(x)
+    if t is str:
+        return x
+    if t is list or t is tuple:
+        return (t is list,) + tuple([_freeze(v) for v in x])
+    if t in _FREEZE_SCALARS or isinstance(x, np.generic):
+        return (t, x)
+    if t is set or t is frozenset:
+        return ('set', frozenset([_freeze(v) for v in x]))
+    if isinstance(x, str):
+        return (t, x)
     raise _Unfreezable()
 
 

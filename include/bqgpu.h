@@ -144,6 +144,8 @@ const char* bqg_last_error(bqg_ctx* ctx);
  * the library's own stream. */
 int bqg_set_stream(bqg_ctx* ctx, void* hip_stream);
 int bqg_synchronize(bqg_ctx* ctx);
+/* on: 0 off; 1 (any other non-zero) HIP events around the scan kernels (scan_ms) and the whole
+ * query (total_ms); 2 the scan events only (total_ms NaN: two fewer event records per query). */
 int bqg_enable_timing(bqg_ctx* ctx, int on);
 int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
 
@@ -173,10 +175,11 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *   part_pack      1  packed 4-byte partition entries when they fit    0 | 1
  *   scd_runs       1  fused distinct pass in 256-row steps for clustered keys  0 | 1
  *   part_win       0  partitioned aggregate: tiles of bounds per LDS window   0 (auto) | 64..4096
- *   compact        1  private / shared / dense global scans read compact  0 | 1
+ *   compact        1  private / shared / dense global scans read compact  0 | 1 | 2
  *                     resident copies of their columns (narrow integer
- *                     offsets, exact int32 codes of float64 columns that
- *                     are only summed)
+ *                     offsets; exact integer codes of float64 columns that
+ *                     are only summed, as 1 / 2-byte offsets when they span
+ *                     < 2^16, else int32; 2: int32 codes only)
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);

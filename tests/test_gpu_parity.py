@@ -881,7 +881,9 @@ def test_compact_resident_copies(mode, oracle_c, engine_options):
     cols = OrderedDict(k=k, t=rng.integers(-30_000, 30_000, n).astype(np.int32),
                        i=rng.integers(-2**40, -2**40 + 200, n).astype(np.int64),
                        c=rng.integers(-50_000, 90_000, n) / 100.0,
-                       d=np.ldexp(rng.integers(-2**20, 2**20, n).astype(np.float64), -5))
+                       d=np.ldexp(rng.integers(-2**20, 2**20, n).astype(np.float64), -5),
+                       f=rng.integers(-20_000, 40_000, n) / 100.0,       # cents spanning < 2^16: 2-byte codes
+                       g=np.ldexp(rng.integers(-100, 100, n).astype(np.float64), -2))  # 1-byte dyadic codes
     aggs = [['c', 'sum', 'cs'], ['c', 'mean', 'cm'], ['d', 'sum', 'ds'], ['i', 'sum', 'is'], ['i', 'count', 'n']]
     terms = [('t', '>=', -12_345)]
     t = ShardTable(cols)
@@ -897,6 +899,20 @@ def test_compact_resident_copies(mode, oracle_c, engine_options):
         ref = oracle_c.groupby(cols, ['k'], aggs, oracle_c.where_terms(cols, terms))
         assert_tables_equal(got, ref, exact_cols={'ds', 'is'})
         assert_tables_equal(full, ref, exact_cols={'ds', 'is'})
+        # float64 sums over codes spanning fewer than 2^16 / 2^8: 2 / 1-byte offsets from the
+        # smallest code
+        aggs4 = [['f', 'sum', 'fs'], ['f', 'mean', 'fm'], ['g', 'sum', 'gs'], ['g', 'count', 'n']]
+        got4, _ = t.groupby(['k'], aggs4, where_terms=terms)
+        info4 = t.dev.last_timing()
+        with t.dev.options(compact=0):
+            full4, _ = t.groupby(['k'], aggs4, where_terms=terms)
+            finfo4 = t.dev.last_timing()
+        # f 8 -> 2 B, g 8 -> 1 B, t 4 -> 2 B per row, k as above
+        kd = {'private': 7, 'shared': 2, 'global_dense': 0}[mode]
+        assert finfo4['bytes'] - info4['bytes'] == (kd + 6 + 7 + 2) * n, (info4['bytes'], finfo4['bytes'])
+        ref4 = oracle_c.groupby(cols, ['k'], aggs4, oracle_c.where_terms(cols, terms))
+        assert_tables_equal(got4, ref4, exact_cols={'gs'})
+        assert_tables_equal(full4, ref4, exact_cols={'gs'})
         # new values in a column: its copy is rebuilt
         cols['t'] = rng.integers(-100, 100_000, n).astype(np.int32)
         t.push('t', cols['t'])

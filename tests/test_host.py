@@ -290,6 +290,11 @@ def test_groupby_plan_cache_key_is_exact():
     with pytest.raises(ValueError):  # bquery: `in` takes lists, sets or tuples
         t._plan(['a'], [['b', 'sum', 's']], [('a', 'in', np.arange(3))], None)
     assert len(t._plans) == 4
+    # equal-comparing values of different types are different keys
+    from bqueryd_amd.engine import _freeze
+    keys = [_freeze(v) for v in ([1], [1.0], [True], (1,), [np.float32(1)], [np.int64(1)], ['1'], [b'1'])]
+    assert len(set(keys)) == len(keys)
+    assert _freeze({'x', 'y'}) == _freeze({'y', 'x'})
 
 
 def test_shard_cache_budget_counts_unions():

@@ -31,7 +31,8 @@ def main():
         t.groupby(cfg['groupby'], cfg['aggs'], where_terms=cfg['where'])
 
     def timed(fn, timing):
-        dev.enable_timing(timing)
+        # timing 0 off, 1 scan + query events, 2 scan events only
+        dev.enable_timing(timing != 0, scan_only=timing == 2)
         dev.synchronize()
         w = []
         dv = []
@@ -39,7 +40,7 @@ def main():
             t0 = time.perf_counter()
             fn()
             w.append(time.perf_counter() - t0)
-            if timing:
+            if timing == 1:
                 dv.append(dev.last_timing()['total_ms'])
         return np.median(w) * 1e6, (np.median(dv) * 1e3 if dv else float('nan'))
 
@@ -54,7 +55,7 @@ def main():
         L.lib().bqg_result_free(res)
 
     for name, fn in (('python groupby', full), ('bare C call', bare)):
-        for timing in (False, True):
+        for timing in (0, 2, 1):
             w, d = timed(fn, timing)
             print('%-16s timing=%d  wall %.1f us  device total %.1f us' % (name, timing, w, d), flush=True)
 
