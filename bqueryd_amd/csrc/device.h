@@ -209,13 +209,42 @@ __device__ __forceinline__ bool cmp_op(int op, T x, T v) {
   }
 }
 
+// A scalar comparison of values known to lie in [0, 2^32) (a compact copy's stored offsets,
+// compile-time in a specialised kernel): the int64 constant folds into a 32-bit bound once
+// (uniform), so each row costs one 32-bit compare instead of a 64-bit one
 template <int R>
-__device__ __forceinline__ uint32_t eval_term(const DevTerm& t, const uint64_t (&v)[R], bool uns) {
+__device__ __forceinline__ uint32_t eval_term_u32(int op, int64_t c, const uint64_t (&v)[R]) {
+  // ge: v >= lo (lo in [0, 2^32]); lt: v < lo; eq / ne: v == c when c is in range
+  const int64_t lo64 = (op == BQG_T_GT || op == BQG_T_LE) ? (c == (int64_t)0x7FFFFFFFFFFFFFFFll ? c : c + 1) : c;
+  const bool lo_neg = lo64 <= 0, lo_big = lo64 > (int64_t)0xFFFFFFFFll;
+  const uint32_t lo = lo_neg ? 0u : (uint32_t)lo64;
+  const bool in_range = c >= 0 && c <= (int64_t)0xFFFFFFFFll;
+  uint32_t m = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t x = (uint32_t)v[r];
+    bool hit;
+    switch (op) {
+      case BQG_T_GE:
+      case BQG_T_GT: hit = !lo_big && x >= lo; break;
+      case BQG_T_LT:
+      case BQG_T_LE: hit = lo_big || (!lo_neg && x < lo); break;
+      case BQG_T_EQ: hit = in_range && x == (uint32_t)c; break;
+      default: hit = !in_range || x != (uint32_t)c; break;  // NE
+    }
+    m |= (uint32_t)hit << r;
+  }
+  return m;
+}
+
+template <int R>
+__device__ __forceinline__ uint32_t eval_term(const DevTerm& t, const uint64_t (&v)[R], bool uns, bool u32 = false) {
   const int op = t.op;
   if (op == BQG_T_TRUE) return (1u << R) - 1u;
   if (op == BQG_T_FALSE) return 0u;
   uint32_t m = 0;
   const bool list = (op == BQG_T_IN || op == BQG_T_NIN);
+  if (u32 && !list && !t.is_float) return eval_term_u32<R>(op, t.iv0, v);
   if (t.is_float) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -257,7 +286,10 @@ __device__ __forceinline__ uint32_t vals_pass(const ScanParams& p, int64_t row0,
     const DevTerm& tm = p.terms[t];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
-      if (tm.col == c) pass &= eval_term<R>(tm, v[c], p.cols[c].dtype == BQG_U64);
+      if (tm.col == c)
+        pass &= eval_term<R>(tm, v[c], p.cols[c].dtype == BQG_U64,
+                             p.cols[c].enc == 0 && (p.cols[c].dtype == BQG_U8 || p.cols[c].dtype == BQG_U16 ||
+                                                    p.cols[c].dtype == BQG_U32));
   }
   if (p.mask_col >= 0) {
 #pragma unroll

@@ -926,3 +926,32 @@ def test_compact_resident_copies(mode, oracle_c, engine_options):
         assert_tables_equal(got3, ref3)
     finally:
         t.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('jit', [1, 0])
+def test_compact_term_bounds(jit, oracle_c, engine_options):
+    """Scalar terms on a compact integer column compare in the copy's domain (stored = value -
+    min, a 32-bit compare in specialised kernels): every operator at and around the column's
+    minimum and maximum, beyond both, and at the int64 extremes -- the same rows pass as in the
+    oracle, in the private scan and in the shared scan."""
+    engine_options(jit=jit, jit_min_rows=0)
+    rng = np.random.default_rng(77)
+    n = 50_000
+    for kvals, vlo, vhi in ((6, -5, 300), (700, 1000, 1200)):
+        cols = OrderedDict(k=rng.integers(0, kvals, n).astype(np.int32),
+                           t=rng.integers(vlo, vhi + 1, n).astype(np.int64),
+                           x=rng.integers(-1000, 1000, n).astype(np.int64))
+        t = ShardTable(cols)
+        try:
+            consts = [vlo - 1, vlo, vlo + 1, vhi - 1, vhi, vhi + 1, -2**40, 2**40, 2**33 + vlo,
+                      -2**63, 2**63 - 1, 0, -1]
+            for op in ('==', '!=', '<', '<=', '>', '>='):
+                for c in consts:
+                    terms = [('t', op, c)]
+                    got, _ = t.groupby(['k'], [['x', 'sum', 'xs'], ['x', 'count', 'n']], where_terms=terms)
+                    ref = oracle_c.groupby(cols, ['k'], [['x', 'sum', 'xs'], ['x', 'count', 'n']],
+                                           oracle_c.where_terms(cols, terms))
+                    assert_tables_equal(got, ref, exact_cols={'xs', 'n'})
+        finally:
+            t.close()
