@@ -1216,8 +1216,14 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     hipFunction_t jfn = nullptr;
     if (c->opt[kOptJit] && N >= c->jit_min_rows()) {
       // tiles in flight per workgroup (profiling option; default in scan_private.h)
+      // (default: 3 when the scan reads at most 4 bytes per row -- compact copies: each tile is
+      // small, and one in flight leaves the waves parked on memory; r4x8: C2 0.072 -> 0.069
+      // ms -- else the kernel's 1)
+      int row_bytes = 0;
+      for (int i = 0; i < sp.ncols; ++i) row_bytes += 1 << sp.cols[i].lg;
+      const int64_t ahead = c->opt[kOptPrivAhead] ? c->opt[kOptPrivAhead] : (row_bytes <= 4 ? 3 : 0);
       std::string extra;
-      if (c->opt[kOptPrivAhead]) extra = std::string("#define BQ_PRIV_AHEAD ") + std::to_string(c->opt[kOptPrivAhead]) + "\n";
+      if (ahead) extra = std::string("#define BQ_PRIV_AHEAD ") + std::to_string(ahead) + "\n";
       jfn = jit_function_for("bq_jit_scan_private", sp, extra);
     }
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));

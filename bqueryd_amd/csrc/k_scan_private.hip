@@ -24,7 +24,14 @@ __device__ void private_finish_body(const FinishParams& f, const SlotArrays& sa,
 constexpr int kPrivReduceThreads = 1024;
 __global__ __launch_bounds__(kPrivReduceThreads) void k_private_reduce(FinishParams f, SlotArrays sa, EmitParams e) {
   __shared__ unsigned long long tot[(2 + kMaxSums) * kMaxPrivateSlots];
+  // the emit description staged in LDS by all threads at once (one parallel load of the ~1.5
+  // KiB kernel argument), so the finish wave's dependent field reads are LDS reads rather than
+  // a chain of first-touch kernel-argument fetches
+  __shared__ EmitParams es;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = kPrivReduceThreads / 64;
+  static_assert(sizeof(EmitParams) % 4 == 0 && sizeof(EmitParams) / 4 <= kPrivReduceThreads, "EmitParams copy: one word per thread");
+  if (tid < (int)(sizeof(EmitParams) / 4))
+    reinterpret_cast<uint32_t*>(&es)[tid] = reinterpret_cast<const uint32_t*>(&e)[tid];
   const int S = f.nslots, nb = f.blocks;
   const int P = (2 + f.nsum) * S;
   // every wave takes its pairs two at a time (pair, pair + 16): the loads of both issued together
@@ -88,7 +95,7 @@ __global__ __launch_bounds__(kPrivReduceThreads) void k_private_reduce(FinishPar
   if (tid < 64) {
     FinishParams g = f;
     g.totals = tot;  // the finish step reads the totals from LDS
-    private_finish_body(g, sa, e, tid);
+    private_finish_body(g, sa, es, tid);
   }
 }
 
@@ -114,7 +121,10 @@ __device__ void private_finish_body(const FinishParams& f, const SlotArrays& sa,
       unsigned int rank = 0;
       for (int q = 0; q < S; ++q)
         if (tot[q] > 0 && (uint32_t)tot[S + q] < first) ++rank;
-      SlotTotals t;
+      // in LDS, not registers: emit_slot indexes the sums by state (a dynamic index into a
+      // register array is a scratch-memory round trip per access)
+      __shared__ SlotTotals st_all[kMaxPrivateSlots];
+      SlotTotals& t = st_all[s];
       t.cnt = tot[s];
       t.fst = first;
 #pragma unroll

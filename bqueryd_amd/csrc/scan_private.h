@@ -11,23 +11,24 @@ namespace bqg {
 #endif
 constexpr int kPrivAhead = BQ_PRIV_AHEAD;  // tiles loaded ahead of the one being aggregated
 
-// Every lane owns a private accumulator row per slot in LDS, laid out [slot][lane] so that
-// the per-row read-modify-writes are conflict-free ds_read/ds_write with no atomics.  Rows
-// of a lane are processed in increasing order, so its first write to a slot is that slot's
-// first row for the lane.  A workgroup streams tiles of 1024 rows (4 per lane, one 16-byte
-// load per 4-byte column) and prefetches the next tile while it aggregates the current one.
+// Every lane owns a private accumulator row per slot in LDS, laid out [slot][lane]: nothing
+// contends, so the per-row updates are LDS atomics without return (no read-modify-write
+// chains).  Rows of a lane are processed in increasing order, so the minimum of its rows in a
+// slot is that slot's first row for the lane.  A workgroup streams tiles of 1024 rows (4 per
+// lane; one load per column: 16 bytes of a 4-byte column, exactly the lane's 4 or 8 bytes of
+// a 1- or 2-byte column in specialised kernels) and prefetches the next tile while it
+// aggregates the current one.
 template <int NC>
 __device__ __forceinline__ void scan_private_body(const ScanParams& p, const PrivateLaunch& L, unsigned char* smem) {
   const int S = (int)p.nslots;
   const int tid = threadIdx.x;
   const int nsum = p.nsum;
-  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);          // [nsum][S][256]
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)nsum * S * kBlock);   // [S][256]
-  uint32_t* fst = cnt + S * kBlock;                                                // [S][256]
-  for (int s = 0; s < S; ++s) {
-    cnt[s * kBlock + tid] = 0;
-    fst[s * kBlock + tid] = kNoRow;
-  }
+  // [S][256] {count, first row} word pairs (one address per row for both), then the sums
+  // [nsum][S][256]
+  uint32_t* cf = reinterpret_cast<uint32_t*>(smem);
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem + (size_t)S * kBlock * 8);
+  for (int s = 0; s < S; ++s)
+    reinterpret_cast<unsigned long long*>(cf)[s * kBlock + tid] = (unsigned long long)kNoRow << 32;
   for (int i = 0; i < nsum * S; ++i) acc[i * kBlock + tid] = 0;
 
   const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
@@ -74,8 +75,8 @@ __device__ __forceinline__ void scan_private_body(const ScanParams& p, const Pri
     for (int r = 0; r < 4; ++r) {
       if (pass & (1u << r)) {
         const int idx = (int)code[r] * kBlock + tid;
-        atomicMin(&fst[idx], (uint32_t)(row0 + r));
-        atomicAdd(&cnt[idx], 1u);
+        atomicAdd(&cf[2 * idx], 1u);
+        atomicMin(&cf[2 * idx + 1], (uint32_t)(row0 + r));
 #pragma unroll
         for (int s = 0; s < (NC < kMaxSums ? NC : kMaxSums); ++s) {
           if (s < nsum) {
@@ -106,8 +107,8 @@ __device__ __forceinline__ void scan_private_body(const ScanParams& p, const Pri
     uint32_t f = kNoRow;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      c += cnt[s * kBlock + lane + 64 * j];
-      f = min(f, fst[s * kBlock + lane + 64 * j]);
+      c += cf[2 * (s * kBlock + lane + 64 * j)];
+      f = min(f, cf[2 * (s * kBlock + lane + 64 * j) + 1]);
     }
     c = wave_sum_u64(c);
     f = wave_min_u32(f);
