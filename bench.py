@@ -544,7 +544,8 @@ def main(argv=None):
             # private mode: the scan reads the columns' compact resident copies
             **({'resident_columns': 'compact copies: integer columns as offsets from their minimum in the '
                                     'fewest bytes holding their range, float64 columns that are only summed as '
-                                    'their exact int32 codes (%d B per row read)' % round(bytes_per_launch / max(rows, 1))}
+                                    'their exact integer codes (offsets from the smallest code in 1-2 bytes when '
+                                    'they span < 2^16, else int32): %d B per row read' % round(bytes_per_launch / max(rows, 1))}
                if mode == 0 and dev.get_option('compact') else {}),
             **cfg_extra,
         },
