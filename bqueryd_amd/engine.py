@@ -545,7 +545,7 @@ class ShardTable:
         plans = self.__dict__.setdefault('_plans', OrderedDict())
         hit = plans.get(key) if cacheable else None
         if hit is not None:
-            return hit[:3]
+            return hit[:3] + hit[4:]
         groupby_cols = list(groupby_cols)
         for c in groupby_cols:
             self.slot(c)
@@ -555,13 +555,16 @@ class ShardTable:
             raise ValueError('duplicate output column names: %s' % names)
         keep = []
         q = self._query(groupby_cols, [(o[0], o[2]) for o in ops], where_terms, mask, keep)
+        # key columns whose device values (codes, ticks) map back to another dtype
+        logical = [c for c in groupby_cols
+                   if self.dtypes.get(c) is not None and (is_string(self.dtypes[c]) or is_time(self.dtypes[c]))]
         if cacheable:
             if len(plans) >= 64:
                 plans.popitem(last=False)
-            plans[key] = (names, ops, q, keep)
+            plans[key] = (names, ops, q, keep, logical)
         else:
             self.__dict__['_last_plan_keep'] = keep  # the struct's arrays live until the next query
-        return names, ops, q
+        return names, ops, q, logical
 
     def _parse_aggs(self, agg_list):
         ops = parse_agg_list(self.dtypes, agg_list)
@@ -572,12 +575,12 @@ class ShardTable:
 
     def groupby(self, groupby_cols, agg_list, where_terms=None, mask=None):
         """bquery ``ctable.groupby`` semantics; returns (OrderedDict of columns, filtered)."""
-        names, ops, q = self._plan(groupby_cols, agg_list, where_terms, mask)
+        names, ops, q, logical = self._plan(groupby_cols, agg_list, where_terms, mask)
         res = ctypes.c_void_p()
         self.dev.check(self._lib.bqg_groupby(self.dev.handle, self.handle, ctypes.byref(q),
                                              ctypes.byref(res)))
         out, filtered = _result_to_columns(self.dev, res, names)
-        for k in list(groupby_cols):
+        for k in logical:
             out[k] = self._to_logical(k, out[k])
         for (in_col, out_col, op, dt) in ops:
             if out[out_col].dtype != dt:
