@@ -16,6 +16,37 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_private(ScanParams p, Privat
 
 __device__ void private_finish_body(const FinishParams& f, const SlotArrays& sa, const EmitParams& e, int tid);
 
+// emit_slot (device.h) restricted to what an inline private emit can hold: dense integer keys
+// (no hash mode, no float keys) and sum / count / mean (distinct counts and std take the
+// generic path) -- a fraction of the general function's code on the finish kernel's one
+// pass through it
+__device__ __forceinline__ void emit_slot_private(const EmitParams& e, uint64_t code, unsigned int rank,
+                                                  const SlotTotals& t) {
+  for (int j = 0; j < e.ncols; ++j) {
+    const EmitCol& c = e.cols[j];
+    uint64_t bits;
+    if (c.kind == 0) {
+      const DevKey& k = e.keys[c.key];
+      bits = (uint64_t)k.min + (code / k.stride) % k.range;
+    } else if (c.op == BQG_COUNT) {
+      bits = t.cnt;
+    } else {
+      const unsigned long long a = t.acc[c.state];
+      const double dec = e.sum_dec[c.state];
+      if (c.op == BQG_MEAN) {
+        const double sv = c.in_float ? (dec != 0.0 ? (double)(long long)a / dec : as_f64(a))
+                                     : (c.in_dtype == BQG_U64 ? (double)(uint64_t)a : (double)(long long)a);
+        bits = as_u64(sv / (double)t.cnt);
+      } else {  // SUM
+        bits = a;
+        if (c.in_float && dec != 0.0) bits = as_u64((double)(long long)a / dec);
+        if (c.in_float && c.out_dtype == BQG_F32) bits = (uint64_t)__float_as_uint((float)as_f64(bits));
+      }
+    }
+    store_elem(c.out, c.out_dtype, rank, bits);
+  }
+}
+
 // ONE workgroup: every (component, slot) pair's per-workgroup partials are reduced by one wave
 // (lane-strided reads in a fixed order, then a fixed shuffle tree: bitwise deterministic) into
 // LDS, and wave 0 runs the finish step -- no grid of reduce workgroups, no device-scope
@@ -132,7 +163,7 @@ __device__ void private_finish_body(const FinishParams& f, const SlotArrays& sa,
         t.acc[q] = (q < nsum) ? tot[(2 + q) * S + s] : 0ull;
         t.acc2[q] = 0ull;
       }
-      emit_slot(e, (uint64_t)s, (uint64_t)s, rank, t);
+      emit_slot_private(e, (uint64_t)s, rank, t);
     }
   }
   if (tid == 0) {
