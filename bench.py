@@ -6,10 +6,19 @@ emit back to host memory) over one synthetic taxi-shaped shard already resident 
 Default workload = BASELINE.json configs[1] (C2): 100 M rows, groupby ``payment_type``,
 sum/mean/count of ``fare_amount`` where ``passenger_count >= 2``.
 
-Multi-GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``): one
-process per GPU, each owns its own 100 M-row shard (weak scaling: shards are independent in
-bqueryd, there is no data-path collective without ``aggregate=True``); barrier + max over
-ranks around the timed region, gloo used only for that bookkeeping.
+The headline scans the columns as stored (engine option ``compact=0``), so
+``roofline.algorithmic_bytes_per_launch`` is SURVEY.md §8(d)'s figure (columns x itemsize x
+rows) and ``frac`` is a bandwidth; the compact resident copies are reported in the
+line's ``compact`` sub-record with their build cost and the query count that repays it.
+
+Multi-GPU: one process per GPU, launched by ``python -m torch.distributed.run
+--nproc-per-node N bench.py --gpus N`` or, with ``--gpus N`` and no ``WORLD_SIZE`` in the
+environment, by this script itself (N rank processes started before anything touches a GPU;
+``--dry-launch`` prints them).  Each rank owns its own 100 M-row shard (weak scaling: shards are
+independent in bqueryd, no data-path collective without ``aggregate=True``); barrier + max over
+ranks around the timed region, gloo only for that bookkeeping.  The line's ``c5`` sub-record is
+north_star's scaling config at the same N: 10 shards x 12.5 M rows per rank, aggregated in one
+pass per rank, then the ``aggregate=True`` merge across the N ranks over RCCL (rpc.py:164-173).
 
 Prints ONE JSON line (rank 0).
 """
@@ -353,9 +362,226 @@ def _c5_local_ranks(args):
     print(json.dumps(line), flush=True)
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(('127.0.0.1', 0))
+        return sk.getsockname()[1]
+
+
+def launch_plan(n, argv):
+    """(command, environment additions) of each of the ``n`` rank processes ``--gpus n``
+    starts when no launcher did (rank r on GPU r, rendezvous on 127.0.0.1)."""
+    port = _free_port()
+    cmd = [sys.executable, os.path.abspath(__file__)] + [a for a in argv if a != '--dry-launch']
+    return [(cmd, {'WORLD_SIZE': str(n), 'RANK': str(r), 'LOCAL_RANK': str(r), 'LOCAL_WORLD_SIZE': str(n),
+                   'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)}) for r in range(n)]
+
+
+def _launch_ranks(n, argv, dry):
+    """Start the N rank processes (before this process touches a GPU) and wait for them; rank
+    0's stdout is this process's, the others' is discarded.  Exit status: the first failing
+    rank's, else 0."""
+    import subprocess
+    plan = launch_plan(n, argv)
+    if dry:
+        print(json.dumps({'launch': 'self', 'ranks': n, 'commands': [c for c, _ in plan], 'env': [e for _, e in plan]}),
+              flush=True)
+        return 0
+    procs = []
+    for r, (cmd, extra) in enumerate(plan):
+        procs.append(subprocess.Popen(cmd, env=dict(os.environ, **extra),
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+class _Watchdog:
+    """Ends this rank if a sub-benchmark hangs (an RCCL collective that never completes):
+    after ``seconds`` it calls ``on_timeout`` (rank 0 prints the line it has, the hung part
+    marked) and exits the process."""
+
+    def __init__(self, seconds, on_timeout):
+        import threading
+        self.done = threading.Event()
+        self.t = threading.Thread(target=self._run, args=(seconds, on_timeout), daemon=True)
+        self.t.start()
+
+    def _run(self, seconds, on_timeout):
+        if not self.done.wait(seconds):
+            try:
+                on_timeout()
+            finally:
+                sys.stdout.flush()
+                os._exit(0)
+
+    def cancel(self):
+        self.done.set()
+
+
+def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
+    """C5 on this node's ranks (north_star's scaling config): 10 shards x 12.5 M rows per rank
+    (80 shards at 8 ranks), each rank's shards aggregated in one pass over their union, then
+    the aggregate=True merge (hash partition, RCCL exchange over xGMI, reduce, gather to rank 0)
+    at world ``ws``.  A step is the rank's shard pass + the merge; ``ms_per_step`` is the max
+    over ranks.  Returns the record on rank 0 (None elsewhere)."""
+    from bqueryd_amd import dist as bdist
+    from bqueryd_amd import synth
+    from bqueryd_amd.engine import ShardTable
+
+    cfg = synth.CONFIGS['c5']
+    per_rank = max(1, cfg['shards'] // 8)
+    shard_rows = shard_rows or cfg['rows'] // cfg['shards']
+    rows = per_rank * shard_rows
+    t_gen = time.perf_counter()
+    from concurrent.futures import ThreadPoolExecutor
+
+    def make(i):
+        return synth.taxi_shard(shard_rows, config_id=5, n_shards=max(cfg['shards'], ws * per_rank),
+                                shard=rank * per_rank + i, variant=args.variant, columns=synth.query_columns(cfg))
+    tables = []
+    with ThreadPoolExecutor(8) as ex:  # numpy's generators release the GIL
+        for sc in ex.map(make, range(per_rank)):
+            tables.append(ShardTable(sc, device=dev))
+            del sc
+    gen_s = time.perf_counter() - t_gen
+    with _stdout_to_stderr():  # librccl prints a banner on stdout at init
+        uid = comm.broadcast_bytes(bdist.new_unique_id() if rank == 0 else None)
+        rccl = bdist.RcclComm(dev, rank, ws, uid)
+    colo = bdist.ColocatedShards(tables)
+    colo.union(synth.query_columns(cfg))  # the rank's shard set, resident once (like the load)
+    probe, _ = colo.groupby_tables(cfg['groupby'], cfg['aggs'])
+    dtypes = {n: np.dtype(probe[0].dtypes[n]) for n in probe[0].names}
+    for p_ in probe:
+        p_.close()
+    phase, timings = [], []
+
+    def step():
+        t0 = time.perf_counter()
+        per, reduced = colo.groupby_tables(cfg['groupby'], cfg['aggs'])
+        timings.append(dev.last_timing())
+        t1 = time.perf_counter()
+        merged = bdist.merge_partials_device(per, cfg['groupby'], cfg['aggs'], dtypes, rccl, reduced=reduced)
+        for p_ in per:
+            p_.close()
+        phase.append((t1 - t0, time.perf_counter() - t1))
+        return merged
+
+    for _ in range(warmup):
+        out = step()
+    ok = None
+    if rank == 0 and out is not None:
+        ok = int(out['n'].sum()) == ws * rows  # every scanned row counted once, across the ranks
+    # timed steps without device timing (with it, the merge waits for each phase's device work)
+    dev.enable_timing(False)
+    del phase[:], timings[:]
+    comm.barrier()
+    dev.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dev.synchronize()
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = comm.max(t1 - t0)
+    shard_ms = comm.max(1e3 * float(np.mean([p[0] for p in phase])))
+    merge_ms = comm.max(1e3 * float(np.mean([p[1] for p in phase])))
+    # the shard pass's scan kernels: HIP events over a few more (untimed) steps
+    dev.enable_timing(True, scan_only=True)
+    del timings[:]
+    for _ in range(3):
+        step()
+    dev.synchronize()
+    scan_ms = comm.max(float(np.mean([t['scan_ms'] for t in timings])))
+    dev.enable_timing(False)
+    rccl.close()
+    colo.close()
+    for t in tables:
+        t.close()
+    if rank != 0:
+        return None
+    alg = timings[-1]['bytes']
+    return {
+        'workload': ('C5: %d ranks x %d shards x %d rows = %d rows, groupby %s, aggs %s, one pass over each rank\'s '
+                     'shards + the aggregate=True merge across the ranks over RCCL (bqg_merge_host at world %d)'
+                     % (ws, per_rank, shard_rows, ws * rows, cfg['groupby'], [a[1] for a in cfg['aggs']], ws)),
+        'value': ws * rows * steps / elapsed,
+        'unit': 'rows/s',
+        'n_gpus': ws,
+        'rows_per_gpu': rows,
+        'ms_per_step': elapsed / steps * 1e3,
+        'shard_pass_ms_max_over_ranks': shard_ms,
+        'merge_ms_max_over_ranks': merge_ms,
+        'scan_kernel_ms_max_over_ranks': scan_ms,
+        'roofline_frac_of_the_shard_pass': alg / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        'merged_row_count_check': ok,
+        'scaling': 'weak',
+        'data_gen_s': gen_s,
+        'note': 'the driver\'s N = 1, 2, 4, 8 runs give the curve: north_star asks value(8) >= 6 x value(1)',
+    }
+
+
+def _compact_record(dev, table, step, timings, steps, warmup, full_ms, full_scan_ms):
+    """The compact resident copies on the same shard and query: their build on
+    the first query that reads them (device time), the steady step and scan over them, the HBM
+    they add, and how many queries repay the build."""
+    table.drop_compact()
+    base_bytes = table.device_bytes()
+    dev.set_option('compact', 1)
+    try:
+        dev.enable_timing(True)
+        dev.synchronize()
+        t0 = time.perf_counter()
+        step()
+        dev.synchronize()
+        first_ms = 1e3 * (time.perf_counter() - t0)
+        first = timings[-1]
+        copy_bytes = table.device_bytes() - base_bytes
+        if copy_bytes <= 0:
+            return {'built': False, 'note': 'no column of this query has a narrower resident form'}
+        for _ in range(warmup):
+            step()
+        dev.enable_timing(True, scan_only=True)
+        del timings[:]
+        dev.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        dev.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        scan = float(np.mean([t['scan_ms'] for t in timings]))
+        last = timings[-1]
+    finally:
+        dev.set_option('compact', 0)
+        table.drop_compact()
+    gain = full_ms - ms
+    return {
+        'built': True,
+        'what': 'integer columns as offsets from their minimum in the fewest bytes holding their range, float64 '
+                'columns that are only summed as their exact integer codes (1-2 byte offsets when they span < 2^16)',
+        'ms_per_step': ms,
+        'rows_per_s': last['rows'] / (ms * 1e-3),
+        'scan_kernel_ms': scan,
+        'bytes_read_per_launch': last['bytes_read'],
+        'read_gbs': last['bytes_read'] / (scan * 1e-3) / 1e9,
+        'read_frac_of_peak': last['bytes_read'] / (scan * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        'build_device_ms': first['compact_ms'],
+        'first_query_ms': first_ms,
+        'first_query_device_ms': first['total_ms'],
+        'hbm_bytes_added': copy_bytes,
+        'break_even_queries': (first['compact_ms'] / gain) if gain > 0 else None,
+        'vs_full_width_step': full_ms / ms if ms > 0 else None,
+        'vs_full_width_scan': full_scan_ms / scan if scan > 0 else None,
+        'note': 'not the headline: the copies are a derived cache built by the first query that reads them '
+                '(its device time is build_device_ms); the headline scans the columns as stored',
+    }
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None, help='ranks (default: WORLD_SIZE, else 1)')
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5'])
@@ -364,15 +590,31 @@ def main(argv=None):
                     help='C5: one groupby per shard + local re-group instead of one pass over the rank\'s shards')
     ap.add_argument('--rows', type=int, default=None, help='override rows per shard')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-c5', action='store_true', help='leave out the c5 sub-record')
+    ap.add_argument('--no-compact-record', action='store_true',
+                    help='leave out the compact sub-record (profiler runs: its scans share the kernel name)')
+    ap.add_argument('--compact', action='store_true',
+                    help='time the compact resident copies as the headline (not §8(d)-consistent; profiling)')
     ap.add_argument('--variant', default='exact', choices=['exact', 'raw', 'wide'])
     ap.add_argument('--local-ranks', type=int, default=1,
                     help='C5: the full 80-shard workload over this many ranks as contexts on one GPU')
+    ap.add_argument('--dry-launch', action='store_true', help='print the rank processes --gpus N would start')
+    ap.add_argument('--c5-timeout', type=float, default=300.0, help='seconds before a hung c5 sub-record is abandoned')
     args = ap.parse_args(argv)
     if args.config == 'c5' and args.local_ranks > 1:
         return _c5_local_ranks(args)
+    if 'WORLD_SIZE' not in os.environ and (args.gpus or 1) > 1:
+        return _launch_ranks(args.gpus, argv, args.dry_launch)
+    if args.dry_launch:
+        print(json.dumps({'launch': 'none', 'ranks': int(os.environ.get('WORLD_SIZE', '1'))}), flush=True)
+        return 0
 
     ws, rank, local = _dist_env()
     comm = _Comm(ws)
+    seen = int(round(comm.sum(1)))
+    if seen != ws or (args.gpus is not None and args.gpus != ws):
+        comm.close()
+        raise SystemExit('bench.py --gpus %s: %d ranks joined, WORLD_SIZE %d' % (args.gpus, seen, ws))
 
     from bqueryd_amd import synth
     from bqueryd_amd.engine import Device, ShardTable
@@ -380,75 +622,42 @@ def main(argv=None):
     cfg = synth.CONFIGS[args.config]
     # BQGPU_BENCH_DEVICE pins every rank to one GPU (rehearsing the multi-rank path on a one-GPU box)
     dev = Device(int(os.environ.get('BQGPU_BENCH_DEVICE', local)))
-    npass_expected = None
-    table = None  # the single-shard configs' table
-    timings = []
-    phase = []  # C5: (shard queries s, merge s) per step
+    if not args.compact:
+        dev.set_option('compact', 0)  # the headline scans the columns as stored (SURVEY §8d bytes)
     if args.config == 'c5':
-        # 80 shards over 8 GPUs: 10 shards of 12.5 M rows per rank (weak scaling), per-shard
-        # groupby + the cross-rank aggregate=True merge (RCCL all-to-all) in every step
-        from bqueryd_amd import dist as bdist
-        per_rank = max(1, cfg['shards'] // 8)
-        shard_rows = args.rows or cfg['rows'] // cfg['shards']
-        rows = per_rank * shard_rows
-        tables = []
-        for i in range(per_rank):
-            sc = synth.taxi_shard(shard_rows, config_id=5, n_shards=max(cfg['shards'], ws * per_rank),
-                                  shard=rank * per_rank + i, variant=args.variant,
-                                  columns=synth.query_columns(cfg))
-            tables.append(ShardTable(sc, device=dev))
-        # RCCL communicator inside libbqgpu (the exchange runs on device buffers); gloo only
-        # hands rank 0's unique id to the other ranks
-        # (librccl prints a version banner on stdout at init: kept off the one-JSON-line stdout)
-        with _stdout_to_stderr():
-            uid = comm.broadcast_bytes(bdist.new_unique_id() if rank == 0 else None)
-            rccl = bdist.RcclComm(dev, rank, ws, uid)
-        colo = bdist.ColocatedShards(tables)
-        fused = not args.c5_per_shard and bdist.decomposable(cfg['aggs'])
-        if fused:
-            colo.union(synth.query_columns(cfg))  # the rank's shard set, resident once (untimed, like the load)
-        # result dtypes from a probe of the same shape as a step (every launch the same size, so
-        # PMC per-launch averages describe the timed kernel)
-        probe, _ = colo.groupby_tables(cfg['groupby'], cfg['aggs'])
-        dtypes = {n: np.dtype(probe[0].dtypes[n]) for n in probe[0].names}
-        for p_ in probe:
-            p_.close()
+        rec = _c5_ranks(args, comm, dev, ws, rank, args.steps, args.warmup,
+                        shard_rows=args.rows)
+        comm.close()
+        if rank == 0:
+            line = {'metric': 'groupby rows/sec (whole node) + achieved HBM GB/s vs peak, 1/2/4/8 GPUs',
+                    'value': rec['value'], 'unit': 'rows/s', 'n_gpus': ws, 'steps': args.steps,
+                    'warmup': args.warmup, 'ms_per_step': rec['ms_per_step'], 'higher_is_better': True,
+                    'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64',
+                    'data': 'synthetic taxi-shaped shards (SURVEY.md §8d generator, %s variant), resident in HBM'
+                            % args.variant,
+                    'config': {'workload': rec['workload'], 'rows_per_gpu': rec['rows_per_gpu'],
+                               'parallelism': 'shard-per-rank x%d + RCCL merge' % ws},
+                    'roofline': None, 'cpu_baseline': None, 'c5': rec}
+            print(json.dumps(line), flush=True)
+        return 0
 
-        def step():
-            # results stay in HBM; the merge (hash partition, RCCL all-to-all, reduce, gather
-            # to rank 0) runs on device buffers.  Fused: the rank's shards in one pass
-            # (sum / count are decomposable); per-shard: one groupby per shard + local re-group
-            t0 = time.perf_counter()
-            if fused:
-                per, reduced = colo.groupby_tables(cfg['groupby'], cfg['aggs'])
-                timings.append(dev.last_timing())
-            else:
-                per, reduced = [], False
-                for t in tables:
-                    per.append(t.groupby_table(cfg['groupby'], cfg['aggs']))
-                    timings.append(dev.last_timing())
-            t1 = time.perf_counter()
-            merged = bdist.merge_partials_device(per, cfg['groupby'], cfg['aggs'], dtypes, rccl, reduced=reduced)
-            for p in per:
-                p.close()
-            phase.append((t1 - t0, time.perf_counter() - t1))
-            return merged
-    else:
-        rows = args.rows or cfg['rows']
-        # --sorted: C4's second variant, rows ordered by (pu_location_id, passenger_count)
-        # (SURVEY.md §8d), the row order sorted_count_distinct is meant for
-        sort_by = ['pu_location_id', 'passenger_count'] if (args.sorted and args.config == 'c4') else None
-        cols = synth.taxi_shard(rows, config_id=synth.CONFIG_ID[args.config], n_shards=max(ws, 1),
-                                shard=rank, variant=args.variant, columns=synth.query_columns(cfg),
-                                sort_by=sort_by)
-        table = ShardTable(cols, device=dev)
-        if cfg['where']:
-            npass_expected = int(np.count_nonzero(cols['passenger_count'] >= 2))
+    npass_expected = None
+    rows = args.rows or cfg['rows']
+    # --sorted: C4's second variant, rows ordered by (pu_location_id, passenger_count)
+    # (SURVEY.md §8d), the row order sorted_count_distinct is meant for
+    sort_by = ['pu_location_id', 'passenger_count'] if (args.sorted and args.config == 'c4') else None
+    cols = synth.taxi_shard(rows, config_id=synth.CONFIG_ID[args.config], n_shards=max(ws, 1),
+                            shard=rank, variant=args.variant, columns=synth.query_columns(cfg),
+                            sort_by=sort_by)
+    table = ShardTable(cols, device=dev)
+    if cfg['where']:
+        npass_expected = int(np.count_nonzero(cols['passenger_count'] >= 2))
+    timings = []
 
-        def step():
-            out, _ = table.groupby(cfg['groupby'], cfg['aggs'], where_terms=cfg['where'])
-            timings.append(dev.last_timing())
-            return out
+    def step():
+        out, _ = table.groupby(cfg['groupby'], cfg['aggs'], where_terms=cfg['where'])
+        timings.append(dev.last_timing())
+        return out
 
     for _ in range(args.warmup):
         out = step()
@@ -462,7 +671,6 @@ def main(argv=None):
     # the scan launches (scan_only: the whole-query events are recorded after the timed steps)
     dev.enable_timing(True, scan_only=True)
     del timings[:]
-    del phase[:]
     comm.barrier()
     dev.synchronize()
     t0 = time.perf_counter()
@@ -477,44 +685,33 @@ def main(argv=None):
     value = total_rows / elapsed
 
     # whole-query device time (first launch to result), from extra untimed steps
-    n_timed, n_phase = len(timings), len(phase)
+    n_timed = len(timings)
     dev.enable_timing(True)
     for _ in range(min(args.steps, 10)):
         step()
     dev.synchronize()
     device_avg = float(np.mean([t['total_ms'] for t in timings[n_timed:]])) if len(timings) > n_timed else float('nan')
     del timings[n_timed:]
-    del phase[n_phase:]
     scan_avg = float(np.mean([t['scan_ms'] for t in timings])) if timings else float('nan')
     bytes_per_launch = timings[-1]['bytes'] if timings else 0
+    read_per_launch = timings[-1]['bytes_read'] if timings else 0
     mode = timings[-1]['mode'] if timings else 0
-    # the query columns at their full widths (what a scan of the columns as stored reads): the
-    # compact resident copies read fewer bytes for the same rows
-    full_width = None
-    if table is not None:
-        full_width = rows * sum(np.dtype(table.dtypes[c]).itemsize for c in synth.query_columns(cfg))
     achieved = bytes_per_launch / (scan_avg * 1e-3) / 1e9 if scan_avg > 0 else 0.0
 
+    compact = None
+    if rank == 0 and not args.compact and not args.no_compact_record and mode in (0, 1, 2, 5):
+        compact = _compact_record(dev, table, step, timings, args.steps, args.warmup, ms_per_step, scan_avg)
     cpu = None
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.config != 'c5':
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         rate, secs = _cpu_baseline(cols, cfg)
         single = {'value': rate, 'unit': 'rows/s', 'cores': 1,
                   'sample': 'one %d-row %s shard, one worker (best of 2: %.2f s)' % (rows, args.config.upper(), secs)}
-        del cols
         cpu = _cpu_cluster_baseline(cfg, args, rows, single)
-    traffic, traffic_source = _load_traffic(args.config, rows)
-    comm.close()
-    if rank != 0:
-        return
-    if phase:
-        cfg_extra = {'shard_queries_ms_per_step': 1e3 * float(np.mean([p[0] for p in phase])),
-                     'merge_ms_per_step': 1e3 * float(np.mean([p[1] for p in phase])),
-                     'merge': 'libbqgpu bqg_merge: results in HBM, hash-partitioned, exchanged over RCCL (world %d), reduced, gathered to rank 0' % ws,
-                     'shard_pass': ('fused: the rank\'s shards aggregated in one pass (sum / count are '
-                                    'decomposable; dist.ColocatedShards)' if fused else
-                                    'per-shard groupby + local re-group')}
-    else:
-        cfg_extra = {}
+    del cols
+    table.close()
+    traffic, traffic_source = _load_traffic(args.config if not args.compact else args.config + '_compact', rows)
+    dev.enable_timing(False)
+
     line = {
         'metric': 'groupby rows/sec (whole node) + achieved HBM GB/s vs peak, 1/2/4/8 GPUs',
         'value': value,
@@ -529,25 +726,16 @@ def main(argv=None):
         'dtype': 'f64',
         'data': 'synthetic taxi-shaped shards (SURVEY.md §8d generator, %s variant), resident in HBM' % args.variant,
         'config': {
-            'workload': '%s: %d rows per GPU (%s), groupby %s, aggs %s, where %s%s' % (
-                args.config.upper(), rows,
-                '%d shards x %d rows' % (rows // (args.rows or cfg['rows'] // cfg['shards']), args.rows or cfg['rows'] // cfg['shards'])
-                if args.config == 'c5' else '1 shard', cfg['groupby'], [a[1] for a in cfg['aggs']], cfg['where'],
-                ', aggregate=True merge across ranks (RCCL all-to-all)' if args.config == 'c5' else
-                (', rows sorted by (pu_location_id, passenger_count)' if (args.sorted and args.config == 'c4')
-                 else '')),
+            'workload': '%s: %d rows per GPU (1 shard), groupby %s, aggs %s, where %s%s' % (
+                args.config.upper(), rows, cfg['groupby'], [a[1] for a in cfg['aggs']], cfg['where'],
+                ', rows sorted by (pu_location_id, passenger_count)' if (args.sorted and args.config == 'c4') else ''),
             'rows_per_gpu': rows,
             'parallelism': 'shard-per-rank x%d' % ws,
             'engine_mode': MODES[mode or 0],
-            # partitioned mode: summed values carried as exact 32-bit integer codes
+            'resident_columns': ('compact copies (--compact; not the §8(d) headline)' if args.compact else
+                                 'as stored (engine option compact=0): the scan reads every query column at its '
+                                 'stored width'),
             **({'narrow_entries': bool(timings[-1].get('narrow'))} if timings and mode == 4 else {}),
-            # private mode: the scan reads the columns' compact resident copies
-            **({'resident_columns': 'compact copies: integer columns as offsets from their minimum in the '
-                                    'fewest bytes holding their range, float64 columns that are only summed as '
-                                    'their exact integer codes (offsets from the smallest code in 1-2 bytes when '
-                                    'they span < 2^16, else int32): %d B per row read' % round(bytes_per_launch / max(rows, 1))}
-               if mode == 0 and dev.get_option('compact') else {}),
-            **cfg_extra,
         },
         'roofline': {
             'bound': 'hbm',
@@ -560,17 +748,33 @@ def main(argv=None):
             'kernel': KERNELS[mode or 0],
             'kernel_avg_ms': scan_avg,
             'algorithmic_bytes_per_launch': bytes_per_launch,
+            'algorithmic_bytes_definition': 'SURVEY.md §8(d): the distinct columns the query reads x their stored '
+                                            'itemsize x rows + the output table (G x columns x 8 B)',
+            'bytes_read_per_launch': read_per_launch,
             'device_ms_per_query': device_avg,
-            **({'full_width_bytes_per_launch': full_width,
-                'full_width_equivalent_gbs': full_width / (scan_avg * 1e-3) / 1e9,
-                'full_width_note': 'the query columns at their stored widths over the same kernel time: the '
-                                   'compact copies\' effect, not a bandwidth (frac uses the bytes read)'}
-               if full_width and bytes_per_launch and full_width > bytes_per_launch * 1.05 and scan_avg > 0 else {}),
         },
         'cpu_baseline': cpu,
+        'compact': compact,
+        'c5': None,
     }
+    if not args.no_c5:
+        def on_timeout():
+            if rank == 0:
+                line['c5'] = {'error': 'did not finish within %.0f s (abandoned; the rest of the line stands)'
+                                       % args.c5_timeout}
+                print(json.dumps(line), flush=True)
+        wd = _Watchdog(args.c5_timeout, on_timeout)
+        try:
+            line['c5'] = _c5_ranks(args, comm, dev, ws, rank, min(args.steps, 10), min(args.warmup, 3))
+        except Exception as e:  # the headline stands; the sub-record says what failed
+            line['c5'] = {'error': '%s: %s' % (type(e).__name__, e)}
+        wd.cancel()
+    comm.close()
+    if rank != 0:
+        return 0
     print(json.dumps(line), flush=True)
+    return 0
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

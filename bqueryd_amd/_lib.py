@@ -29,7 +29,7 @@ T_FALSE, T_TRUE, T_EQ, T_NE, T_IN, T_NIN, T_GT, T_GE, T_LT, T_LE = -1, 0, 1, 2, 
 
 E_INVALID, E_UNSUPPORTED, E_HIP, E_OOM, E_STATE = -1, -2, -3, -4, -5
 UNIQUE_ID_BYTES = 128
-ABI_VERSION = 7
+ABI_VERSION = 8
 OPTIONS = ('jit', 'jit_min_rows', 'partition', 'part_wbits', 'part_k', 'part_threads', 'part_per_cu',
            'part_splits', 'part_narrow', 'fused_scd', 'scd_compact', 'scd_pack16', 'priv_ahead',
            'private_per_cu', 'small_emit', 'hash_slots', 'distinct_slots', 'part_pack', 'scd_runs', 'part_win', 'compact')
@@ -61,7 +61,8 @@ class Timing(ctypes.Structure):
     _fields_ = [('scan_ms', ctypes.c_double), ('scan_launches', ctypes.c_int32),
                 ('total_ms', ctypes.c_double), ('rows', ctypes.c_int64),
                 ('bytes', ctypes.c_int64), ('mode', ctypes.c_int32), ('specialized', ctypes.c_int32),
-                ('narrow', ctypes.c_int32), ('regrows', ctypes.c_int32)]
+                ('narrow', ctypes.c_int32), ('regrows', ctypes.c_int32),
+                ('bytes_read', ctypes.c_int64), ('compact_ms', ctypes.c_double)]
 
 
 # enum bqg_decode
@@ -122,6 +123,9 @@ _PROTOS = {
     'bqg_select_rows_table': ([_P, _P, ctypes.POINTER(Query), _I32, _P, ctypes.POINTER(_P)],
                               ctypes.c_int),
     'bqg_table_nrows': ([_P, ctypes.POINTER(_I64)], ctypes.c_int),
+    'bqg_table_device_bytes': ([_P, ctypes.POINTER(_I64)], ctypes.c_int),
+    'bqg_table_build_compact': ([_P, _I32, _P, ctypes.POINTER(_I32)], ctypes.c_int),
+    'bqg_table_drop_compact': ([_P], ctypes.c_int),
     'bqg_table_ncols': ([_P, ctypes.POINTER(_I32)], ctypes.c_int),
     'bqg_table_dtype': ([_P, _I32, ctypes.POINTER(_I32)], ctypes.c_int),
     'bqg_comm_unique_id': ([_P], ctypes.c_int),

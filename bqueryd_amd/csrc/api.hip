@@ -381,6 +381,7 @@ struct bqg_ctx {
   ColumnPool colpool;
   IngestPool ingest;  // cold-path staging: streams + pinned double buffers per decode thread
   int cu = 256;
+  size_t max_lds = 160 * 1024;  // LDS one gfx950 workgroup may take (the CU's 160 KiB; MI355X_MICROARCH.md)
   int64_t jit_min_rows() const { return opt[kOptJitMinRows]; }
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
@@ -393,6 +394,7 @@ struct bqg_ctx {
   // scratch
   DevBuf partials, counter, hdr, slots, terms, outcols, lists, bitmap, prefix, cdbuf, scdbuf, mask, misc, done;
   DevBuf strings;  // bqg_encode_bytes: the staged bytes and the dictionary's work arrays
+  DevBuf nfbuf;    // the nonfinite pass's per-slot rows and counts
   HostBuf hhdr, hout;
   // pinned blocks for results (returned by bqg_result_free); shared with outstanding results
   // so a result may outlive its context
@@ -404,12 +406,49 @@ struct bqg_ctx {
   // timing
   int timing = 0;  // 1: query window and scan window events, 2: the scan window only
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // timing level 1: the first and last compact-copy build of the current query
+  hipEvent_t ev_sh[2] = {nullptr, nullptr};
+  bool sh_timed = false;
   bqg_timing last{};
+  // the context's live tables: an allocation that fails releases their compact copies (a
+  // derived, rebuildable cache) and retries before it reports OOM
+  std::vector<bqg_table*> tables;
 };
 
 namespace {
 
 void set_stream_device(bqg_ctx* c) { HIPCHECK(hipSetDevice(c->device)); }
+
+// Release every compact resident copy of one table (their memory back to the pool); they are
+// rebuilt by the next query that reads them.  Returns whether any was held.
+bool drop_shadows(bqg_ctx* c, bqg_table* t) {
+  bool any = false;
+  for (Column& col : t->cols) {
+    if (!col.shadow.dev) continue;
+    c->colpool.put(col.shadow.dev, col.shadow.bytes);
+    col.shadow = Shadow{};
+    any = true;
+  }
+  return any;
+}
+
+// Column memory from the pool.  A failed hipMalloc leaves its error as the thread's last HIP
+// error: it is cleared here (an expected failure must not fail the next launch check), and
+// before giving up the compact copies of every table of the context are released -- they are
+// a rebuildable cache, the base columns are not.
+void* col_alloc(bqg_ctx* c, size_t need, size_t* cap, bool may_drop_shadows = true) {
+  void* p = c->colpool.get(need, cap);
+  if (p) return p;
+  (void)hipGetLastError();
+  if (!may_drop_shadows) return nullptr;
+  bool any = false;
+  for (bqg_table* t : c->tables) any |= drop_shadows(c, t);
+  if (!any) return nullptr;
+  c->colpool.release();  // hipFree synchronises: the released copies are no longer read
+  p = c->colpool.get(need, cap);
+  if (!p) (void)hipGetLastError();
+  return p;
+}
 
 template <typename F>
 int guard(bqg_ctx* ctx, F&& f) {
@@ -558,8 +597,13 @@ struct Plan {
   int32_t agg_state[kMaxAggs];
   int wbits = 12;
   bool has_filter = false;
-  int64_t alg_bytes = 0;
+  int64_t alg_bytes = 0;       // the query's distinct columns at their stored widths
+  int64_t read_bytes = 0;      // what the scan reads of them (compact copies: fewer)
   bool dummy_col = false;      // the one scan column of a plan that reads none (not in alg_bytes)
+  // mean / std states whose float column holds NaN or infinities (column statistics): bquery's
+  // row-order update turns such a group's mean into NaN unless its only non-finite value is its
+  // last row, which the extra nonfinite pass decides per slot
+  int nf_states = 0;           // bit q: sum state q needs it
 };
 
 int scan_col(Plan& pl, int tc) {
@@ -685,6 +729,14 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
       if (q->aggs[a].op != BQG_COUNT) sc.push_back(q->aggs[a].col);
     compute_stats_many(t, sc);
   }
+  // mean / std of a float column holding NaN or an infinity: the nonfinite pass decides those
+  // groups' values the way bquery's row-order update does
+  for (int a = 0; a < q->n_aggs; ++a) {
+    const bqg_agg& g = q->aggs[a];
+    if ((g.op != BQG_MEAN && g.op != BQG_STD) || !dtype_is_float(t->cols[g.col].dtype)) continue;
+    const ColStats& cs = t->cols[g.col].stats;
+    if (cs.has_nan || (!cs.empty && (std::isinf(cs.fmin) || std::isinf(cs.fmax)))) pl.nf_states |= 1 << pl.agg_state[a];
+  }
   // 3. keys
   pl.p.nkeys = q->n_keys;
   bool any_float = false;
@@ -732,6 +784,7 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
           std::find(distinct.begin(), distinct.end(), q->aggs[a].col) == distinct.end())
         distinct.push_back(q->aggs[a].col);
     for (int tc : distinct) pl.alg_bytes += (int64_t)dtype_size(t->cols[tc].dtype) * t->nrows;
+    pl.read_bytes = pl.alg_bytes;
   }
   if (pl.tcol.empty()) {
     // no keys, terms, mask or summed columns (e.g. groupby([], count / count_distinct)): the
@@ -866,16 +919,25 @@ bool ensure_shadow(bqg_ctx* c, bqg_table* t, int tc, int kind) {
   if (sh.bytes < need) {
     c->colpool.put(sh.dev, sh.bytes);
     size_t cap = 0;
-    sh.dev = (unsigned char*)c->colpool.get(need, &cap);
+    // no other table's copy is dropped for this one (a scan being planned may already read it)
+    sh.dev = (unsigned char*)col_alloc(c, need, &cap, false);
     sh.bytes = sh.dev ? cap : 0;
-    if (!sh.dev) return false;  // no room: the scan reads the column itself
+    if (!sh.dev) {  // no room: the scan reads the column itself
+      sh = Shadow{};
+      return false;
+    }
   }
+  if (c->timing == 1 && !c->sh_timed) HIPCHECK(hipEventRecord(c->ev_sh[0], c->stream));
   // zero padding past the last row (the scans' vector loads read it), then the rows
   const size_t used = (size_t)t->nrows * dtype_size(dtype);
   HIPCHECK(hipMemsetAsync(sh.dev + used, 0, sh.bytes - used, c->stream));
   if (enc == 1) launch_shadow_int(DevCol{col.dev, col.dtype, dtype_lg(col.dtype)}, t->nrows, off, sh.dev, dtype_lg(dtype), c->stream);
   else launch_shadow_code((const double*)col.dev, t->nrows, cs.enc, mul, off, sh.dev, dtype_lg(dtype), c->stream);
   HIPCHECK(hipGetLastError());
+  if (c->timing == 1) {
+    HIPCHECK(hipEventRecord(c->ev_sh[1], c->stream));
+    c->sh_timed = true;
+  }
   sh.valid = true;
   sh.dtype = dtype;
   sh.enc = enc;
@@ -912,8 +974,8 @@ ScanParams compact_scan(bqg_ctx* c, bqg_table* t, Plan& pl, EmitParams& e) {
       sp.sum_enc[i] = 0;
       e.sum_dec[i] = col.shadow.mul;
     }
-    // algorithmic bytes: what the scan reads of this column
-    if (!pl.dummy_col) pl.alg_bytes -= ((int64_t)dtype_size(col.dtype) - ((int64_t)1 << sp.cols[i].lg)) * N;
+    // bytes read (the algorithmic bytes keep the stored width)
+    if (!pl.dummy_col) pl.read_bytes -= ((int64_t)dtype_size(col.dtype) - ((int64_t)1 << sp.cols[i].lg)) * N;
     // a key / term column that is not summed works in its copy's own domain (stored = value
     // - off): key minima and scalar term constants shift by -off instead of every row adding
     // off back (an `in` / `nin` list keeps the decode offset; its values stay canonical)
@@ -981,6 +1043,7 @@ void build_emit(bqg_table* t, const bqg_query* q, const Plan& pl, EmitParams& e,
     ec.out_dtype = agg_out_dtype(g.op, in_dt);
     // a mean over an integer column's float64 sum state (plan_query: 64-bit sums that can wrap)
     if (g.op == BQG_MEAN) ec.in_float = pl.p.sum_is_float[pl.agg_state[a]];
+    if (g.op == BQG_MEAN || g.op == BQG_STD) ec.sum_state = pl.agg_state[a];
     if (g.op == BQG_SUM || g.op == BQG_MEAN) ec.state = pl.agg_state[a];
     else if (g.op == BQG_STD) {
       int idx = 0;
@@ -1004,6 +1067,16 @@ int scan_blocks(bqg_ctx* c, int64_t nrows, int per_cu) {
   if (b > tiles) b = tiles;
   if (b < 1) b = 1;
   return (int)b;
+}
+
+// Every planned launch is checked against the device's limits before it is issued: a shape the
+// planner (or an engine option) gets wrong fails the query with BQG_E_INVALID and a message
+// instead of surfacing as a launch failure from hipGetLastError.
+void check_launch(bqg_ctx* c, const char* what, size_t lds, int64_t blocks, int threads = kBlock) {
+  if (lds > c->max_lds)
+    fail(BQG_E_INVALID, "%s: %zu bytes of LDS per workgroup exceed the device's %zu", what, lds, c->max_lds);
+  if (blocks < 1 || blocks > 0x7FFFFFFFll) fail(BQG_E_INVALID, "%s: grid of %lld workgroups", what, (long long)blocks);
+  if (threads < 64 || threads > 1024 || threads % 64) fail(BQG_E_INVALID, "%s: %d threads per workgroup", what, threads);
 }
 
 bqg_result* empty_result(const std::vector<int>& dts, int filtered) {
@@ -1038,7 +1111,7 @@ bqg_result* block_result(bqg_ctx* c, PinnedBlock b, int64_t n, int filtered, con
 void alloc_column(bqg_ctx* c, Column& col, int64_t nrows, bool zero_all) {
   const size_t need = column_bytes(nrows, col.dtype);
   size_t cap = 0;
-  col.dev = (unsigned char*)c->colpool.get(need, &cap);
+  col.dev = (unsigned char*)col_alloc(c, need, &cap);
   if (!col.dev) fail(BQG_E_OOM, "device allocation of a column (%zu bytes) failed", need);
   col.bytes = cap;
   const size_t used = zero_all ? 0 : (size_t)nrows * dtype_size(col.dtype);
@@ -1067,6 +1140,7 @@ void table_from_device(bqg_ctx* c, const std::vector<int>& dts, const std::vecto
     if (n > 0) HIPCHECK(hipMemcpyAsync(t->cols[j].dev, src[j], (size_t)n * dtype_size(dts[j]), hipMemcpyDeviceToDevice, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   undo.t = nullptr;
+  c->tables.push_back(t.get());
   *c->dev_target = t.release();
 }
 
@@ -1084,8 +1158,32 @@ void table_from_host_result(bqg_ctx* c, bqg_result* r) {
   *c->dev_target = t;
 }
 
+// After the query's last synchronisation: the byte counts of the last call (algorithmic and
+// read, each + the G x ncols output) and, with timing on, its HIP-event times
+void finish_query(bqg_ctx* c, const Plan& pl, int64_t G, int ncols) {
+  const int64_t out = G * (int64_t)ncols * 8;
+  c->last.bytes = pl.alg_bytes + out;
+  c->last.bytes_read = pl.read_bytes + out;
+  c->last.compact_ms = NAN;
+  if (!c->timing) return;
+  float ms = 0;
+  HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+  c->last.scan_ms = ms;
+  c->last.total_ms = NAN;
+  if (c->timing == 1) {
+    HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
+    c->last.total_ms = ms;
+    c->last.compact_ms = 0.0;
+    if (c->sh_timed) {
+      HIPCHECK(hipEventElapsedTime(&ms, c->ev_sh[0], c->ev_sh[1]));
+      c->last.compact_ms = ms;
+    }
+  }
+}
+
 // Runs the passes of one groupby; returns the device output columns through `res`.
 void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out) {
+  c->sh_timed = false;
   Plan pl;
   plan_query(c, t, q, pl);
   EmitParams e;
@@ -1122,7 +1220,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   bool distinct_ops = false;
   for (int a = 0; a < q->n_aggs; ++a)
     if (q->aggs[a].op == BQG_COUNT_DISTINCT || q->aggs[a].op == BQG_SORTED_COUNT_DISTINCT) distinct_ops = true;
-  const bool need_generic = distinct_ops || !pl.std_cols.empty() || pl.mode != kPrivate;
+  const bool need_generic = distinct_ops || !pl.std_cols.empty() || pl.mode != kPrivate || pl.nf_states != 0;
 
   const uint64_t S = pl.nslots;
   const int nsum = pl.nsum;
@@ -1226,6 +1324,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       if (ahead) extra = std::string("#define BQ_PRIV_AHEAD ") + std::to_string(ahead) + "\n";
       jfn = jit_function_for("bq_jit_scan_private", sp, extra);
     }
+    check_launch(c, "private scan", L.lds_bytes, L.blocks);
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
     if (jfn) {
       void* args[] = {(void*)&sp, (void*)&L};
@@ -1247,18 +1346,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       std::vector<const void*> src;
       for (int j = 0; j < e.ncols; ++j) src.push_back(e.cols[j].out);
       table_from_device(c, out_dt, src, (int64_t)hh[0]);
-      if (c->timing) {
-        float ms = 0;
-        HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
-        c->last.scan_ms = ms;
-        c->last.scan_launches = 1;
-        c->last.total_ms = NAN;
-        if (c->timing == 1) {
-          HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
-          c->last.total_ms = ms;
-        }
-      }
-      c->last.bytes = pl.alg_bytes + (int64_t)hh[0] * (int64_t)e.ncols * 8;
+      finish_query(c, pl, (int64_t)hh[0], e.ncols);
       return;
     }
     if (!need_generic) {
@@ -1269,18 +1357,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       std::vector<size_t> offs;
       for (int j = 0; j < e.ncols; ++j) offs.push_back(64 + (size_t)j * S * 8);
       bqg_result* r = block_result(c, hblk.release(), (int64_t)G, pl.has_filter && (int64_t)total < N, out_dt, offs);
-      if (c->timing) {
-        float ms = 0;
-        HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
-        c->last.scan_ms = ms;
-        c->last.scan_launches = 1;
-        c->last.total_ms = NAN;
-        if (c->timing == 1) {
-          HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
-          c->last.total_ms = ms;
-        }
-      }
-      c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
+      finish_query(c, pl, (int64_t)G, e.ncols);
       *out = r;
       return;
     }
@@ -1299,6 +1376,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     if (pl.mode == kShared) {
       const size_t lds = (size_t)S * (8 + 8 * (size_t)nsum);
       int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
+      check_launch(c, "shared scan", lds, scan_blocks(c, N, std::max(per_cu, 1)));
       launch_scan_shared(sp, sa, scan_blocks(c, N, std::max(per_cu, 1)), lds, st);
     } else if (pl.mode == kPartitioned) {
       PartLaunch L{};
@@ -1438,6 +1516,9 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         if (pk) ff = jit_function_for("bq_jit_part_first_rows", pl.p, extra);
         c->last.specialized = fs ? 1 : 0;
       }
+      check_launch(c, "partitioned scatter", part_scatter_lds(L.nparts, L.threads, nsum, L.k, nw, pk), L.blocks, L.threads);
+      check_launch(c, "partitioned aggregate", part_agg_lds_launch(L.wbits, nsum, pk, L.win),
+                   (int64_t)L.nparts * L.splits, 1024);
       launch_partitioned(pl.p, sa, L, st, fs, ff);
     } else {
       launch_scan_global(sp, sa, scan_blocks(c, N, 8), st);
@@ -1529,6 +1610,32 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         launch_scan_global(q2, sa2, scan_blocks(c, N, 8), st);
       }
     }
+    HIPCHECK(hipGetLastError());
+  }
+
+  // ---- nonfinite pass: mean / std of float columns holding NaN or infinities
+  if (pl.nf_states) {
+    int nst = 0;
+    for (int q = 0; q < nsum; ++q) nst += (pl.nf_states >> q) & 1;
+    const size_t words = (size_t)S * (1 + 2 * (size_t)nst);
+    uint32_t* nb = (uint32_t*)c->nfbuf.ensure(words * 4 + 256);
+    HIPCHECK(hipMemsetAsync(nb, 0, words * 4, st));
+    NonfiniteLaunch nf{};
+    nf.states = pl.nf_states;
+    nf.lds = S <= kNonfiniteLdsSlots ? 1 : 0;
+    nf.last_row = nb;
+    e.nf_last = nb;
+    int k = 0;
+    for (int q = 0; q < nsum; ++q) {
+      if (!((pl.nf_states >> q) & 1)) continue;
+      nf.cnt[q] = nb + (size_t)S * (1 + 2 * k);
+      nf.row[q] = nf.cnt[q] + S;
+      e.nf_cnt[q] = nf.cnt[q];
+      e.nf_row[q] = nf.row[q];
+      e.nf_col[q] = pl.p.cols[q];
+      ++k;
+    }
+    launch_nonfinite(pl.p, sa, nf, scan_blocks(c, N, 8), st);
     HIPCHECK(hipGetLastError());
   }
 
@@ -1712,7 +1819,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
           Column& k2 = t->cols[tc2];
           if (!ensure_shadow(c, t, tc2, 1)) continue;
           pc.p.cols[ci] = DevCol{k2.shadow.dev, k2.shadow.dtype, dtype_lg(k2.shadow.dtype), 1, 0, k2.shadow.off};
-          if (!pl.dummy_col) pl.alg_bytes -= ((int64_t)dtype_size(k2.dtype) - (int64_t)dtype_size(k2.shadow.dtype)) * N;
+          if (!pl.dummy_col) pl.read_bytes -= ((int64_t)dtype_size(k2.dtype) - (int64_t)dtype_size(k2.shadow.dtype)) * N;
         }
       }
       hipFunction_t sfn = nullptr;
@@ -1766,17 +1873,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     HIPCHECK(hipStreamSynchronize(st));
     const int64_t G = (int64_t)hh[0];
     const int filtered = pl.has_filter && (int64_t)hh[1] < N;
-    if (c->timing) {
-      float ms = 0;
-      HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
-      c->last.scan_ms = ms;
-      c->last.total_ms = NAN;
-      if (c->timing == 1) {
-        HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
-        c->last.total_ms = ms;
-      }
-    }
-    c->last.bytes = pl.alg_bytes + G * (int64_t)e.ncols * 8;
+    finish_query(c, pl, (int64_t)G, e.ncols);
     if (G == 0) {
       *out = empty_result(out_dt, filtered);  // the guard returns the block
     } else if (c->dev_target) {
@@ -1844,17 +1941,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     std::vector<const void*> src;
     for (int j = 0; j < e.ncols; ++j) src.push_back(e.cols[j].out);
     table_from_device(c, out_dt, src, (int64_t)G);
-    if (c->timing) {
-      float ms = 0;
-      HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
-      c->last.scan_ms = ms;
-      c->last.total_ms = NAN;
-      if (c->timing == 1) {
-        HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
-        c->last.total_ms = ms;
-      }
-    }
-    c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
+    finish_query(c, pl, (int64_t)G, e.ncols);
     return;
   }
   BlockGuard blk;
@@ -1871,17 +1958,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     }
   }
   bqg_result* r = block_result(c, blk.release(), G, pl.has_filter && (int64_t)total < N, out_dt, offs);
-  if (c->timing) {
-    float ms = 0;
-    HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
-    c->last.scan_ms = ms;
-    c->last.total_ms = NAN;
-    if (c->timing == 1) {
-      HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
-      c->last.total_ms = ms;
-    }
-  }
-  c->last.bytes = pl.alg_bytes + (int64_t)G * (int64_t)e.ncols * 8;
+  finish_query(c, pl, (int64_t)G, e.ncols);
   *out = r;
 }
 
@@ -2037,6 +2114,7 @@ int bqg_create(int device_ordinal, bqg_ctx** out) {
     }
     // timing-only events: no system-scope fence (cache writeback) at each record
     for (int i = 0; i < 4; ++i) HIPCHECK(hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence));
+    for (int i = 0; i < 2; ++i) HIPCHECK(hipEventCreateWithFlags(&c->ev_sh[i], hipEventDisableSystemFence));
     // last-workgroup-done counters of the finish kernels (each reset by its last workgroup)
     HIPCHECK(hipMemset(c->done.ensure(256), 0, 256));
     *out = c;
@@ -2054,7 +2132,7 @@ int bqg_destroy(bqg_ctx* c) {
   int rc = guard(c, [&] {
     HIPCHECK(hipStreamSynchronize(c->stream));
     for (DevBuf* b : {&c->partials, &c->counter, &c->hdr, &c->slots, &c->terms, &c->outcols, &c->lists,
-                      &c->bitmap, &c->prefix, &c->cdbuf, &c->scdbuf, &c->mask, &c->misc, &c->done})
+                      &c->bitmap, &c->prefix, &c->cdbuf, &c->scdbuf, &c->mask, &c->misc, &c->done, &c->strings, &c->nfbuf})
       b->release();
     c->hhdr.release();
     c->hout.release();
@@ -2066,6 +2144,8 @@ int bqg_destroy(bqg_ctx* c) {
     }
     for (int i = 0; i < 4; ++i)
       if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    for (int i = 0; i < 2; ++i)
+      if (c->ev_sh[i]) (void)hipEventDestroy(c->ev_sh[i]);
     if (c->own) (void)hipStreamDestroy(c->own);
   });
   delete c;
@@ -2120,6 +2200,7 @@ int bqg_table_create(bqg_ctx* c, int64_t nrows, int32_t ncols, const int32_t* dt
       (void)slot;
     }
     for (Column& col : t->cols) alloc_column(c, col, nrows, true);
+    c->tables.push_back(t);
     *out = t;
   });
   if (rc != BQG_OK && t) {
@@ -2138,8 +2219,42 @@ int bqg_table_destroy(bqg_table* t) {
       t->ctx->colpool.put(col.shadow.dev, col.shadow.bytes);
     }
   });
+  auto& v = t->ctx->tables;
+  v.erase(std::remove(v.begin(), v.end(), t), v.end());
   delete t;
   return rc;
+}
+
+int bqg_table_device_bytes(bqg_table* t, int64_t* bytes) {
+  if (!t || !bytes) return BQG_E_INVALID;
+  return guard(t->ctx, [&] {
+    int64_t b = 0;
+    for (const Column& col : t->cols) b += (int64_t)col.bytes + (int64_t)col.shadow.bytes;
+    *bytes = b;
+  });
+}
+
+int bqg_table_build_compact(bqg_table* t, int32_t n, const int32_t* cols, int32_t* built) {
+  if (!t) return BQG_E_INVALID;
+  return guard(t->ctx, [&] {
+    if (n < 0 || (n && !cols)) fail(BQG_E_INVALID, "bad column list");
+    int32_t k = 0;
+    for (int i = 0; i < n; ++i) {
+      if (cols[i] < 0 || cols[i] >= (int)t->cols.size()) fail(BQG_E_INVALID, "column %d out of range", cols[i]);
+      // an integer column's narrow offsets, else a float64 column's exact codes
+      if (ensure_shadow(t->ctx, t, cols[i], 1) || ensure_shadow(t->ctx, t, cols[i], 2)) ++k;
+    }
+    HIPCHECK(hipStreamSynchronize(t->ctx->stream));
+    if (built) *built = k;
+  });
+}
+
+int bqg_table_drop_compact(bqg_table* t) {
+  if (!t) return BQG_E_INVALID;
+  return guard(t->ctx, [&] {
+    HIPCHECK(hipStreamSynchronize(t->ctx->stream));
+    drop_shadows(t->ctx, t);
+  });
 }
 
 int bqg_table_add_column(bqg_table* t, int32_t dtype, int32_t* slot_out) {
@@ -2548,6 +2663,16 @@ int bqg_encode_bytes(bqg_ctx* c, bqg_table* t, int32_t out_col, const void* byte
                  o_slot = o_first + al(cap * 4), o_bits = o_slot + al((size_t)n * 4),
                  o_wp = o_bits + al(nwords * 4 + 4), o_bs = o_wp + al(nwords * 4 + 4),
                  o_cnt = o_bs + al(nblocks * 4 + 4), o_vals = o_cnt + 256, total = o_vals + al((size_t)n * width);
+    // the staging (raw bytes, table, per-row slots, values: ~2 x n x width) is released when
+    // the call returns, however it returns -- a 100 M-row 'U8' column would otherwise keep
+    // 7 GB of HBM for the context's lifetime
+    struct Release {
+      bqg_ctx* c;
+      ~Release() {
+        (void)hipStreamSynchronize(c->stream);
+        c->strings.release();
+      }
+    } release{c};
     unsigned char* b = (unsigned char*)c->strings.ensure(total);
     hipStream_t st = c->stream;
     HIPCHECK(hipMemcpyAsync(b + o_data, bytes, (size_t)n * width,

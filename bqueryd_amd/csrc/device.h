@@ -372,13 +372,18 @@ __device__ __forceinline__ uint64_t hash_slot(const SlotArrays& sa, uint64_t mas
   return kEmpty;
 }
 
-// key value of column `kc` at `row` (a slot's representative row), canonical
-__device__ __forceinline__ uint64_t key_at_row(const DevCol& kc, bool is_float, uint32_t row) {
+// canonical value of column `kc` at `row` (floats: float64 bits)
+__device__ __forceinline__ uint64_t value_at_row(const DevCol& kc, uint32_t row) {
   Chunk c;
   row_word_to_chunk(c, kc, row, load_row_word(kc, row));
   uint64_t v[1];
   decode<1>(c, kc.dtype, v);
-  return key_identity(v[0], is_float);
+  return v[0];
+}
+
+// key value of column `kc` at `row` (a slot's representative row), canonical
+__device__ __forceinline__ uint64_t key_at_row(const DevCol& kc, bool is_float, uint32_t row) {
+  return key_identity(value_at_row(kc, row), is_float);
 }
 
 // Slot of row r's key: hash modes 1 (packed code stored in the table) and 2 (wide keys: the
@@ -490,10 +495,25 @@ __device__ __forceinline__ void emit_slot(const EmitParams& e, uint64_t slot, ui
           const double s = c.in_float ? (e.sum_dec[c.state] != 0.0 ? (double)(long long)a / e.sum_dec[c.state] : as_f64(a))
                                       : (c.in_dtype == BQG_U64 ? (double)(uint64_t)a : (double)(long long)a);
           bits = as_u64(s / (double)t.cnt);
+          if (e.nf_cnt[c.sum_state]) {
+            // bquery's m += (x - m) / c: an infinity stays only as the group's last row and its
+            // one non-finite value (the next row makes inf - inf); NaN otherwise
+            const uint32_t k = e.nf_cnt[c.sum_state][slot];
+            if (k) {
+              double m = __builtin_nan("");
+              if (k == 1 && e.nf_row[c.sum_state][slot] == e.nf_last[slot]) {
+                const double x = as_f64(value_at_row(e.nf_col[c.sum_state], e.nf_row[c.sum_state][slot]));
+                if (__builtin_isinf(x)) m = x;
+              }
+              bits = as_u64(m);
+            }
+          }
         } break;
         case BQG_STD: {
           const double m2 = as_f64(t.acc2[c.state]);
           bits = as_u64(t.cnt ? sqrt(m2 / (double)t.cnt) : __builtin_nan(""));
+          // Welford: d * (x - mean) is inf * (inf - inf) at the first non-finite value
+          if (e.nf_cnt[c.sum_state] && e.nf_cnt[c.sum_state][slot]) bits = as_u64(__builtin_nan(""));
         } break;
         case BQG_COUNT_DISTINCT: bits = e.cd[c.state][slot]; break;
         case BQG_SORTED_COUNT_DISTINCT: {

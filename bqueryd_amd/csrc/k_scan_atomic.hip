@@ -139,6 +139,69 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_global(ScanParams p, SlotArr
   }
 }
 
+// The nonfinite pass (kernels.h NonfiniteLaunch): the same rows, terms and slots as pass 1;
+// per slot the last passing row (an LDS table per workgroup when the slot space is small, one
+// atomicMax per slot at the end), per checked sum state the count and last row of its
+// non-finite values (rare: global atomics).
+template <int NC, bool HASH>
+__global__ __launch_bounds__(kBlock) void k_nonfinite(ScanParams p, SlotArrays sa, NonfiniteLaunch nf) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint32_t* slast = reinterpret_cast<uint32_t*>(smem);
+  const int tid = threadIdx.x;
+  const uint64_t hmask = p.nslots - 1;
+  if (nf.lds) {
+    for (uint64_t i = tid; i < p.nslots; i += kBlock) slast[i] = 0;
+    __syncthreads();
+  }
+  const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
+    Chunk raw[NC];
+    load_rows4<NC>(p, row0, raw);
+    uint64_t v[NC][4];
+    decode_all<NC, 4>(p, raw, v);
+    const uint32_t pass = vals_pass<NC, 4>(p, row0, v);
+    uint64_t code[4];
+    vals_code<NC, 4>(p, v, code);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (!(pass & (1u << r))) continue;
+      uint64_t s = code[r];
+      const uint32_t row = (uint32_t)(row0 + r);
+      if (HASH) {
+        s = slot_lookup<NC, 4>(p, sa, hmask, v, code, r, row, false);
+        if (s == kEmpty) continue;
+      }
+      if (nf.lds) atomicMax(&slast[s], row);
+      else if (nf.last_row[s] < row) atomicMax(&nf.last_row[s], row);
+#pragma unroll
+      for (int q = 0; q < (NC < kMaxSums ? NC : kMaxSums); ++q) {
+        if (!((nf.states >> q) & 1)) continue;
+        const double x = value_f64(v[q][r], p.sum_conv[q]);
+        if (!__builtin_isfinite(x)) {
+          atomicAdd(&nf.cnt[q][s], 1u);
+          atomicMax(&nf.row[q][s], row);
+        }
+      }
+    }
+  }
+  if (nf.lds) {
+    __syncthreads();
+    for (uint64_t i = tid; i < p.nslots; i += kBlock)
+      if (slast[i]) atomicMax(&nf.last_row[i], slast[i]);
+  }
+}
+
+void launch_nonfinite(const ScanParams& p, const SlotArrays& s, const NonfiniteLaunch& nf, int blocks,
+                      hipStream_t st) {
+  const size_t lds = nf.lds ? (size_t)p.nslots * 4 : 0;
+  if (p.hash) {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_nonfinite<NC, true>), dim3(blocks), dim3(kBlock), lds, st, p, s, nf));
+  } else {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_nonfinite<NC, false>), dim3(blocks), dim3(kBlock), lds, st, p, s, nf));
+  }
+}
+
 __global__ void k_init_slots(SlotArrays sa, int nsum, uint64_t nslots) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * blockDim.x) {
     sa.cnt[i] = 0;

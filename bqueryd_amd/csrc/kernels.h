@@ -14,7 +14,7 @@ struct EmitCol {
   int32_t key;        // key index (keys)
   int32_t in_float;   // aggregation input column is float
   int32_t in_dtype;   // aggregation input dtype
-  int32_t pad;
+  int32_t sum_state;  // MEAN / STD: the sum-state index of the input column (nonfinite pass)
   void* out;          // device output array (capacity >= groups)
 };
 
@@ -31,6 +31,14 @@ struct EmitParams {
   const unsigned long long* scd_changes[kMaxAggs];
   const unsigned long long* scd_first[kMaxAggs]; // first value bits per slot
   double sum_dec[kMaxSums];  // != 0: sum state q holds int64 codes, value = code / sum_dec[q]
+  // nonfinite pass (a mean / std over a float column holding NaN or infinities): per slot the
+  // last passing row, and per such sum state q its non-finite values' count and last row; the
+  // value column is read at that row (bquery's row-order mean keeps an infinity only when it is
+  // the group's one non-finite value and its last row)
+  const uint32_t* nf_last;
+  const uint32_t* nf_cnt[kMaxSums];
+  const uint32_t* nf_row[kMaxSums];
+  DevCol nf_col[kMaxSums];
 };
 
 // Private-LDS mode (small dense slot spaces): the scan writes per-workgroup partials, the
@@ -63,6 +71,22 @@ void launch_scan_shared(const ScanParams& p, const SlotArrays& s, int blocks, si
                         hipStream_t st);
 void launch_scan_global(const ScanParams& p, const SlotArrays& s, int blocks, hipStream_t st);
 void launch_init_slots(const SlotArrays& s, int nsum, uint64_t nslots, hipStream_t st);
+
+// The nonfinite pass (EmitParams::nf_*): one scan over the rows with the query's terms and key
+// coding (hash modes look the slot up in pass 1's table), recording per slot the last passing
+// row and, for each sum state in `states`, the count and last row of its non-finite values.
+// Arrays zeroed by the caller.  lds: slot space small enough for a per-workgroup LDS table of
+// last rows (flushed with one atomicMax per slot).
+constexpr uint64_t kNonfiniteLdsSlots = 16384;
+struct NonfiniteLaunch {
+  int32_t states;           // bit q: sum state q (ScanParams::cols[q]) is checked
+  int32_t lds;
+  uint32_t* last_row;       // [nslots]
+  uint32_t* cnt[kMaxSums];  // [nslots] per checked state
+  uint32_t* row[kMaxSums];  // [nslots] per checked state
+};
+void launch_nonfinite(const ScanParams& p, const SlotArrays& s, const NonfiniteLaunch& nf, int blocks,
+                      hipStream_t st);
 
 // count_distinct: pair (slot, value-code) set; bitmap when bitmap != nullptr, else hash set
 struct DistinctLaunch {

@@ -246,7 +246,7 @@ class ColocatedShards:
     def resident_bytes(self):
         """HBM held by the union (0 when none is built)."""
         u = self._union
-        return 0 if u is None else sum(u.nrows * dt.itemsize for dt in u.dtypes.values())
+        return 0 if u is None or not getattr(u, 'handle', None) else u.device_bytes()
 
     def close(self):
         if self._union is not None:

@@ -56,7 +56,8 @@ class Device:
         t = L.Timing()
         self.check(self._lib.bqg_last_timing(self.handle, ctypes.byref(t)))
         return {'scan_ms': t.scan_ms, 'scan_launches': t.scan_launches, 'total_ms': t.total_ms,
-                'rows': t.rows, 'bytes': t.bytes, 'mode': t.mode, 'specialized': bool(t.specialized),
+                'rows': t.rows, 'bytes': t.bytes, 'bytes_read': t.bytes_read, 'compact_ms': t.compact_ms,
+                'mode': t.mode, 'specialized': bool(t.specialized),
                 'narrow': bool(t.narrow), 'pack16': t.narrow == 2, 'regrows': t.regrows}
 
     def set_option(self, name, value):
@@ -329,6 +330,9 @@ class ShardTable:
 
     def _touch(self):
         self.__dict__['_version'] = self.version + 1
+        # cached plans hold where-terms on string columns as dictionary codes: new data means a
+        # new dictionary, so every plan is rebuilt
+        self.__dict__.pop('_plans', None)
 
     def _logical(self, col):
         s = self.slot(col)
@@ -412,6 +416,25 @@ class ShardTable:
 
     def sync(self):
         self.dev.check(self._lib.bqg_table_sync(self.handle))
+
+    def device_bytes(self):
+        """HBM this table holds: its column allocations plus their compact resident copies."""
+        b = ctypes.c_int64()
+        self.dev.check(self._lib.bqg_table_device_bytes(self.handle, ctypes.byref(b)))
+        return b.value
+
+    def build_compact(self, cols=None):
+        """Build the compact resident copies of ``cols`` (default: every column)
+        now rather than on the first query that reads them; returns how many were built."""
+        cols = list(self.names if cols is None else cols)
+        arr = (ctypes.c_int32 * max(1, len(cols)))(*[self.slot(c) for c in cols])
+        built = ctypes.c_int32()
+        self.dev.check(self._lib.bqg_table_build_compact(self.handle, len(cols), arr, ctypes.byref(built)))
+        return built.value
+
+    def drop_compact(self):
+        """Release the table's compact resident copies (rebuilt on demand)."""
+        self.dev.check(self._lib.bqg_table_drop_compact(self.handle))
 
     def add_column(self, name, dtype):
         s = ctypes.c_int32()

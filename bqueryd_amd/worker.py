@@ -91,8 +91,10 @@ class ShardCache:
         return ct
 
     def _resident(self, ct):
+        # what the table holds in HBM, its compact resident copies included (a copy is built by
+        # the first query that reads it)
         t = ct._table
-        return 0 if t is None else sum(t.nrows * dt.itemsize for dt in t.dtypes.values())
+        return 0 if t is None or not getattr(t, 'handle', None) else t.device_bytes()
 
     def resident_bytes(self):
         return sum(self._resident(c) for c in self._items.values()) + (self.extra.bytes() if self.extra else 0)

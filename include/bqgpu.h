@@ -45,8 +45,12 @@ extern "C" {
 /* ABI history: 5 -- bqg_timing.narrow (exact 32-bit codes on the partitioned path);
  * 6 -- bqg_timing.narrow == 2 (packed entries) and the engine options (bqg_set_option);
  * 7 -- bqg_merge_host / bqg_merge_group_host (merged table straight to host memory),
- *      bqg_encode_bytes (string columns as dictionary codes). */
-#define BQG_ABI_VERSION 7
+ *      bqg_encode_bytes (string columns as dictionary codes);
+ * 8 -- bqg_timing.bytes is always the algorithmic bytes (the query's columns at
+ *      their stored widths) and bqg_timing.bytes_read the bytes the scan actually read (less
+ *      when it read compact resident copies); bqg_table_device_bytes, bqg_table_build_compact,
+ *      bqg_table_drop_compact (the compact copies' HBM, built and released explicitly). */
+#define BQG_ABI_VERSION 8
 
 /* error codes */
 #define BQG_OK 0
@@ -122,7 +126,8 @@ typedef struct {
   int32_t scan_launches;
   double total_ms;       /* all device work of the last call */
   int64_t rows;          /* input rows scanned */
-  int64_t bytes;         /* algorithmic bytes: distinct input columns x itemsize x rows + output */
+  int64_t bytes;         /* algorithmic bytes: distinct input columns x their stored
+                            itemsize x rows + output -- the same whichever copy the scan read */
   int32_t mode;          /* 0 private-LDS, 1 shared-LDS, 2 global dense, 3 global hash,
                             4 partitioned, 5 fused distinct pass (sorted_count_distinct) */
   int32_t specialized;   /* 1: the scan ran a query-specialised (run-time compiled) kernel */
@@ -132,6 +137,10 @@ typedef struct {
   int32_t regrows;       /* times the last query was re-run after its group hash table or
                             count_distinct set filled past half, each time with twice the slots
                             (ABI 6) */
+  int64_t bytes_read;    /* the column bytes the scan read + output (ABI 8): `bytes` unless it
+                            read compact resident copies (option compact), then fewer */
+  double compact_ms;     /* device time of the compact copies this query built on first use
+                            (0 when none was built; timing level 1 only, else NaN) (ABI 8) */
 } bqg_timing;
 
 /* ---------------- lifecycle ---------------- */
@@ -242,6 +251,17 @@ int bqg_table_stats(bqg_table* t, int32_t col, int64_t* imin, int64_t* imax, dou
                     double* fmax, int32_t* has_nan);
 /* Copy rows of a device column back to host memory (or into device memory). */
 int bqg_table_read(bqg_table* t, int32_t col, void* host, int64_t nrows, int64_t row_offset);
+/* HBM held by the table (ABI 8): every column allocation plus its compact resident copy, if
+ * one was built -- what a shard cache's byte budget has to count. */
+int bqg_table_device_bytes(bqg_table* t, int64_t* bytes);
+/* Compact resident copies (option compact) of columns `cols[0..n)` built now
+ * instead of on the first query that reads them: an integer column whose range fits fewer
+ * bytes as its offset from the minimum, a float64 column with exact integer codes as those
+ * codes.  *built (optional) receives the copies built.  A column without a narrower form is
+ * skipped.  bqg_table_drop_compact releases every copy of the table (a cache under memory
+ * pressure; the next query that wants one builds it again). */
+int bqg_table_build_compact(bqg_table* t, int32_t n, const int32_t* cols, int32_t* built);
+int bqg_table_drop_compact(bqg_table* t);
 int bqg_table_nrows(bqg_table* t, int64_t* nrows);
 int bqg_table_ncols(bqg_table* t, int32_t* ncols);
 int bqg_table_dtype(bqg_table* t, int32_t col, int32_t* dtype);

@@ -89,6 +89,31 @@ def test_distinct_counts_of_strings_and_times():
     _run(cols, ['payment_type'], aggs, [('passenger_count', '>', 1)])
 
 
+def test_cached_string_term_after_repush():
+    """A where-term on a string column is planned as a list of dictionary codes and the plan is
+    cached per query text; pushing the column again builds a new dictionary, so the cached plan
+    must not survive it (engine.ShardTable._touch drops the plans)."""
+    rng = np.random.default_rng(4)
+    n = 50_000
+    cols = OrderedDict(s=np.array([b'A', b'B', b'C'], dtype='S1')[rng.integers(0, 3, n)],
+                       v=rng.integers(0, 100, n).astype(np.int64))
+    terms = [('s', '==', 'C')]
+    aggs = [['v', 'sum', 'vs'], ['v', 'count', 'n']]
+    t = ShardTable(cols)
+    try:
+        for _ in range(2):  # the second query runs the cached plan
+            got, _ = t.groupby([], aggs, where_terms=terms)
+            assert_tables_equal(got, bo.handle_work(cols, [], aggs, terms))
+        # new data, different first-appearance order: 'C' gets another dictionary code
+        cols['s'] = np.array([b'C', b'Z', b'A'], dtype='S1')[rng.integers(0, 3, n)]
+        t.push('s', cols['s'])
+        t.sync()
+        got, _ = t.groupby([], aggs, where_terms=terms)
+        assert_tables_equal(got, bo.handle_work(cols, [], aggs, terms))
+    finally:
+        t.close()
+
+
 def test_wide_strings_many_values_and_select_rows():
     """40-byte keys with ~20 K distinct values (a dictionary larger than the first guess of the
     binding), values that differ only in their last byte, and raw-row selection of strings."""

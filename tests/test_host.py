@@ -253,7 +253,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(declared) == set(_lib._PROTOS), set(declared) ^ set(_lib._PROTOS)
-    assert lib.bqg_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.bqg_abi_version() == _lib.ABI_VERSION == 8
 
 
 def test_library_fails_loudly_without_gpu():
@@ -302,8 +302,13 @@ def test_shard_cache_budget_counts_unions():
     budget, unions are dropped first, then the least recently used shards -- and a union built
     over an evicted shard goes with it."""
     class FakeTable:
+        handle = 1
+
         def __init__(self, n):
             self.nrows, self.dtypes = n, OrderedDict(a=np.dtype(np.int64))
+
+        def device_bytes(self):  # HBM held, compact copies included (bqg_table_device_bytes)
+            return self.nrows * 8
 
     class FakeCt:
         def __init__(self, n):
