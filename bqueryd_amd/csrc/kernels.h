@@ -172,7 +172,7 @@ void launch_emit_small(const EmitParams& e, const SlotArrays& s, uint32_t nslots
                        unsigned long long* hdr, hipStream_t st);
 
 // column statistics (min / max / nan) of one column
-constexpr int kStatsMaxBlocks = 1024;
+constexpr int kStatsMaxBlocks = 2048;
 void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, unsigned long long* scratch,
                   hipStream_t st);
 // value runs of one column: rows whose value differs from the row before (out: one counter,
