@@ -328,7 +328,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -356,6 +356,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"scd_runs", 1, 0, 1},                  // fused distinct pass: 256-row steps for clustered keys
     {"part_win", 0, 0, 4096},               // partitioned aggregate: tiles per window (0: auto; 64..4096)
     {"compact", 1, 0, 2},                   // private / shared / dense global scans read compact column copies
+    {"part_first", 0, 0, 2},                // packed partitioned path: rows in tile recorded for 0 auto / 1 no / 2 every tile
 };
 
 static int opt_index(const char* name) {
@@ -1411,7 +1412,9 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       // column whose codes span at most 2^16 values -- {code16, slot_low} per entry
       L.pack = 0;
       uint64_t span16 = 0;
-      if (c->opt[kOptPartPack] && pl.wbits <= 16 && (nsum == 0 || (nsum == 1 && L.narrow))) {
+      // (packed entries key first appearances by 32-bit tile x tile rows: tables below 2^32 - 2^14 rows)
+      if (c->opt[kOptPartPack] && pl.wbits <= 16 && (nsum == 0 || (nsum == 1 && L.narrow)) &&
+          N < (int64_t)0xFFFFFFFFll - 16384) {
         L.pack = 1;
         L.enc_base16 = 0;
         const ColStats& cs = nsum ? t->cols[pl.tcol[0]].stats : ColStats{};
@@ -1499,14 +1502,34 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       L.partial_bytes = ((pk ? ((size_t)1 << L.wbits) * 20 : part_agg_lds(L.wbits, nsum, pk)) + 255) & ~size_t(255);
       const size_t pbytes = (L.splits > 1 || pk) ? (size_t)L.nparts * L.splits * L.partial_bytes : 0;
       const size_t tbytes = pk ? (((size_t)L.nparts << L.wbits) + 255) & ~size_t(255) : 0;
-      unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + mbytes + pbytes + tbytes +
-                                                           (pk ? (size_t)L.ntiles : 0) + 512);
+      // rows in tile (PartLaunch::rit) for the tiles where first appearances fall: on uniform
+      // keys over S slots a slot's first row is ~exponential with mean N / (rows per slot) and
+      // the last first appearance comes near S (ln S + 4) rows (C3: 1 M slots -> the first 18 %
+      // of the rows); those tiles' entries then carry their exact rows into the aggregate and
+      // the first-row pass only re-reads the tiles of slots first seen later (option
+      // part_first: 1 none, 2 every tile)
+      L.rit_tiles = 0;
+      if (pk) {
+        const double S = (double)std::max<uint64_t>(pl.nslots, 2);
+        const double rows = std::min<double>((double)N, S * (std::log(S) + 4.0));
+        L.rit_tiles = c->opt[kOptPartFirst] == 1 ? 0
+                      : c->opt[kOptPartFirst] == 2 ? L.ntiles
+                                                   : std::min<int64_t>(L.ntiles, (int64_t)std::ceil(rows / (double)tr));
+      }
+      const size_t rbytes = pk ? (((size_t)std::max<int64_t>(L.rit_tiles, 1) * (size_t)tr * 2) + 255) & ~size_t(255) : 0;
+      // packed: first tags | tile marks + marked count [ntiles + 64] u32 | marked list [ntiles] u32 | rit
+      const size_t kbytes = pk ? (((size_t)L.ntiles + 64) * 4 + 255) & ~size_t(255) : 0;
+      const size_t lbytes = pk ? ((size_t)L.ntiles * 4 + 255) & ~size_t(255) : 0;
+      unsigned char* eb = (unsigned char*)c->bitmap.ensure(vbytes + mbytes + pbytes + tbytes + kbytes + lbytes + rbytes + 256);
       L.vals = (unsigned long long*)eb;
       L.meta = (uint32_t*)(eb + vbytes);
       L.partial = eb + vbytes + mbytes;
       if (pk) {
         L.first_tag = eb + vbytes + mbytes + pbytes;
-        L.tile_mark = L.first_tag + tbytes;
+        L.tile_mark = (uint32_t*)(L.first_tag + tbytes);
+        L.nmarked = L.tile_mark + L.ntiles;
+        L.marked = (uint32_t*)(L.first_tag + tbytes + kbytes);
+        L.rit = (uint16_t*)(L.first_tag + tbytes + kbytes + lbytes);
       }
       hipFunction_t fs = nullptr, ff = nullptr;
       if (c->opt[kOptJit] && N >= c->jit_min_rows()) {

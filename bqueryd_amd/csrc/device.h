@@ -332,6 +332,28 @@ __device__ __forceinline__ void vals_code(const ScanParams& p, const uint64_t (&
     }
     return;
   }
+  if (p.hash == 0) {
+    // dense slot spaces (< 2^27 slots, integer keys only): every term (v - min) * stride and
+    // their sum are below the slot count, so 32-bit arithmetic gives the exact code -- a third
+    // of the 64-bit sub / mul / add chain per key and row
+    uint32_t c32[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) c32[r] = 0;
+#pragma unroll
+    for (int k = 0; k < BQ_LOOP_BOUND(p.nkeys, kMaxKeys); ++k) {
+      if (k >= p.nkeys) break;
+      const DevKey& key = p.keys[k];
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (key.col == c) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) c32[r] += ((uint32_t)v[c][r] - (uint32_t)key.min) * (uint32_t)key.stride;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) code[r] = c32[r];
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < BQ_LOOP_BOUND(p.nkeys, kMaxKeys); ++k) {
     if (k >= p.nkeys) break;

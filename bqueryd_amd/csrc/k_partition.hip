@@ -44,8 +44,9 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ScanParams p, PartL
 //
 // PACK entries (PartLaunch::pack): one 32-bit word {code16, slot_low}; the slot table is one
 // packed 64-bit accumulator (count << sbits | code16 sum: ONE LDS atomic per entry) and the
-// slot's first tile, and the combine leaves first rows to k_part_first_rows.
-// One split's record of a slot: count, first row (PACK: first tile), sums (PACK: 64-bit count
+// slot's first-appearance key (PartLaunch::rit: the exact first row where the tile recorded its
+// rows, else the first tile), and the combine leaves the rest to k_part_first_rows.
+// One split's record of a slot: count, first row (PACK: first-appearance key), sums (PACK: 64-bit count
 // c64 and the code16 sum a[0]).
 // the exact int64 code of a summed float value of a wide entry (ScanParams::sum_enc)
 __device__ __forceinline__ long long part_sum_code(const ScanParams& p, int q, uint64_t v) {
@@ -80,12 +81,16 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
       f = r.f < f ? r.f : f;
     }
     sa.cnt[gs] = c;
-    sa.fst[gs] = kNoRow;  // k_part_first_rows
-    if (f != kNoRow) {
-      // a few hundred marked tiles take ~1 M marks (random keys): a read first (an L2 hit once
-      // the XCD has seen the line) instead of 1 M contended byte stores
-      if (!L.tile_mark[f]) L.tile_mark[f] = 1;
-      L.first_tag[gs] = (unsigned char)f;
+    // f: the least first-appearance key (PartLaunch::rit): an exact row when its tile recorded
+    // rows in tile, else the first tile's last row -- then k_part_first_rows finds the row
+    const uint32_t ft = f == kNoRow ? kNoRow : f / (uint32_t)L.tile_rows;
+    sa.fst[gs] = (f != kNoRow && (int64_t)ft < L.rit_tiles) ? f : kNoRow;
+    if (f != kNoRow && (int64_t)ft >= L.rit_tiles) {
+      // a few hundred marked tiles take ~1 M marks (random keys without row records): a read
+      // first (an L2 hit once the XCD has seen the line) instead of 1 M contended byte stores
+      // each marked tile joins the first-row pass's list once
+      if (!L.tile_mark[ft] && atomicCAS(&L.tile_mark[ft], 0u, 1u) == 0u) L.marked[atomicAdd(L.nmarked, 1u)] = ft;
+      L.first_tag[gs] = (unsigned char)ft;
     }
     if (nsum) {
       unsigned long long tot = cs + c * (unsigned long long)L.enc_base16;
@@ -138,7 +143,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   constexpr int nsum = NSUM;
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][W] (PACK: [W] packed)
   uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)(PACK ? 1 : nsum) * W);  // [W] (PACK: unused)
-  uint32_t* fst = PACK ? cnt : cnt + W;                                    // [W] first row (PACK: first tile)
+  uint32_t* fst = PACK ? cnt : cnt + W;                                    // [W] first row (PACK: first-appearance key)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = (int)(blockDim.x >> 6);
   for (int i = tid; i < W; i += blockDim.x) {
     if (!PACK) cnt[i] = 0;
@@ -172,9 +177,11 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   // index of its first entry and the segment's entry range
   struct Ent {
     uint4 m[U];
+    uint2 rr[PACK ? U : 1];  // PACK: the granule's 4 rows in tile (tiles below L.rit_tiles)
     uint32_t t[U], e0[U], ab[U];
     unsigned long long v[U][4][NV];
   };
+  const uint32_t rit_tiles = (uint32_t)min(L.rit_tiles, (int64_t)0xFFFFFFFF);
   // PACK: the packed accumulator's fields hold L.pack_flush entries (count < 2^(64 - sbits),
   // code16 sum < 2^sbits); a window holds at most that many entries (4 per granule), and before
   // a window that would pass it the accumulators are flushed (unpacked, added) into the
@@ -307,7 +314,13 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
         en.e0[u] = eb + 4u * fc;
         en.ab[u] = abk;
         en.m[u] = reinterpret_cast<const uint4*>(L.meta)[gidx];
-        if (PACK) continue;
+        if (PACK) {
+          // rows in tile where the tile recorded them; the other lanes re-read word 0 (the
+          // same number of loads on every path: counted waits, no drain)
+          const uint32_t tt = (uint32_t)w0 + (uint32_t)j_next + j;
+          en.rr[u] = reinterpret_cast<const uint2*>(L.rit)[(valid && tt < rit_tiles) ? gidx : 0u];
+          continue;
+        }
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
           if (NARROW) {  // the exact 32-bit codes: float codes signed, integer offsets unsigned
@@ -345,9 +358,13 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
           if (ei < a || ei >= b) continue;            // a neighbouring partition's entry
           const uint32_t sl = mm[e] & lowmask;
           if (PACK) {
-            // fire-and-forget LDS atomics: nothing in the loop waits on the LDS
+            // fire-and-forget LDS atomics: nothing in the loop waits on the LDS; the first-
+            // appearance key is the exact row in a tile with row records, else the tile's last
+            const uint32_t rw = e < 2 ? en.rr[u].x : en.rr[u].y;
+            const uint32_t rit = (e & 1) ? rw >> 16 : rw & 0xFFFFu;
+            const uint32_t key = en.t[u] * TR + (en.t[u] < rit_tiles ? rit : TR - 1u);
             atomicAdd(&acc[sl], inc + (unsigned long long)(mm[e] >> 16));
-            atomicMin(&fst[sl], en.t[u]);
+            atomicMin(&fst[sl], key);
             continue;
           }
           const uint32_t row = en.t[u] * TR + (mm[e] >> L.wbits);
@@ -540,7 +557,7 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
   const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
   const unsigned cgrid = (unsigned)std::min<uint64_t>((p.nslots + 255) / 256, 4096);
   if (L.pack) {
-    (void)hipMemsetAsync(L.tile_mark, 0, (size_t)L.ntiles, st);
+    (void)hipMemsetAsync(L.tile_mark, 0, (size_t)L.ntiles * 4 + 256, st);  // marks + the list's count
 #define BQG_AGGP(NS) hipLaunchKernelGGL((k_part_aggregate<2, 2, NS, true, true>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
     if (p.nsum == 0) BQG_AGGP(0); else BQG_AGGP(1);
 #undef BQG_AGGP
@@ -550,8 +567,9 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
     }
     // grid-stride over 4096-row units of the tiles (the marked ones are mostly a prefix on
     // random keys)
+    // (grid-stride over the marked tiles' units; the list's length is read on the device)
     const int64_t funits = L.ntiles * ((L.tile_rows + kFirstRowsUnit - 1) / kFirstRowsUnit);
-    const unsigned fgrid = (unsigned)std::min<int64_t>(funits, 8192);
+    const unsigned fgrid = (unsigned)std::min<int64_t>(funits, 512);
     if (ffirst) {
       PartLaunch Lc = L;
       ScanParams pc = p;

@@ -225,14 +225,24 @@ struct PartLaunch {
   // per entry; flushed into the split record every pack_flush entries so neither field can
   // overflow), and it
   // marks each slot's first TILE: tile_mark [ntiles] (1 = some slot's first tile, zeroed
-  // before the aggregate) and first_tag [nslots] (its low 8 bits), then k_part_first_rows
-  // re-reads only the marked tiles for the exact first rows
+  // before the aggregate; each marked tile appended once to marked [nmarked]) and first_tag
+  // [nslots] (its low 8 bits), then k_part_first_rows re-reads only the marked tiles for the
+  // exact first rows
   int pack;
   int sbits;
   int64_t pack_flush;  // entries between flushes of the packed accumulators
   int64_t enc_base16;
-  unsigned char* tile_mark;
+  uint32_t* tile_mark;
+  uint32_t* nmarked;  // tile_mark + ntiles (zeroed with it)
+  uint32_t* marked;
   unsigned char* first_tag;
+  // PACK: the tiles [0, rit_tiles) also store each entry's row in the tile (rit [rit_tiles x
+  // tile_rows] u16, at the entry's own position): the aggregate keys a slot's first appearance
+  // by t * tile_rows + rit -- the exact first row of every slot seen in those tiles (where
+  // first appearances fall on random keys) -- and by t * tile_rows + tile_rows - 1 in later
+  // tiles (its first tile only: k_part_first_rows re-reads the tiles marked for such slots)
+  int64_t rit_tiles;
+  uint16_t* rit;
   // splits > 1: [nparts][splits] split tables of partial_bytes each, added by k_part_combine
   unsigned char* partial;
   size_t partial_bytes;      // 2^wbits * (8 + 8 * nsum)
@@ -241,7 +251,8 @@ struct PartLaunch {
 // LDS bytes of a scatter workgroup: the staged tile (values, meta), tile counts (two
 // buffers) / offsets and two sets of scan totals
 inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1, bool narrow = false, bool pack = false) {
-  return (size_t)threads * 4 * k * (4 + (pack ? 0 : (narrow ? 4 : 8) * (size_t)nsum)) + (size_t)nparts * 12 + 2 * 16 * 4;
+  // pack: + the tile's rows in tile (u16) staged beside the entry words
+  return (size_t)threads * 4 * k * (4 + (pack ? 2 : (narrow ? 4 : 8) * (size_t)nsum)) + (size_t)nparts * 12 + 2 * 16 * 4;
 }
 // LDS bytes of an aggregate workgroup's slot table: count + first row + 8-byte sums, or
 // (pack) the packed 8-byte accumulator + first tile

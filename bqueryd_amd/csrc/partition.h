@@ -104,7 +104,8 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   unsigned long long* sval = reinterpret_cast<unsigned long long*>(smem);  // [nsum][TR] (wide)
   uint32_t* sval32 = reinterpret_cast<uint32_t*>(smem);                    // [nsum][TR] (narrow)
   uint32_t* smeta = reinterpret_cast<uint32_t*>(smem) + (PACK ? 0 : (size_t)nsum * TR * (NARROW ? 1 : 2));  // [TR]
-  uint32_t* hist2 = smeta + TR;                                            // [2][P] tile counts
+  uint16_t* srit = reinterpret_cast<uint16_t*>(smeta + TR);                // PACK: [TR] rows in tile
+  uint32_t* hist2 = smeta + TR + (PACK ? TR / 2 : 0);                      // [2][P] tile counts
   uint32_t* toff = hist2 + 2 * P;                                          // [P] tile offsets
   uint32_t* wsum2 = toff + P;                                              // [2][16] scan totals
   for (int i = tid; i < 2 * P; i += T) hist2[i] = 0;
@@ -175,6 +176,8 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
     }
     if (tid == 0) th[P] = (uint16_t)n_tile;
     lds_barrier();
+    // PACK: this tile records its entries' rows in tile (PartLaunch::rit; uniform)
+    const bool with_rit = PACK && base / TR < L.rit_tiles;
     // stage the tile sorted by partition
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -183,7 +186,9 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
       for (int r = 0; r < 4; ++r) {
         if (!(pass[k] & (1u << r))) continue;
         if (PACK) {
-          smeta[toff[part[k][r] >> 16] + (part[k][r] & 0xFFFFu)] = low[k][r];
+          const uint32_t pos = toff[part[k][r] >> 16] + (part[k][r] & 0xFFFFu);
+          smeta[pos] = low[k][r];
+          if (with_rit) srit[pos] = (uint16_t)(rit0 + r);
           continue;
         }
         const uint32_t pos = toff[part[k][r]] + rank[k][r];
@@ -201,6 +206,9 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
 #pragma unroll
     for (int k = 0; k < K; ++k)
       *reinterpret_cast<uint4*>(L.meta + base + 4 * (tid + k * T)) = *reinterpret_cast<const uint4*>(smeta + 4 * (tid + k * T));
+    if (with_rit)
+      for (int i = tid; i < TR / 8; i += T)
+        *reinterpret_cast<uint4*>(L.rit + base + 8 * i) = *reinterpret_cast<const uint4*>(srit + 8 * i);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (PACK || s >= nsum) break;
@@ -233,9 +241,10 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
 // (each slot's first appearance falls early: ~10-15 % of the tiles at C3's 1 M groups); on
 // sorted keys every tile is marked.
 // Work unit: one 4096-row quarter of a tile (kFirstRowsBlock threads x 16 rows, every load of
-// the unit issued before the first is used); the grid strides over the units of the table, and
-// units of unmarked tiles return at once, so the few hundred marked tiles of a random-key query
-// spread over every CU instead of queueing behind one large workgroup each.
+// the unit issued before the first is used); the grid strides over the units of the marked
+// tiles' list, so the marked tiles spread over every CU instead of queueing behind one large
+// workgroup each.  With the rows in tile recorded where first appearances fall
+// (PartLaunch::rit) the list is usually empty and the pass ends at once.
 constexpr int kFirstRowsBlock = 256;
 constexpr int kFirstRowsUnit = kFirstRowsBlock * 16;
 template <int NC>
@@ -246,12 +255,13 @@ __device__ __forceinline__ void part_first_rows_body(const ScanParams& p, const 
   for (int i = 0; i < p.nterms; ++i) need |= 1u << p.terms[i].col;
   const int64_t TR = L.tile_rows;
   const int64_t per_tile = (TR + kFirstRowsUnit - 1) / kFirstRowsUnit;
-  const int64_t units = L.ntiles * per_tile;
+  // the marked tiles' list (k_part_aggregate / k_part_combine append each tile once): empty
+  // when every slot's first row came from the rows in tile (PartLaunch::rit)
+  const int64_t units = (int64_t)*L.nmarked * per_tile;
   for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
-    const int64_t t = u / per_tile;
-    if (!L.tile_mark[t]) continue;
+    const int64_t t = L.marked[u / per_tile];
     const unsigned char tag = (unsigned char)t;
-    const int64_t base = t * TR + (u - t * per_tile) * kFirstRowsUnit;
+    const int64_t base = t * TR + (u % per_tile) * kFirstRowsUnit;
     const int64_t end = min(min(p.nrows, (t + 1) * TR), base + kFirstRowsUnit);
     Chunk raw[4][NC];
 #pragma unroll

@@ -189,6 +189,10 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *                     offsets; exact integer codes of float64 columns that
  *                     are only summed, as 1 / 2-byte offsets when they span
  *                     < 2^16, else int32; 2: int32 codes only)
+ *   part_first     0  packed partitioned path: tiles whose entries also   0 (auto) | 1 none | 2 all
+ *                     record their rows in tile (exact first rows in the
+ *                     aggregate; auto: the tiles where first appearances
+ *                     fall on uniform keys), the rest by the first-row pass
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);

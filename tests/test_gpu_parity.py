@@ -519,6 +519,40 @@ def test_partitioned_window_and_tile_options(part_win, part_k, oracle_c, engine_
     assert_tables_equal(got, ref, exact_cols={'vs'})
 
 
+@pytest.mark.parametrize('order', ['random', 'sorted', 'late'])
+@pytest.mark.parametrize('part_first', [0, 1, 2])
+def test_partitioned_first_rows_recorded(part_first, order, oracle_c, engine_options):
+    """First appearances on the packed path: the tiles below PartLaunch::rit_tiles record each
+    entry's row in tile, so the aggregate keys a slot by its exact first row; slots first seen
+    in later tiles are keyed by their first tile and resolved by the first-row pass.  Option
+    part_first: 0 auto (the tiles where first appearances fall on uniform keys), 1 none (every
+    slot through the pass), 2 every tile (no pass) -- on random keys, keys sorted (first
+    appearances spread over every tile) and keys whose first appearances come late (a block
+    of new keys at the end), with and without a filter; group order must be bquery's."""
+    engine_options(part_first=part_first, jit=1, jit_min_rows=0)
+    rng = np.random.default_rng(40 + part_first)
+    n = 1_200_000
+    k = rng.integers(0, 150_000, n).astype(np.int32)
+    if order == 'sorted':
+        k = np.sort(k)
+    elif order == 'late':
+        k[-50_000:] = rng.integers(150_000, 260_000, 50_000)
+    cols = OrderedDict(k=k, g=rng.integers(1, 3, n).astype(np.int32),
+                       v=np.round(rng.lognormal(2.3, 0.6, n).clip(2.5, 500) * 64) / 64,
+                       f=rng.integers(0, 5, n).astype(np.int8))
+    aggs = [['v', 'sum', 'vs'], ['v', 'count', 'n']]
+    for terms in ([], [('f', '>', 0)]):
+        t = ShardTable(cols)
+        try:
+            got, _ = t.groupby(['k', 'g'], aggs, where_terms=terms)
+            info = t.dev.last_timing()
+        finally:
+            t.close()
+        assert info['mode'] == 4 and info['pack16'], info
+        ref = oracle_c.groupby(cols, ['k', 'g'], aggs, oracle_c.where_terms(cols, terms) if terms else None)
+        assert_tables_equal(got, ref, exact_cols={'vs'})
+
+
 def _groupby_info(cols, keys, aggs, opts=None):
     t = ShardTable(cols)
     try:
