@@ -522,7 +522,7 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
     }
 
 
-def _compact_record(dev, table, step, timings, steps, warmup, full_ms, full_scan_ms):
+def _compact_record(dev, table, step, steps, warmup, full_ms, full_scan_ms):
     """The compact resident copies on the same shard and query: their build on
     the first query that reads them (device time), the steady step and scan over them, the HBM
     they add, and how many queries repay the build."""
@@ -536,22 +536,21 @@ def _compact_record(dev, table, step, timings, steps, warmup, full_ms, full_scan
         step()
         dev.synchronize()
         first_ms = 1e3 * (time.perf_counter() - t0)
-        first = timings[-1]
+        first = dev.last_timing()
         copy_bytes = table.device_bytes() - base_bytes
         if copy_bytes <= 0:
             return {'built': False, 'note': 'no column of this query has a narrower resident form'}
         for _ in range(warmup):
             step()
         dev.enable_timing(True, scan_only=True)
-        del timings[:]
         dev.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         dev.synchronize()
         ms = (time.perf_counter() - t0) / steps * 1e3
-        scan = float(np.mean([t['scan_ms'] for t in timings]))
-        last = timings[-1]
+        last = dev.last_timing()
+        scan = last['scan_ms_sum'] / max(1, last['timed_queries'])
     finally:
         dev.set_option('compact', 0)
         table.drop_compact()
@@ -653,9 +652,14 @@ def main(argv=None):
     if cfg['where']:
         npass_expected = int(np.count_nonzero(cols['passenger_count'] >= 2))
     timings = []
+    g_cols, g_aggs, g_where = cfg['groupby'], cfg['aggs'], cfg['where']
 
     def step():
-        out, _ = table.groupby(cfg['groupby'], cfg['aggs'], where_terms=cfg['where'])
+        # (timed steps: the library sums each query's scan events, read once after the loop)
+        return table.groupby(g_cols, g_aggs, where_terms=g_where)[0]
+
+    def step_t():
+        out = step()
         timings.append(dev.last_timing())
         return out
 
@@ -669,8 +673,7 @@ def main(argv=None):
 
     # device timing of the dominant (scan) kernel: HIP events on the library's stream around
     # the scan launches (scan_only: the whole-query events are recorded after the timed steps)
-    dev.enable_timing(True, scan_only=True)
-    del timings[:]
+    dev.enable_timing(True, scan_only=True)  # (resets the library's running scan-time sum)
     comm.barrier()
     dev.synchronize()
     t0 = time.perf_counter()
@@ -683,24 +686,26 @@ def main(argv=None):
     total_rows = comm.sum(rows * args.steps)
     ms_per_step = elapsed / args.steps * 1e3
     value = total_rows / elapsed
+    last = dev.last_timing()
+    if last['timed_queries'] != args.steps:
+        raise SystemExit('timing: %d scan windows for %d steps' % (last['timed_queries'], args.steps))
+    scan_avg = last['scan_ms_sum'] / last['timed_queries']
+    bytes_per_launch = last['bytes']
+    read_per_launch = last['bytes_read']
+    mode = last['mode']
 
     # whole-query device time (first launch to result), from extra untimed steps
-    n_timed = len(timings)
     dev.enable_timing(True)
+    del timings[:]
     for _ in range(min(args.steps, 10)):
-        step()
+        step_t()
     dev.synchronize()
-    device_avg = float(np.mean([t['total_ms'] for t in timings[n_timed:]])) if len(timings) > n_timed else float('nan')
-    del timings[n_timed:]
-    scan_avg = float(np.mean([t['scan_ms'] for t in timings])) if timings else float('nan')
-    bytes_per_launch = timings[-1]['bytes'] if timings else 0
-    read_per_launch = timings[-1]['bytes_read'] if timings else 0
-    mode = timings[-1]['mode'] if timings else 0
+    device_avg = float(np.mean([t['total_ms'] for t in timings])) if timings else float('nan')
     achieved = bytes_per_launch / (scan_avg * 1e-3) / 1e9 if scan_avg > 0 else 0.0
 
     compact = None
     if rank == 0 and not args.compact and not args.no_compact_record and mode in (0, 1, 2, 5):
-        compact = _compact_record(dev, table, step, timings, args.steps, args.warmup, ms_per_step, scan_avg)
+        compact = _compact_record(dev, table, step, args.steps, args.warmup, ms_per_step, scan_avg)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         rate, secs = _cpu_baseline(cols, cfg)
@@ -735,7 +740,7 @@ def main(argv=None):
             'resident_columns': ('compact copies (--compact; not the §8(d) headline)' if args.compact else
                                  'as stored (engine option compact=0): the scan reads every query column at its '
                                  'stored width'),
-            **({'narrow_entries': bool(timings[-1].get('narrow'))} if timings and mode == 4 else {}),
+            **({'narrow_entries': bool(last.get('narrow'))} if mode == 4 else {}),
         },
         'roofline': {
             'bound': 'hbm',

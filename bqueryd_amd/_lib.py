@@ -62,7 +62,8 @@ class Timing(ctypes.Structure):
                 ('total_ms', ctypes.c_double), ('rows', ctypes.c_int64),
                 ('bytes', ctypes.c_int64), ('mode', ctypes.c_int32), ('specialized', ctypes.c_int32),
                 ('narrow', ctypes.c_int32), ('regrows', ctypes.c_int32),
-                ('bytes_read', ctypes.c_int64), ('compact_ms', ctypes.c_double)]
+                ('bytes_read', ctypes.c_int64), ('compact_ms', ctypes.c_double),
+                ('scan_ms_sum', ctypes.c_double), ('timed_queries', ctypes.c_int64)]
 
 
 # enum bqg_decode

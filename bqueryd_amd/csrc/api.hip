@@ -411,6 +411,8 @@ struct bqg_ctx {
   hipEvent_t ev_sh[2] = {nullptr, nullptr};
   bool sh_timed = false;
   bqg_timing last{};
+  double scan_ms_sum = 0;  // since timing was last enabled
+  int64_t timed_queries = 0;
   // the context's live tables: an allocation that fails releases their compact copies (a
   // derived, rebuildable cache) and retries before it reports OOM
   std::vector<bqg_table*> tables;
@@ -1170,6 +1172,8 @@ void finish_query(bqg_ctx* c, const Plan& pl, int64_t G, int ncols) {
   float ms = 0;
   HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
   c->last.scan_ms = ms;
+  c->scan_ms_sum += ms;
+  ++c->timed_queries;
   c->last.total_ms = NAN;
   if (c->timing == 1) {
     HIPCHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[3]));
@@ -2186,13 +2190,19 @@ int bqg_synchronize(bqg_ctx* c) {
 }
 
 int bqg_enable_timing(bqg_ctx* c, int on) {
-  return guard(c, [&] { c->timing = on == 2 ? 2 : (on != 0 ? 1 : 0); });
+  return guard(c, [&] {
+    c->timing = on == 2 ? 2 : (on != 0 ? 1 : 0);
+    c->scan_ms_sum = 0;
+    c->timed_queries = 0;
+  });
 }
 
 int bqg_last_timing(bqg_ctx* c, bqg_timing* out) {
   return guard(c, [&] {
     *out = c->last;
     out->regrows = c->last_regrows;
+    out->scan_ms_sum = c->scan_ms_sum;
+    out->timed_queries = c->timed_queries;
   });
 }
 

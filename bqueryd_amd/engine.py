@@ -57,6 +57,7 @@ class Device:
         self.check(self._lib.bqg_last_timing(self.handle, ctypes.byref(t)))
         return {'scan_ms': t.scan_ms, 'scan_launches': t.scan_launches, 'total_ms': t.total_ms,
                 'rows': t.rows, 'bytes': t.bytes, 'bytes_read': t.bytes_read, 'compact_ms': t.compact_ms,
+                'scan_ms_sum': t.scan_ms_sum, 'timed_queries': t.timed_queries,
                 'mode': t.mode, 'specialized': bool(t.specialized),
                 'narrow': bool(t.narrow), 'pack16': t.narrow == 2, 'regrows': t.regrows}
 
@@ -150,6 +151,20 @@ class _ResultHolder:
             self.handle = None
 
 
+_CHAR_ARRAYS = {}
+
+
+def _char_array(n):
+    """ctypes.c_char * n, created once per size (a new array type per result column costs more
+    than the rest of wrapping it)."""
+    t = _CHAR_ARRAYS.get(n)
+    if t is None:
+        if len(_CHAR_ARRAYS) > 4096:
+            _CHAR_ARRAYS.clear()
+        t = _CHAR_ARRAYS[n] = ctypes.c_char * n
+    return t
+
+
 def _result_to_columns(dev, res_handle, names):
     """Zero-copy numpy views of a result's columns (pinned host memory of the library)."""
     view = L.ResultView()
@@ -164,7 +179,7 @@ def _result_to_columns(dev, res_handle, names):
         if nbytes == 0:
             out[name] = np.zeros(0, dtype=dt)
             continue
-        buf = (ctypes.c_char * nbytes).from_address(view.cols[j])
+        buf = _char_array(nbytes).from_address(view.cols[j])
         buf._bqg_holder = holder
         out[name] = np.frombuffer(buf, dtype=dt)
     return out, bool(view.filtered)

@@ -141,6 +141,8 @@ typedef struct {
                             read compact resident copies (option compact), then fewer */
   double compact_ms;     /* device time of the compact copies this query built on first use
                             (0 when none was built; timing level 1 only, else NaN) (ABI 8) */
+  double scan_ms_sum;    /* scan_ms summed over every query since timing was (re-)enabled, and */
+  int64_t timed_queries; /* how many (ABI 8): a benchmark loop reads them once at its end */
 } bqg_timing;
 
 /* ---------------- lifecycle ---------------- */
@@ -154,7 +156,8 @@ const char* bqg_last_error(bqg_ctx* ctx);
 int bqg_set_stream(bqg_ctx* ctx, void* hip_stream);
 int bqg_synchronize(bqg_ctx* ctx);
 /* on: 0 off; 1 (any other non-zero) HIP events around the scan kernels (scan_ms) and the whole
- * query (total_ms); 2 the scan events only (total_ms NaN: two fewer event records per query). */
+ * query (total_ms); 2 the scan events only (total_ms NaN: two fewer event records per query).
+ * Every call resets the running sums (bqg_timing.scan_ms_sum / timed_queries). */
 int bqg_enable_timing(bqg_ctx* ctx, int on);
 int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
 
