@@ -72,7 +72,8 @@ class _Comm:
         if ws > 1:
             import torch.distributed as dist
             os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-            dist.init_process_group('gloo')
+            with _stdout_to_stderr():  # gloo announces its peers on stdout: the JSON line is the only stdout
+                dist.init_process_group('gloo')
             self.dist = dist
 
     def broadcast_bytes(self, b):

@@ -31,3 +31,33 @@ def test_launcher_present_means_no_self_launch():
     plan = _run(['--gpus', '4', '--dry-launch'], {'WORLD_SIZE': '4'})
     assert plan == {'launch': 'none', 'ranks': 4}
     assert _run(['--dry-launch'])['ranks'] == 1
+
+
+def test_rank_bookkeeping_keeps_stdout_clean(tmp_path):
+    """Two gloo ranks through bench._Comm (barrier, max, sum, the unique-id broadcast): nothing
+    reaches stdout but what rank 0 prints -- gloo announces its peers on stdout, which would
+    break the driver's one-JSON-line contract."""
+    script = tmp_path / 'ranks.py'
+    script.write_text(
+        'import json, os, sys\n'
+        'sys.path.insert(0, %r)\n'
+        'import bench\n'
+        'c = bench._Comm(2)\n'
+        'r = int(os.environ["RANK"])\n'
+        'm = c.max(r + 1.5); s = c.sum(r + 1); b = c.broadcast_bytes(b"id" if r == 0 else None)\n'
+        'c.barrier(); c.close()\n'
+        'if r == 0: print(json.dumps([m, s, b.decode()]))\n' % ROOT)
+    import socket
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, WORLD_SIZE='2', RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR='127.0.0.1',
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-500:] for o in outs]
+    assert json.loads(outs[0][0]) == [2.5, 3, 'id'] and outs[0][0].count('\n') == 1, outs[0][0]
+    assert outs[1][0] == ''

@@ -1055,3 +1055,39 @@ def test_compact_copies_accounting(oracle_c):
             assert_tables_equal(g, ref, exact_cols={'s'})
     finally:
         t.close()
+
+
+@pytest.mark.parametrize('opt,val', [('part_wbits', 6), ('part_wbits', 10), ('part_wbits', 13), ('scd_compact', 0),
+                                     ('priv_ahead', 1), ('priv_ahead', 2), ('priv_ahead', 4),
+                                     ('private_per_cu', 1), ('private_per_cu', 3), ('small_emit', 0)])
+def test_remaining_engine_options(opt, val, oracle_c, engine_options):
+    """The engine options no other test sets, each at non-default values, on the query shape
+    it steers (partition width: a partitioned C3-shaped query; the fused distinct pass's value
+    codes: C4; the private scan's tiles in flight and workgroups per CU, run-time specialised:
+    C2; the one-workgroup emit off: a shared-mode query), against the C restatement -- so that
+    every option value the header lists has run against the oracle."""
+    engine_options(**{opt: val, 'jit': 1, 'jit_min_rows': 0})
+    rng = np.random.default_rng(sum(map(ord, opt)) * 16 + val)
+    n = 400_003
+    if opt == 'part_wbits':
+        cols = OrderedDict(k=rng.integers(0, 90_000, n).astype(np.int32), g=rng.integers(1, 3, n).astype(np.int32),
+                           v=np.round(rng.normal(size=n) * 64) / 64)
+        keys, aggs, terms, mode = ['k', 'g'], [['v', 'sum', 's'], ['v', 'count', 'n']], [], 4
+    elif opt == 'scd_compact':
+        cols = synth.taxi_shard(n, config_id=4, columns=synth.query_columns(C4))
+        keys, aggs, terms, mode = C4['groupby'], C4['aggs'], C4['where'], 5
+    elif opt == 'small_emit':
+        cols = OrderedDict(k=rng.integers(0, 900, n).astype(np.int32), v=rng.integers(-50, 50, n).astype(np.int64))
+        keys, aggs, terms, mode = ['k'], [['v', 'sum', 's'], ['v', 'mean', 'm'], ['v', 'count', 'n']], [('v', '!=', 3)], 1
+    else:
+        cols = synth.taxi_shard(n, config_id=2, columns=synth.query_columns(C2))
+        keys, aggs, terms, mode = C2['groupby'], C2['aggs'], C2['where'], 0
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(keys, aggs, where_terms=terms)
+        info = t.dev.last_timing()
+    finally:
+        t.close()
+    assert info['mode'] == mode, info
+    ref = oracle_c.groupby(cols, keys, aggs, oracle_c.where_terms(cols, terms) if terms else None)
+    assert_tables_equal(got, ref)
