@@ -1278,19 +1278,23 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     // the scan is the fused distinct pass below
     c->last.mode = 5;
   } else if (pl.mode == kPrivate) {
-    const size_t lds = (size_t)S * kBlock * (8 + 8 * (size_t)nsum);
-    int per_cu = (int)std::min<size_t>(kPrivatePerCu, (160 * 1024) / std::max<size_t>(lds, 1));
-    if (c->opt[kOptPrivatePerCu]) per_cu = std::min(per_cu, (int)c->opt[kOptPrivatePerCu]);
-    if (per_cu < 1) per_cu = 1;
-    PrivateLaunch L{};
-    L.blocks = scan_blocks(c, N, per_cu);
-    L.lds_bytes = lds;
-    L.partials = (unsigned long long*)c->partials.ensure((size_t)(2 + nsum) * L.blocks * S * 8);
     // the scan's columns as their compact resident copies where they have one (option
     // compact): integer keys / terms / sums as narrow offsets (the decode restores the
     // canonical value), float64 columns that are only summed as their exact int32 codes,
     // summed as integers and scaled back once at emit -- fewer HBM bytes for the same rows
     ScanParams sp = compact_scan(c, t, pl, e);
+    int row_bytes = 0;
+    for (int i = 0; i < sp.ncols; ++i) row_bytes += 1 << sp.cols[i].lg;
+    const size_t lds = (size_t)S * kBlock * (8 + 8 * (size_t)nsum);
+    // workgroups per CU: 3 when a row reads more than 4 bytes (C2 as stored, 16 B/row: 0.2441 ->
+    // 0.2363 ms against 4, profiles/r5g_c2_launch_sweep.txt), 4 for the narrow compact rows
+    int per_cu = (int)std::min<size_t>(row_bytes > 4 ? 3 : kPrivatePerCu, (160 * 1024) / std::max<size_t>(lds, 1));
+    if (c->opt[kOptPrivatePerCu]) per_cu = std::min<int>((int)(160 * 1024 / std::max<size_t>(lds, 1)), (int)c->opt[kOptPrivatePerCu]);
+    if (per_cu < 1) per_cu = 1;
+    PrivateLaunch L{};
+    L.blocks = scan_blocks(c, N, per_cu);
+    L.lds_bytes = lds;
+    L.partials = (unsigned long long*)c->partials.ensure((size_t)(2 + nsum) * L.blocks * S * 8);
     FinishParams F{};
     F.nslots = (int)S;
     F.blocks = L.blocks;
@@ -1322,8 +1326,6 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       // (default: 3 when the scan reads at most 4 bytes per row -- compact copies: each tile is
       // small, and one in flight leaves the waves parked on memory; r4x8: C2 0.072 -> 0.069
       // ms -- else the kernel's 1)
-      int row_bytes = 0;
-      for (int i = 0; i < sp.ncols; ++i) row_bytes += 1 << sp.cols[i].lg;
       const int64_t ahead = c->opt[kOptPrivAhead] ? c->opt[kOptPrivAhead] : (row_bytes <= 4 ? 3 : 0);
       std::string extra;
       if (ahead) extra = std::string("#define BQ_PRIV_AHEAD ") + std::to_string(ahead) + "\n";

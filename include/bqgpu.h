@@ -180,7 +180,7 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *   scd_compact    1  ... with 32-bit value codes when they fit         0 | 1
  *   scd_pack16     1  ... first value and first row in one LDS word     0 | 1
  *   priv_ahead     0  private scan: tiles in flight (0: default)       0..4
- *   private_per_cu 0  private scan: workgroups per CU cap (0: auto)    0..8
+ *   private_per_cu 0  private scan: workgroups per CU (0: auto, 3 or 4) 0..8
  *   small_emit     1  one-workgroup emit for <= 8192 slots              0 | 1
  *   hash_slots     0  initial group hash-table slots (0: from rows)    0..2^31
  *   distinct_slots 0  initial count_distinct set slots (0: from rows)  0..2^31
