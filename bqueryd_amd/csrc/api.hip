@@ -328,7 +328,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -357,6 +357,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"part_win", 0, 0, 4096},               // partitioned aggregate: tiles per window (0: auto; 64..4096)
     {"compact", 1, 0, 2},                   // private / shared / dense global scans read compact column copies
     {"part_first", 0, 0, 2},                // packed partitioned path: rows in tile recorded for 0 auto / 1 no / 2 every tile
+    {"fx_sums", 1, 0, 1},                   // atomic modes: fixed-point float sums (bit-reproducible)
 };
 
 static int opt_index(const char* name) {
@@ -607,7 +608,28 @@ struct Plan {
   // row-order update turns such a group's mean into NaN unless its only non-finite value is its
   // last row, which the extra nonfinite pass decides per slot
   int nf_states = 0;           // bit q: sum state q needs it
+  // float sum states the atomic / partitioned modes accumulate as fixed-point limbs
+  // (ScanParams::sum_enc 3): finite columns without an exact int64 code (fx_states, pass 1),
+  // and the std pass's centred squares (fx2_states, bit i: the i-th std column)
+  int fx_states = 0;
+  int fx2_states = 0;
+  int32_t fx2_shift[kMaxSums] = {};
 };
+
+// the fixed-point shift of values of magnitude at most m: m * 2^shift < 2^95 (ScanParams::
+// sum_fx_shift; limbs of 32 bits, three of them)
+int fx_shift_for(double m) {
+  if (!(m > 0.0)) return 0;
+  int e;
+  std::frexp(m, &e);  // m < 2^e
+  return 95 - e;
+}
+
+// bytes of one workgroup's shared-mode LDS table (k_scan_shared): [nsum][S] sums, [S] counts,
+// [S] first rows, then with fixed-point sums [nsum][2][S] limbs
+size_t shared_lds(uint64_t S, int nsum, bool fx) {
+  return (size_t)S * (8 + 8 * (size_t)nsum) + (S & 1) * 4 + (fx ? 16 * (size_t)nsum * S : 0);
+}
 
 int scan_col(Plan& pl, int tc) {
   for (size_t i = 0; i < pl.tcol.size(); ++i)
@@ -740,6 +762,30 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     const ColStats& cs = t->cols[g.col].stats;
     if (cs.has_nan || (!cs.empty && (std::isinf(cs.fmin) || std::isinf(cs.fmax)))) pl.nf_states |= 1 << pl.agg_state[a];
   }
+  // float sums the atomic / partitioned modes cannot keep as exact integer codes: fixed-point
+  // limbs, summed as integers whatever the arrival order (bit-reproducible); the
+  // column finite, below 2^31 rows (the int64 limb sums cannot wrap)
+  if (c->opt[kOptFxSums] && t->nrows < ((int64_t)1 << 31)) {
+    for (int q = 0; q < pl.nsum; ++q) {
+      if (!pl.p.sum_is_float[q] || pl.p.sum_conv[q] != 0) continue;
+      const ColStats& cs = t->cols[pl.tcol[q]].stats;
+      if (cs.empty || cs.has_nan || std::isinf(cs.fmin) || std::isinf(cs.fmax)) continue;
+      pl.p.sum_fx_shift[q] = fx_shift_for(std::max(std::fabs(cs.fmin), std::fabs(cs.fmax)));
+      if (cs.enc64 && c->opt[kOptPartNarrow] != 0) continue;  // integer codes already (set_sum_codes)
+      pl.fx_states |= 1 << q;
+    }
+    // the std pass's (x - mean)^2 <= (max - min)^2
+    for (size_t i = 0; i < pl.std_cols.size(); ++i) {
+      const int q = pl.std_cols[i];
+      if (!pl.p.sum_is_float[q] || pl.p.sum_conv[q] != 0) continue;
+      const ColStats& cs = t->cols[pl.tcol[q]].stats;
+      if (cs.empty || cs.has_nan || std::isinf(cs.fmin) || std::isinf(cs.fmax)) continue;
+      const double span = cs.fmax - cs.fmin, sq = span * span * 1.0000001;
+      if (!std::isfinite(sq)) continue;
+      pl.fx2_states |= 1 << i;
+      pl.fx2_shift[i] = fx_shift_for(sq);
+    }
+  }
   // 3. keys
   pl.p.nkeys = q->n_keys;
   bool any_float = false;
@@ -850,7 +896,7 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     pl.nslots = (uint64_t)space;
     pl.p.hash = 0;
     const size_t per_slot_private = 8 + 8 * (size_t)pl.nsum;  // bytes per lane per slot
-    const size_t per_slot_shared = 8 + 8 * (size_t)pl.nsum;
+    const size_t per_slot_shared = 8 + 8 * (size_t)pl.nsum + (pl.fx_states ? 16 * (size_t)pl.nsum : 0);
     if (pl.nslots <= (uint64_t)kMaxPrivateSlots && pl.nslots * per_slot_private * kBlock <= 80 * 1024)
       pl.mode = kPrivate;
     else if (pl.nslots * per_slot_shared <= 64 * 1024) pl.mode = kShared;
@@ -858,7 +904,7 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
       // partitioned aggregation: 2^wbits slots of LDS state per partition (64 KiB: two
       // aggregate workgroups per CU; up to 128 KiB when the slot space needs it), at most
       // kPartMaxParts partitions
-      const size_t per_slot = 8 + 8 * (size_t)pl.nsum;
+      const size_t per_slot = 8 + 8 * (size_t)pl.nsum + (pl.fx_states ? 16 * (size_t)pl.nsum : 0);
       int wbits = 12;
       if (c->opt[kOptPartWbits]) wbits = (int)c->opt[kOptPartWbits];
       while (wbits > 6 && ((size_t)1 << wbits) * per_slot > 128 * 1024) --wbits;
@@ -1016,6 +1062,13 @@ void set_sum_codes(bqg_table* t, Plan& pl, EmitParams* e) {
     pl.p.sum_mul[q] = cs.enc64 == 1 ? std::ldexp(1.0, cs.enc64_k) : 100.0;
     if (e) e->sum_dec[q] = pl.p.sum_mul[q];
   }
+}
+
+// The fixed-point states of pass 1 (Plan::fx_states; the atomic / partitioned-wide modes, after
+// set_sum_codes): ScanParams::sum_enc 3, the shift set by plan_query
+void set_sum_fx(Plan& pl) {
+  for (int q = 0; q < pl.nsum; ++q)
+    if ((pl.fx_states >> q) & 1) pl.p.sum_enc[q] = 3;
 }
 
 void build_emit(bqg_table* t, const bqg_query* q, const Plan& pl, EmitParams& e, std::vector<int>& out_dt) {
@@ -1230,7 +1283,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   const uint64_t S = pl.nslots;
   const int nsum = pl.nsum;
   const int nsum2 = (int)pl.std_cols.size();
-  // slot arrays: cnt | fst | acc | acc2 | keys | hash counters
+  // slot arrays: cnt | fst | acc | acc2 | keys | hash counters | fixed-point limbs (pass 1, std pass)
   size_t off = 0;
   auto carve = [&](size_t bytes) {
     size_t o = off;
@@ -1240,6 +1293,12 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   const size_t o_cnt = carve(S * 8), o_fst = carve(S * 4), o_acc = carve(S * 8 * std::max(nsum, 1)),
                o_acc2 = carve(S * 8 * std::max(nsum2, 1)), o_keys = carve(pl.p.hash ? S * 8 : 8),
                o_hc = carve(16);
+  const bool atomic_mode = pl.mode != kPrivate;
+  // (the std pass's shared table with limbs: one workgroup per CU at most; past the LDS its
+  // centred squares keep the float64 atomics)
+  const bool fx1 = atomic_mode && pl.fx_states != 0,
+             fx2 = atomic_mode && pl.fx2_states != 0 && !(pl.mode == kShared && shared_lds(S, nsum2, true) > 160 * 1024);
+  const size_t o_fx = fx1 ? carve(S * 16 * (size_t)nsum) : 0, o_fx2 = fx2 ? carve(S * 16 * (size_t)nsum2) : 0;
   unsigned char* sbase = (unsigned char*)c->slots.ensure(off);
   SlotArrays sa{};
   sa.cnt = (unsigned long long*)(sbase + o_cnt);
@@ -1249,6 +1308,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   sa.keys = pl.p.hash ? (unsigned long long*)(sbase + o_keys) : nullptr;
   sa.hash_fill = (unsigned int*)(sbase + o_hc);
   sa.overflow = sa.hash_fill + 1;
+  sa.fx = fx1 ? (unsigned long long*)(sbase + o_fx) : nullptr;
 
   // output columns (device), capacity S rows (private) or G rows (generic, sized later)
   hipStream_t st = c->stream;
@@ -1375,13 +1435,15 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     // column statistics as the partitioned narrow entries) -- bit-reproducible sums; the emit
     // scales them back
     if (pl.mode != kPartitioned && c->opt[kOptPartNarrow] != 0) set_sum_codes(t, pl, &e);
+    // the other float sums as fixed-point limbs (the same bits on every run)
+    if (pl.mode != kPartitioned) set_sum_fx(pl);
     HIPCHECK(hipMemsetAsync(sa.hash_fill, 0, 8, st));
     // shared / dense global scans read the columns' compact copies (after set_sum_codes: a
     // code-copy column's state sums the codes as integers)
     ScanParams sp = pl.mode == kPartitioned ? pl.p : compact_scan(c, t, pl, e);
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
     if (pl.mode == kShared) {
-      const size_t lds = (size_t)S * (8 + 8 * (size_t)nsum);
+      const size_t lds = shared_lds(S, nsum, fx1);
       int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
       check_launch(c, "shared scan", lds, scan_blocks(c, N, std::max(per_cu, 1)));
       launch_scan_shared(sp, sa, scan_blocks(c, N, std::max(per_cu, 1)), lds, st);
@@ -1414,6 +1476,9 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       // wide entries: float sums of int64-codable columns add codes (deterministic); the
       // combine scales them back
       if (!L.narrow && c->opt[kOptPartNarrow] != 0) set_sum_codes(t, pl, nullptr);
+      // ... and the other float sums of wide entries as fixed-point limbs
+      if (!L.narrow) set_sum_fx(pl);
+      L.fx = !L.narrow && pl.fx_states != 0;
       // packed 4-byte entries (option part_pack): no summed column, or one narrow-coded
       // column whose codes span at most 2^16 values -- {code16, slot_low} per entry
       L.pack = 0;
@@ -1468,8 +1533,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         // table holds (up to kAggWinMax, in 1024-tile steps; option part_win) -- fewer windows,
         // fewer header-scan prologues; workgroups per CU stay what the slot table allows
         {
-          const size_t table = part_agg_lds(L.wbits, nsum, pk);
-          const int per_cu_agg = std::max(1, (int)((160 * 1024) / part_agg_lds_launch(L.wbits, nsum, pk, kAggWin)));
+          const size_t table = part_agg_lds(L.wbits, nsum, pk, L.fx);
+          const int per_cu_agg = std::max(1, (int)((160 * 1024) / part_agg_lds_launch(L.wbits, nsum, pk, kAggWin, L.fx)));
           const size_t budget = (160 * 1024) / per_cu_agg - 1024;  // static LDS of the scans
           L.win = kAggWin;
           while (L.win + 1024 <= kAggWinMax && table + 16 * (size_t)(L.win + 1024 + kAggK + 1) <= budget) L.win += 1024;
@@ -1481,7 +1546,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         }
         // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
         // slot table allows one per CU)
-        const size_t agg_lds = part_agg_lds_launch(L.wbits, nsum, pk, L.win);
+        const size_t agg_lds = part_agg_lds_launch(L.wbits, nsum, pk, L.win, L.fx);
         const int fit = std::max(1, (int)((160 * 1024) / agg_lds));
         L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, (c->cu * fit + L.nparts / 2) / L.nparts));
         if (c->opt[kOptPartSplits]) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, c->opt[kOptPartSplits]));
@@ -1505,7 +1570,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       const size_t mbytes = ((size_t)L.capacity * 4 + 255) & ~size_t(255);
       // split records: [W] counts, [W] sums ([W] first rows / tiles); packed entries always
       // have one (an aggregate that flushes its accumulators adds into it)
-      L.partial_bytes = ((pk ? ((size_t)1 << L.wbits) * 20 : part_agg_lds(L.wbits, nsum, pk)) + 255) & ~size_t(255);
+      L.partial_bytes = ((pk ? ((size_t)1 << L.wbits) * 20 : part_agg_lds(L.wbits, nsum, pk, L.fx)) + 255) & ~size_t(255);
       const size_t pbytes = (L.splits > 1 || pk) ? (size_t)L.nparts * L.splits * L.partial_bytes : 0;
       const size_t tbytes = pk ? (((size_t)L.nparts << L.wbits) + 255) & ~size_t(255) : 0;
       // rows in tile (PartLaunch::rit) for the tiles where first appearances fall: on uniform
@@ -1546,13 +1611,20 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         c->last.specialized = fs ? 1 : 0;
       }
       check_launch(c, "partitioned scatter", part_scatter_lds(L.nparts, L.threads, nsum, L.k, nw, pk), L.blocks, L.threads);
-      check_launch(c, "partitioned aggregate", part_agg_lds_launch(L.wbits, nsum, pk, L.win),
+      check_launch(c, "partitioned aggregate", part_agg_lds_launch(L.wbits, nsum, pk, L.win, L.fx),
                    (int64_t)L.nparts * L.splits, 1024);
       launch_partitioned(pl.p, sa, L, st, fs, ff);
     } else {
       launch_scan_global(sp, sa, scan_blocks(c, N, 8), st);
     }
     HIPCHECK(hipGetLastError());
+    // fixed-point sums to float64 (the partitioned path's combine rounds them itself)
+    if (fx1 && pl.mode != kPartitioned) {
+      FxShifts sh{};
+      for (int q = 0; q < nsum; ++q) sh.shift[q] = pl.p.sum_fx_shift[q];
+      launch_fx_finalize(sa.acc, sa.fx, nsum, pl.fx_states, sh, S, st);
+      HIPCHECK(hipGetLastError());
+    }
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[2], st));
     if (pl.p.hash) {
       unsigned int hc[2];
@@ -1599,11 +1671,14 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       q2.sum_is_float[i] = 1;
       q2.sum_conv[i] = pl.p.sum_conv[pl.std_cols[i]];
       q2.sum_centered[i] = 1;
-      q2.sum_enc[i] = 0;
+      // atomic modes: the centred squares as fixed-point limbs (bit-reproducible)
+      q2.sum_enc[i] = fx2 && ((pl.fx2_states >> i) & 1) ? 3 : 0;
+      q2.sum_fx_shift[i] = pl.fx2_shift[i];
       q2.centers[i] = centers + (size_t)i * S;
     }
     SlotArrays sa2 = sa;
     sa2.acc = sa.acc2;
+    sa2.fx = fx2 ? (unsigned long long*)(sbase + o_fx2) : nullptr;
     // pass 2 recomputes cnt/fst identically into scratch copies
     unsigned char* b2 = (unsigned char*)c->cdbuf.ensure(S * 12 + 512);
     sa2.cnt = (unsigned long long*)b2;
@@ -1632,11 +1707,17 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       launch_init_slots(sa2, nsum2, S, st);
       sa2.keys = sa.keys;
       if (pl.mode == kShared) {
-        const size_t lds = (size_t)S * (8 + 8 * (size_t)nsum2);
+        const size_t lds = shared_lds(S, nsum2, fx2);
         int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
+        check_launch(c, "shared scan (std pass)", lds, scan_blocks(c, N, std::max(per_cu, 1)));
         launch_scan_shared(q2, sa2, scan_blocks(c, N, std::max(per_cu, 1)), lds, st);
       } else {
         launch_scan_global(q2, sa2, scan_blocks(c, N, 8), st);
+      }
+      if (fx2) {
+        FxShifts sh{};
+        for (int i = 0; i < nsum2; ++i) sh.shift[i] = q2.sum_fx_shift[i];
+        launch_fx_finalize(sa2.acc, sa2.fx, nsum2, pl.fx2_states, sh, S, st);
       }
     }
     HIPCHECK(hipGetLastError());

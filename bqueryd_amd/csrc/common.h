@@ -95,6 +95,12 @@ struct ScanParams {
   // sum independent of the arrival order (bit-reproducible); EmitParams::sum_dec scales it back.
   int32_t sum_enc[kMaxSums];
   double sum_mul[kMaxSums];
+  // sum_enc 3 (the atomic modes' float sums without an exact code): each value as a
+  // fixed-point integer |x| * 2^sum_fx_shift (< 2^95; the shift from the column statistics'
+  // largest magnitude) in three 32-bit limbs carrying x's sign, each limb summed as an int64 --
+  // integer atomics, so the sum no longer depends on the arrival order (k_fx_finalize rounds it
+  // to float64 once)
+  int32_t sum_fx_shift[kMaxSums];
 };
 
 // Per-slot aggregation state in device memory (global modes, and the target of the
@@ -104,6 +110,8 @@ struct SlotArrays {
   uint32_t* fst;             // [nslots]  first passing row (kNoRow = none)
   unsigned long long* acc;   // [nsum][nslots]  f64 or i64 bit patterns
   unsigned long long* acc2;  // [nsum2][nslots] centered second moments (std), or null
+  unsigned long long* fx;    // [nsum][2][nslots] limbs 1 and 2 of fixed-point sums (sum_enc 3;
+                             // limb 0 is acc), or null
   unsigned long long* keys;  // hash mode: [nslots] packed key code or kEmpty
   unsigned int* hash_fill;   // hash mode: number of occupied positions
   unsigned int* overflow;    // hash mode: set when the table is over-full

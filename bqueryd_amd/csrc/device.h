@@ -164,6 +164,40 @@ __device__ __forceinline__ double value_f64(uint64_t v, int conv) {
   return conv == 0 ? as_f64(v) : (conv == 1 ? (double)(int64_t)v : (double)v);
 }
 
+// Fixed-point limbs of a finite float64 (ScanParams::sum_enc 3): X = |x| * 2^shift, truncated to
+// an integer (below 2^95 by the choice of shift), split into three 32-bit limbs that carry x's
+// sign.  Limb sums of fewer than 2^31 rows fit int64; integer adds make the total independent of
+// the order the rows arrive in.
+__device__ __forceinline__ void fx_limbs(double x, int shift, long long (&l)[3]) {
+  const uint64_t b = as_u64(x);
+  const int ex = (int)((b >> 52) & 0x7FFu);
+  const uint64_t mant = (b & 0xFFFFFFFFFFFFFull) | (ex ? (1ull << 52) : 0ull);
+  const int k = (ex ? ex - 1075 : -1074) + shift;  // X = mant * 2^k, k <= 42
+  uint64_t lo, hi;
+  if (k >= 64) {
+    lo = 0;
+    hi = mant << (k - 64);
+  } else if (k > 0) {
+    lo = mant << k;
+    hi = mant >> (64 - k);
+  } else {
+    lo = k > -64 ? mant >> -k : 0ull;
+    hi = 0;
+  }
+  const long long sg = (b >> 63) ? -1ll : 1ll;
+  l[0] = sg * (long long)(lo & 0xFFFFFFFFull);
+  l[1] = sg * (long long)(lo >> 32);
+  l[2] = sg * (long long)(hi & 0xFFFFFFFFull);
+}
+
+// The float64 nearest the exact limb total (s0 + s1 * 2^32 + s2 * 2^64) * 2^-shift: the limb
+// sums are combined exactly in 128 bits (|s2| < 2^62, so the total stays below 2^127) and
+// rounded once
+__device__ __forceinline__ double fx_value(long long s0, long long s1, long long s2, int shift) {
+  const __int128 t = (((__int128)s2 << 32) + (__int128)s1) * ((__int128)1 << 32) + (__int128)s0;
+  return ldexp((double)t, -shift);
+}
+
 template <int NC, int R>
 __device__ __forceinline__ void decode_all(const ScanParams& p, const Chunk (&raw)[NC], uint64_t (&v)[NC][R]) {
 #pragma unroll

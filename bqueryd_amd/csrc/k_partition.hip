@@ -57,6 +57,7 @@ __device__ __forceinline__ long long part_sum_code(const ScanParams& p, int q, u
 template <int NV>
 struct PartRec {
   unsigned long long a[NV];
+  unsigned long long x[NV][2];  // fixed-point sums: limbs 1 and 2 (a holds limb 0)
   unsigned long long c64;  // PACK: count
   uint32_t c, f;
 };
@@ -101,9 +102,9 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
     return;
   }
   uint32_t c = 0, f = kNoRow;
-  unsigned long long a[NV];
+  unsigned long long a[NV], x[NV][2];
 #pragma unroll
-  for (int q = 0; q < NV; ++q) a[q] = 0;
+  for (int q = 0; q < NV; ++q) a[q] = x[q][0] = x[q][1] = 0;
   for (int o = 0; o < S; ++o) {
     PartRec<NV> r;
     rec(o, r);
@@ -113,6 +114,8 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
     for (int q = 0; q < nsum; ++q) {
       if (!NARROW && p.sum_is_float[q] && !p.sum_enc[q]) a[q] = as_u64(as_f64(a[q]) + as_f64(r.a[q]));
       else a[q] += r.a[q];
+      x[q][0] += r.x[q][0];
+      x[q][1] += r.x[q][1];
     }
   }
   sa.cnt[gs] = c;
@@ -124,6 +127,8 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
     if (NARROW) {
       if (L.enc_kind[q] == 3) a[q] += (unsigned long long)c * (unsigned long long)L.enc_off[q];
       else a[q] = as_u64((double)(long long)a[q] / L.enc_mul[q]);
+    } else if (p.sum_is_float[q] && p.sum_enc[q] == 3) {
+      a[q] = as_u64(fx_value((long long)a[q], (long long)x[q][0], (long long)x[q][1], p.sum_fx_shift[q]));
     } else if (p.sum_is_float[q] && p.sum_enc[q]) {
       a[q] = as_u64((double)(long long)a[q] / p.sum_mul[q]);
     }
@@ -144,12 +149,17 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][W] (PACK: [W] packed)
   uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)(PACK ? 1 : nsum) * W);  // [W] (PACK: unused)
   uint32_t* fst = PACK ? cnt : cnt + W;                                    // [W] first row (PACK: first-appearance key)
+  // fixed-point sums (L.fx): limbs 1 and 2 [nsum][2][W] after the table (limb 0 is acc)
+  const bool fx = !PACK && !NARROW && L.fx;
+  unsigned long long* fxl = reinterpret_cast<unsigned long long*>(smem + part_agg_lds(L.wbits, nsum, PACK));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = (int)(blockDim.x >> 6);
   for (int i = tid; i < W; i += blockDim.x) {
     if (!PACK) cnt[i] = 0;
     fst[i] = kNoRow;
   }
   for (int i = tid; i < (PACK ? 1 : nsum) * W; i += blockDim.x) acc[i] = 0;
+  if (fx)
+    for (int i = tid; i < 2 * nsum * W; i += blockDim.x) fxl[i] = 0;
   const unsigned long long inc = PACK ? 1ull << L.sbits : 0ull;  // one row in the packed count field
   __syncthreads();
   const int64_t nt = L.ntiles;
@@ -167,7 +177,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   // the tile of a flattened granule's first entry = E[j] + 4 x position) and the segment's
   // entry range AB[j] = a | b << 16; K + 1 sentinels past the last tile.
   const int WIN = L.win;  // <= kAggWinMax: the header loads below are 4 tiles per thread at most
-  uint32_t* wF = reinterpret_cast<uint32_t*>(smem + part_agg_lds(L.wbits, nsum, PACK));
+  uint32_t* wF = reinterpret_cast<uint32_t*>(smem + part_agg_lds(L.wbits, nsum, PACK, !PACK && L.fx));
   uint32_t* wB = wF + WIN + kAggK + 1;
   uint32_t* wE = wB + WIN + kAggK + 1;
   uint32_t* wAB = wE + WIN + kAggK + 1;
@@ -374,7 +384,14 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
           for (int q = 0; q < nsum; ++q) {
             // wide entries of an int64-codable float column (ScanParams::sum_enc): integer
             // code sums, the same whatever order the entries arrive in
-            if (!NARROW && p.sum_is_float[q] && p.sum_enc[q]) atomicAdd(&acc[(size_t)q * W + sl], (unsigned long long)part_sum_code(p, q, en.v[u][e][q]));
+            if (!NARROW && p.sum_is_float[q] && p.sum_enc[q] == 3) {
+              // fixed-point limbs: integer sums, the same whatever order the entries arrive in
+              long long l[3];
+              fx_limbs(value_f64(en.v[u][e][q], p.sum_conv[q]), p.sum_fx_shift[q], l);
+              atomicAdd(&acc[(size_t)q * W + sl], (unsigned long long)l[0]);
+              atomicAdd(&fxl[(size_t)(2 * q) * W + sl], (unsigned long long)l[1]);
+              atomicAdd(&fxl[(size_t)(2 * q + 1) * W + sl], (unsigned long long)l[2]);
+            } else if (!NARROW && p.sum_is_float[q] && p.sum_enc[q]) atomicAdd(&acc[(size_t)q * W + sl], (unsigned long long)part_sum_code(p, q, en.v[u][e][q]));
             else if (!NARROW && p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][e][q], p.sum_conv[q]));
             else atomicAdd(&acc[(size_t)q * W + sl], en.v[u][e][q]);
           }
@@ -435,7 +452,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   }
   if (L.splits > 1) {
     unsigned char* rec = L.partial + ((size_t)part * L.splits + split) * L.partial_bytes;
-    {  // [W] counts, [W] first rows, then [nsum][W] sums
+    {  // [W] counts, [W] first rows, then [nsum][W] sums (fx: then [nsum][2][W] limbs)
       uint32_t* pc = reinterpret_cast<uint32_t*>(rec);
       uint32_t* pf = pc + W;
       unsigned long long* pa = reinterpret_cast<unsigned long long*>(pf + W);
@@ -444,6 +461,8 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
         pf[s] = fst[s];
 #pragma unroll
         for (int q = 0; q < nsum; ++q) pa[(size_t)q * W + s] = acc[(size_t)q * W + s];
+        if (fx)
+          for (int h = 0; h < 2 * nsum; ++h) pa[(size_t)(nsum + h) * W + s] = fxl[(size_t)h * W + s];
       }
     }
     return;
@@ -453,7 +472,11 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     r.f = fst[s];
     r.c = PACK ? 0u : cnt[s];
 #pragma unroll
-    for (int q = 0; q < (PACK ? 1 : nsum); ++q) r.a[q] = acc[(size_t)q * W + s];
+    for (int q = 0; q < (PACK ? 1 : nsum); ++q) {
+      r.a[q] = acc[(size_t)q * W + s];
+      r.x[q][0] = fx ? fxl[(size_t)(2 * q) * W + s] : 0ull;
+      r.x[q][1] = fx ? fxl[(size_t)(2 * q + 1) * W + s] : 0ull;
+    }
     part_finish_slot<NSUM, NARROW, PACK>(p, L, sa, slot0 + s, 1, [&](int, PartRec<NV>& o) { o = r; });
   }
 }
@@ -478,8 +501,13 @@ __global__ __launch_bounds__(256) void k_part_combine(ScanParams p, PartLaunch L
         const unsigned long long* pa = reinterpret_cast<const unsigned long long*>(pc + 2 * W);
         r.c = pc[s];
         r.f = pc[W + s];
+        const bool fx = !NARROW && L.fx;
 #pragma unroll
-        for (int q = 0; q < NSUM; ++q) r.a[q] = pa[(size_t)q * W + s];
+        for (int q = 0; q < NSUM; ++q) {
+          r.a[q] = pa[(size_t)q * W + s];
+          r.x[q][0] = fx ? pa[(size_t)(NSUM + 2 * q) * W + s] : 0ull;
+          r.x[q][1] = fx ? pa[(size_t)(NSUM + 2 * q + 1) * W + s] : 0ull;
+        }
       }
     });
   }
@@ -553,7 +581,7 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
     }
 #undef BQG_SCATTER
   }
-  const size_t agg_lds = part_agg_lds_launch(L.wbits, p.nsum, L.pack != 0, L.win);
+  const size_t agg_lds = part_agg_lds_launch(L.wbits, p.nsum, L.pack != 0, L.win, L.fx != 0);
   const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
   const unsigned cgrid = (unsigned)std::min<uint64_t>((p.nslots + 255) / 256, 4096);
   if (L.pack) {

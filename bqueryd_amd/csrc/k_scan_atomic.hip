@@ -25,11 +25,15 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][S]
   uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)nsum * S);    // [S]
   uint32_t* fst = cnt + S;                                                 // [S]
+  // fixed-point sums (sum_enc 3): limbs 1 and 2 [nsum][2][S] after the table (sa.fx set)
+  unsigned long long* fxl = reinterpret_cast<unsigned long long*>(fst + S + (S & 1));
   for (int i = tid; i < S; i += kBlock) {
     cnt[i] = 0;
     fst[i] = kNoRow;
   }
   for (int i = tid; i < nsum * S; i += kBlock) acc[i] = 0;
+  if (sa.fx)
+    for (int i = tid; i < 2 * nsum * S; i += kBlock) fxl[i] = 0;
   __syncthreads();
 
   const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
@@ -55,7 +59,18 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
 #pragma unroll
         for (int q = 0; q < (NC < kMaxSums ? NC : kMaxSums); ++q) {
           if (q < nsum) {
-            if (p.sum_is_float[q] && p.sum_enc[q]) {
+            if (p.sum_is_float[q] && p.sum_enc[q] == 3) {
+              double x = value_f64(v[q][r], p.sum_conv[q]);
+              if (p.sum_centered[q]) {
+                const double d = x - p.centers[q][s];
+                x = d * d;
+              }
+              long long l[3];
+              fx_limbs(x, p.sum_fx_shift[q], l);
+              atomicAdd(&acc[(size_t)q * S + s], (unsigned long long)l[0]);
+              atomicAdd(&fxl[(size_t)(2 * q) * S + s], (unsigned long long)l[1]);
+              atomicAdd(&fxl[(size_t)(2 * q + 1) * S + s], (unsigned long long)l[2]);
+            } else if (p.sum_is_float[q] && p.sum_enc[q]) {
               atomicAdd(&acc[(size_t)q * S + s], (unsigned long long)sum_code(p, q, v[q][r]));
             } else if (p.sum_is_float[q]) {
               double x = value_f64(v[q][r], p.sum_conv[q]);
@@ -82,6 +97,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
       const unsigned long long a = acc[(size_t)q * S + s];
       if (p.sum_is_float[q] && !p.sum_enc[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)q * p.nslots + s]), as_f64(a));
       else atomicAdd(&sa.acc[(size_t)q * p.nslots + s], a);
+      if (p.sum_is_float[q] && p.sum_enc[q] == 3)
+        for (int h = 0; h < 2; ++h)
+          atomicAdd(&sa.fx[(size_t)(2 * q + h) * p.nslots + s], fxl[(size_t)(2 * q + h) * S + s]);
     }
   }
 }
@@ -120,7 +138,18 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_global(ScanParams p, SlotArr
 #pragma unroll
         for (int q = 0; q < (NC < kMaxSums ? NC : kMaxSums); ++q) {
           if (q < nsum) {
-            if (p.sum_is_float[q] && p.sum_enc[q]) {
+            if (p.sum_is_float[q] && p.sum_enc[q] == 3) {
+              double x = value_f64(v[q][r], p.sum_conv[q]);
+              if (p.sum_centered[q]) {
+                const double d = x - p.centers[q][s];
+                x = d * d;
+              }
+              long long l[3];
+              fx_limbs(x, p.sum_fx_shift[q], l);
+              atomicAdd(&sa.acc[(size_t)q * p.nslots + s], (unsigned long long)l[0]);
+              atomicAdd(&sa.fx[(size_t)(2 * q) * p.nslots + s], (unsigned long long)l[1]);
+              atomicAdd(&sa.fx[(size_t)(2 * q + 1) * p.nslots + s], (unsigned long long)l[2]);
+            } else if (p.sum_is_float[q] && p.sum_enc[q]) {
               atomicAdd(&sa.acc[(size_t)q * p.nslots + s], (unsigned long long)sum_code(p, q, v[q][r]));
             } else if (p.sum_is_float[q]) {
               double x = value_f64(v[q][r], p.sum_conv[q]);
@@ -207,8 +236,33 @@ __global__ void k_init_slots(SlotArrays sa, int nsum, uint64_t nslots) {
     sa.cnt[i] = 0;
     sa.fst[i] = kNoRow;
     for (int v = 0; v < nsum; ++v) sa.acc[(size_t)v * nslots + i] = 0;
+    if (sa.fx)
+      for (int v = 0; v < 2 * nsum; ++v) sa.fx[(size_t)v * nslots + i] = 0;
     if (sa.keys) sa.keys[i] = kEmpty;
   }
+}
+
+// Fixed-point sums (sum_enc 3) to float64 bits in place: acc[q][s] = the nearest double of the
+// limbs' exact total (one rounding; fx_value), for every state q in `states`.  Order-free
+// integer limbs, one deterministic rounding: the same bits on every run.
+__global__ void k_fx_finalize(unsigned long long* acc, const unsigned long long* fx, int nsum, int states,
+                              FxShifts sh, uint64_t nslots) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * blockDim.x)
+    for (int q = 0; q < nsum; ++q) {
+      if (!((states >> q) & 1)) continue;
+      const long long s0 = (long long)acc[(size_t)q * nslots + i];
+      const long long s1 = (long long)fx[(size_t)(2 * q) * nslots + i];
+      const long long s2 = (long long)fx[(size_t)(2 * q + 1) * nslots + i];
+      acc[(size_t)q * nslots + i] = as_u64(fx_value(s0, s1, s2, sh.shift[q]));
+    }
+}
+
+void launch_fx_finalize(unsigned long long* acc, const unsigned long long* fx, int nsum, int states, const FxShifts& sh,
+                        uint64_t nslots, hipStream_t st) {
+  if (!states || !nslots) return;
+  uint64_t blocks = (nslots + kBlock - 1) / kBlock;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_fx_finalize, dim3((unsigned)blocks), dim3(kBlock), 0, st, acc, fx, nsum, states, sh, nslots);
 }
 
 void launch_scan_shared(const ScanParams& p, const SlotArrays& s, int blocks, size_t lds, hipStream_t st) {

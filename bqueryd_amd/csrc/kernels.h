@@ -71,6 +71,12 @@ void launch_scan_shared(const ScanParams& p, const SlotArrays& s, int blocks, si
                         hipStream_t st);
 void launch_scan_global(const ScanParams& p, const SlotArrays& s, int blocks, hipStream_t st);
 void launch_init_slots(const SlotArrays& s, int nsum, uint64_t nslots, hipStream_t st);
+// fixed-point float sums (ScanParams::sum_enc 3) of the states in `states` to float64 bits in acc
+struct FxShifts {
+  int32_t shift[kMaxSums];
+};
+void launch_fx_finalize(unsigned long long* acc, const unsigned long long* fx, int nsum, int states, const FxShifts& sh,
+                        uint64_t nslots, hipStream_t st);
 
 // The nonfinite pass (EmitParams::nf_*): one scan over the rows with the query's terms and key
 // coding (hash modes look the slot up in pass 1's table), recording per slot the last passing
@@ -245,8 +251,11 @@ struct PartLaunch {
   uint16_t* rit;
   // splits > 1: [nparts][splits] split tables of partial_bytes each, added by k_part_combine
   unsigned char* partial;
-  size_t partial_bytes;      // 2^wbits * (8 + 8 * nsum)
+  size_t partial_bytes;      // 2^wbits * (8 + 8 * nsum) (+ 16 * nsum with fx)
   int win;                   // aggregate window: tiles whose bounds are staged in LDS at once
+  // wide entries with fixed-point float sums (ScanParams::sum_enc 3): the slot table and split
+  // records carry limbs 1 and 2 of every sum state ([nsum][2][W] after the table)
+  int fx;
 };
 // LDS bytes of a scatter workgroup: the staged tile (values, meta), tile counts (two
 // buffers) / offsets and two sets of scan totals
@@ -254,18 +263,18 @@ inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1, boo
   // pack: + the tile's rows in tile (u16) staged beside the entry words
   return (size_t)threads * 4 * k * (4 + (pack ? 2 : (narrow ? 4 : 8) * (size_t)nsum)) + (size_t)nparts * 12 + 2 * 16 * 4;
 }
-// LDS bytes of an aggregate workgroup's slot table: count + first row + 8-byte sums, or
-// (pack) the packed 8-byte accumulator + first tile
-__host__ __device__ inline size_t part_agg_lds(int wbits, int nsum, bool pack) {
-  return ((size_t)1 << wbits) * (pack ? 12 : 8 + 8 * (size_t)nsum);
+// LDS bytes of an aggregate workgroup's slot table: count + first row + 8-byte sums (+ two
+// 8-byte limbs per sum with fixed-point sums), or (pack) the packed 8-byte accumulator + first tile
+__host__ __device__ inline size_t part_agg_lds(int wbits, int nsum, bool pack, bool fx = false) {
+  return ((size_t)1 << wbits) * (pack ? 12 : 8 + 8 * (size_t)nsum + (fx ? 16 * (size_t)nsum : 0));
 }
 // the aggregate walks its split's tiles in windows of PartLaunch::win tiles (four words of
 // bounds per tile in LDS, up to kAggWinMax); a chunk of entry granules spans at most kAggK tiles
 constexpr int kAggWin = 1024;     // the default window (option part_win = 0 and no room for more)
 constexpr int kAggWinMax = 4096;  // 1024 threads x 4 tiles of header loads
 constexpr int kAggK = 8;
-inline size_t part_agg_lds_launch(int wbits, int nsum, bool pack, int win = kAggWin) {
-  return part_agg_lds(wbits, nsum, pack) + 4 * (size_t)(win + kAggK + 1) * 4;
+inline size_t part_agg_lds_launch(int wbits, int nsum, bool pack, int win = kAggWin, bool fx = false) {
+  return part_agg_lds(wbits, nsum, pack, fx) + 4 * (size_t)(win + kAggK + 1) * 4;
 }
 // fscatter: the query-specialised (JIT) scatter kernel, or nullptr for the precompiled one
 // ffirst: the query-specialised (JIT) first-row pass of packed entries, or nullptr

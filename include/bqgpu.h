@@ -196,6 +196,11 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *                     record their rows in tile (exact first rows in the
  *                     aggregate; auto: the tiles where first appearances
  *                     fall on uniform keys), the rest by the first-row pass
+ *   fx_sums        1  shared / global / hash / partitioned-wide modes:     0 | 1
+ *                     float sums of finite columns without an exact int64
+ *                     code (and the std pass's centred squares) as
+ *                     fixed-point limbs in integer atomics -- the same bits
+ *                     on every run (0: float64 atomics, arrival order)
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);

@@ -812,6 +812,24 @@ def test_engine_options_validate(gpu_device):
     assert gpu_device.get_option('jit') in (0, 1) and gpu_device.get_option('part_narrow') == 1
 
 
+def _fx_trunc(v, col):
+    """v as the fixed-point sums see it: truncated toward zero at 2^-shift, the shift from the
+    largest magnitude of the whole column (ScanParams::sum_fx_shift: 95 - frexp exponent)."""
+    shift = 95 - int(np.frexp(np.max(np.abs(col)))[1])
+    return np.ldexp(np.trunc(np.ldexp(v, shift)), -shift)
+
+
+def _fsum_by_group(k, v, gk):
+    """The correctly rounded exact sum of each group's values (math.fsum), in gk's order."""
+    import math
+    order = np.argsort(k, kind='stable')
+    ks, vs = k[order], v[order]
+    starts = np.flatnonzero(np.r_[True, ks[1:] != ks[:-1]])
+    ends = np.r_[starts[1:], len(ks)]
+    sums = {ks[a]: math.fsum(vs[a:b]) for a, b in zip(starts, ends)}
+    return np.array([sums[g] for g in gk], np.float64)
+
+
 def _code_sums(keys_codes, ngroups, codes):
     out = np.zeros(ngroups, np.int64)
     np.add.at(out, keys_codes, codes)
@@ -825,8 +843,10 @@ def test_atomic_mode_float_sums_reproducible(mode, values, oracle_c, engine_opti
     a float column with an exact integer code per value (cents, dyadic; _big: codes beyond
     32 bits whose int64 sums cannot overflow) as int64 codes: the sums are the same bits on
     every run and equal the exact code sum scaled back once (one correctly rounded division per
-    group); means follow.  Arbitrary doubles (raw) keep the float64 arrival-order sum: within
-    tolerance of the row-order oracle, not bit-reproducible.  bquery sums in row order
+    group); means follow.  Arbitrary doubles (raw) accumulate as fixed-point limbs (integer
+    atomics, ScanParams::sum_enc 3): the same bits on every run, and -- no value of this data
+    has bits below the fixed point -- the correctly rounded exact sum per group (math.fsum);
+    their std's centred pass the same.  bquery sums in row order
     (/root/reference/bqueryd/worker.py:313 via bquery's groupby) -- within tolerance of it."""
     rng = np.random.default_rng(11)
     n = 1_500_000
@@ -860,6 +880,8 @@ def test_atomic_mode_float_sums_reproducible(mode, values, oracle_c, engine_opti
         v, mul = rng.normal(size=n) * 1e3, None
     cols = OrderedDict(k=k, v=v)
     aggs = [['v', 'sum', 's'], ['v', 'mean', 'm'], ['v', 'count', 'n']]
+    if mul is None:
+        aggs.append(['v', 'std', 'sd'])
     runs = []
     t = ShardTable(cols)
     try:
@@ -872,10 +894,13 @@ def test_atomic_mode_float_sums_reproducible(mode, values, oracle_c, engine_opti
     assert info['mode'] == {'shared': 1, 'global_dense': 2, 'hash': 3, 'partitioned': 4}[mode], info
     ref = oracle_c.groupby(cols, ['k'], aggs, None)
     assert_tables_equal(runs[0], ref)
-    if mul is None:
-        return
     for r in runs[1:]:
         assert_tables_equal(r, runs[0], exact_float_sums=True)
+        for name in ('s', 'm') + (('sd',) if mul is None else ()):
+            np.testing.assert_array_equal(r[name].view(np.uint64), runs[0][name].view(np.uint64))
+    if mul is None:
+        np.testing.assert_array_equal(runs[0]['s'], _fsum_by_group(k, _fx_trunc(v, v), runs[0]['k']))
+        return
     # the exact code sum per group, scaled back once
     gk = runs[0]['k']
     if mode == 'hash':
@@ -885,6 +910,62 @@ def test_atomic_mode_float_sums_reproducible(mode, values, oracle_c, engine_opti
         exp = _code_sums(k, ng, codes)[gk]
     np.testing.assert_array_equal(runs[0]['s'], exp.astype(np.float64) / mul)
     np.testing.assert_array_equal(runs[0]['m'], (exp.astype(np.float64) / mul) / runs[0]['n'].astype(np.float64))
+
+
+@pytest.mark.parametrize('splits', [0, 3])
+@pytest.mark.parametrize('mode', ['shared', 'global_dense', 'hash', 'partitioned'])
+def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
+    """Fixed-point float sums (float64, float32) beside integer-coded ones, with filters; the
+    partitioned path's split records (part_splits=3) add the limbs in split order; std of a
+    coded column (pass 1 integer codes, the centred pass in fixed point); a column holding a
+    NaN keeps the float64 atomics (no fixed point: tolerance only).  Every run the same bits
+    but the NaN column's; option fx_sums=0 restores the float64 atomics for all."""
+    if splits and mode != 'partitioned':
+        pytest.skip('split records are the partitioned path\'s')
+    rng = np.random.default_rng(21 + splits)
+    n = 900_000
+    if mode == 'global_dense':
+        engine_options(partition=0)
+    if splits:
+        engine_options(part_splits=splits)
+    ng = {'shared': 400, 'global_dense': 150_000, 'hash': 0, 'partitioned': 150_000}[mode]
+    if mode == 'hash':
+        pool = np.unique(rng.integers(-2**40, 2**40, 20_000))
+        k = pool[rng.integers(0, len(pool), n)]
+    else:
+        k = rng.integers(0, ng, n).astype(np.int32)
+    raw = rng.standard_cauchy(n) * 50.0          # heavy tails: wide magnitude range
+    raw32 = (rng.normal(size=n) * 7).astype(np.float32)
+    cents = rng.integers(-90_000, 90_000, n) / 100.0
+    withnan = rng.normal(size=n)
+    withnan[rng.integers(0, n, 3)] = np.nan
+    t = (rng.random(n) < 0.8).astype(np.int32)
+    cols = OrderedDict(k=k, raw=raw, raw32=raw32, cents=cents, withnan=withnan, t=t)
+    aggs = [['raw', 'sum', 'a'], ['raw', 'mean', 'am'], ['raw32', 'sum', 'b'], ['cents', 'sum', 'c'],
+            ['cents', 'std', 'csd'], ['withnan', 'sum', 'e'], ['raw', 'count', 'n']]
+    terms = [('t', '==', 1)]
+    if mode == 'partitioned':
+        aggs = [a for a in aggs if a[1] != 'std']  # pass-2 std runs the global scan
+    runs = []
+    tb = ShardTable(cols)
+    try:
+        for _ in range(2):
+            got, _ = tb.groupby(['k'], aggs, where_terms=terms)
+            runs.append(got)
+            info = tb.dev.last_timing()
+        tb.dev.set_option('fx_sums', 0)
+        off, _ = tb.groupby(['k'], aggs, where_terms=terms)
+    finally:
+        tb.close()
+    assert info['mode'] == {'shared': 1, 'global_dense': 2, 'hash': 3, 'partitioned': 4}[mode], info
+    mask = oracle_c.where_terms(cols, terms)
+    ref = oracle_c.groupby(cols, ['k'], aggs, mask)
+    assert_tables_equal(runs[0], ref)
+    assert_tables_equal(off, ref)
+    for name in [a[2] for a in aggs if a[2] not in ('e', 'n')]:
+        assert runs[1][name].tobytes() == runs[0][name].tobytes(), name
+    sel = mask.astype(bool)
+    np.testing.assert_array_equal(runs[0]['a'], _fsum_by_group(k[sel], _fx_trunc(raw[sel], raw), runs[0]['k']))
 
 
 @pytest.mark.parametrize('mode', ['private', 'shared', 'global_dense', 'partitioned', 'hash'])
