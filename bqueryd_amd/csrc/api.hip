@@ -628,7 +628,7 @@ int fx_shift_for(double m) {
 // bytes of one workgroup's shared-mode LDS table (k_scan_shared): [nsum][S] sums, [S] counts,
 // [S] first rows, then with fixed-point sums [nsum][2][S] limbs
 size_t shared_lds(uint64_t S, int nsum, bool fx) {
-  return (size_t)S * (8 + 8 * (size_t)nsum) + (S & 1) * 4 + (fx ? 16 * (size_t)nsum * S : 0);
+  return (size_t)S * (8 + 8 * (size_t)nsum) + (fx ? 16 * (size_t)nsum * S : 0);
 }
 
 int scan_col(Plan& pl, int tc) {
@@ -1524,7 +1524,9 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         const int64_t tr = L.tile_rows;
         L.ntiles = (N + tr - 1) / tr;
         // contiguous whole-tile row ranges, as many scatter workgroups per CU as fit in LDS
-        int per_cu = L.k == 2 ? 1 : 2;
+        // (2-chunk tiles: three workgroups per CU in turn -- one fits at a time (VGPRs), the
+        // shorter ranges balance the tail: scatter 0.420 -> 0.396 ms at C3, r5k)
+        int per_cu = L.k == 2 ? 3 : 2;
         if (c->opt[kOptPartPerCu]) per_cu = (int)c->opt[kOptPartPerCu];
         L.blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->cu * per_cu, L.ntiles));
         L.rows_per_block = ((L.ntiles + L.blocks - 1) / L.blocks) * tr;

@@ -161,6 +161,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   if (fx)
     for (int i = tid; i < 2 * nsum * W; i += blockDim.x) fxl[i] = 0;
   const unsigned long long inc = PACK ? 1ull << L.sbits : 0ull;  // one row in the packed count field
+  const uint32_t inc_hi = (uint32_t)(inc >> 32);                  // (sbits >= 32)
   __syncthreads();
   const int64_t nt = L.ntiles;
   // (splits <= ntiles: every split's tile range is non-empty, and every split must reach the
@@ -172,15 +173,14 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   // Entries are read in 16-byte granules (4 entries, a lane's one load; a segment's edge
   // granules also hold neighbouring partitions' entries, masked off by their index in the tile):
   // 4-byte loads kept too few bytes in flight -- a loads-only probe of the 4-byte version took
-  // 0.178 of the aggregate's 0.195 ms.  The window's tiles, in LDS: flattened granule start
-  // F[j], global granule base B[j] (granule = B[j] + flattened position), E[j] (entry index in
-  // the tile of a flattened granule's first entry = E[j] + 4 x position) and the segment's
-  // entry range AB[j] = a | b << 16; K + 1 sentinels past the last tile.
+  // 0.178 of the aggregate's 0.195 ms.  The window's tiles, in LDS, one 16-byte record each
+  // (wT[j] = {F, B, E, AB}): flattened granule start F, global granule base B (granule = B +
+  // flattened position), E (entry index in the tile of a flattened granule's first entry = E +
+  // 4 x position) and the segment's entry range AB = a | b << 16; K + 1 sentinels past the
+  // last tile.  A granule's lane finds its tile by comparing against the chunk's K tile starts
+  // (read once per chunk) and fetches that tile's record with one 16-byte LDS read.
   const int WIN = L.win;  // <= kAggWinMax: the header loads below are 4 tiles per thread at most
-  uint32_t* wF = reinterpret_cast<uint32_t*>(smem + part_agg_lds(L.wbits, nsum, PACK, !PACK && L.fx));
-  uint32_t* wB = wF + WIN + kAggK + 1;
-  uint32_t* wE = wB + WIN + kAggK + 1;
-  uint32_t* wAB = wE + WIN + kAggK + 1;
+  uint4* wT = reinterpret_cast<uint4*>(smem + part_agg_lds(L.wbits, nsum, PACK, !PACK && L.fx));
   const uint32_t TG = TR >> 2;  // granules per tile
   // one chunk of at most U x 64 consecutive granules of a wave's range, spanning at most K
   // tiles: per granule its 4 entries, its tile (global index; kNoRow past the chunk), the tile
@@ -246,12 +246,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
 #pragma unroll
     for (int k = 0; k < kHdr; ++k) {
       const int j = per * tid + k;
-      if (k < per && j < nw) {
-        wF[j] = fj;
-        wB[j] = (uint32_t)(w0 + j) * TG + ga[k] - fj;
-        wE[j] = 4u * ga[k] - 4u * fj;
-        wAB[j] = ab[k];
-      }
+      if (k < per && j < nw) wT[j] = make_uint4(fj, (uint32_t)(w0 + j) * TG + ga[k] - fj, 4u * ga[k] - 4u * fj, ab[k]);
       fj += glen[k];
     }
     lds_barrier();
@@ -261,18 +256,13 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
       int lo = 1, hi = nw;  // largest j with F[j] <= gflush
       while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
-        if (wF[mid] <= gflush) lo = mid; else hi = mid;
+        if (wT[mid].x <= gflush) lo = mid; else hi = mid;
       }
-      tot = wF[lo];
+      tot = wT[lo].x;
       nw = lo;
       lds_barrier();
     }
-    for (int j = nw + tid; j <= nw + kAggK; j += blockDim.x) {
-      wF[j] = tot;
-      wB[j] = 0u;
-      wE[j] = 0u;
-      wAB[j] = 0u;
-    }
+    for (int j = nw + tid; j <= nw + kAggK; j += blockDim.x) wT[j] = make_uint4(tot, 0u, 0u, 0u);
     lds_barrier();
     if (PACK) {
       if (since + tot > gflush) {
@@ -286,43 +276,32 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     int jlo = 0, jhi = nw;  // largest j < nw with F[j] <= e_lo
     while (jhi - jlo > 1) {
       const int mid = (jlo + jhi) >> 1;
-      if (wF[mid] <= e_lo) jlo = mid; else jhi = mid;
+      if (wT[mid].x <= e_lo) jlo = mid; else jhi = mid;
     }
     uint32_t f_next = e_lo;
     int j_next = __builtin_amdgcn_readfirstlane(jlo);
-    // issue the next chunk into `en`: lanes 0..K read the chunk's tile bounds, the chunk ends
+    // issue the next chunk into `en`: lanes 0..K read the chunk's tile starts, the chunk ends
     // at U x 64 granules, the wave's range end or the K-th tile boundary
     auto issue = [&](Ent& en) {
-      const int jl = j_next + min(lane, kAggK);
-      const uint32_t lf = wF[jl], lb = wB[jl], le = wE[jl], lab = wAB[jl];
-      uint32_t Fk[kAggK + 1], Bk[kAggK], Ek[kAggK], ABk[kAggK];
+      const uint32_t lf = wT[j_next + min(lane, kAggK)].x;
+      uint32_t Fk[kAggK + 1];
 #pragma unroll
       for (int k = 0; k <= kAggK; ++k) Fk[k] = (uint32_t)__builtin_amdgcn_readlane((int)lf, k);
-#pragma unroll
-      for (int k = 0; k < kAggK; ++k) {
-        Bk[k] = (uint32_t)__builtin_amdgcn_readlane((int)lb, k);
-        Ek[k] = (uint32_t)__builtin_amdgcn_readlane((int)le, k);
-        ABk[k] = (uint32_t)__builtin_amdgcn_readlane((int)lab, k);
-      }
       const uint32_t fe = min(min(f_next + 64u * U, e_hi), max(Fk[kAggK], f_next));
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t f = f_next + u * 64u + lane;
         const bool valid = f < fe;
         const uint32_t fc = valid ? f : f_next;
-        uint32_t j = 0, base = Bk[0], eb = Ek[0], abk = ABk[0];
+        // the granule's tile: the last of the chunk's tiles starting at or before it
+        uint32_t j = 0;
 #pragma unroll
-        for (int k = 1; k < kAggK; ++k) {
-          const bool ge = fc >= Fk[k];
-          j = ge ? (uint32_t)k : j;
-          base = ge ? Bk[k] : base;
-          eb = ge ? Ek[k] : eb;
-          abk = ge ? ABk[k] : abk;
-        }
-        const uint32_t gidx = f_next < fe ? base + fc : 0u;
-        en.t[u] = valid ? (uint32_t)w0 + (uint32_t)j_next + j : kNoRow;
-        en.e0[u] = eb + 4u * fc;
-        en.ab[u] = abk;
+        for (int k = 1; k < kAggK; ++k) j += fc >= Fk[k] ? 1u : 0u;
+        const uint4 tr = wT[j_next + j];
+        const uint32_t gidx = f_next < fe ? tr.y + fc : 0u;
+        en.t[u] = (uint32_t)w0 + (uint32_t)j_next + j;
+        en.e0[u] = tr.z + 4u * fc;
+        en.ab[u] = valid ? tr.w : 0u;  // an empty entry range past the chunk
         en.m[u] = reinterpret_cast<const uint4*>(L.meta)[gidx];
         if (PACK) {
           // rows in tile where the tile recorded them; the other lanes re-read word 0 (the
@@ -359,21 +338,26 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
     auto consume = [&](const Ent& en) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (en.t[u] == kNoRow) continue;
+        // entry e of the granule is the segment's iff a <= e0 + e < b: (e0 - a) + e < b - a
+        // unsigned (an entry below a wraps past it); granules past the chunk have a = b = 0
         const uint32_t a = en.ab[u] & 0xFFFFu, b = en.ab[u] >> 16;
+        const uint32_t d = en.e0[u] - a, n = b - a;
         const uint32_t mm[4] = {en.m[u].x, en.m[u].y, en.m[u].z, en.m[u].w};
+        // PACK: the first-appearance key is the exact row in a tile with row records, else the
+        // tile's last row (per granule: the base key, and the rows in tile or zero)
+        const bool hr = en.t[u] < rit_tiles;
+        const uint32_t kb = en.t[u] * TR + (hr ? 0u : TR - 1u);
+        const uint32_t r01 = PACK && hr ? en.rr[u].x : 0u, r23 = PACK && hr ? en.rr[u].y : 0u;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const uint32_t ei = en.e0[u] + (uint32_t)e;  // entry index in the tile
-          if (ei < a || ei >= b) continue;            // a neighbouring partition's entry
+          if (d + (uint32_t)e >= n) continue;  // a neighbouring partition's entry
           const uint32_t sl = mm[e] & lowmask;
           if (PACK) {
-            // fire-and-forget LDS atomics: nothing in the loop waits on the LDS; the first-
-            // appearance key is the exact row in a tile with row records, else the tile's last
-            const uint32_t rw = e < 2 ? en.rr[u].x : en.rr[u].y;
-            const uint32_t rit = (e & 1) ? rw >> 16 : rw & 0xFFFFu;
-            const uint32_t key = en.t[u] * TR + (en.t[u] < rit_tiles ? rit : TR - 1u);
-            atomicAdd(&acc[sl], inc + (unsigned long long)(mm[e] >> 16));
+            // fire-and-forget LDS atomics: nothing in the loop waits on the LDS
+            const uint32_t rw = e < 2 ? r01 : r23;
+            const uint32_t key = kb + ((e & 1) ? rw >> 16 : rw & 0xFFFFu);
+            // count field + code16 (inc has no low bits, code16 < 2^16: an OR, one shift)
+            atomicAdd(&acc[sl], ((unsigned long long)inc_hi << 32) | (mm[e] >> 16));
             atomicMin(&fst[sl], key);
             continue;
           }

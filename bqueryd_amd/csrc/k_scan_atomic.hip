@@ -25,8 +25,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][S]
   uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)nsum * S);    // [S]
   uint32_t* fst = cnt + S;                                                 // [S]
-  // fixed-point sums (sum_enc 3): limbs 1 and 2 [nsum][2][S] after the table (sa.fx set)
-  unsigned long long* fxl = reinterpret_cast<unsigned long long*>(fst + S + (S & 1));
+  // fixed-point sums (sum_enc 3): limbs 1 and 2 [nsum][2][S] after the table (sa.fx set;
+  // 8-byte aligned: the table is 8 (nsum + 1) S bytes)
+  unsigned long long* fxl = reinterpret_cast<unsigned long long*>(fst + S);
   for (int i = tid; i < S; i += kBlock) {
     cnt[i] = 0;
     fst[i] = kNoRow;
