@@ -1606,8 +1606,12 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       }
       hipFunction_t fs = nullptr, ff = nullptr;
       if (c->opt[kOptJit] && N >= c->jit_min_rows()) {
-        const std::string extra = "#define BQ_PART_K " + std::to_string(L.k) + "\n#define BQ_PART_NARROW " +
-                                  std::to_string(L.narrow) + "\n#define BQ_PART_PACK " + std::to_string(L.pack) + "\n";
+        std::string extra = "#define BQ_PART_K " + std::to_string(L.k) + "\n#define BQ_PART_NARROW " +
+                            std::to_string(L.narrow) + "\n#define BQ_PART_PACK " + std::to_string(L.pack) + "\n";
+        if (L.narrow) {  // the summed columns' code kinds (partition.h part_kind)
+          extra += "#define BQ_PART_ENC ";
+          for (int q = 0; q < kMaxSums; ++q) extra += std::to_string(q < nsum ? L.enc_kind[q] : 0) + (q + 1 < kMaxSums ? "," : "\n");
+        }
         fs = jit_function_for("bq_jit_part_scatter", pl.p, extra);
         if (pk) ff = jit_function_for("bq_jit_part_first_rows", pl.p, extra);
         c->last.specialized = fs ? 1 : 0;

@@ -79,10 +79,22 @@ constexpr int kPartBlock = 1024;
 // entries into P far-apart regions and ran at 3.4 TB/s of moved bytes; the linear tile
 // writes run at copy speed (2.8 GB in 0.57 ms), with no count pass and no scan.
 // The exact 32-bit code of a summed float value (narrow entries, PartLaunch::enc_kind)
+// (the query-specialised build fixes the code kinds -- BQ_PART_ENC, one per summed column --
+// so a dyadic code is one multiply and conversion, with no per-row branch to the cents rounding)
+__device__ __forceinline__ int part_kind(const PartLaunch& L, int q) {
+#ifdef BQ_PART_ENC
+  constexpr int kinds[kMaxSums] = {BQ_PART_ENC};
+  return kinds[q];
+#else
+  return L.enc_kind[q];
+#endif
+}
+
 __device__ __forceinline__ uint32_t part_enc(const ScanParams& p, const PartLaunch& L, int q, uint64_t v) {
-  if (L.enc_kind[q] == 3) return (uint32_t)(v - (uint64_t)L.enc_off[q]);  // canonical int64 value
+  const int kind = part_kind(L, q);
+  if (kind == 3) return (uint32_t)(v - (uint64_t)L.enc_off[q]);  // canonical int64 value
   const double d = value_f64(v, p.sum_conv[q]) * L.enc_mul[q];
-  return (uint32_t)(int32_t)(L.enc_kind[q] == 1 ? d : rint(d));
+  return (uint32_t)(int32_t)(kind == 1 ? d : rint(d));
 }
 
 // PACK (PartLaunch::pack): one 32-bit word per entry, the summed column's 16-bit code (if
