@@ -284,6 +284,11 @@ struct ColumnPool {
   std::multimap<size_t, void*> idle;  // capacity -> block
   size_t idle_bytes = 0;
   static constexpr size_t kMaxIdle = size_t(8) << 30;
+  // column memory held from the device (handed out + idle), and the context's budget for it
+  // (option mem_cap_mb; 0 = the device's memory): past the budget an allocation fails as an
+  // out-of-memory hipMalloc would
+  size_t allocated = 0;
+  size_t budget = 0;
   void* get(size_t bytes, size_t* cap) {
     auto it = idle.lower_bound(bytes);
     if (it != idle.end() && it->first <= bytes + bytes / 2 + (size_t(1) << 20)) {
@@ -294,11 +299,16 @@ struct ColumnPool {
       return p;
     }
     void* p = nullptr;
+    if (budget && allocated + bytes > budget) {
+      release();
+      if (allocated + bytes > budget) return nullptr;
+    }
     if (hipMalloc(&p, bytes) != hipSuccess) {
       // release the idle blocks and retry once
       release();
       if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
     }
+    allocated += bytes;
     *cap = bytes;
     return p;
   }
@@ -309,6 +319,7 @@ struct ColumnPool {
     while (idle_bytes > kMaxIdle && !idle.empty()) {
       auto last = std::prev(idle.end());
       idle_bytes -= last->first;
+      allocated -= last->first;
       (void)hipFree(last->second);
       idle.erase(last);
     }
@@ -316,6 +327,7 @@ struct ColumnPool {
   void release() {
     for (auto& kv : idle) (void)hipFree(kv.second);
     idle.clear();
+    allocated -= idle_bytes;
     idle_bytes = 0;
   }
 };
@@ -328,7 +340,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kOptMemCap, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -358,6 +370,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"compact", 1, 0, 2},                   // private / shared / dense global scans read compact column copies
     {"part_first", 0, 0, 2},                // packed partitioned path: rows in tile recorded for 0 auto / 1 no / 2 every tile
     {"fx_sums", 1, 0, 1},                   // atomic modes: fixed-point float sums (bit-reproducible)
+    {"mem_cap_mb", 0, 0, 1ll << 24},        // column memory budget of the context in MiB (0: the device's)
 };
 
 static int opt_index(const char* name) {
@@ -441,6 +454,7 @@ bool drop_shadows(bqg_ctx* c, bqg_table* t) {
 // before giving up the compact copies of every table of the context are released -- they are
 // a rebuildable cache, the base columns are not.
 void* col_alloc(bqg_ctx* c, size_t need, size_t* cap, bool may_drop_shadows = true) {
+  c->colpool.budget = (size_t)c->opt[kOptMemCap] << 20;
   void* p = c->colpool.get(need, cap);
   if (p) return p;
   (void)hipGetLastError();

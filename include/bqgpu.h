@@ -201,6 +201,12 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *                     code (and the std pass's centred squares) as
  *                     fixed-point limbs in integer atomics -- the same bits
  *                     on every run (0: float64 atomics, arrival order)
+ *   mem_cap_mb     0  the context's budget for resident column memory     0 | MiB
+ *                     (tables' columns and compact copies, pooled blocks
+ *                     included; 0: the device's memory).  Past it a copy is
+ *                     not built (the scan reads the column as stored) and a
+ *                     column allocation first releases every table's
+ *                     copies, then fails with BQG_E_OOM
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);

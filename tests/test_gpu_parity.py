@@ -1139,6 +1139,64 @@ def test_compact_copies_accounting(oracle_c):
         t.close()
 
 
+def test_column_memory_budget(oracle_c):
+    """Option mem_cap_mb (a context's budget for resident column memory): compact copies that do
+    not fit are not built -- the scan reads the columns as stored, same answer; a table that
+    fits only without another table's copies releases them (a rebuildable cache) instead of
+    failing, and the copies are not rebuilt past the budget; a table that cannot fit fails with
+    an out-of-memory error and leaves the context and its tables usable (the shadow
+    allocation failure path)."""
+    from bqueryd_amd._lib import BqgError
+    from bqueryd_amd.engine import Device
+    rng = np.random.default_rng(13)
+    n = 2_000_000
+    MB = 1 << 20
+
+    def shard():
+        return OrderedDict(k=rng.integers(0, 9, n).astype(np.int32), p=rng.integers(0, 10, n).astype(np.int32),
+                           v=np.round(rng.lognormal(2.3, 0.6, n).clip(2.5, 500) * 64) / 64)
+    aggs = [['v', 'sum', 's'], ['v', 'count', 'n']]
+    terms = [('p', '>=', 2)]
+    dev = Device(0)  # a context of its own: its pool holds this test's columns only
+    tables = []
+    try:
+        dev.set_option('compact', 1)
+        a_cols = shard()
+        ref = oracle_c.groupby(a_cols, ['k'], aggs, oracle_c.where_terms(a_cols, terms))
+        a = ShardTable(a_cols, device=dev)
+        tables.append(a)
+        base = a.device_bytes()  # 16 B/row; the copies take 4 B/row (1 + 1 + 2-byte codes)
+        # (budgets in whole MiB: base + 0.5 MiB rounded up leaves less headroom than the smallest
+        # copy, 2 M one-byte codes)
+        dev.set_option('mem_cap_mb', -(-(base + MB // 2) // MB))
+        dev.enable_timing(True)
+        got, _ = a.groupby(['k'], aggs, where_terms=terms)
+        info = dev.last_timing()
+        assert info['bytes_read'] == info['bytes'] and a.device_bytes() == base, info
+        assert_tables_equal(got, ref, exact_cols={'s'})
+        # room for A and its copies, and for B only without them
+        dev.set_option('mem_cap_mb', -(-(2 * base + MB // 2) // MB))
+        got, _ = a.groupby(['k'], aggs, where_terms=terms)
+        assert dev.last_timing()['bytes_read'] < info['bytes'] and a.device_bytes() > base
+        b_cols = shard()
+        b = ShardTable(b_cols, device=dev)
+        tables.append(b)
+        assert a.device_bytes() == base and b.device_bytes() == base
+        for t, c in ((a, a_cols), (b, b_cols)):
+            got, _ = t.groupby(['k'], aggs, where_terms=terms)
+            assert dev.last_timing()['bytes_read'] == info['bytes']  # no room to rebuild the copies
+            assert_tables_equal(got, oracle_c.groupby(c, ['k'], aggs, oracle_c.where_terms(c, terms)), exact_cols={'s'})
+        with pytest.raises(BqgError, match='allocation'):
+            tables.append(ShardTable(shard(), device=dev))
+        got, _ = b.groupby(['k'], aggs, where_terms=terms)
+        assert_tables_equal(got, oracle_c.groupby(b_cols, ['k'], aggs, oracle_c.where_terms(b_cols, terms)),
+                            exact_cols={'s'})
+    finally:
+        for t in tables:
+            t.close()
+        dev.close()
+
+
 @pytest.mark.parametrize('opt,val', [('part_wbits', 6), ('part_wbits', 10), ('part_wbits', 13), ('scd_compact', 0),
                                      ('priv_ahead', 1), ('priv_ahead', 2), ('priv_ahead', 4),
                                      ('private_per_cu', 1), ('private_per_cu', 3), ('small_emit', 0)])
