@@ -340,7 +340,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kOptMemCap, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kOptMemCap, kOptPartRing, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -371,6 +371,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"part_first", 0, 0, 2},                // packed partitioned path: rows in tile recorded for 0 auto / 1 no / 2 every tile
     {"fx_sums", 1, 0, 1},                   // atomic modes: fixed-point float sums (bit-reproducible)
     {"mem_cap_mb", 0, 0, 1ll << 24},        // column memory budget of the context in MiB (0: the device's)
+    {"part_ring", 0, 0, 2},                 // packed scatter (JIT): tiles of row loads in flight (0: 1)
 };
 
 static int opt_index(const char* name) {
@@ -1579,11 +1580,13 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       c->last.narrow = pk ? 2 : L.narrow;
       const int64_t tr = L.tile_rows;
       L.capacity = (uint64_t)L.ntiles * (uint64_t)tr;
-      L.hdr = (uint16_t*)c->prefix.ensure((size_t)L.ntiles * (size_t)(L.nparts + 1) * 2 + 256);
+      // (+ one spare tile of header and entry words: the packed scatter's ring writes a block's
+      // tiles past its rows there, partition.h)
+      L.hdr = (uint16_t*)c->prefix.ensure((size_t)(L.ntiles + 1) * (size_t)(L.nparts + 1) * 2 + 256);
       // one scratch block: entry values | entry meta | split partial tables
       // (| pack: first tile tags, tile marks)
       const size_t vbytes = pk ? 0 : ((size_t)L.capacity * (nw ? 4 : 8) * (size_t)std::max(nsum, 1) + 255) & ~size_t(255);
-      const size_t mbytes = ((size_t)L.capacity * 4 + 255) & ~size_t(255);
+      const size_t mbytes = (((size_t)L.capacity + (size_t)tr) * 4 + 255) & ~size_t(255);
       // split records: [W] counts, [W] sums ([W] first rows / tiles); packed entries always
       // have one (an aggregate that flushes its accumulators adds into it)
       L.partial_bytes = ((pk ? ((size_t)1 << L.wbits) * 20 : part_agg_lds(L.wbits, nsum, pk, L.fx)) + 255) & ~size_t(255);
@@ -1622,6 +1625,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       if (c->opt[kOptJit] && N >= c->jit_min_rows()) {
         std::string extra = "#define BQ_PART_K " + std::to_string(L.k) + "\n#define BQ_PART_NARROW " +
                             std::to_string(L.narrow) + "\n#define BQ_PART_PACK " + std::to_string(L.pack) + "\n";
+        // packed entries: tiles of row loads in flight per scatter workgroup (option part_ring)
+        if (pk && c->opt[kOptPartRing] > 1) extra += "#define BQ_PART_RING " + std::to_string(c->opt[kOptPartRing]) + "\n";
         if (L.narrow) {  // the summed columns' code kinds (partition.h part_kind)
           extra += "#define BQ_PART_ENC ";
           for (int q = 0; q < kMaxSums; ++q) extra += std::to_string(q < nsum ? L.enc_kind[q] : 0) + (q + 1 < kMaxSums ? "," : "\n");

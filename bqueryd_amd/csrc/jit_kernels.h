@@ -20,6 +20,9 @@
 #ifndef BQ_PART_PACK
 #define BQ_PART_PACK 0
 #endif
+#ifndef BQ_PART_RING
+#define BQ_PART_RING 1
+#endif
 
 namespace bqg {
 __device__ __forceinline__ void jit_specialize(ScanParams& p) { BQ_SPEC }
@@ -32,11 +35,14 @@ extern "C" __global__ __launch_bounds__(256, 4) void bq_jit_scan_private(bqg::Sc
   bqg::scan_private_body<BQ_NC>(p, L, smem);
 }
 
-extern "C" __global__ __launch_bounds__(1024) void bq_jit_part_scatter(bqg::ScanParams pin, bqg::PartLaunch L) {
+#ifndef BQ_PART_THREADS
+#define BQ_PART_THREADS 1024
+#endif
+extern "C" __global__ __launch_bounds__(BQ_PART_THREADS) void bq_jit_part_scatter(bqg::ScanParams pin, bqg::PartLaunch L) {
   extern __shared__ __align__(16) unsigned char smem[];
   bqg::ScanParams p = pin;
   bqg::jit_specialize(p);
-  bqg::part_scatter_body<BQ_NC, BQ_PART_K, BQ_PART_NARROW != 0, BQ_PART_PACK != 0>(p, L, smem);
+  bqg::part_scatter_body<BQ_NC, BQ_PART_K, BQ_PART_NARROW != 0, BQ_PART_PACK != 0, BQ_PART_RING>(p, L, smem);
 }
 
 extern "C" __global__ __launch_bounds__(bqg::kFirstRowsBlock) void bq_jit_part_first_rows(bqg::ScanParams pin, bqg::PartLaunch L,

@@ -104,8 +104,14 @@ __device__ __forceinline__ uint32_t part_code16(const ScanParams& p, const PartL
   return (part_enc(p, L, 0, v) - (uint32_t)L.enc_base16) << 16;
 }
 
-template <int NC, int K = 1, bool NARROW = false, bool PACK = false>
+// RING (packed entries): the tiles' row loads are issued RING tiles ahead (RING register sets
+// used in turn), so a workgroup keeps RING tiles of reads in flight across the barriers of the
+// tile it sorts; a block's last group of RING tiles may run past its rows -- such a tile
+// passes no row and writes its header and entry words to the spare tile past the last
+// (PartLaunch::ntiles; allocated, never read).
+template <int NC, int K = 1, bool NARROW = false, bool PACK = false, int RING = 1>
 __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const PartLaunch& L, unsigned char* smem) {
+  static_assert(RING == 1 || PACK, "only packed entries have a spare tile for the ring's tail");
   // K 4-row chunks per thread and tile (TR = T * 4 * K rows): chunk k of thread t covers rows
   // base + k * T * 4 + t * 4 .. + 3, so every chunk load of the workgroup is one coalesced block
   const int T = blockDim.x, tid = threadIdx.x;
@@ -131,11 +137,22 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   const int q1 = min(P, q0 + per);
   const uint32_t all = (1u << NC) - 1u;
   const int64_t CH = (int64_t)T * kRowsPerThread;  // rows of one chunk block
-  Chunk raw[K][NC];
+  Chunk ring[RING][K][NC];
 #pragma unroll
-  for (int k = 0; k < K; ++k) load_rows4_clamped<NC>(p, begin + k * CH + (int64_t)tid * kRowsPerThread, end, raw[k], all, begin);
+  for (int g = 0; g < RING; ++g)
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      load_rows4_clamped<NC>(p, begin + g * TR + k * CH + (int64_t)tid * kRowsPerThread, end, ring[g][k], all, begin);
   int parity = 0;
-  for (int64_t base = begin; base < end; base += TR, parity ^= 1) {
+  for (int64_t gbase = begin; gbase < end; gbase += RING * TR) {
+#pragma unroll
+  for (int g = 0; g < RING; ++g, parity ^= 1) {
+    const int64_t base = gbase + g * TR;
+    Chunk (&raw)[K][NC] = ring[g];
+    // the tile whose header and entries this one writes (RING: the spare tile past the last
+    // when the block's rows ended before it)
+    const int64_t tile = RING == 1 || base < end ? base / TR : L.ntiles;
+    const int64_t obase = tile * TR;
     // the tile histogram alternates between two buffers: the one this tile zeroes at its end
     // is next counted into two tiles later, past the next tile's barriers
     uint32_t* hist = hist2 + parity * P;
@@ -149,7 +166,7 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
       const int64_t row0 = base + k * CH + (int64_t)tid * kRowsPerThread;
       uint64_t v[NC][4], code[4];
       decode_all<NC, 4>(p, raw[k], v);
-      load_rows4_clamped<NC>(p, row0 + TR, end, raw[k], all, begin);
+      load_rows4_clamped<NC>(p, row0 + RING * TR, end, raw[k], all, begin);
       pass[k] = vals_pass<NC, 4>(p, row0, v);
       const int64_t rem = end - row0;
       pass[k] &= rem >= 4 ? 0xFu : (rem > 0 ? ((1u << rem) - 1u) : 0u);
@@ -180,7 +197,7 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
     for (int i = q0; i < q1; ++i) local += hist[i];
     uint32_t n_tile;
     uint32_t run = block_excl_scan_1b(local, wsum2 + parity * 16, &n_tile);
-    uint16_t* th = L.hdr + (size_t)(base / TR) * (size_t)(P + 1);
+    uint16_t* th = L.hdr + (size_t)tile * (size_t)(P + 1);
     for (int i = q0; i < q1; ++i) {
       toff[i] = run;
       th[i] = (uint16_t)run;
@@ -189,7 +206,7 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
     if (tid == 0) th[P] = (uint16_t)n_tile;
     lds_barrier();
     // PACK: this tile records its entries' rows in tile (PartLaunch::rit; uniform)
-    const bool with_rit = PACK && base / TR < L.rit_tiles;
+    const bool with_rit = PACK && tile < L.rit_tiles;
     // stage the tile sorted by partition
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -217,21 +234,21 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
     // linear copy-out: K 16-byte stores of meta and 2K per summed column, every thread
 #pragma unroll
     for (int k = 0; k < K; ++k)
-      *reinterpret_cast<uint4*>(L.meta + base + 4 * (tid + k * T)) = *reinterpret_cast<const uint4*>(smeta + 4 * (tid + k * T));
+      *reinterpret_cast<uint4*>(L.meta + obase + 4 * (tid + k * T)) = *reinterpret_cast<const uint4*>(smeta + 4 * (tid + k * T));
     if (with_rit)
       for (int i = tid; i < TR / 8; i += T)
-        *reinterpret_cast<uint4*>(L.rit + base + 8 * i) = *reinterpret_cast<const uint4*>(srit + 8 * i);
+        *reinterpret_cast<uint4*>(L.rit + obase + 8 * i) = *reinterpret_cast<const uint4*>(srit + 8 * i);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (PACK || s >= nsum) break;
       if (NARROW) {
-        uint32_t* dv = reinterpret_cast<uint32_t*>(L.vals) + (size_t)s * L.capacity + base;
+        uint32_t* dv = reinterpret_cast<uint32_t*>(L.vals) + (size_t)s * L.capacity + obase;
         const uint32_t* lv = sval32 + (size_t)s * TR;
 #pragma unroll
         for (int k = 0; k < K; ++k)
           *reinterpret_cast<uint4*>(dv + 4 * (tid + k * T)) = *reinterpret_cast<const uint4*>(lv + 4 * (tid + k * T));
       } else {
-        unsigned long long* dv = L.vals + (size_t)s * L.capacity + base;
+        unsigned long long* dv = L.vals + (size_t)s * L.capacity + obase;
         const unsigned long long* lv = sval + (size_t)s * TR;
 #pragma unroll
         for (int k = 0; k < 2 * K; ++k)
@@ -239,6 +256,7 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
       }
     }
     for (int i = q0; i < q1; ++i) hist[i] = 0;
+  }
   }
 }
 

@@ -207,6 +207,8 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *                     not built (the scan reads the column as stored) and a
  *                     column allocation first releases every table's
  *                     copies, then fails with BQG_E_OOM
+ *   part_ring      0  packed partitioned scatter (query-specialised): tiles 0 (1) | 1 | 2
+ *                     of row loads in flight per workgroup
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);
