@@ -1199,17 +1199,18 @@ def test_column_memory_budget(oracle_c):
 
 @pytest.mark.parametrize('opt,val', [('part_wbits', 6), ('part_wbits', 10), ('part_wbits', 13), ('scd_compact', 0),
                                      ('priv_ahead', 1), ('priv_ahead', 2), ('priv_ahead', 4),
-                                     ('private_per_cu', 1), ('private_per_cu', 3), ('small_emit', 0)])
+                                     ('private_per_cu', 1), ('private_per_cu', 3), ('small_emit', 0),
+                                     ('part_ring', 1), ('part_ring', 2)])
 def test_remaining_engine_options(opt, val, oracle_c, engine_options):
     """The engine options no other test sets, each at non-default values, on the query shape
-    it steers (partition width: a partitioned C3-shaped query; the fused distinct pass's value
+    it steers (partition width and the scatter's ring: a partitioned C3-shaped query; the fused distinct pass's value
     codes: C4; the private scan's tiles in flight and workgroups per CU, run-time specialised:
     C2; the one-workgroup emit off: a shared-mode query), against the C restatement -- so that
     every option value the header lists has run against the oracle."""
     engine_options(**{opt: val, 'jit': 1, 'jit_min_rows': 0})
     rng = np.random.default_rng(sum(map(ord, opt)) * 16 + val)
     n = 400_003
-    if opt == 'part_wbits':
+    if opt in ('part_wbits', 'part_ring'):  # (part_ring: packed entries, each block's spare tile)
         cols = OrderedDict(k=rng.integers(0, 90_000, n).astype(np.int32), g=rng.integers(1, 3, n).astype(np.int32),
                            v=np.round(rng.normal(size=n) * 64) / 64)
         keys, aggs, terms, mode = ['k', 'g'], [['v', 'sum', 's'], ['v', 'count', 'n']], [], 4
