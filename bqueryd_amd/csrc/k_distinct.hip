@@ -264,25 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_scd_fused(ScanParams p, ScdLaunch d)
   scd_fused_body<NC, COMPACT, RUNS>(p, d, smem);
 }
 
-struct ScdState {
-  uint32_t present;
-  uint32_t first_row;
-  unsigned long long first, last, changes, rows;
-};
-
-__device__ __forceinline__ ScdState scd_combine(const ScdState& a, const ScdState& b, bool isf) {
-  if (!a.present) return b;
-  if (!b.present) return a;
-  ScdState r;
-  r.present = 1;
-  r.first_row = a.first_row;
-  r.rows = a.rows + b.rows;
-  r.first = a.first;
-  r.last = b.last;
-  r.changes = a.changes + b.changes + (scd_equal(a.last, b.first, isf) ? 0ull : 1ull);
-  return r;
-}
-
+// (ScdState / scd_combine: scd.h, shared with the fused pass's in-workgroup fold)
 __device__ __forceinline__ ScdState scd_load(const ScdLaunch& d, size_t idx, bool valid) {
   ScdState x;
   x.first_row = d.st_first_row[idx];
@@ -416,20 +398,28 @@ void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hi
   int isf = 0;
   for (int c = 0; c < p.ncols; ++c)
     if (c == d.vcol) isf = dtype_is_float(p.cols[c].dtype);
+  // the fused pass folds its workgroup's waves and flushes one state per workgroup: `blocks`
+  // chunks; the per-wave pass flushes one per wave
+  ScdLaunch dc = d;
+  if (d.fused) dc.waves = blocks;
   // stage 1: ~2 threads per CU lane over (slot, run of chunks); stage 2 folds the runs per slot
   const uint64_t S = p.nslots;
   const uint64_t target = (uint64_t)device_cu_count() * kBlock * 2;
   uint64_t want = (target + S - 1) / S;
-  if (want > (uint64_t)d.waves) want = (uint64_t)d.waves;
+  if (want > (uint64_t)dc.waves) want = (uint64_t)dc.waves;
   if (want < 1) want = 1;
-  const int per = (int)(((uint64_t)d.waves + want - 1) / want);
-  const int runs = (int)(((uint64_t)d.waves + per - 1) / per);
+  int per = (int)(((uint64_t)dc.waves + want - 1) / want);
+  // few slots: runs of up to 32 chunks, ~64 runs per slot -- stage 2 then folds one run per
+  // lane (C4's 1792 chunks x 265 slots: 29.7 + 13.7 us against 20.5 + 34.0 us at 4 chunks a
+  // run, profiles/r5s_c4_combine.txt)
+  if (per < 32 && dc.waves > 64 * per) per = std::min(32, (int)((dc.waves + 63) / 64));
+  const int runs = (int)(((uint64_t)dc.waves + per - 1) / per);
   const uint64_t items = S * (uint64_t)runs;
-  hipLaunchKernelGGL(k_scd_combine_runs, dim3((unsigned)((items + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, d, S,
+  hipLaunchKernelGGL(k_scd_combine_runs, dim3((unsigned)((items + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, dc, S,
                      per, runs, isf);
   if (runs > 1) {
     const uint64_t cblocks = S < 65536 ? S : 65536;  // grid-stride over slots beyond
-    hipLaunchKernelGGL(k_scd_combine, dim3((unsigned)cblocks), dim3(kBlock), 0, st, d, S, per, runs, isf);
+    hipLaunchKernelGGL(k_scd_combine, dim3((unsigned)cblocks), dim3(kBlock), 0, st, dc, S, per, runs, isf);
   }
 }
 }  // namespace bqg

@@ -46,6 +46,28 @@ __device__ __forceinline__ bool scd_equal(uint64_t a, uint64_t b, bool isf) {
   return isf ? (as_f64(a) == as_f64(b)) : (a == b);
 }
 
+// One chunk's state of one slot as the chunk combine folds it (k_distinct.hip): two
+// consecutive chunks fold as rows and changes added, plus one change where the first chunk's
+// last value differs from the second's first.
+struct ScdState {
+  uint32_t present;
+  uint32_t first_row;
+  unsigned long long first, last, changes, rows;
+};
+
+__device__ __forceinline__ ScdState scd_combine(const ScdState& a, const ScdState& b, bool isf) {
+  if (!a.present) return b;
+  if (!b.present) return a;
+  ScdState r;
+  r.present = 1;
+  r.first_row = a.first_row;
+  r.rows = a.rows + b.rows;
+  r.first = a.first;
+  r.last = b.last;
+  r.changes = a.changes + b.changes + (scd_equal(a.last, b.first, isf) ? 0ull : 1ull);
+  return r;
+}
+
 // Row loads of one 64-row step: rows are addressed relative to the wave's chunk (32-bit lane
 // offsets from a uniform base, so the address math is one VALU op per column), 4- and 8-byte
 // columns load their element directly, narrower ones the aligned 8-byte word holding it.
@@ -463,33 +485,51 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       }
     }
   }
-  if (!live) return;
-  // every lane's state writes precede the flush reads (wave-private LDS, program order)
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  for (int i = lane; i < S; i += 64) {
-    const size_t o = (size_t)w * S + i;
-    if (COMPACT) {
-      const ScdSlot32 c = st32[i];
-      const uint32_t rows = c.rc & 0xFFFFu;
-      if (p16) {
-        d.st_first_row[o] = rows ? (uint32_t)start + (fv32[i] >> 16) : kNoRow;
-        d.st_first[o] = (uint64_t)d.vmin + (fv32[i] & 0xFFFFu);
+  // the workgroup's waves own consecutive chunks: their states are folded here, in chunk order,
+  // and flushed as ONE chunk state per (workgroup, slot) -- a quarter of the per-wave states for
+  // the chunk combine to read (C4: 53 -> 13 MB; launch_scd combines `blocks` chunks)
+  __syncthreads();  // every wave's LDS state is final
+  const int nwv = (int)(blockDim.x >> 6);
+  for (int i = threadIdx.x; i < S; i += blockDim.x) {
+    ScdState acc = {0u, kNoRow, 0ull, 0ull, 0ull, 0ull};
+    for (int v = 0; v < nwv; ++v) {
+      const int wv = blockIdx.x * nwv + v;
+      if (wv >= d.waves) break;
+      const unsigned char* vb = smem + (size_t)v * d.wave_lds;
+      ScdState x;
+      if (COMPACT) {
+        const ScdSlot32* s32 = reinterpret_cast<const ScdSlot32*>(vb);
+        const uint32_t* f32 = reinterpret_cast<const uint32_t*>(s32 + S);
+        const ScdSlot32 c = s32[i];
+        const uint32_t rows = c.rc & 0xFFFFu;
+        x.present = rows != 0;
+        x.rows = rows;
+        x.changes = c.rc >> 16;
+        x.last = (uint64_t)d.vmin + c.last;
+        if (p16) {
+          x.first_row = (uint32_t)((int64_t)wv * d.chunk_rows) + (f32[i] >> 16);
+          x.first = (uint64_t)d.vmin + (f32[i] & 0xFFFFu);
+        } else {
+          x.first_row = f32[S + i];
+          x.first = (uint64_t)d.vmin + f32[i];
+        }
       } else {
-        d.st_first_row[o] = rows ? fr32[i] : kNoRow;
-        d.st_first[o] = (uint64_t)d.vmin + fv32[i];
+        const ScdSlot c = reinterpret_cast<const ScdSlot*>(vb)[i];
+        x.present = c.rows != 0;
+        x.first_row = c.first_row;
+        x.first = c.first;
+        x.last = c.last;
+        x.changes = c.changes;
+        x.rows = c.rows;
       }
-      d.st_last[o] = (uint64_t)d.vmin + c.last;
-      d.st_changes[o] = c.rc >> 16;
-      d.st_count[o] = rows;
-    } else {
-      const ScdSlot c = st[i];
-      d.st_first_row[o] = c.rows ? c.first_row : kNoRow;
-      d.st_first[o] = c.first;
-      d.st_last[o] = c.last;
-      d.st_changes[o] = c.changes;
-      d.st_count[o] = c.rows;
+      acc = scd_combine(acc, x, isf);
     }
+    const size_t o = (size_t)blockIdx.x * S + i;
+    d.st_first_row[o] = acc.present ? acc.first_row : kNoRow;
+    d.st_first[o] = acc.first;
+    d.st_last[o] = acc.last;
+    d.st_changes[o] = (uint32_t)acc.changes;
+    d.st_count[o] = (uint32_t)acc.rows;
   }
 }
 
