@@ -142,6 +142,11 @@ struct ColStats {
   // cannot overflow; the atomic modes and the wide partitioned entries): a superset of enc
   int enc64 = 0;
   int enc64_k = 0;
+  // float columns: the weight 2^lsb_exp of the lowest set bit over every finite nonzero value
+  // (INT_MAX: none), and whether a subnormal occurs -- a fixed-point sum at shift s is exact iff
+  // lsb_exp >= -s and no subnormal
+  int lsb_exp = INT_MAX;
+  bool subnormal = false;
   int64_t runs = -1;  // value runs (rows differing from the row before + 1), -1 = not measured
 };
 
@@ -514,6 +519,9 @@ void finish_stats(Column& k, const unsigned long long* r, int64_t nrows) {
       // exact 32-bit codes (k_stats): dyadic first (the code's sum times 2^-k is the exact sum
       // whenever it is below 2^53), else whole hundredths; |code| < 2^31 for every value
       const double maxabs = std::max(std::fabs(k.stats.fmin), std::fabs(k.stats.fmax));
+      k.stats.lsb_exp = lsb == ~0ull ? INT_MAX : (int)lsb - 4096;
+      // (k_stats sets enc bit 0 for infinities and subnormals)
+      k.stats.subnormal = (enc & 1ull) && !std::isinf(k.stats.fmin) && !std::isinf(k.stats.fmax);
       if (!k.stats.has_nan) {
         const int kk = lsb == ~0ull ? 0 : std::max(0, 4096 - (int)lsb);
         if (!(enc & 1ull) && kk <= 62 && std::ldexp(maxabs, kk) < 2147483647.0) {
@@ -787,6 +795,10 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
       if (cs.empty || cs.has_nan || std::isinf(cs.fmin) || std::isinf(cs.fmax)) continue;
       pl.p.sum_fx_shift[q] = fx_shift_for(std::max(std::fabs(cs.fmin), std::fabs(cs.fmax)));
       if (cs.enc64 && c->opt[kOptPartNarrow] != 0) continue;  // integer codes already (set_sum_codes)
+      // only where every value is a multiple of 2^-shift: the limb sums are then the EXACT sums
+      // (one rounding at the end) -- a column whose values span more than 2^42 in magnitude
+      // (an outlier beside small values) keeps the float64 atomics, whose error is relative
+      if (cs.subnormal || (cs.lsb_exp != INT_MAX && cs.lsb_exp < -pl.p.sum_fx_shift[q])) continue;
       pl.fx_states |= 1 << q;
     }
     // the std pass's (x - mean)^2 <= (max - min)^2

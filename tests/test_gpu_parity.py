@@ -915,7 +915,7 @@ def test_atomic_mode_float_sums_reproducible(mode, values, oracle_c, engine_opti
 @pytest.mark.parametrize('splits', [0, 3])
 @pytest.mark.parametrize('mode', ['shared', 'global_dense', 'hash', 'partitioned'])
 def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
-    """Fixed-point float sums (float64, float32) beside integer-coded ones, with filters (an odd
+    """Fixed-point float sums (float64 over six decades, float32) beside integer-coded ones, with filters (an odd
     slot count in shared mode: the LDS limb table after an odd-length table stays 8-aligned); the
     partitioned path's split records (part_splits=3) add the limbs in split order; std of a
     coded column (pass 1 integer codes, the centred pass in fixed point); a column holding a
@@ -935,7 +935,7 @@ def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
         k = pool[rng.integers(0, len(pool), n)]
     else:
         k = rng.integers(0, ng, n).astype(np.int32)
-    raw = rng.standard_cauchy(n) * 50.0          # heavy tails: wide magnitude range
+    raw = rng.normal(size=n) * 10.0 ** rng.integers(-2, 4, n)  # magnitudes over six decades
     raw32 = (rng.normal(size=n) * 7).astype(np.float32)
     cents = rng.integers(-90_000, 90_000, n) / 100.0
     withnan = rng.normal(size=n)
@@ -967,6 +967,37 @@ def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
         assert runs[1][name].tobytes() == runs[0][name].tobytes(), name
     sel = mask.astype(bool)
     np.testing.assert_array_equal(runs[0]['a'], _fsum_by_group(k[sel], _fx_trunc(raw[sel], raw), runs[0]['k']))
+
+
+@pytest.mark.parametrize('mode', ['shared', 'global_dense', 'hash'])
+def test_fixed_point_sums_only_when_exact(mode, oracle_c, engine_options):
+    """The fixed point is taken only where every value of the column is a multiple of 2^-shift
+    (column statistics: the lowest set bit over all values, no subnormals), so the limb sums are
+    exact: a column of values near 1 with one 1e20 outlier would lose their low bits at the
+    outlier's shift -- it keeps the float64 atomics, and the groups without the outlier stay
+    within the usual tolerance of the row-order oracle (a truncating fixed point would be off
+    by ~1e-9 relative there)."""
+    rng = np.random.default_rng(33)
+    n = 600_000
+    if mode == 'global_dense':
+        engine_options(partition=0)
+    if mode == 'hash':
+        pool = np.unique(rng.integers(-2**40, 2**40, 4_000))
+        k = pool[rng.integers(0, len(pool), n)]
+    else:
+        k = rng.integers(0, {'shared': 500, 'global_dense': 120_000}[mode], n).astype(np.int32)
+    v = rng.normal(size=n)
+    v[rng.integers(0, n)] = 1e20
+    cols = OrderedDict(k=k, v=v)
+    aggs = [['v', 'sum', 's'], ['v', 'mean', 'm'], ['v', 'count', 'n']]
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(['k'], aggs)
+        info = t.dev.last_timing()
+    finally:
+        t.close()
+    assert info['mode'] == {'shared': 1, 'global_dense': 2, 'hash': 3}[mode], info
+    assert_tables_equal(got, oracle_c.groupby(cols, ['k'], aggs, None))
 
 
 @pytest.mark.parametrize('mode', ['private', 'shared', 'global_dense', 'partitioned', 'hash'])
