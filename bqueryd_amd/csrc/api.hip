@@ -147,6 +147,7 @@ struct ColStats {
   // lsb_exp >= -s and no subnormal
   int lsb_exp = INT_MAX;
   bool subnormal = false;
+  double fmaxabs = 0;  // the largest finite magnitude (0: none)
   int64_t runs = -1;  // value runs (rows differing from the row before + 1), -1 = not measured
 };
 
@@ -520,8 +521,8 @@ void finish_stats(Column& k, const unsigned long long* r, int64_t nrows) {
       // whenever it is below 2^53), else whole hundredths; |code| < 2^31 for every value
       const double maxabs = std::max(std::fabs(k.stats.fmin), std::fabs(k.stats.fmax));
       k.stats.lsb_exp = lsb == ~0ull ? INT_MAX : (int)lsb - 4096;
-      // (k_stats sets enc bit 0 for infinities and subnormals)
-      k.stats.subnormal = (enc & 1ull) && !std::isinf(k.stats.fmin) && !std::isinf(k.stats.fmax);
+      k.stats.subnormal = (r[6] & 1ull) != 0;
+      memcpy(&k.stats.fmaxabs, &r[5], 8);
       if (!k.stats.has_nan) {
         const int kk = lsb == ~0ull ? 0 : std::max(0, 4096 - (int)lsb);
         if (!(enc & 1ull) && kk <= 62 && std::ldexp(maxabs, kk) < 2147483647.0) {
@@ -567,7 +568,7 @@ void compute_stats_many(bqg_table* t, const std::vector<int>& cols) {
   const size_t n = todo.size();
   // results [n][8] words, then one column's per-block partials at a time (the launches of
   // one stream run in order)
-  unsigned long long* d = (unsigned long long*)c->misc.ensure((n * 8 + (size_t)kStatsMaxBlocks * 5) *
+  unsigned long long* d = (unsigned long long*)c->misc.ensure((n * 8 + (size_t)kStatsMaxBlocks * kStatsWords) *
                                                               sizeof(unsigned long long));
   unsigned long long* h = (unsigned long long*)c->hhdr.ensure(2 * n * 8 * sizeof(unsigned long long));
   static const unsigned long long init[8] = {~0ull, 0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
@@ -649,9 +650,9 @@ int fx_shift_for(double m) {
 }
 
 // bytes of one workgroup's shared-mode LDS table (k_scan_shared): [nsum][S] sums, [S] counts,
-// [S] first rows, then with fixed-point sums [nsum][2][S] limbs
+// [S] first rows, then with fixed-point sums [nsum][kFxWords][S] limbs and flags
 size_t shared_lds(uint64_t S, int nsum, bool fx) {
-  return (size_t)S * (8 + 8 * (size_t)nsum) + (fx ? 16 * (size_t)nsum * S : 0);
+  return (size_t)S * (8 + 8 * (size_t)nsum) + (fx ? 8 * kFxWords * (size_t)nsum * S : 0);
 }
 
 int scan_col(Plan& pl, int tc) {
@@ -792,8 +793,10 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     for (int q = 0; q < pl.nsum; ++q) {
       if (!pl.p.sum_is_float[q] || pl.p.sum_conv[q] != 0) continue;
       const ColStats& cs = t->cols[pl.tcol[q]].stats;
-      if (cs.empty || cs.has_nan || std::isinf(cs.fmin) || std::isinf(cs.fmax)) continue;
-      pl.p.sum_fx_shift[q] = fx_shift_for(std::max(std::fabs(cs.fmin), std::fabs(cs.fmax)));
+      if (cs.empty) continue;
+      // (NaN / infinities are flags beside the limbs: a group's sum is NaN or +-inf whatever
+      // the order its values arrive in; the shift follows the finite values)
+      pl.p.sum_fx_shift[q] = fx_shift_for(cs.fmaxabs);
       if (cs.enc64 && c->opt[kOptPartNarrow] != 0) continue;  // integer codes already (set_sum_codes)
       // only where every value is a multiple of 2^-shift: the limb sums are then the EXACT sums
       // (one rounding at the end) -- a column whose values span more than 2^42 in magnitude
@@ -923,7 +926,7 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
     pl.nslots = (uint64_t)space;
     pl.p.hash = 0;
     const size_t per_slot_private = 8 + 8 * (size_t)pl.nsum;  // bytes per lane per slot
-    const size_t per_slot_shared = 8 + 8 * (size_t)pl.nsum + (pl.fx_states ? 16 * (size_t)pl.nsum : 0);
+    const size_t per_slot_shared = 8 + 8 * (size_t)pl.nsum + (pl.fx_states ? 8 * kFxWords * (size_t)pl.nsum : 0);
     if (pl.nslots <= (uint64_t)kMaxPrivateSlots && pl.nslots * per_slot_private * kBlock <= 80 * 1024)
       pl.mode = kPrivate;
     else if (pl.nslots * per_slot_shared <= 64 * 1024) pl.mode = kShared;
@@ -931,7 +934,7 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
       // partitioned aggregation: 2^wbits slots of LDS state per partition (64 KiB: two
       // aggregate workgroups per CU; up to 128 KiB when the slot space needs it), at most
       // kPartMaxParts partitions
-      const size_t per_slot = 8 + 8 * (size_t)pl.nsum + (pl.fx_states ? 16 * (size_t)pl.nsum : 0);
+      const size_t per_slot = 8 + 8 * (size_t)pl.nsum + (pl.fx_states ? 8 * kFxWords * (size_t)pl.nsum : 0);
       int wbits = 12;
       if (c->opt[kOptPartWbits]) wbits = (int)c->opt[kOptPartWbits];
       while (wbits > 6 && ((size_t)1 << wbits) * per_slot > 128 * 1024) --wbits;
@@ -1325,7 +1328,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   // centred squares keep the float64 atomics)
   const bool fx1 = atomic_mode && pl.fx_states != 0,
              fx2 = atomic_mode && pl.fx2_states != 0 && !(pl.mode == kShared && shared_lds(S, nsum2, true) > 160 * 1024);
-  const size_t o_fx = fx1 ? carve(S * 16 * (size_t)nsum) : 0, o_fx2 = fx2 ? carve(S * 16 * (size_t)nsum2) : 0;
+  const size_t o_fx = fx1 ? carve(S * 8 * kFxWords * (size_t)nsum) : 0,
+               o_fx2 = fx2 ? carve(S * 8 * kFxWords * (size_t)nsum2) : 0;
   unsigned char* sbase = (unsigned char*)c->slots.ensure(off);
   SlotArrays sa{};
   sa.cnt = (unsigned long long*)(sbase + o_cnt);

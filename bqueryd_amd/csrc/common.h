@@ -103,6 +103,9 @@ struct ScanParams {
   int32_t sum_fx_shift[kMaxSums];
 };
 
+// words per fixed-point sum state beside its limb 0 (SlotArrays::fx): limbs 1, 2, flags
+constexpr int kFxWords = 3;
+
 // Per-slot aggregation state in device memory (global modes, and the target of the
 // private/shared modes' block flush).
 struct SlotArrays {
@@ -110,8 +113,8 @@ struct SlotArrays {
   uint32_t* fst;             // [nslots]  first passing row (kNoRow = none)
   unsigned long long* acc;   // [nsum][nslots]  f64 or i64 bit patterns
   unsigned long long* acc2;  // [nsum2][nslots] centered second moments (std), or null
-  unsigned long long* fx;    // [nsum][2][nslots] limbs 1 and 2 of fixed-point sums (sum_enc 3;
-                             // limb 0 is acc), or null
+  unsigned long long* fx;    // [nsum][kFxWords][nslots]: limbs 1 and 2 of fixed-point sums
+                             // (sum_enc 3; limb 0 is acc) and their non-finite flags, or null
   unsigned long long* keys;  // hash mode: [nslots] packed key code or kEmpty
   unsigned int* hash_fill;   // hash mode: number of occupied positions
   unsigned int* overflow;    // hash mode: set when the table is over-full

@@ -168,6 +168,16 @@ __device__ __forceinline__ double value_f64(uint64_t v, int conv) {
 // an integer (below 2^95 by the choice of shift), split into three 32-bit limbs that carry x's
 // sign.  Limb sums of fewer than 2^31 rows fit int64; integer adds make the total independent of
 // the order the rows arrive in.
+// Non-finite values of a fixed-point sum are flags beside its limbs (SlotArrays::fx word 2):
+// 1 NaN, 2 +inf, 4 -inf, ORed in any order; the sum is then NaN (a NaN, or both infinities)
+// or the one infinity -- what float64 addition gives in any order
+__device__ __forceinline__ bool fx_finite(double x) { return (as_u64(x) & 0x7FF0000000000000ull) != 0x7FF0000000000000ull; }
+__device__ __forceinline__ unsigned long long fx_flag(double x) { return x != x ? 1ull : (x > 0 ? 2ull : 4ull); }
+__device__ __forceinline__ double fx_nonfinite(unsigned long long fl) {
+  if ((fl & 1ull) || (fl & 6ull) == 6ull) return __longlong_as_double(0x7FF8000000000000ll);
+  return (fl & 2ull) ? __longlong_as_double(0x7FF0000000000000ll) : __longlong_as_double((long long)0xFFF0000000000000ull);
+}
+
 __device__ __forceinline__ void fx_limbs(double x, int shift, long long (&l)[3]) {
   const uint64_t b = as_u64(x);
   const int ex = (int)((b >> 52) & 0x7FFu);

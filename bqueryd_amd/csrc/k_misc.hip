@@ -354,6 +354,9 @@ __device__ __forceinline__ void load_chunk_dt(Chunk& c, const unsigned char* ptr
 template <int DT>
 __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsigned long long* partial) {
   unsigned long long mn = ~0ull, mx = 0ull, nan = 0ull, lsb = ~0ull, enc = 0ull;
+  // floats: the largest finite magnitude (its bits: nonnegative doubles order as their bits)
+  // and flags (bit 0: a subnormal value)
+  unsigned long long fab = 0ull, flg = 0ull;
   constexpr bool isf = DT == BQG_F32 || DT == BQG_F64;
   constexpr bool u64 = DT == BQG_U64;
   const int64_t stride = (int64_t)gridDim.x * kBlock * 4;
@@ -381,6 +384,8 @@ __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsig
           // -0.0 codes as 0: bquery's sum starts at +0.0 and +0.0 + -0.0 == +0.0, so a sum
           // never keeps the sign of a zero either way
           const bool zero = (b << 1) == 0ull;
+          if (ex != 0x7FFu) fab = max(fab, b & 0x7FFFFFFFFFFFFFFFull);
+          if (ex == 0u && !zero) flg |= 1ull;
           if (ex == 0x7FFu || (ex == 0u && !zero)) {
             enc |= 1ull;
           } else if (!zero) {
@@ -410,14 +415,19 @@ __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsig
     nan |= (unsigned long long)__shfl_xor(nan, o, 64);
     lsb = min(lsb, (unsigned long long)__shfl_xor(lsb, o, 64));
     enc |= (unsigned long long)__shfl_xor(enc, o, 64);
+    fab = max(fab, (unsigned long long)__shfl_xor(fab, o, 64));
+    flg |= (unsigned long long)__shfl_xor(flg, o, 64);
   }
-  __shared__ unsigned long long smn[kBlock / 64], smx[kBlock / 64], snan[kBlock / 64], slsb[kBlock / 64], senc[kBlock / 64];
+  __shared__ unsigned long long smn[kBlock / 64], smx[kBlock / 64], snan[kBlock / 64], slsb[kBlock / 64], senc[kBlock / 64],
+      sfab[kBlock / 64], sflg[kBlock / 64];
   if ((threadIdx.x & 63) == 0) {
     smn[threadIdx.x >> 6] = mn;
     smx[threadIdx.x >> 6] = mx;
     snan[threadIdx.x >> 6] = nan;
     slsb[threadIdx.x >> 6] = lsb;
     senc[threadIdx.x >> 6] = enc;
+    sfab[threadIdx.x >> 6] = fab;
+    sflg[threadIdx.x >> 6] = flg;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -427,28 +437,34 @@ __global__ __launch_bounds__(kBlock) void k_stats(DevCol c, int64_t nrows, unsig
       nan |= snan[q];
       lsb = min(lsb, slsb[q]);
       enc |= senc[q];
+      fab = max(fab, sfab[q]);
+      flg |= sflg[q];
     }
     // the block's partial (k_stats_final reduces them: ~1000 blocks' same-address device
-    // atomics on five words serialised at the memory side, 25 us and more per column)
-    unsigned long long* o = partial + (size_t)blockIdx.x * 5;
+    // atomics on these words serialised at the memory side, 25 us and more per column)
+    unsigned long long* o = partial + (size_t)blockIdx.x * kStatsWords;
     o[0] = mn;
     o[1] = mx;
     o[2] = nan;
     o[3] = lsb;
     o[4] = enc;
+    o[5] = fab;
+    o[6] = flg;
   }
 }
 
 __global__ __launch_bounds__(kBlock) void k_stats_final(const unsigned long long* partial, int blocks,
                                                         unsigned long long* out) {
-  unsigned long long mn = ~0ull, mx = 0ull, nan = 0ull, lsb = ~0ull, enc = 0ull;
+  unsigned long long mn = ~0ull, mx = 0ull, nan = 0ull, lsb = ~0ull, enc = 0ull, fab = 0ull, flg = 0ull;
   for (int b = threadIdx.x; b < blocks; b += kBlock) {
-    const unsigned long long* o = partial + (size_t)b * 5;
+    const unsigned long long* o = partial + (size_t)b * kStatsWords;
     mn = min(mn, o[0]);
     mx = max(mx, o[1]);
     nan |= o[2];
     lsb = min(lsb, o[3]);
     enc |= o[4];
+    fab = max(fab, o[5]);
+    flg |= o[6];
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
@@ -457,14 +473,18 @@ __global__ __launch_bounds__(kBlock) void k_stats_final(const unsigned long long
     nan |= (unsigned long long)__shfl_xor(nan, o, 64);
     lsb = min(lsb, (unsigned long long)__shfl_xor(lsb, o, 64));
     enc |= (unsigned long long)__shfl_xor(enc, o, 64);
+    fab = max(fab, (unsigned long long)__shfl_xor(fab, o, 64));
+    flg |= (unsigned long long)__shfl_xor(flg, o, 64);
   }
-  __shared__ unsigned long long s[5][kBlock / 64];
+  __shared__ unsigned long long s[kStatsWords][kBlock / 64];
   if ((threadIdx.x & 63) == 0) {
     s[0][threadIdx.x >> 6] = mn;
     s[1][threadIdx.x >> 6] = mx;
     s[2][threadIdx.x >> 6] = nan;
     s[3][threadIdx.x >> 6] = lsb;
     s[4][threadIdx.x >> 6] = enc;
+    s[5][threadIdx.x >> 6] = fab;
+    s[6][threadIdx.x >> 6] = flg;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -474,12 +494,16 @@ __global__ __launch_bounds__(kBlock) void k_stats_final(const unsigned long long
       nan |= s[2][q];
       lsb = min(lsb, s[3][q]);
       enc |= s[4][q];
+      fab = max(fab, s[5][q]);
+      flg |= s[6][q];
     }
     out[0] = min(out[0], mn);
     out[1] = max(out[1], mx);
     out[2] |= nan ? 1ull : 0ull;
     out[3] = min(out[3], lsb);
     out[4] |= enc;
+    out[5] = max(out[5], fab);
+    out[6] |= flg;
   }
 }
 
@@ -1234,7 +1258,7 @@ void launch_runs(const DevCol& c, int64_t nrows, unsigned long long* out, hipStr
 }
 
 void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, unsigned long long* scratch,
-                  hipStream_t st) {  // out4: 5 words; scratch: kStatsMaxBlocks x 5 words
+                  hipStream_t st) {  // out4: kStatsWords words; scratch: kStatsMaxBlocks x kStatsWords words
   int64_t blocks = (nrows + kTileRows - 1) / kTileRows;
   if (blocks > kStatsMaxBlocks) blocks = kStatsMaxBlocks;
   if (blocks < 1) blocks = 1;

@@ -57,7 +57,7 @@ __device__ __forceinline__ long long part_sum_code(const ScanParams& p, int q, u
 template <int NV>
 struct PartRec {
   unsigned long long a[NV];
-  unsigned long long x[NV][2];  // fixed-point sums: limbs 1 and 2 (a holds limb 0)
+  unsigned long long x[NV][kFxWords];  // fixed-point sums: limbs 1, 2, non-finite flags (a holds limb 0)
   unsigned long long c64;  // PACK: count
   uint32_t c, f;
 };
@@ -102,9 +102,9 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
     return;
   }
   uint32_t c = 0, f = kNoRow;
-  unsigned long long a[NV], x[NV][2];
+  unsigned long long a[NV], x[NV][kFxWords];
 #pragma unroll
-  for (int q = 0; q < NV; ++q) a[q] = x[q][0] = x[q][1] = 0;
+  for (int q = 0; q < NV; ++q) a[q] = x[q][0] = x[q][1] = x[q][2] = 0;
   for (int o = 0; o < S; ++o) {
     PartRec<NV> r;
     rec(o, r);
@@ -116,6 +116,7 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
       else a[q] += r.a[q];
       x[q][0] += r.x[q][0];
       x[q][1] += r.x[q][1];
+      x[q][2] |= r.x[q][2];
     }
   }
   sa.cnt[gs] = c;
@@ -128,7 +129,8 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
       if (L.enc_kind[q] == 3) a[q] += (unsigned long long)c * (unsigned long long)L.enc_off[q];
       else a[q] = as_u64((double)(long long)a[q] / L.enc_mul[q]);
     } else if (p.sum_is_float[q] && p.sum_enc[q] == 3) {
-      a[q] = as_u64(fx_value((long long)a[q], (long long)x[q][0], (long long)x[q][1], p.sum_fx_shift[q]));
+      a[q] = as_u64(x[q][2] ? fx_nonfinite(x[q][2])
+                            : fx_value((long long)a[q], (long long)x[q][0], (long long)x[q][1], p.sum_fx_shift[q]));
     } else if (p.sum_is_float[q] && p.sum_enc[q]) {
       a[q] = as_u64((double)(long long)a[q] / p.sum_mul[q]);
     }
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][W] (PACK: [W] packed)
   uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)(PACK ? 1 : nsum) * W);  // [W] (PACK: unused)
   uint32_t* fst = PACK ? cnt : cnt + W;                                    // [W] first row (PACK: first-appearance key)
-  // fixed-point sums (L.fx): limbs 1 and 2 [nsum][2][W] after the table (limb 0 is acc)
+  // fixed-point sums (L.fx): limbs 1, 2 and flags [nsum][kFxWords][W] after the table (limb 0 is acc)
   const bool fx = !PACK && !NARROW && L.fx;
   unsigned long long* fxl = reinterpret_cast<unsigned long long*>(smem + part_agg_lds(L.wbits, nsum, PACK));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = (int)(blockDim.x >> 6);
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   }
   for (int i = tid; i < (PACK ? 1 : nsum) * W; i += blockDim.x) acc[i] = 0;
   if (fx)
-    for (int i = tid; i < 2 * nsum * W; i += blockDim.x) fxl[i] = 0;
+    for (int i = tid; i < kFxWords * nsum * W; i += blockDim.x) fxl[i] = 0;
   const unsigned long long inc = PACK ? 1ull << L.sbits : 0ull;  // one row in the packed count field
   const uint32_t inc_hi = (uint32_t)(inc >> 32);                  // (sbits >= 32)
   __syncthreads();
@@ -370,11 +372,16 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
             // code sums, the same whatever order the entries arrive in
             if (!NARROW && p.sum_is_float[q] && p.sum_enc[q] == 3) {
               // fixed-point limbs: integer sums, the same whatever order the entries arrive in
-              long long l[3];
-              fx_limbs(value_f64(en.v[u][e][q], p.sum_conv[q]), p.sum_fx_shift[q], l);
-              atomicAdd(&acc[(size_t)q * W + sl], (unsigned long long)l[0]);
-              atomicAdd(&fxl[(size_t)(2 * q) * W + sl], (unsigned long long)l[1]);
-              atomicAdd(&fxl[(size_t)(2 * q + 1) * W + sl], (unsigned long long)l[2]);
+              const double xv = value_f64(en.v[u][e][q], p.sum_conv[q]);
+              if (fx_finite(xv)) {
+                long long l[3];
+                fx_limbs(xv, p.sum_fx_shift[q], l);
+                atomicAdd(&acc[(size_t)q * W + sl], (unsigned long long)l[0]);
+                atomicAdd(&fxl[(size_t)(kFxWords * q) * W + sl], (unsigned long long)l[1]);
+                atomicAdd(&fxl[(size_t)(kFxWords * q + 1) * W + sl], (unsigned long long)l[2]);
+              } else {
+                atomicOr(&fxl[(size_t)(kFxWords * q + 2) * W + sl], fx_flag(xv));
+              }
             } else if (!NARROW && p.sum_is_float[q] && p.sum_enc[q]) atomicAdd(&acc[(size_t)q * W + sl], (unsigned long long)part_sum_code(p, q, en.v[u][e][q]));
             else if (!NARROW && p.sum_is_float[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&acc[(size_t)q * W + sl]), value_f64(en.v[u][e][q], p.sum_conv[q]));
             else atomicAdd(&acc[(size_t)q * W + sl], en.v[u][e][q]);
@@ -436,7 +443,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
   }
   if (L.splits > 1) {
     unsigned char* rec = L.partial + ((size_t)part * L.splits + split) * L.partial_bytes;
-    {  // [W] counts, [W] first rows, then [nsum][W] sums (fx: then [nsum][2][W] limbs)
+    {  // [W] counts, [W] first rows, then [nsum][W] sums (fx: then [nsum][kFxWords][W] limbs / flags)
       uint32_t* pc = reinterpret_cast<uint32_t*>(rec);
       uint32_t* pf = pc + W;
       unsigned long long* pa = reinterpret_cast<unsigned long long*>(pf + W);
@@ -446,7 +453,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
 #pragma unroll
         for (int q = 0; q < nsum; ++q) pa[(size_t)q * W + s] = acc[(size_t)q * W + s];
         if (fx)
-          for (int h = 0; h < 2 * nsum; ++h) pa[(size_t)(nsum + h) * W + s] = fxl[(size_t)h * W + s];
+          for (int h = 0; h < kFxWords * nsum; ++h) pa[(size_t)(nsum + h) * W + s] = fxl[(size_t)h * W + s];
       }
     }
     return;
@@ -458,8 +465,9 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
 #pragma unroll
     for (int q = 0; q < (PACK ? 1 : nsum); ++q) {
       r.a[q] = acc[(size_t)q * W + s];
-      r.x[q][0] = fx ? fxl[(size_t)(2 * q) * W + s] : 0ull;
-      r.x[q][1] = fx ? fxl[(size_t)(2 * q + 1) * W + s] : 0ull;
+      r.x[q][0] = fx ? fxl[(size_t)(kFxWords * q) * W + s] : 0ull;
+      r.x[q][1] = fx ? fxl[(size_t)(kFxWords * q + 1) * W + s] : 0ull;
+      r.x[q][2] = fx ? fxl[(size_t)(kFxWords * q + 2) * W + s] : 0ull;
     }
     part_finish_slot<NSUM, NARROW, PACK>(p, L, sa, slot0 + s, 1, [&](int, PartRec<NV>& o) { o = r; });
   }
@@ -489,8 +497,9 @@ __global__ __launch_bounds__(256) void k_part_combine(ScanParams p, PartLaunch L
 #pragma unroll
         for (int q = 0; q < NSUM; ++q) {
           r.a[q] = pa[(size_t)q * W + s];
-          r.x[q][0] = fx ? pa[(size_t)(NSUM + 2 * q) * W + s] : 0ull;
-          r.x[q][1] = fx ? pa[(size_t)(NSUM + 2 * q + 1) * W + s] : 0ull;
+          r.x[q][0] = fx ? pa[(size_t)(NSUM + kFxWords * q) * W + s] : 0ull;
+          r.x[q][1] = fx ? pa[(size_t)(NSUM + kFxWords * q + 1) * W + s] : 0ull;
+          r.x[q][2] = fx ? pa[(size_t)(NSUM + kFxWords * q + 2) * W + s] : 0ull;
         }
       }
     });

@@ -25,8 +25,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [nsum][S]
   uint32_t* cnt = reinterpret_cast<uint32_t*>(acc + (size_t)nsum * S);    // [S]
   uint32_t* fst = cnt + S;                                                 // [S]
-  // fixed-point sums (sum_enc 3): limbs 1 and 2 [nsum][2][S] after the table (sa.fx set;
-  // 8-byte aligned: the table is 8 (nsum + 1) S bytes)
+  // fixed-point sums (sum_enc 3): limbs 1, 2 and the non-finite flags [nsum][3][S] after the
+  // table (sa.fx set; 8-byte aligned: the table is 8 (nsum + 1) S bytes)
   unsigned long long* fxl = reinterpret_cast<unsigned long long*>(fst + S);
   for (int i = tid; i < S; i += kBlock) {
     cnt[i] = 0;
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
   }
   for (int i = tid; i < nsum * S; i += kBlock) acc[i] = 0;
   if (sa.fx)
-    for (int i = tid; i < 2 * nsum * S; i += kBlock) fxl[i] = 0;
+    for (int i = tid; i < kFxWords * nsum * S; i += kBlock) fxl[i] = 0;
   __syncthreads();
 
   const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
@@ -66,11 +66,15 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
                 const double d = x - p.centers[q][s];
                 x = d * d;
               }
-              long long l[3];
-              fx_limbs(x, p.sum_fx_shift[q], l);
-              atomicAdd(&acc[(size_t)q * S + s], (unsigned long long)l[0]);
-              atomicAdd(&fxl[(size_t)(2 * q) * S + s], (unsigned long long)l[1]);
-              atomicAdd(&fxl[(size_t)(2 * q + 1) * S + s], (unsigned long long)l[2]);
+              if (fx_finite(x)) {
+                long long l[3];
+                fx_limbs(x, p.sum_fx_shift[q], l);
+                atomicAdd(&acc[(size_t)q * S + s], (unsigned long long)l[0]);
+                atomicAdd(&fxl[(size_t)(kFxWords * q) * S + s], (unsigned long long)l[1]);
+                atomicAdd(&fxl[(size_t)(kFxWords * q + 1) * S + s], (unsigned long long)l[2]);
+              } else {
+                atomicOr(&fxl[(size_t)(kFxWords * q + 2) * S + s], fx_flag(x));
+              }
             } else if (p.sum_is_float[q] && p.sum_enc[q]) {
               atomicAdd(&acc[(size_t)q * S + s], (unsigned long long)sum_code(p, q, v[q][r]));
             } else if (p.sum_is_float[q]) {
@@ -98,9 +102,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
       const unsigned long long a = acc[(size_t)q * S + s];
       if (p.sum_is_float[q] && !p.sum_enc[q]) unsafeAtomicAdd(reinterpret_cast<double*>(&sa.acc[(size_t)q * p.nslots + s]), as_f64(a));
       else atomicAdd(&sa.acc[(size_t)q * p.nslots + s], a);
-      if (p.sum_is_float[q] && p.sum_enc[q] == 3)
+      if (p.sum_is_float[q] && p.sum_enc[q] == 3) {
         for (int h = 0; h < 2; ++h)
-          atomicAdd(&sa.fx[(size_t)(2 * q + h) * p.nslots + s], fxl[(size_t)(2 * q + h) * S + s]);
+          atomicAdd(&sa.fx[(size_t)(kFxWords * q + h) * p.nslots + s], fxl[(size_t)(kFxWords * q + h) * S + s]);
+        const unsigned long long fl = fxl[(size_t)(kFxWords * q + 2) * S + s];
+        if (fl) atomicOr(&sa.fx[(size_t)(kFxWords * q + 2) * p.nslots + s], fl);
+      }
     }
   }
 }
@@ -145,11 +152,15 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_global(ScanParams p, SlotArr
                 const double d = x - p.centers[q][s];
                 x = d * d;
               }
-              long long l[3];
-              fx_limbs(x, p.sum_fx_shift[q], l);
-              atomicAdd(&sa.acc[(size_t)q * p.nslots + s], (unsigned long long)l[0]);
-              atomicAdd(&sa.fx[(size_t)(2 * q) * p.nslots + s], (unsigned long long)l[1]);
-              atomicAdd(&sa.fx[(size_t)(2 * q + 1) * p.nslots + s], (unsigned long long)l[2]);
+              if (fx_finite(x)) {
+                long long l[3];
+                fx_limbs(x, p.sum_fx_shift[q], l);
+                atomicAdd(&sa.acc[(size_t)q * p.nslots + s], (unsigned long long)l[0]);
+                atomicAdd(&sa.fx[(size_t)(kFxWords * q) * p.nslots + s], (unsigned long long)l[1]);
+                atomicAdd(&sa.fx[(size_t)(kFxWords * q + 1) * p.nslots + s], (unsigned long long)l[2]);
+              } else {
+                atomicOr(&sa.fx[(size_t)(kFxWords * q + 2) * p.nslots + s], fx_flag(x));
+              }
             } else if (p.sum_is_float[q] && p.sum_enc[q]) {
               atomicAdd(&sa.acc[(size_t)q * p.nslots + s], (unsigned long long)sum_code(p, q, v[q][r]));
             } else if (p.sum_is_float[q]) {
@@ -238,7 +249,7 @@ __global__ void k_init_slots(SlotArrays sa, int nsum, uint64_t nslots) {
     sa.fst[i] = kNoRow;
     for (int v = 0; v < nsum; ++v) sa.acc[(size_t)v * nslots + i] = 0;
     if (sa.fx)
-      for (int v = 0; v < 2 * nsum; ++v) sa.fx[(size_t)v * nslots + i] = 0;
+      for (int v = 0; v < kFxWords * nsum; ++v) sa.fx[(size_t)v * nslots + i] = 0;
     if (sa.keys) sa.keys[i] = kEmpty;
   }
 }
@@ -252,9 +263,10 @@ __global__ void k_fx_finalize(unsigned long long* acc, const unsigned long long*
     for (int q = 0; q < nsum; ++q) {
       if (!((states >> q) & 1)) continue;
       const long long s0 = (long long)acc[(size_t)q * nslots + i];
-      const long long s1 = (long long)fx[(size_t)(2 * q) * nslots + i];
-      const long long s2 = (long long)fx[(size_t)(2 * q + 1) * nslots + i];
-      acc[(size_t)q * nslots + i] = as_u64(fx_value(s0, s1, s2, sh.shift[q]));
+      const long long s1 = (long long)fx[(size_t)(kFxWords * q) * nslots + i];
+      const long long s2 = (long long)fx[(size_t)(kFxWords * q + 1) * nslots + i];
+      const unsigned long long fl = fx[(size_t)(kFxWords * q + 2) * nslots + i];
+      acc[(size_t)q * nslots + i] = as_u64(fl ? fx_nonfinite(fl) : fx_value(s0, s1, s2, sh.shift[q]));
     }
 }
 

@@ -179,6 +179,7 @@ void launch_emit_small(const EmitParams& e, const SlotArrays& s, uint32_t nslots
 
 // column statistics (min / max / nan) of one column
 constexpr int kStatsMaxBlocks = 2048;
+constexpr int kStatsWords = 7;  // min, max, NaN, lowest set bit, code flags, finite |max| bits, flags
 void launch_stats(const DevCol& c, int64_t nrows, unsigned long long* out4, unsigned long long* scratch,
                   hipStream_t st);
 // value runs of one column: rows whose value differs from the row before (out: one counter,
@@ -251,10 +252,11 @@ struct PartLaunch {
   uint16_t* rit;
   // splits > 1: [nparts][splits] split tables of partial_bytes each, added by k_part_combine
   unsigned char* partial;
-  size_t partial_bytes;      // 2^wbits * (8 + 8 * nsum) (+ 16 * nsum with fx)
+  size_t partial_bytes;      // 2^wbits * (8 + 8 * nsum) (+ 24 * nsum with fx)
   int win;                   // aggregate window: tiles whose bounds are staged in LDS at once
   // wide entries with fixed-point float sums (ScanParams::sum_enc 3): the slot table and split
-  // records carry limbs 1 and 2 of every sum state ([nsum][2][W] after the table)
+  // records carry limbs 1, 2 and the non-finite flags of every sum state ([nsum][3][W] after
+  // the table)
   int fx;
 };
 // LDS bytes of a scatter workgroup: the staged tile (values, meta), tile counts (two
@@ -264,9 +266,10 @@ inline size_t part_scatter_lds(int nparts, int threads, int nsum, int k = 1, boo
   return (size_t)threads * 4 * k * (4 + (pack ? 2 : (narrow ? 4 : 8) * (size_t)nsum)) + (size_t)nparts * 12 + 2 * 16 * 4;
 }
 // LDS bytes of an aggregate workgroup's slot table: count + first row + 8-byte sums (+ two
-// 8-byte limbs per sum with fixed-point sums), or (pack) the packed 8-byte accumulator + first tile
+// 8-byte limbs and a flags word per sum with fixed-point sums), or (pack) the packed 8-byte
+// accumulator + first tile
 __host__ __device__ inline size_t part_agg_lds(int wbits, int nsum, bool pack, bool fx = false) {
-  return ((size_t)1 << wbits) * (pack ? 12 : 8 + 8 * (size_t)nsum + (fx ? 16 * (size_t)nsum : 0));
+  return ((size_t)1 << wbits) * (pack ? 12 : 8 + 8 * (size_t)nsum + (fx ? 8 * kFxWords * (size_t)nsum : 0));
 }
 // the aggregate walks its split's tiles in windows of PartLaunch::win tiles (four words of
 // bounds per tile in LDS, up to kAggWinMax); a chunk of entry granules spans at most kAggK tiles

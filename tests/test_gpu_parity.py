@@ -918,9 +918,10 @@ def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
     """Fixed-point float sums (float64 over six decades, float32) beside integer-coded ones, with filters (an odd
     slot count in shared mode: the LDS limb table after an odd-length table stays 8-aligned); the
     partitioned path's split records (part_splits=3) add the limbs in split order; std of a
-    coded column (pass 1 integer codes, the centred pass in fixed point); a column holding a
-    NaN keeps the float64 atomics (no fixed point: tolerance only).  Every run the same bits
-    but the NaN column's; option fx_sums=0 restores the float64 atomics for all."""
+    coded column (pass 1 integer codes, the centred pass in fixed point); a column holding NaN
+    and infinities sums its finite values in fixed point with the non-finite values as flags
+    (NaN / +-inf groups whatever the order).  Every run the same bits; option fx_sums=0
+    restores the float64 atomics for all."""
     if splits and mode != 'partitioned':
         pytest.skip('split records are the partitioned path\'s')
     rng = np.random.default_rng(21 + splits)
@@ -940,6 +941,8 @@ def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
     cents = rng.integers(-90_000, 90_000, n) / 100.0
     withnan = rng.normal(size=n)
     withnan[rng.integers(0, n, 3)] = np.nan
+    withnan[rng.integers(0, n, 3)] = np.inf
+    withnan[rng.integers(0, n, 3)] = -np.inf
     t = (rng.random(n) < 0.8).astype(np.int32)
     cols = OrderedDict(k=k, raw=raw, raw32=raw32, cents=cents, withnan=withnan, t=t)
     aggs = [['raw', 'sum', 'a'], ['raw', 'mean', 'am'], ['raw32', 'sum', 'b'], ['cents', 'sum', 'c'],
@@ -963,8 +966,9 @@ def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
     ref = oracle_c.groupby(cols, ['k'], aggs, mask)
     assert_tables_equal(runs[0], ref)
     assert_tables_equal(off, ref)
-    for name in [a[2] for a in aggs if a[2] not in ('e', 'n')]:
+    for name in [a[2] for a in aggs]:
         assert runs[1][name].tobytes() == runs[0][name].tobytes(), name
+    assert np.isnan(runs[0]['e']).any() and np.isinf(runs[0]['e']).any()
     sel = mask.astype(bool)
     np.testing.assert_array_equal(runs[0]['a'], _fsum_by_group(k[sel], _fx_trunc(raw[sel], raw), runs[0]['k']))
 
