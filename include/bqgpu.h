@@ -197,11 +197,12 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *                     aggregate; auto: the tiles where first appearances
  *                     fall on uniform keys), the rest by the first-row pass
  *   fx_sums        1  shared / global / hash / partitioned-wide modes:     0 | 1
- *                     float sums of finite columns without an exact int64
- *                     code whose values are all multiples of 2^-shift (the
- *                     sums are then exact), and the std pass's centred
- *                     squares, as fixed-point limbs in integer atomics --
- *                     the same bits on every run (0: float64 atomics)
+ *                     float sums of columns without an exact int64 code
+ *                     whose finite values are all multiples of 2^-shift
+ *                     (the sums are then exact; NaN / infinities are flags
+ *                     beside the limbs), and the std pass's centred squares,
+ *                     as fixed-point limbs in integer atomics -- the same
+ *                     bits on every run (0: float64 atomics)
  *   mem_cap_mb     0  the context's budget for resident column memory     0 | MiB
  *                     (tables' columns and compact copies, pooled blocks
  *                     included; 0: the device's memory).  Past it a copy is
