@@ -375,7 +375,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"part_win", 0, 0, 4096},               // partitioned aggregate: tiles per window (0: auto; 64..4096)
     {"compact", 1, 0, 2},                   // private / shared / dense global scans read compact column copies
     {"part_first", 0, 0, 2},                // packed partitioned path: rows in tile recorded for 0 auto / 1 no / 2 every tile
-    {"fx_sums", 1, 0, 1},                   // atomic modes: fixed-point float sums (bit-reproducible)
+    {"fx_sums", 1, 0, 2},                   // atomic modes: fixed-point float sums (bit-reproducible; 2: per-slot shifts)
     {"mem_cap_mb", 0, 0, 1ll << 24},        // column memory budget of the context in MiB (0: the device's)
     {"part_ring", 0, 0, 2},                 // packed scatter (JIT): tiles of row loads in flight (0: 1)
 };
@@ -637,6 +637,9 @@ struct Plan {
   // and the std pass's centred squares (fx2_states, bit i: the i-th std column)
   int fx_states = 0;
   int fx2_states = 0;
+  // ... of those, the states that take their shift per slot (ScanParams::fx_emax): columns whose
+  // values span more than the 2^42 a column-wide shift keeps exact (option fx_sums=2: all)
+  int fx_slot_states = 0;
   int32_t fx2_shift[kMaxSums] = {};
 };
 
@@ -801,7 +804,11 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
       // only where every value is a multiple of 2^-shift: the limb sums are then the EXACT sums
       // (one rounding at the end) -- a column whose values span more than 2^42 in magnitude
       // (an outlier beside small values) keeps the float64 atomics, whose error is relative
-      if (cs.subnormal || (cs.lsb_exp != INT_MAX && cs.lsb_exp < -pl.p.sum_fx_shift[q])) continue;
+      if (cs.subnormal) continue;
+      // (an outlier beside small values: a shift per slot, from the slot's own largest value --
+      // exact again unless one slot holds both; within 2^-95 of that slot's largest magnitude
+      // per value otherwise, and the same bits on every run)
+      if (c->opt[kOptFxSums] == 2 || (cs.lsb_exp != INT_MAX && cs.lsb_exp < -pl.p.sum_fx_shift[q])) pl.fx_slot_states |= 1 << q;
       pl.fx_states |= 1 << q;
     }
     // the std pass's (x - mean)^2 <= (max - min)^2
@@ -1329,7 +1336,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   const bool fx1 = atomic_mode && pl.fx_states != 0,
              fx2 = atomic_mode && pl.fx2_states != 0 && !(pl.mode == kShared && shared_lds(S, nsum2, true) > 160 * 1024);
   const size_t o_fx = fx1 ? carve(S * 8 * kFxWords * (size_t)nsum) : 0,
-               o_fx2 = fx2 ? carve(S * 8 * kFxWords * (size_t)nsum2) : 0;
+               o_fx2 = fx2 ? carve(S * 8 * kFxWords * (size_t)nsum2) : 0,
+               o_fxe = fx1 && pl.fx_slot_states ? carve(S * 4 * (size_t)nsum) : 0;
   unsigned char* sbase = (unsigned char*)c->slots.ensure(off);
   SlotArrays sa{};
   sa.cnt = (unsigned long long*)(sbase + o_cnt);
@@ -1469,6 +1477,19 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     // the other float sums as fixed-point limbs (the same bits on every run)
     if (pl.mode != kPartitioned) set_sum_fx(pl);
     HIPCHECK(hipMemsetAsync(sa.hash_fill, 0, 8, st));
+    // fixed-point states with per-slot shifts: each slot's largest exponent first (one pass over
+    // the same rows; the hash modes insert their keys here already)
+    auto fx_emax_pass = [&]() {
+      if (!fx1 || !pl.fx_slot_states) return;
+      FxEmaxLaunch fe{};
+      int32_t* em = (int32_t*)(sbase + o_fxe);
+      HIPCHECK(hipMemsetAsync(em, 0, S * 4 * (size_t)nsum, st));
+      for (int q = 0; q < nsum; ++q)
+        if ((pl.fx_slot_states >> q) & 1) pl.p.fx_emax[q] = fe.emax[q] = em + (size_t)q * S;
+      launch_fx_emax(pl.p, sa, fe, scan_blocks(c, N, 8), st);
+      HIPCHECK(hipGetLastError());
+    };
+    if (pl.mode != kPartitioned) fx_emax_pass();
     // shared / dense global scans read the columns' compact copies (after set_sum_codes: a
     // code-copy column's state sums the codes as integers)
     ScanParams sp = pl.mode == kPartitioned ? pl.p : compact_scan(c, t, pl, e);
@@ -1510,6 +1531,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       // ... and the other float sums of wide entries as fixed-point limbs
       if (!L.narrow) set_sum_fx(pl);
       L.fx = !L.narrow && pl.fx_states != 0;
+      if (L.fx) fx_emax_pass();
       // packed 4-byte entries (option part_pack): no summed column, or one narrow-coded
       // column whose codes span at most 2^16 values -- {code16, slot_low} per entry
       L.pack = 0;
@@ -1662,7 +1684,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     // fixed-point sums to float64 (the partitioned path's combine rounds them itself)
     if (fx1 && pl.mode != kPartitioned) {
       FxShifts sh{};
-      for (int q = 0; q < nsum; ++q) sh.shift[q] = pl.p.sum_fx_shift[q];
+      for (int q = 0; q < nsum; ++q) sh.shift[q] = pl.p.sum_fx_shift[q], sh.emax[q] = pl.p.fx_emax[q];
       launch_fx_finalize(sa.acc, sa.fx, nsum, pl.fx_states, sh, S, st);
       HIPCHECK(hipGetLastError());
     }
@@ -1708,6 +1730,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     for (int k = 0; k < q2.nkeys; ++k) q2.keys[k].col = remap(pl.p.keys[k].col);
     if (q2.mask_col >= 0) q2.mask_col = remap(pl.p.mask_col);
     q2.nsum = nsum2;
+    for (int i = 0; i < kMaxSums; ++i) q2.fx_emax[i] = nullptr;  // (pass 2: column-wide shifts)
     for (int i = 0; i < nsum2; ++i) {
       q2.sum_is_float[i] = 1;
       q2.sum_conv[i] = pl.p.sum_conv[pl.std_cols[i]];

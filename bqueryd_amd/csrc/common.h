@@ -101,6 +101,11 @@ struct ScanParams {
   // integer atomics, so the sum no longer depends on the arrival order (k_fx_finalize rounds it
   // to float64 once)
   int32_t sum_fx_shift[kMaxSums];
+  // ... or, for a column the column-wide shift would truncate (values spanning more than ~2^42
+  // in magnitude), a shift per slot from the slot's own largest magnitude: fx_emax[q][slot] =
+  // 2048 + e for the slot's largest finite |x| < 2^e (0: none; k_fx_emax fills it before the
+  // sums), the slot's shift 95 - e (fx_shift)
+  const int32_t* fx_emax[kMaxSums];
 };
 
 // words per fixed-point sum state beside its limb 0 (SlotArrays::fx): limbs 1, 2, flags

@@ -178,6 +178,18 @@ __device__ __forceinline__ double fx_nonfinite(unsigned long long fl) {
   return (fl & 2ull) ? __longlong_as_double(0x7FF0000000000000ll) : __longlong_as_double((long long)0xFFF0000000000000ull);
 }
 
+// the fixed-point shift of state q at a slot: the column's, or the slot's own (fx_emax)
+__device__ __forceinline__ int fx_shift(const ScanParams& p, int q, uint64_t s) {
+  if (!p.fx_emax[q]) return p.sum_fx_shift[q];
+  const int32_t e = p.fx_emax[q][s];
+  return e ? 95 - (e - 2048) : 0;
+}
+// 2048 + e for a finite nonzero |x| < 2^e (its exponent field + 1 - 1023; subnormals as 2^-1022)
+__device__ __forceinline__ int32_t fx_exp_key(double x) {
+  const int ex = (int)((as_u64(x) >> 52) & 0x7FFu);
+  return (ex ? ex : 1) - 1022 + 2048;
+}
+
 __device__ __forceinline__ void fx_limbs(double x, int shift, long long (&l)[3]) {
   const uint64_t b = as_u64(x);
   const int ex = (int)((b >> 52) & 0x7FFu);

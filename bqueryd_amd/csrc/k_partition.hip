@@ -130,7 +130,7 @@ __device__ __forceinline__ void part_finish_slot(const ScanParams& p, const Part
       else a[q] = as_u64((double)(long long)a[q] / L.enc_mul[q]);
     } else if (p.sum_is_float[q] && p.sum_enc[q] == 3) {
       a[q] = as_u64(x[q][2] ? fx_nonfinite(x[q][2])
-                            : fx_value((long long)a[q], (long long)x[q][0], (long long)x[q][1], p.sum_fx_shift[q]));
+                            : fx_value((long long)a[q], (long long)x[q][0], (long long)x[q][1], fx_shift(p, q, gs)));
     } else if (p.sum_is_float[q] && p.sum_enc[q]) {
       a[q] = as_u64((double)(long long)a[q] / p.sum_mul[q]);
     }
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(1024) void k_part_aggregate(ScanParams p, PartLaunc
               const double xv = value_f64(en.v[u][e][q], p.sum_conv[q]);
               if (fx_finite(xv)) {
                 long long l[3];
-                fx_limbs(xv, p.sum_fx_shift[q], l);
+                fx_limbs(xv, fx_shift(p, q, ((uint64_t)part << L.wbits) + sl), l);
                 atomicAdd(&acc[(size_t)q * W + sl], (unsigned long long)l[0]);
                 atomicAdd(&fxl[(size_t)(kFxWords * q) * W + sl], (unsigned long long)l[1]);
                 atomicAdd(&fxl[(size_t)(kFxWords * q + 1) * W + sl], (unsigned long long)l[2]);

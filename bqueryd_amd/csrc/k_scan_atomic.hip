@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_scan_shared(ScanParams p, SlotArr
               }
               if (fx_finite(x)) {
                 long long l[3];
-                fx_limbs(x, p.sum_fx_shift[q], l);
+                fx_limbs(x, fx_shift(p, q, (uint64_t)s), l);
                 atomicAdd(&acc[(size_t)q * S + s], (unsigned long long)l[0]);
                 atomicAdd(&fxl[(size_t)(kFxWords * q) * S + s], (unsigned long long)l[1]);
                 atomicAdd(&fxl[(size_t)(kFxWords * q + 1) * S + s], (unsigned long long)l[2]);
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_scan_global(ScanParams p, SlotArr
               }
               if (fx_finite(x)) {
                 long long l[3];
-                fx_limbs(x, p.sum_fx_shift[q], l);
+                fx_limbs(x, fx_shift(p, q, s), l);
                 atomicAdd(&sa.acc[(size_t)q * p.nslots + s], (unsigned long long)l[0]);
                 atomicAdd(&sa.fx[(size_t)(kFxWords * q) * p.nslots + s], (unsigned long long)l[1]);
                 atomicAdd(&sa.fx[(size_t)(kFxWords * q + 1) * p.nslots + s], (unsigned long long)l[2]);
@@ -233,6 +233,51 @@ __global__ __launch_bounds__(kBlock) void k_nonfinite(ScanParams p, SlotArrays s
   }
 }
 
+// Per-slot fixed-point shifts (ScanParams::fx_emax): before the sums, the same rows, terms and
+// slots (hash mode: inserting, as pass 1 will) -- per slot and state the largest exponent of a
+// finite nonzero value, one integer atomicMax (order-free)
+template <int NC, bool HASH>
+__global__ __launch_bounds__(kBlock) void k_fx_emax(ScanParams p, SlotArrays sa, FxEmaxLaunch fe) {
+  const int tid = threadIdx.x;
+  const uint64_t hmask = p.nslots - 1;
+  const int64_t ntiles = (p.nrows + kTileRows - 1) / kTileRows;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row0 = tile * kTileRows + (int64_t)tid * kRowsPerThread;
+    Chunk raw[NC];
+    load_rows4<NC>(p, row0, raw);
+    uint64_t v[NC][4];
+    decode_all<NC, 4>(p, raw, v);
+    const uint32_t pass = vals_pass<NC, 4>(p, row0, v);
+    uint64_t code[4];
+    vals_code<NC, 4>(p, v, code);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (!(pass & (1u << r))) continue;
+      uint64_t s = code[r];
+      if (HASH) {
+        s = slot_lookup<NC, 4>(p, sa, hmask, v, code, r, (uint32_t)(row0 + r), true);
+        if (s == kEmpty) continue;
+      }
+#pragma unroll
+      for (int q = 0; q < (NC < kMaxSums ? NC : kMaxSums); ++q) {
+        if (!fe.emax[q]) continue;
+        const double x = value_f64(v[q][r], p.sum_conv[q]);
+        if (x == 0.0 || !fx_finite(x)) continue;
+        const int32_t k = fx_exp_key(x);
+        if (fe.emax[q][s] < k) atomicMax(&fe.emax[q][s], k);
+      }
+    }
+  }
+}
+
+void launch_fx_emax(const ScanParams& p, const SlotArrays& s, const FxEmaxLaunch& fe, int blocks, hipStream_t st) {
+  if (p.hash) {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_fx_emax<NC, true>), dim3(blocks), dim3(kBlock), 0, st, p, s, fe));
+  } else {
+    BQG_DISPATCH_NC(p.ncols, hipLaunchKernelGGL((k_fx_emax<NC, false>), dim3(blocks), dim3(kBlock), 0, st, p, s, fe));
+  }
+}
+
 void launch_nonfinite(const ScanParams& p, const SlotArrays& s, const NonfiniteLaunch& nf, int blocks,
                       hipStream_t st) {
   const size_t lds = nf.lds ? (size_t)p.nslots * 4 : 0;
@@ -266,7 +311,8 @@ __global__ void k_fx_finalize(unsigned long long* acc, const unsigned long long*
       const long long s1 = (long long)fx[(size_t)(kFxWords * q) * nslots + i];
       const long long s2 = (long long)fx[(size_t)(kFxWords * q + 1) * nslots + i];
       const unsigned long long fl = fx[(size_t)(kFxWords * q + 2) * nslots + i];
-      acc[(size_t)q * nslots + i] = as_u64(fl ? fx_nonfinite(fl) : fx_value(s0, s1, s2, sh.shift[q]));
+      const int shift = sh.emax[q] ? (sh.emax[q][i] ? 95 - (sh.emax[q][i] - 2048) : 0) : sh.shift[q];
+      acc[(size_t)q * nslots + i] = as_u64(fl ? fx_nonfinite(fl) : fx_value(s0, s1, s2, shift));
     }
 }
 

@@ -74,7 +74,13 @@ void launch_init_slots(const SlotArrays& s, int nsum, uint64_t nslots, hipStream
 // fixed-point float sums (ScanParams::sum_enc 3) of the states in `states` to float64 bits in acc
 struct FxShifts {
   int32_t shift[kMaxSums];
+  const int32_t* emax[kMaxSums];  // per-slot shifts (ScanParams::fx_emax), or null
 };
+// the per-slot exponent pass of fixed-point sums with per-slot shifts (ScanParams::fx_emax)
+struct FxEmaxLaunch {
+  int32_t* emax[kMaxSums];  // [nslots] for the states that have them, else null
+};
+void launch_fx_emax(const ScanParams& p, const SlotArrays& s, const FxEmaxLaunch& fe, int blocks, hipStream_t st);
 void launch_fx_finalize(unsigned long long* acc, const unsigned long long* fx, int nsum, int states, const FxShifts& sh,
                         uint64_t nslots, hipStream_t st);
 

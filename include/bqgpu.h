@@ -196,13 +196,16 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *                     record their rows in tile (exact first rows in the
  *                     aggregate; auto: the tiles where first appearances
  *                     fall on uniform keys), the rest by the first-row pass
- *   fx_sums        1  shared / global / hash / partitioned-wide modes:     0 | 1
- *                     float sums of columns without an exact int64 code
- *                     whose finite values are all multiples of 2^-shift
- *                     (the sums are then exact; NaN / infinities are flags
- *                     beside the limbs), and the std pass's centred squares,
- *                     as fixed-point limbs in integer atomics -- the same
- *                     bits on every run (0: float64 atomics)
+ *   fx_sums        1  shared / global / hash / partitioned-wide modes:     0 | 1 | 2
+ *                     float sums of columns without an exact int64 code,
+ *                     and the std pass's centred squares, as fixed-point
+ *                     limbs in integer atomics -- the same bits on every
+ *                     run (NaN / infinities are flags beside the limbs).
+ *                     The shift is the column's when its finite values are
+ *                     all multiples of 2^-shift (exact sums), else each
+ *                     slot's own from its largest value (an extra pass;
+ *                     2: per-slot shifts for every such column;
+ *                     0: float64 atomics)
  *   mem_cap_mb     0  the context's budget for resident column memory     0 | MiB
  *                     (tables' columns and compact copies, pooled blocks
  *                     included; 0: the device's memory).  Past it a copy is

@@ -920,8 +920,8 @@ def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
     partitioned path's split records (part_splits=3) add the limbs in split order; std of a
     coded column (pass 1 integer codes, the centred pass in fixed point); a column holding NaN
     and infinities sums its finite values in fixed point with the non-finite values as flags
-    (NaN / +-inf groups whatever the order).  Every run the same bits; option fx_sums=0
-    restores the float64 atomics for all."""
+    (NaN / +-inf groups whatever the order).  Every run the same bits; per-slot shifts
+    (fx_sums=2) the same bits again; option fx_sums=0 restores the float64 atomics for all."""
     if splits and mode != 'partitioned':
         pytest.skip('split records are the partitioned path\'s')
     rng = np.random.default_rng(21 + splits)
@@ -957,11 +957,16 @@ def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
             got, _ = tb.groupby(['k'], aggs, where_terms=terms)
             runs.append(got)
             info = tb.dev.last_timing()
+        tb.dev.set_option('fx_sums', 2)
+        slot, _ = tb.groupby(['k'], aggs, where_terms=terms)
         tb.dev.set_option('fx_sums', 0)
         off, _ = tb.groupby(['k'], aggs, where_terms=terms)
     finally:
         tb.close()
     assert info['mode'] == {'shared': 1, 'global_dense': 2, 'hash': 3, 'partitioned': 4}[mode], info
+    # per-slot shifts (fx_sums=2) are never below the column's: the same exact sums, bit for bit
+    for name in [a[2] for a in aggs]:
+        assert slot[name].tobytes() == runs[0][name].tobytes(), name
     mask = oracle_c.where_terms(cols, terms)
     ref = oracle_c.groupby(cols, ['k'], aggs, mask)
     assert_tables_equal(runs[0], ref)
@@ -973,14 +978,13 @@ def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
     np.testing.assert_array_equal(runs[0]['a'], _fsum_by_group(k[sel], _fx_trunc(raw[sel], raw), runs[0]['k']))
 
 
-@pytest.mark.parametrize('mode', ['shared', 'global_dense', 'hash'])
-def test_fixed_point_sums_only_when_exact(mode, oracle_c, engine_options):
-    """The fixed point is taken only where every value of the column is a multiple of 2^-shift
-    (column statistics: the lowest set bit over all values, no subnormals), so the limb sums are
-    exact: a column of values near 1 with one 1e20 outlier would lose their low bits at the
-    outlier's shift -- it keeps the float64 atomics, and the groups without the outlier stay
-    within the usual tolerance of the row-order oracle (a truncating fixed point would be off
-    by ~1e-9 relative there)."""
+@pytest.mark.parametrize('mode', ['shared', 'global_dense', 'hash', 'partitioned'])
+def test_fixed_point_sums_outlier_column(mode, oracle_c, engine_options):
+    """A column of values near 1 with one 1e20 outlier: at the column-wide shift (from 1e20) the
+    small values would lose their low bits, so its fixed point takes a shift per slot from the
+    slot's own largest magnitude (an extra pass, ScanParams::fx_emax) -- every group without
+    the outlier is again the correctly rounded exact sum (math.fsum), the outlier's group
+    within tolerance of the row-order oracle, and every run the same bits."""
     rng = np.random.default_rng(33)
     n = 600_000
     if mode == 'global_dense':
@@ -989,19 +993,25 @@ def test_fixed_point_sums_only_when_exact(mode, oracle_c, engine_options):
         pool = np.unique(rng.integers(-2**40, 2**40, 4_000))
         k = pool[rng.integers(0, len(pool), n)]
     else:
-        k = rng.integers(0, {'shared': 500, 'global_dense': 120_000}[mode], n).astype(np.int32)
+        k = rng.integers(0, {'shared': 500, 'global_dense': 120_000, 'partitioned': 120_000}[mode], n).astype(np.int32)
     v = rng.normal(size=n)
-    v[rng.integers(0, n)] = 1e20
+    out = rng.integers(0, n)
+    v[out] = 1e20
     cols = OrderedDict(k=k, v=v)
     aggs = [['v', 'sum', 's'], ['v', 'mean', 'm'], ['v', 'count', 'n']]
     t = ShardTable(cols)
     try:
-        got, _ = t.groupby(['k'], aggs)
+        runs = [t.groupby(['k'], aggs)[0] for _ in range(2)]
         info = t.dev.last_timing()
     finally:
         t.close()
-    assert info['mode'] == {'shared': 1, 'global_dense': 2, 'hash': 3}[mode], info
-    assert_tables_equal(got, oracle_c.groupby(cols, ['k'], aggs, None))
+    assert info['mode'] == {'shared': 1, 'global_dense': 2, 'hash': 3, 'partitioned': 4}[mode], info
+    assert_tables_equal(runs[0], oracle_c.groupby(cols, ['k'], aggs, None))
+    for name in ('s', 'm'):
+        assert runs[1][name].tobytes() == runs[0][name].tobytes(), name
+    exact = _fsum_by_group(k, v, runs[0]['k'])
+    keep = runs[0]['k'] != k[out]
+    np.testing.assert_array_equal(runs[0]['s'][keep], exact[keep])
 
 
 @pytest.mark.parametrize('mode', ['private', 'shared', 'global_dense', 'partitioned', 'hash'])
