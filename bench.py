@@ -246,8 +246,10 @@ def _c5_local_ranks(args):
                 p.close()
         return merged
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         out = step()
+        if i == 0:
+            devs[0].jit_wait(900)
     if int(out['n'].sum()) != n_shards * shard_rows:
         raise SystemExit('sanity check failed: %d merged rows' % int(out['n'].sum()))
     for d in devs:
@@ -379,12 +381,14 @@ def launch_plan(n, argv):
                    'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)}) for r in range(n)]
 
 
-def _launch_ranks(n, argv, dry):
+def _launch_ranks(n, argv, dry, plan=None, grace_s=15.0, poll_s=0.2):
     """Start the N rank processes (before this process touches a GPU) and wait for them; rank
-    0's stdout is this process's, the others' is discarded.  Exit status: the first failing
-    rank's, else 0."""
+    0's stdout is this process's, the others' is discarded.  When a rank fails (non-zero exit,
+    e.g. a watchdog that found a collective hung), the others get ``grace_s`` seconds to end
+    on their own -- rank 0 prints the line it has -- and are then terminated, so a hung peer
+    never keeps the job alive.  Exit status: the first failing rank's, else 0."""
     import subprocess
-    plan = launch_plan(n, argv)
+    plan = plan if plan is not None else launch_plan(n, argv)
     if dry:
         print(json.dumps({'launch': 'self', 'ranks': n, 'commands': [c for c, _ in plan], 'env': [e for _, e in plan]}),
               flush=True)
@@ -393,29 +397,109 @@ def _launch_ranks(n, argv, dry):
     for r, (cmd, extra) in enumerate(plan):
         procs.append(subprocess.Popen(cmd, env=dict(os.environ, **extra),
                                       stdout=None if r == 0 else subprocess.DEVNULL))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    first_bad, t_bad = None, None
+    while True:
+        rcs = [p.poll() for p in procs]
+        for r, rc in enumerate(rcs):
+            if rc not in (None, 0) and first_bad is None:
+                first_bad, t_bad = rc, time.monotonic()
+                sys.stderr.write('bench.py: rank %d exited with status %d\n' % (r, rc))
+        if all(rc is not None for rc in rcs):
+            break
+        if first_bad is not None and time.monotonic() - t_bad > grace_s:
+            for r, p in enumerate(procs):
+                if p.poll() is None:
+                    sys.stderr.write('bench.py: terminating rank %d (a peer failed)\n' % r)
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(poll_s)
+    return first_bad if first_bad is not None else 0
+
+
+# Where each rank is (a watchdog reports it when a sub-benchmark hangs): the stage the bench is
+# in, and the libbqgpu context whose merge progress (bqg_comm_progress) names the collective.
+_PROGRESS = {'stage': 'start', 'device': None}
+
+
+def _stage(text):
+    _PROGRESS['stage'] = text
+
+
+def _status_dir():
+    """Per-job directory the ranks' watchdogs leave their status in (one node: MASTER_PORT
+    names the job)."""
+    import tempfile
+    return os.path.join(tempfile.gettempdir(), 'bqgpu-bench-%s' % os.environ.get('MASTER_PORT', 'solo'))
+
+
+def _rank_status(rank):
+    st = {'rank': rank, 'stage': _PROGRESS['stage']}
+    dev = _PROGRESS.get('device')
+    if dev is not None:
+        try:
+            from bqueryd_amd import dist as bdist
+            st['merge'] = bdist.merge_progress(dev)
+        except Exception as e:  # no communicator yet, or the library is gone
+            st['merge'] = 'n/a (%s)' % e
+    return st
 
 
 class _Watchdog:
     """Ends this rank if a sub-benchmark hangs (an RCCL collective that never completes):
-    after ``seconds`` it calls ``on_timeout`` (rank 0 prints the line it has, the hung part
-    marked) and exits the process."""
+    after ``seconds`` every rank records where it is (stage + merge phase) in the job's status
+    directory; rank 0 waits briefly for its peers' records, calls ``on_timeout(statuses)`` (it
+    prints the line it has, the hung part marked with them) and every rank exits with status
+    ``EXIT_HUNG`` -- a hang is a failed run, never rc 0."""
 
-    def __init__(self, seconds, on_timeout):
+    EXIT_HUNG = 3
+
+    def __init__(self, seconds, on_timeout, rank=0, ws=1, peer_wait_s=8.0):
         import threading
         self.done = threading.Event()
-        self.t = threading.Thread(target=self._run, args=(seconds, on_timeout), daemon=True)
+        self.t = threading.Thread(target=self._run, args=(seconds, on_timeout, rank, ws, peer_wait_s), daemon=True)
         self.t.start()
 
-    def _run(self, seconds, on_timeout):
-        if not self.done.wait(seconds):
+    def _run(self, seconds, on_timeout, rank, ws, peer_wait_s):
+        if self.done.wait(seconds):
+            return
+        try:
+            mine = _rank_status(rank)
+            sys.stderr.write('bench.py: rank %d hung: %s\n' % (rank, json.dumps(mine)))
+            d = _status_dir()
+            statuses = {rank: mine}
             try:
-                on_timeout()
-            finally:
-                sys.stdout.flush()
-                os._exit(0)
+                os.makedirs(d, exist_ok=True)
+                with open(os.path.join(d, 'rank%d.json' % rank), 'w') as f:
+                    json.dump(mine, f)
+            except OSError:
+                pass
+            if rank == 0:
+                t_end = time.monotonic() + (peer_wait_s if ws > 1 else 0.0)
+                while True:
+                    for r in range(1, ws):
+                        if r not in statuses:
+                            try:
+                                with open(os.path.join(d, 'rank%d.json' % r)) as f:
+                                    statuses[r] = json.load(f)
+                            except (OSError, ValueError):
+                                pass
+                    if len(statuses) == ws or time.monotonic() > t_end:
+                        break
+                    time.sleep(0.1)
+                on_timeout([statuses.get(r, {'rank': r, 'stage': 'no status (exited or hung before its watchdog)'})
+                            for r in range(ws)])
+            else:
+                time.sleep(peer_wait_s + 2.0)  # rank 0 reads the status and prints before the launcher reaps
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(self.EXIT_HUNG)
 
     def cancel(self):
         self.done.set()
@@ -435,6 +519,7 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
     per_rank = max(1, cfg['shards'] // 8)
     shard_rows = shard_rows or cfg['rows'] // cfg['shards']
     rows = per_rank * shard_rows
+    _stage('c5: generating shards')
     t_gen = time.perf_counter()
     from concurrent.futures import ThreadPoolExecutor
 
@@ -447,9 +532,12 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
             tables.append(ShardTable(sc, device=dev))
             del sc
     gen_s = time.perf_counter() - t_gen
+    _stage('c5: RCCL communicator init (world %d)' % ws)
     with _stdout_to_stderr():  # librccl prints a banner on stdout at init
         uid = comm.broadcast_bytes(bdist.new_unique_id() if rank == 0 else None)
         rccl = bdist.RcclComm(dev, rank, ws, uid)
+    _PROGRESS['device'] = dev
+    _stage('c5: shard union + probe groupby')
     colo = bdist.ColocatedShards(tables)
     colo.union(synth.query_columns(cfg))  # the rank's shard set, resident once (like the load)
     probe, _ = colo.groupby_tables(cfg['groupby'], cfg['aggs'])
@@ -457,11 +545,14 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
     for p_ in probe:
         p_.close()
     phase, timings = [], []
+    where = ['']
 
     def step():
+        _PROGRESS['stage'] = where[0] + ' shard pass'
         t0 = time.perf_counter()
         per, reduced = colo.groupby_tables(cfg['groupby'], cfg['aggs'])
         timings.append(dev.last_timing())
+        _PROGRESS['stage'] = where[0] + ' merge'
         t1 = time.perf_counter()
         merged = bdist.merge_partials_device(per, cfg['groupby'], cfg['aggs'], dtypes, rccl, reduced=reduced)
         for p_ in per:
@@ -469,21 +560,28 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
         phase.append((t1 - t0, time.perf_counter() - t1))
         return merged
 
-    for _ in range(warmup):
+    for i in range(warmup):
+        where[0] = 'c5: warmup step %d/%d:' % (i + 1, warmup)
         out = step()
+        if i == 0:
+            _stage('c5: waiting for background kernel compiles')
+            dev.jit_wait(900)
     ok = None
     if rank == 0 and out is not None:
         ok = int(out['n'].sum()) == ws * rows  # every scanned row counted once, across the ranks
     # timed steps without device timing (with it, the merge waits for each phase's device work)
     dev.enable_timing(False)
     del phase[:], timings[:]
+    _stage('c5: barrier before the timed steps')
     comm.barrier()
     dev.synchronize()
+    where[0] = 'c5: timed steps:'
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     dev.synchronize()
     t1 = time.perf_counter()
+    _stage('c5: barrier after the timed steps')
     comm.barrier()
     elapsed = comm.max(t1 - t0)
     shard_ms = comm.max(1e3 * float(np.mean([p[0] for p in phase])))
@@ -491,15 +589,19 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
     # the shard pass's scan kernels: HIP events over a few more (untimed) steps
     dev.enable_timing(True, scan_only=True)
     del timings[:]
+    where[0] = 'c5: device-timed steps:'
     for _ in range(3):
         step()
     dev.synchronize()
+    _stage('c5: closing')
     scan_ms = comm.max(float(np.mean([t['scan_ms'] for t in timings])))
     dev.enable_timing(False)
+    _PROGRESS['device'] = None
     rccl.close()
     colo.close()
     for t in tables:
         t.close()
+    _stage('c5: done')
     if rank != 0:
         return None
     alg = timings[-1]['bytes']
@@ -523,6 +625,69 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
     }
 
 
+def _run_c5_guarded(line, run_c5, comm, rank, ws, timeout_s):
+    """The c5 sub-record under a watchdog.  Every rank starts it together (a barrier first),
+    so a collective that hangs on a new node ends every rank within ``timeout_s``: rank 0
+    prints the line with ``c5.error`` naming each rank's stage and merge phase, and the
+    process exits non-zero (``_Watchdog.EXIT_HUNG``).  An exception inside c5 only marks
+    the sub-record (the headline stands)."""
+    def on_timeout(statuses):
+        if rank == 0:
+            line['c5'] = {'error': 'did not finish within %.0f s: the run fails with status %d; each rank\'s stage '
+                                   'and merge phase when it was abandoned are in `ranks`' % (timeout_s,
+                                                                                            _Watchdog.EXIT_HUNG),
+                          'ranks': statuses}
+            print(json.dumps(line), flush=True)
+    try:  # a previous job's record under the same port is not this rank's
+        os.remove(os.path.join(_status_dir(), 'rank%d.json' % rank))
+    except OSError:
+        pass
+    _stage('c5: barrier before the sub-record')
+    comm.barrier()
+    wd = _Watchdog(timeout_s, on_timeout, rank=rank, ws=ws)
+    try:
+        line['c5'] = run_c5()
+    except Exception as e:  # the headline stands; the sub-record says what failed
+        line['c5'] = {'error': '%s: %s' % (type(e).__name__, e), 'stage': _PROGRESS['stage']}
+    wd.cancel()
+
+
+def _cold_first_query(dev, step):
+    """The first query of the bench's shape on a fresh worker, as on a new box: the run-time
+    specialiser's disk cache pointed at an empty directory (BQGPU_JIT_CACHE), so the query finds
+    no compiled kernel for its shape.  With option jit_async (the default) it runs the
+    precompiled generic kernel while a host thread compiles the specialised one; the bench then
+    waits for that compile (bqg_jit_wait) so every timed step runs the specialised kernel."""
+    import shutil
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix='bqgpu-jit-cold-')
+    old = os.environ.get('BQGPU_JIT_CACHE')
+    os.environ['BQGPU_JIT_CACHE'] = tmp
+    try:
+        dev.synchronize()
+        t0 = time.perf_counter()
+        step()
+        dev.synchronize()
+        first_ms = 1e3 * (time.perf_counter() - t0)
+        first_spec = dev.last_timing()['specialized']
+        t1 = time.perf_counter()
+        w = dev.jit_wait(900)
+        wait_s = time.perf_counter() - t1
+    finally:
+        if old is None:
+            os.environ.pop('BQGPU_JIT_CACHE', None)
+        else:
+            os.environ['BQGPU_JIT_CACHE'] = old
+        shutil.rmtree(tmp, ignore_errors=True)
+    return {'first_query_ms': first_ms,
+            'first_query_kernel': 'specialised' if first_spec else 'generic (precompiled; the specialised one compiling '
+                                                                   'on a host thread)',
+            'jit_async': bool(dev.get_option('jit_async')),
+            'background_compile_wait_s': wait_s, 'background_compiles': w,
+            'what': 'wall time of the first query on the freshly loaded shard with an empty run-time-compile cache '
+                    '(a new box): plan, statistics, slot arrays, scan, emit, result to host'}
+
+
 def _compact_record(dev, table, step, steps, warmup, full_ms, full_scan_ms):
     """The compact resident copies on the same shard and query: their build on
     the first query that reads them (device time), the steady step and scan over them, the HBM
@@ -541,6 +706,7 @@ def _compact_record(dev, table, step, steps, warmup, full_ms, full_scan_ms):
         copy_bytes = table.device_bytes() - base_bytes
         if copy_bytes <= 0:
             return {'built': False, 'note': 'no column of this query has a narrower resident form'}
+        dev.jit_wait(900)  # the copies' query shape, compiled in the background: timed specialised
         for _ in range(warmup):
             step()
         dev.enable_timing(True, scan_only=True)
@@ -664,6 +830,9 @@ def main(argv=None):
         timings.append(dev.last_timing())
         return out
 
+    # the first query on a fresh worker: an empty JIT cache (a new box), the query shape's
+    # specialised kernel compiled in the background while this query runs the generic one
+    cold = _cold_first_query(dev, step)
     for _ in range(args.warmup):
         out = step()
     cnt_col = [a[2] for a in cfg['aggs'] if a[1] == 'count']
@@ -704,6 +873,19 @@ def main(argv=None):
     device_avg = float(np.mean([t['total_ms'] for t in timings])) if timings else float('nan')
     achieved = bytes_per_launch / (scan_avg * 1e-3) / 1e9 if scan_avg > 0 else 0.0
 
+    # the generic (precompiled) kernel's steady step: what a cold shape's first query is held to
+    if cold is not None:
+        with dev.options(jit=0):
+            for _ in range(2):
+                step()
+            dev.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            dev.synchronize()
+            gen_ms = (time.perf_counter() - t0) / args.steps * 1e3
+        cold['generic_steady_ms_per_step'] = gen_ms
+        cold['first_over_generic_steady'] = cold['first_query_ms'] / gen_ms if gen_ms > 0 else None
     compact = None
     if rank == 0 and not args.compact and not args.no_compact_record and mode in (0, 1, 2, 5):
         compact = _compact_record(dev, table, step, args.steps, args.warmup, ms_per_step, scan_avg)
@@ -760,21 +942,14 @@ def main(argv=None):
             'device_ms_per_query': device_avg,
         },
         'cpu_baseline': cpu,
+        'cold_first_query_ms': cold['first_query_ms'] if cold else None,
+        'cold_start': cold,
         'compact': compact,
         'c5': None,
     }
     if not args.no_c5:
-        def on_timeout():
-            if rank == 0:
-                line['c5'] = {'error': 'did not finish within %.0f s (abandoned; the rest of the line stands)'
-                                       % args.c5_timeout}
-                print(json.dumps(line), flush=True)
-        wd = _Watchdog(args.c5_timeout, on_timeout)
-        try:
-            line['c5'] = _c5_ranks(args, comm, dev, ws, rank, min(args.steps, 10), min(args.warmup, 3))
-        except Exception as e:  # the headline stands; the sub-record says what failed
-            line['c5'] = {'error': '%s: %s' % (type(e).__name__, e)}
-        wd.cancel()
+        _run_c5_guarded(line, lambda: _c5_ranks(args, comm, dev, ws, rank, min(args.steps, 10), min(args.warmup, 3)),
+                        comm, rank, ws, args.c5_timeout)
     comm.close()
     if rank != 0:
         return 0

@@ -29,7 +29,7 @@ T_FALSE, T_TRUE, T_EQ, T_NE, T_IN, T_NIN, T_GT, T_GE, T_LT, T_LE = -1, 0, 1, 2, 
 
 E_INVALID, E_UNSUPPORTED, E_HIP, E_OOM, E_STATE = -1, -2, -3, -4, -5
 UNIQUE_ID_BYTES = 128
-ABI_VERSION = 8
+ABI_VERSION = 9
 OPTIONS = ('jit', 'jit_min_rows', 'partition', 'part_wbits', 'part_k', 'part_threads', 'part_per_cu',
            'part_splits', 'part_narrow', 'fused_scd', 'scd_compact', 'scd_pack16', 'priv_ahead',
            'private_per_cu', 'small_emit', 'hash_slots', 'distinct_slots', 'part_pack', 'scd_runs', 'part_win', 'compact', 'part_first',
@@ -137,6 +137,9 @@ _PROTOS = {
     'bqg_comm_destroy': ([_P], ctypes.c_int),
     'bqg_comm_info': ([_P, ctypes.POINTER(_I32), ctypes.POINTER(_I32)], ctypes.c_int),
     'bqg_comm_last_phases': ([_P, ctypes.POINTER(ctypes.c_double), _I32], ctypes.c_int),
+    'bqg_jit_wait': ([_P, ctypes.c_double, ctypes.POINTER(_I32), ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
+                     ctypes.c_int),
+    'bqg_comm_progress': ([_P, ctypes.POINTER(_I32), ctypes.POINTER(_I64), ctypes.POINTER(_I64)], ctypes.c_int),
     'bqg_merge': ([_P, _I32, _P, _I32, _I32, _P, _I32, ctypes.POINTER(_P)], ctypes.c_int),
     'bqg_merge_group': ([_I32, _P, _P, _P, _I32, _I32, _P, _I32, _P], ctypes.c_int),
     'bqg_merge_host': ([_P, _I32, _P, _I32, _I32, _P, _I32, ctypes.POINTER(_P)], ctypes.c_int),

@@ -346,7 +346,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kOptMemCap, kOptPartRing, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kOptMemCap, kOptPartRing, kOptJitAsync, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -378,6 +378,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"fx_sums", 1, 0, 2},                   // atomic modes: fixed-point float sums (bit-reproducible; 2: per-slot shifts)
     {"mem_cap_mb", 0, 0, 1ll << 24},        // column memory budget of the context in MiB (0: the device's)
     {"part_ring", 0, 0, 2},                 // packed scatter (JIT): tiles of row loads in flight (0: 1)
+    {"jit_async", 1, 0, 1},                 // a shape not compiled yet runs the generic kernel while hiprtc compiles it
 };
 
 static int opt_index(const char* name) {
@@ -1059,6 +1060,10 @@ ScanParams compact_scan(bqg_ctx* c, bqg_table* t, Plan& pl, EmitParams& e) {
       sp.sum_conv[i] = 1;
       sp.sum_enc[i] = 0;
       e.sum_dec[i] = col.shadow.mul;
+      // the state now sums integer codes: it is no fixed-point limb sum (with part_narrow=0 the
+      // plan may have made it one), so k_fx_finalize must leave its accumulator alone
+      pl.fx_states &= ~(1 << i);
+      pl.fx_slot_states &= ~(1 << i);
     }
     // bytes read (the algorithmic bytes keep the stored width)
     if (!pl.dummy_col) pl.read_bytes -= ((int64_t)dtype_size(col.dtype) - ((int64_t)1 << sp.cols[i].lg)) * N;
@@ -1428,7 +1433,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       const int64_t ahead = c->opt[kOptPrivAhead] ? c->opt[kOptPrivAhead] : (row_bytes <= 4 ? 3 : 0);
       std::string extra;
       if (ahead) extra = std::string("#define BQ_PRIV_AHEAD ") + std::to_string(ahead) + "\n";
-      jfn = jit_function_for("bq_jit_scan_private", sp, extra);
+      jfn = jit_function_for("bq_jit_scan_private", sp, extra, c->opt[kOptJitAsync] != 0);
     }
     check_launch(c, "private scan", L.lds_bytes, L.blocks);
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
@@ -1669,8 +1674,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
           extra += "#define BQ_PART_ENC ";
           for (int q = 0; q < kMaxSums; ++q) extra += std::to_string(q < nsum ? L.enc_kind[q] : 0) + (q + 1 < kMaxSums ? "," : "\n");
         }
-        fs = jit_function_for("bq_jit_part_scatter", pl.p, extra);
-        if (pk) ff = jit_function_for("bq_jit_part_first_rows", pl.p, extra);
+        fs = jit_function_for("bq_jit_part_scatter", pl.p, extra, c->opt[kOptJitAsync] != 0);
+        if (pk) ff = jit_function_for("bq_jit_part_first_rows", pl.p, extra, c->opt[kOptJitAsync] != 0);
         c->last.specialized = fs ? 1 : 0;
       }
       check_launch(c, "partitioned scatter", part_scatter_lds(L.nparts, L.threads, nsum, L.k, nw, pk), L.blocks, L.threads);
@@ -2007,7 +2012,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
                                   std::to_string(vc) + "\n#define BQ_SCD_CC " + std::to_string(cc) +
                                   "\n#define BQ_SCD_P16 " + std::to_string(d.pack16) + "\n";
         sfn = jit_function_for(d.runs ? "bq_jit_scd_runs32" : d.compact ? "bq_jit_scd_fused32" : "bq_jit_scd_fused",
-                               pc.p, extra);
+                               pc.p, extra, c->opt[kOptJitAsync] != 0);
         c->last.specialized = sfn ? 1 : 0;
       }
       if (fused && c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
@@ -2207,6 +2212,13 @@ int bqg_internal_host_result(bqg_ctx* c, int64_t n, const std::vector<int32_t>& 
 extern "C" {
 
 int bqg_abi_version(void) { return BQG_ABI_VERSION; }
+
+int bqg_jit_wait(bqg_ctx* ctx, double timeout_ms, int32_t* idle, int64_t* compiled, int64_t* failed) {
+  return guard(ctx, [&] {
+    const bool done = jit_wait(timeout_ms, compiled, failed);
+    if (idle) *idle = done ? 1 : 0;
+  });
+}
 
 int bqg_device_count(int* n) {
   return guard(nullptr, [&] {

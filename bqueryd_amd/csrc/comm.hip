@@ -35,6 +35,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -160,6 +161,10 @@ struct CommState {
     return hcnt;
   }
   double phase_ms[kMergePhases] = {};  // host wall time of this rank's part of the last merge
+  // bqg_comm_progress (read from another host thread while a merge runs, e.g. a watchdog
+  // naming the collective a hung rank waits in): the phase entered last, -1 between merges
+  std::atomic<int32_t> cur_phase{-1};
+  std::atomic<int64_t> merges_started{0}, merges_done{0};
   // in-process transport: an event on this rank's stream, and (rank 0) the copy descriptors
   // of a transfer step -- page-locked staging, its reuse guarded by desc_ev -- and their
   // device copy
@@ -589,6 +594,10 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
   // charged to every rank of the call (with timing on, after its device work has finished)
   for (Local& l : ranks)
     for (double& x : l.st->phase_ms) x = 0.0;
+  auto enter = [&](int ph) {
+    for (Local& l : ranks) l.st->cur_phase.store(ph, std::memory_order_relaxed);
+  };
+  enter(0);
   auto collective = [&](int ph, double t0) {
     if (timing) sync_all(ranks);
     const double dt = now_ms() - t0;
@@ -702,11 +711,13 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
   }
   // world 1 with a host result: the rank's reduced rows are the answer (no exchange)
   if (W == 1 && mode != MergeOut::kDeviceRoot) {
+    enter(5);
     to_host({ranks[0].Lv});
     for (Local& l : ranks) l.L.reset();
     return;
   }
   // 3a. count matrix: every rank's row counts per destination
+  enter(1);
   double tc = now_ms();
   xfer_allgather_i64(ranks, (size_t)W);
   collective(1, tc);
@@ -737,12 +748,14 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
         return W == 1 ? col_ptr(l.ctx, l.Lv, j) : (void*)((unsigned char*)l.st->send.p + packed_base(l.to_peer, d, j));
       }, dst, sends[i], recvs[i]);
     }
+    enter(2);
     tc = now_ms();
     xfer_p2p(ranks, sends, recvs);
     collective(2, tc);
   }
   // 4. reduce the received rows: one source's rows are already unique by key, rows from two or
   // more sources are summed by key (MergeReduce: one hash table, source order)
+  enter(3);
   {
     std::vector<TableOwner> red(ranks.size());
     for (size_t i = 0; i < ranks.size(); ++i) {
@@ -777,6 +790,7 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
   }
   if (mode == MergeOut::kHostDirect) {
     // 5. every rank's partition straight into its slice of the host result
+    enter(5);
     std::vector<bqg_table*> src;
     for (Local& l : ranks) src.push_back(l.R.t);
     to_host(src);
@@ -786,6 +800,7 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
   // 5. gather to rank 0: the partitions' row counts (all-local: known here; else an
   // all-gather), then the reduced partitions column by column
   std::vector<int64_t> part_rows(W, 0);
+  enter(4);
   tc = now_ms();
   if (all_local) {
     for (Local& l : ranks) part_rows[l.st->rank] = l.R.t ? nrows_of(l.ctx, l.R.t) : 0;
@@ -804,6 +819,7 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       if (l.st->rank != 0) part_rows[l.st->rank] = l.R.t ? nrows_of(l.ctx, l.R.t) : 0;
   }
   collective(4, tc);
+  enter(5);
   tc = now_ms();
   int64_t others = 0;
   for (int s = 1; s < W; ++s) others += part_rows[s];
@@ -890,6 +906,17 @@ int merge_entry(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, 
       if (n_tables[i] < 0) comm_fail(BQG_E_INVALID, "negative table count");
       for (int j = 0; j < n_tables[i]; ++j) ranks[i].tables.push_back(tables[k++]);
     }
+    // progress marks (bqg_comm_progress): started now; idle and done at every exit
+    struct Progress {
+      std::vector<Local>& r;
+      ~Progress() {
+        for (Local& l : r) {
+          l.st->cur_phase.store(-1, std::memory_order_relaxed);
+          l.st->merges_done.fetch_add(1, std::memory_order_relaxed);
+        }
+      }
+    } progress{ranks};
+    for (Local& l : ranks) l.st->merges_started.fetch_add(1, std::memory_order_relaxed);
     merge_impl(ranks, n_keys, dts, reduced, mode, host_out);
   });
 }
@@ -1000,6 +1027,15 @@ int bqg_comm_last_phases(bqg_ctx* ctx, double* ms, int32_t n) {
     if (!ms || n < 0) comm_fail(BQG_E_INVALID, "null output");
     CommState* s = state_of(ctx);
     for (int i = 0; i < n && i < kMergePhases; ++i) ms[i] = s->phase_ms[i];
+  });
+}
+
+int bqg_comm_progress(bqg_ctx* ctx, int32_t* phase, int64_t* started, int64_t* done) {
+  return comm_guard(ctx, [&] {
+    CommState* s = state_of(ctx);
+    if (phase) *phase = s->cur_phase.load(std::memory_order_relaxed);
+    if (started) *started = s->merges_started.load(std::memory_order_relaxed);
+    if (done) *done = s->merges_done.load(std::memory_order_relaxed);
   });
 }
 

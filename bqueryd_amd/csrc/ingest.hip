@@ -67,8 +67,6 @@ const BloscApi& blosc_api() {
   return api;
 }
 
-constexpr size_t kBloscpackHeader = 16;
-constexpr size_t kBloscHeader = 16;
 
 bool read_file(const std::string& path, std::vector<unsigned char>& buf, std::string& err) {
   const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
@@ -290,7 +288,6 @@ size_t batch_bytes() {
   }();
   return b;
 }
-constexpr size_t kRawPiece = size_t(64) << 10;      // stored-raw bytes per copy task
 
 bool grow_host(void*& p, size_t& cap, size_t want) {
   if (cap >= want) return true;
@@ -318,105 +315,6 @@ bool grow_dev(void*& p, size_t& cap, size_t want) {
   }
   cap = want;
   return true;
-}
-
-int32_t le32(const unsigned char* p) {
-  int32_t v;
-  memcpy(&v, p, 4);
-  return v;
-}
-
-struct ChunkFile {
-  int job;      // column (index into the jobs)
-  int64_t index;
-  size_t off;   // of the file in the slot's host buffer
-  size_t size;  // file bytes
-};
-
-enum class Plan { kTasks, kFallback, kError };
-
-// Task lists for one chunk file (bloscpack header + blosc1 frame) already in the host buffer
-// at f.off.  dst / tmp: the chunk's place in the column / in the slot's shuffle scratch.
-Plan plan_chunk(const unsigned char* file, const ChunkFile& f, uint64_t dst, uint64_t tmp, size_t want,
-                size_t chunk_bytes, const std::string& dir, std::vector<BloscSplit>& splits,
-                std::vector<BloscBlock>& blocks, std::string& err) {
-  const std::string where = "chunk " + std::to_string(f.index) + " of " + dir;
-  if (f.size < kBloscpackHeader + kBloscHeader || memcmp(file, "blpk", 4) != 0) {
-    err = where + " is not a bloscpack chunk";
-    return Plan::kError;
-  }
-  const unsigned char* frame = file + kBloscpackHeader;
-  const size_t avail = f.size - kBloscpackHeader;
-  const unsigned flags = frame[2], ts = frame[3];
-  const int64_t nbytes = le32(frame + 4), blocksize = le32(frame + 8), cbytes = le32(frame + 12);
-  if (cbytes < (int64_t)kBloscHeader || (size_t)cbytes > avail || nbytes < (int64_t)want ||
-      nbytes > (int64_t)chunk_bytes) {
-    err = where + ": frame holds " + std::to_string(nbytes) + " bytes, expected " + std::to_string(want);
-    return Plan::kError;
-  }
-  if ((size_t)nbytes != want) return Plan::kFallback;  // a padded last frame: host copies `want`
-  if (nbytes == 0) return Plan::kTasks;
-  // flag bits the device decoder does not implement go to host libblosc: 0x8 (the delta
-  // filter of newer c-blosc 1.x) and the reserved 0x40 / 0x80 bits of non-codec use
-  if (flags & 0x8) return Plan::kFallback;
-  const uint64_t frame_src = f.off + kBloscpackHeader;
-  if (flags & 0x2) {  // memcpyed: the items follow the header as they are
-    if (kBloscHeader + (size_t)nbytes > (size_t)cbytes) {
-      err = where + ": truncated memcpyed frame";
-      return Plan::kError;
-    }
-    for (size_t k = 0; k < (size_t)nbytes; k += kRawPiece) {
-      const uint32_t n = (uint32_t)std::min(kRawPiece, (size_t)nbytes - k);
-      splits.push_back({frame_src + kBloscHeader + k, dst + k, n, n, kSplitRaw, 0});
-    }
-    return Plan::kTasks;
-  }
-  const int codec = (int)(flags >> 5);
-  if ((flags & 0x4) || (codec != kSplitBloscLz && codec != kSplitLz4) || ts == 0) return Plan::kFallback;
-  if (blocksize <= 0) {
-    err = where + ": bad blocksize";
-    return Plan::kError;
-  }
-  const int64_t nblocks = (nbytes + blocksize - 1) / blocksize;
-  const int64_t leftover = nbytes % blocksize;
-  if ((int64_t)kBloscHeader + 4 * nblocks > cbytes) {
-    err = where + ": truncated block table";
-    return Plan::kError;
-  }
-  const bool shuffle = (flags & 0x1) && ts > 1;
-  const uint64_t out = shuffle ? tmp : dst;
-  const size_t splits0 = splits.size(), blocks0 = blocks.size();
-  for (int64_t b = 0; b < nblocks; ++b) {
-    const bool last_partial = b == nblocks - 1 && leftover != 0;
-    const int64_t bsize = last_partial ? leftover : blocksize;
-    const int64_t nsplits =
-        (!(flags & 0x10) && ts <= 16 && blocksize / (int64_t)ts >= 128 && !last_partial) ? (int64_t)ts : 1;
-    if (bsize % nsplits != 0) {
-      splits.resize(splits0);
-      blocks.resize(blocks0);
-      return Plan::kFallback;
-    }
-    const int64_t neblock = bsize / nsplits;
-    int64_t p = le32(frame + kBloscHeader + 4 * b);
-    const uint64_t boff = (uint64_t)(b * blocksize);
-    for (int64_t j = 0; j < nsplits; ++j) {
-      if (p < 0 || p + 4 > cbytes) {
-        err = where + ": block " + std::to_string(b) + " out of the frame";
-        return Plan::kError;
-      }
-      const int64_t csize = le32(frame + p);
-      p += 4;
-      if (csize < 0 || p + csize > cbytes) {
-        err = where + ": block " + std::to_string(b) + " out of the frame";
-        return Plan::kError;
-      }
-      splits.push_back({frame_src + (uint64_t)p, out + boff + (uint64_t)(j * neblock), (uint32_t)csize,
-                        (uint32_t)neblock, csize == neblock ? (int32_t)kSplitRaw : (int32_t)codec, 0});
-      p += csize;
-    }
-    if (shuffle) blocks.push_back({tmp + boff, dst + boff, (uint32_t)bsize, ts});
-  }
-  return Plan::kTasks;
 }
 
 // host libblosc decode of one chunk file already in memory, `want` bytes to dst (synchronous)

@@ -18,10 +18,19 @@ std::string jit_spec(const ScanParams& p);
 // module function `kernel` specialised by `spec` for the current device, or nullptr when the
 // JIT is unavailable or failed (the failure is remembered, not retried); whether to use it at
 // all is the caller's choice (context options "jit" / "jit_min_rows", api.hip)
-hipFunction_t jit_function(const char* kernel, const std::string& spec);
+// `async`: a shape in neither the memory nor the disk cache is queued for a background
+// compile and nullptr returned (*final_answer = false) -- the caller runs the generic kernel
+// this time and gets the specialised one on a later call, so no query waits for hiprtc
+hipFunction_t jit_function(const char* kernel, const std::string& spec, bool async = false,
+                           bool* final_answer = nullptr);
 
 // jit_function(kernel, jit_spec(p) + extra), looked up first by the binary image of p's
 // specialised fields (the per-query path: no prologue text is built for a known shape)
-hipFunction_t jit_function_for(const char* kernel, const ScanParams& p, const std::string& extra = std::string());
+hipFunction_t jit_function_for(const char* kernel, const ScanParams& p, const std::string& extra = std::string(),
+                               bool async = false);
+
+// wait until no background compile is queued or running (timeout_ms < 0: no limit); false on
+// timeout.  compiled / failed (optional): background compiles finished so far, per outcome.
+bool jit_wait(double timeout_ms, int64_t* compiled, int64_t* failed);
 
 }  // namespace bqg

@@ -6,13 +6,18 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <map>
 #include <mutex>
+#include <set>
 #include <sstream>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -101,15 +106,35 @@ struct JitState {
   bool tried = false;
   std::map<std::string, hipFunction_t> fns;  // device:kernel:hash -> function (nullptr = failed)
   // per-query front cache (jit_function_for): binary shape key -> function, so a repeated query
-  // shape costs one hash lookup instead of formatting and hashing its prologue
+  // shape costs one hash lookup instead of formatting and hashing its prologue (final answers
+  // only: a shape whose compile is still queued is looked up again)
   std::unordered_map<std::string, hipFunction_t> by_shape;
+  // background compiles (jit_function(..., async)): a cache miss queues the source and the
+  // query runs the precompiled generic kernel; the worker thread compiles, writes the disk
+  // cache and leaves the code object here, and the next query of that shape loads it (module
+  // loads stay on the querying thread, on its device)
+  struct Job {
+    std::string key, src, path;
+  };
+  std::deque<Job> queue;
+  std::set<std::string> pending;                   // keys queued or compiling
+  std::map<std::string, std::vector<char>> ready;  // key -> code object (empty: compile failed)
+  std::thread worker;
+  std::condition_variable cv, cv_idle;
+  bool worker_started = false, stopping = false;
+  int64_t compiled = 0, failed = 0;
 
-  bool compile(const std::string& src, std::vector<char>& code) {
+  bool rtc_ok() {
     if (!tried) {
       tried = true;
       rtc = new Rtc();
     }
-    if (!rtc->ok) return false;
+    return rtc->ok;
+  }
+
+  // (the caller holds mu only when it is the synchronous path; hiprtc itself is thread-safe)
+  bool compile(const std::string& src, std::vector<char>& code) {
+    if (!rtc || !rtc->ok) return false;
     std::vector<const char*> names(kJitHeaderNames, kJitHeaderNames + kJitHeaderCount);
     std::vector<const char*> texts(kJitHeaderTexts, kJitHeaderTexts + kJitHeaderCount);
     names.push_back("stddef.h");
@@ -140,11 +165,76 @@ struct JitState {
     rtc->destroy(&prog);
     return ok;
   }
+
+  void run_worker() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return stopping || !queue.empty(); });
+      if (stopping) break;
+      Job j = std::move(queue.front());
+      queue.pop_front();
+      lk.unlock();
+      std::vector<char> code;
+      const bool ok = compile(j.src, code);
+      if (ok) {
+        const std::string dir = j.path.substr(0, j.path.rfind('/'));
+        mkdirs(dir);
+        write_file(j.path, code);
+      }
+      lk.lock();
+      (ok ? compiled : failed) += 1;
+      if (!ok) code.clear();
+      ready[j.key] = std::move(code);
+      pending.erase(j.key);
+      if (pending.empty()) cv_idle.notify_all();
+    }
+    pending.clear();
+    cv_idle.notify_all();
+  }
+
+  // (mu held) start the worker on first use; at process exit it finishes the compile in
+  // flight and drops the rest (a detached compile racing the runtime's teardown could crash)
+  void enqueue(Job j) {
+    pending.insert(j.key);
+    queue.push_back(std::move(j));
+    if (!worker_started) {
+      worker_started = true;
+      worker = std::thread([this] { run_worker(); });
+      std::atexit([] { shutdown(); });
+    }
+    cv.notify_one();
+  }
+
+  static void shutdown();
+
+  // (mu held) load a code object into a function of the current device (nullptr on failure)
+  static hipFunction_t load(const std::vector<char>& code, const char* kernel) {
+    hipFunction_t fn = nullptr;
+    if (code.empty()) return nullptr;
+    hipModule_t mod = nullptr;
+    if (hipModuleLoadData(&mod, code.data()) == hipSuccess) {
+      if (hipModuleGetFunction(&fn, mod, kernel) != hipSuccess) fn = nullptr;
+    } else {
+      (void)hipGetLastError();
+    }
+    return fn;
+  }
 };
 
 JitState& state() {
   static JitState* s = new JitState();  // never destroyed: modules live as long as the process
   return *s;
+}
+
+void JitState::shutdown() {
+  JitState& js = state();
+  {
+    std::lock_guard<std::mutex> lk(js.mu);
+    js.stopping = true;
+    js.queue.clear();
+  }
+  js.cv.notify_all();
+  if (js.worker.joinable()) js.worker.join();
 }
 
 }  // namespace
@@ -203,7 +293,7 @@ std::string jit_spec(const ScanParams& p) {
   return s.str();
 }
 
-hipFunction_t jit_function_for(const char* kernel, const ScanParams& p, const std::string& extra) {
+hipFunction_t jit_function_for(const char* kernel, const ScanParams& p, const std::string& extra, bool async) {
   // the key: device, kernel, extra defines, then (field, value) for every specialised field --
   // the field names' addresses mark which conditional fields are present
   int dev = 0;
@@ -226,15 +316,19 @@ hipFunction_t jit_function_for(const char* kernel, const ScanParams& p, const st
     auto it = js.by_shape.find(key);
     if (it != js.by_shape.end()) return it->second;
   }
-  hipFunction_t fn = jit_function(kernel, jit_spec(p) + extra);
-  std::lock_guard<std::mutex> lk(js.mu);
-  js.by_shape.emplace(std::move(key), fn);
+  bool final_answer = true;
+  hipFunction_t fn = jit_function(kernel, jit_spec(p) + extra, async, &final_answer);
+  if (final_answer) {
+    std::lock_guard<std::mutex> lk(js.mu);
+    js.by_shape.emplace(std::move(key), fn);
+  }
   return fn;
 }
 
-hipFunction_t jit_function(const char* kernel, const std::string& spec) {
+hipFunction_t jit_function(const char* kernel, const std::string& spec, bool async, bool* final_answer) {
   JitState& js = state();
   std::lock_guard<std::mutex> lk(js.mu);
+  if (final_answer) *final_answer = true;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   const std::string src = spec + "#include \"jit_kernels.h\"\n";
@@ -251,28 +345,52 @@ hipFunction_t jit_function(const char* kernel, const std::string& spec) {
   const std::string key = std::to_string(dev) + ":" + kernel + ":" + hex;
   auto it = js.fns.find(key);
   if (it != js.fns.end()) return it->second;
-  hipFunction_t fn = nullptr;
+  // compiled in the background since the last query of this shape: load it now
+  const std::string ck = std::string(kernel) + ":" + hex;  // the code object serves every device
+  auto rd = js.ready.find(ck);
+  if (rd != js.ready.end()) {
+    hipFunction_t fn = JitState::load(rd->second, kernel);
+    js.fns[key] = fn;
+    return fn;
+  }
+  if (js.pending.count(ck)) {
+    if (final_answer) *final_answer = false;
+    return nullptr;  // still compiling: the generic kernel runs this query
+  }
   std::vector<char> code;
-  const std::string dir = cache_dir();
-  const std::string path = dir + "/" + hex + ".hsaco";
+  const std::string path = cache_dir() + "/" + hex + ".hsaco";
   if (!read_file(path, code)) {
-    if (js.compile(src, code)) {
-      mkdirs(dir);
+    if (!js.rtc_ok()) {
+      code.clear();
+    } else if (async) {
+      js.enqueue(JitState::Job{ck, src, path});
+      if (final_answer) *final_answer = false;
+      return nullptr;
+    } else if (js.compile(src, code)) {
+      mkdirs(cache_dir());
       write_file(path, code);
     } else {
       code.clear();
     }
   }
-  if (!code.empty()) {
-    hipModule_t mod = nullptr;
-    if (hipModuleLoadData(&mod, code.data()) == hipSuccess) {
-      if (hipModuleGetFunction(&fn, mod, kernel) != hipSuccess) fn = nullptr;
-    } else {
-      (void)hipGetLastError();
-    }
-  }
+  hipFunction_t fn = JitState::load(code, kernel);
   js.fns[key] = fn;
   return fn;
+}
+
+bool jit_wait(double timeout_ms, int64_t* compiled, int64_t* failed) {
+  JitState& js = state();
+  std::unique_lock<std::mutex> lk(js.mu);
+  bool idle = true;
+  if (timeout_ms < 0) {
+    js.cv_idle.wait(lk, [&] { return js.pending.empty(); });
+  } else {
+    idle = js.cv_idle.wait_for(lk, std::chrono::duration<double, std::milli>(timeout_ms),
+                               [&] { return js.pending.empty(); });
+  }
+  if (compiled) *compiled = js.compiled;
+  if (failed) *failed = js.failed;
+  return idle;
 }
 
 }  // namespace bqg
@@ -286,6 +404,6 @@ extern "C" int bqg_internal_jit_compile_check(const char* spec) {
   std::lock_guard<std::mutex> lk(js.mu);
   std::vector<char> code;
   setenv("BQGPU_JIT_VERBOSE", "1", 0);
-  if (js.compile(std::string(spec) + "#include \"jit_kernels.h\"\n", code)) return 0;
+  if (js.rtc_ok() && js.compile(std::string(spec) + "#include \"jit_kernels.h\"\n", code)) return 0;
   return js.rtc && js.rtc->ok ? 2 : 1;
 }

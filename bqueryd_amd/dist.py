@@ -99,6 +99,18 @@ def merge_phases(device):
     return OrderedDict(zip(MERGE_PHASES, list(out)))
 
 
+def merge_progress(device):
+    """Where this context's rank is in its merges (``bqg_comm_progress``; safe while a merge
+    runs on another thread): the phase entered last (``'idle'`` between merges) and the merges
+    begun / ended -- what a watchdog reports for a rank whose collective does not return."""
+    from . import _lib as L
+    ph, started, done = ctypes.c_int32(-1), ctypes.c_int64(0), ctypes.c_int64(0)
+    device.check(L.lib().bqg_comm_progress(device.handle, ctypes.byref(ph), ctypes.byref(started),
+                                           ctypes.byref(done)))
+    return {'phase': MERGE_PHASES[ph.value] if 0 <= ph.value < len(MERGE_PHASES) else 'idle',
+            'merges_started': started.value, 'merges_done': done.value}
+
+
 def _schema(groupby_cols, agg_list, dtypes):
     """(column names, C dtype codes) of the merge: datetime64 keys travel as their int64 ticks;
     string keys cannot merge on the device (each table's dictionary codes are its own)."""

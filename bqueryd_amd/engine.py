@@ -74,6 +74,14 @@ class Device:
     def reset_options(self):
         self.check(self._lib.bqg_reset_options(self.handle))
 
+    def jit_wait(self, timeout_s=None):
+        """Wait for the background compiles of query-specialised kernels (option jit_async):
+        ``{'idle': bool, 'compiled': n, 'failed': n}`` (``idle`` False after a timeout)."""
+        idle, comp, fail = ctypes.c_int32(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        self.check(self._lib.bqg_jit_wait(self.handle, -1.0 if timeout_s is None else 1e3 * float(timeout_s),
+                                          ctypes.byref(idle), ctypes.byref(comp), ctypes.byref(fail)))
+        return {'idle': bool(idle.value), 'compiled': comp.value, 'failed': fail.value}
+
     def options(self, **values):
         """Context manager: the given options set for the block, the previous values restored
         after it."""

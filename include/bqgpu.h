@@ -49,8 +49,10 @@ extern "C" {
  * 8 -- bqg_timing.bytes is always the algorithmic bytes (the query's columns at
  *      their stored widths) and bqg_timing.bytes_read the bytes the scan actually read (less
  *      when it read compact resident copies); bqg_table_device_bytes, bqg_table_build_compact,
- *      bqg_table_drop_compact (the compact copies' HBM, built and released explicitly). */
-#define BQG_ABI_VERSION 8
+ *      bqg_table_drop_compact (the compact copies' HBM, built and released explicitly);
+ * 9 -- bqg_comm_progress (the merge phase a rank is in, readable while it runs); option
+ *      jit_async and bqg_jit_wait (no query waits for a run-time compile). */
+#define BQG_ABI_VERSION 9
 
 /* error codes */
 #define BQG_OK 0
@@ -214,11 +216,23 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *                     copies, then fails with BQG_E_OOM
  *   part_ring      0  packed partitioned scatter (query-specialised): tiles 0 (1) | 1 | 2
  *                     of row loads in flight per workgroup
+ *   jit_async      1  a query shape whose specialised kernel is in neither  0 | 1
+ *                     the memory nor the disk cache runs the precompiled
+ *                     generic kernel while a background host thread compiles
+ *                     it with hiprtc; later queries of the shape run it
+ *                     (0: the query compiles and waits, seconds on a cold
+ *                     cache).  Both kernels give the same bits
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);
 int bqg_get_option(bqg_ctx* ctx, const char* name, int64_t* value);
 int bqg_reset_options(bqg_ctx* ctx);
+/* Wait for the background compiles of query-specialised kernels (option jit_async; ABI 9):
+ * until none is queued or running, or timeout_ms (< 0: no limit).  *idle 1 when none is left
+ * (0 on timeout); *compiled / *failed the background compiles finished so far in this process.
+ * Any out pointer may be NULL.  A benchmark calls it before its timed loop; a worker never
+ * needs to. */
+int bqg_jit_wait(bqg_ctx* ctx, double timeout_ms, int32_t* idle, int64_t* compiled, int64_t* failed);
 
 /* ---------------- pinned host memory ---------------- */
 int bqg_alloc_pinned(bqg_ctx* ctx, size_t bytes, void** out);
@@ -391,6 +405,11 @@ int bqg_comm_info(bqg_ctx* ctx, int32_t* rank, int32_t* nranks);
  * every step waits for the device work it queued, so each phase holds its own device time.
  * Up to n values. */
 int bqg_comm_last_phases(bqg_ctx* ctx, double* ms, int32_t n);
+/* Progress of this rank's merges (ABI 9), safe to call from another host thread while a merge
+ * runs -- a watchdog naming the step a hung collective waits in: *phase the merge phase entered
+ * last (numbered as above) or -1 between merges, *started / *done the merges begun / ended
+ * (done counts failures too).  Any pointer may be NULL. */
+int bqg_comm_progress(bqg_ctx* ctx, int32_t* phase, int64_t* started, int64_t* done);
 int bqg_merge(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int32_t n_keys, int32_t n_cols,
               const int32_t* dtypes, int32_t reduced, bqg_table** out);
 int bqg_merge_group(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,

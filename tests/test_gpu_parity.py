@@ -1049,6 +1049,45 @@ def test_moments_of_wrapping_int64_and_coded_columns(mode, oracle_c, engine_opti
     assert_tables_equal(got, ref, exact_cols={'bs'})
 
 
+@pytest.mark.parametrize('compact', [1, 2])
+@pytest.mark.parametrize('mode', ['shared', 'global_dense'])
+def test_code_copies_without_narrow_codes(mode, compact, oracle_c, engine_options):
+    """part_narrow=0 turns the atomic modes' integer-coded float sums off, so the plan gives a
+    cents / dyadic column fixed-point limbs; the compact scan then still reads the column's code
+    copy and sums the codes as integers -- that state is no limb sum any more and must not be
+    finalized as one (the emit decoded a double's bits as a code sum).  Against the
+    oracle and against the full-width scan."""
+    rng = np.random.default_rng(41 + compact)
+    n = 250_000
+    engine_options(part_narrow=0, compact=compact)
+    if mode == 'global_dense':
+        engine_options(partition=0)
+    k = rng.integers(0, 700 if mode == 'shared' else 140_000, n).astype(np.int32)
+    cols = OrderedDict(k=k, c=rng.integers(-50_000, 90_000, n) / 100.0,
+                       f=rng.integers(-20_000, 40_000, n) / 100.0,
+                       d=np.ldexp(rng.integers(-2**20, 2**20, n).astype(np.float64), -5),
+                       r=rng.normal(size=n) * 1e3, t=rng.integers(0, 4, n).astype(np.int32))
+    aggs = [['c', 'sum', 'cs'], ['f', 'sum', 'fs'], ['f', 'mean', 'fm'], ['d', 'sum', 'ds'], ['r', 'sum', 'rs'],
+            ['c', 'count', 'n']]
+    terms = [('t', '!=', 2)]
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(['k'], aggs, where_terms=terms)
+        info = t.dev.last_timing()
+        with t.dev.options(compact=0):
+            full, _ = t.groupby(['k'], aggs, where_terms=terms)
+    finally:
+        t.close()
+    assert info['mode'] == {'shared': 1, 'global_dense': 2}[mode], info
+    assert info['bytes_read'] < info['bytes'], info  # the code copies were read
+    ref = oracle_c.groupby(cols, ['k'], aggs, oracle_c.where_terms(cols, terms))
+    assert_tables_equal(got, ref, exact_cols={'ds'})
+    assert_tables_equal(full, ref, exact_cols={'ds'})
+    np.testing.assert_array_equal(got['ds'], full['ds'])  # dyadic: the exact sum either way
+    for name in ('cs', 'fs'):  # the correctly rounded decimal sum vs limbs truncated at 2^-95 of the slot's max
+        np.testing.assert_allclose(got[name], full[name], rtol=1e-15, atol=0)
+
+
 @pytest.mark.parametrize('mode', ['private', 'shared', 'global_dense'])
 def test_compact_resident_copies(mode, oracle_c, engine_options):
     """Compact resident copies (option compact): narrow integer offsets for keys / terms /
