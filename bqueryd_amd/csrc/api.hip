@@ -346,7 +346,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kOptMemCap, kOptPartRing, kOptJitAsync, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kOptMemCap, kOptPartRing, kOptJitAsync, kOptWarm, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -379,6 +379,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"mem_cap_mb", 0, 0, 1ll << 24},        // column memory budget of the context in MiB (0: the device's)
     {"part_ring", 0, 0, 2},                 // packed scatter (JIT): tiles of row loads in flight (0: 1)
     {"jit_async", 1, 0, 1},                 // a shape not compiled yet runs the generic kernel while hiprtc compiles it
+    {"warm", 1, 0, 1},                      // bqg_create runs one small query (read at context creation only)
 };
 
 static int opt_index(const char* name) {
@@ -2280,6 +2281,53 @@ int bqg_reset_options(bqg_ctx* c) {
   });
 }
 
+// Start-up work a worker's first query would otherwise pay (option warm, at context creation):
+// the first launch from the library's code object loads it (~0.7 ms, measured: a cold C2
+// query's generic scan 1.04 ms against 0.36 ms steady, profiles/r6b_cold_probe.json), each
+// kernel's first launch resolves its symbol, and the private scan's partials / the pooled
+// pinned result blocks are allocated on first use.  One small C2-shaped query -- 3 columns, a
+// filter, sum / mean / count over 10 groups, 768 tiles so the partials reach their steady size
+// on a 256-CU device -- does all of it once; the table is freed before bqg_create returns.
+static void warm_context(bqg_ctx* c) {
+  const int64_t n = (int64_t)std::max(c->cu, 1) * 3 * 1024;
+  const int32_t dts[3] = {BQG_I32, BQG_F64, BQG_I8};
+  std::vector<int32_t> k((size_t)n);
+  std::vector<double> v((size_t)n);
+  std::vector<int8_t> f((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    k[(size_t)i] = (int32_t)(i % 10);
+    v[(size_t)i] = (double)(i % 97) * 0.25;
+    f[(size_t)i] = (int8_t)(i % 5);
+  }
+  bqg_table* t = nullptr;
+  auto ok = [&](int rc) {
+    if (rc != BQG_OK) fail(rc, "context warm-up query failed: %s", bqg_last_error(c));
+  };
+  ok(bqg_table_create(c, n, 3, dts, &t));
+  std::unique_ptr<bqg_table, int (*)(bqg_table*)> own(t, bqg_table_destroy);
+  ok(bqg_push_chunk(t, 0, k.data(), n, 0));
+  ok(bqg_push_chunk(t, 1, v.data(), n, 0));
+  ok(bqg_push_chunk(t, 2, f.data(), n, 0));
+  ok(bqg_table_sync(t));
+  const int64_t two = 2;
+  const bqg_term term{2, BQG_T_GE, 1, &two, nullptr};
+  const int32_t key = 0;
+  const bqg_agg aggs[3] = {{1, BQG_SUM}, {1, BQG_MEAN}, {1, BQG_COUNT}};
+  const bqg_query q{1, &key, 1, &term, -1, 3, aggs};
+  for (int64_t compact = 0; compact <= 1; ++compact) {  // the scan over the columns as stored, then over copies
+    const int64_t saved = c->opt[kOptCompact];
+    c->opt[kOptCompact] = compact ? saved : 0;
+    bqg_result* r = nullptr;
+    const int rc = bqg_groupby(c, t, &q, &r);
+    c->opt[kOptCompact] = saved;
+    ok(rc);
+    bqg_result_free(r);
+  }
+  own.reset();
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  c->last = bqg_timing{};
+}
+
 int bqg_create(int device_ordinal, bqg_ctx** out) {
   bqg_ctx* c = nullptr;
   int rc = guard(nullptr, [&] {
@@ -2303,6 +2351,7 @@ int bqg_create(int device_ordinal, bqg_ctx** out) {
     for (int i = 0; i < 2; ++i) HIPCHECK(hipEventCreateWithFlags(&c->ev_sh[i], hipEventDisableSystemFence));
     // last-workgroup-done counters of the finish kernels (each reset by its last workgroup)
     HIPCHECK(hipMemset(c->done.ensure(256), 0, 256));
+    if (c->opt[kOptWarm]) warm_context(c);
     *out = c;
   });
   if (rc != BQG_OK && c) {

@@ -114,7 +114,9 @@ struct JitState {
   // cache and leaves the code object here, and the next query of that shape loads it (module
   // loads stay on the querying thread, on its device)
   struct Job {
-    std::string key, src, path;
+    std::string key, src, path;  // key: kernel:hash (the code object serves every device)
+    std::string fkey, kernel;    // the function's key in `fns` and its name, on device `dev`
+    int dev;
   };
   std::deque<Job> queue;
   std::set<std::string> pending;                   // keys queued or compiling
@@ -124,11 +126,14 @@ struct JitState {
   bool worker_started = false, stopping = false;
   int64_t compiled = 0, failed = 0;
 
+  // hiprtc is dlopen'ed once, by whichever thread needs it first (the background worker, for
+  // async queries: the ~1 ms load of hiprtc and comgr stays off the query path)
+  std::once_flag rtc_once;
   bool rtc_ok() {
-    if (!tried) {
+    std::call_once(rtc_once, [this] {
       tried = true;
       rtc = new Rtc();
-    }
+    });
     return rtc->ok;
   }
 
@@ -175,15 +180,23 @@ struct JitState {
       queue.pop_front();
       lk.unlock();
       std::vector<char> code;
-      const bool ok = compile(j.src, code);
+      // the disk cache first (another process compiled it), else hiprtc
+      const bool cached = read_file(j.path, code);
+      const bool ok = cached || (rtc_ok() && compile(j.src, code));
+      hipFunction_t fn = nullptr;
       if (ok) {
-        const std::string dir = j.path.substr(0, j.path.rfind('/'));
-        mkdirs(dir);
-        write_file(j.path, code);
+        if (!cached) {
+          const std::string dir = j.path.substr(0, j.path.rfind('/'));
+          mkdirs(dir);
+          write_file(j.path, code);
+        }
+        // the module load too (~1 ms): the query that next meets this shape just launches it
+        if (hipSetDevice(j.dev) == hipSuccess) fn = load(code, j.kernel.c_str());
       }
       lk.lock();
       (ok ? compiled : failed) += 1;
       if (!ok) code.clear();
+      fns[j.fkey] = fn;
       ready[j.key] = std::move(code);
       pending.erase(j.key);
       if (pending.empty()) cv_idle.notify_all();
@@ -359,13 +372,16 @@ hipFunction_t jit_function(const char* kernel, const std::string& spec, bool asy
   }
   std::vector<char> code;
   const std::string path = cache_dir() + "/" + hex + ".hsaco";
+  if (async) {
+    // the disk read, the compile on a miss and the module load (~1 ms even for a cached code
+    // object) all run on the worker: this query runs the generic kernel
+    js.enqueue(JitState::Job{ck, src, path, key, kernel, dev});
+    if (final_answer) *final_answer = false;
+    return nullptr;
+  }
   if (!read_file(path, code)) {
     if (!js.rtc_ok()) {
       code.clear();
-    } else if (async) {
-      js.enqueue(JitState::Job{ck, src, path});
-      if (final_answer) *final_answer = false;
-      return nullptr;
     } else if (js.compile(src, code)) {
       mkdirs(cache_dir());
       write_file(path, code);

@@ -222,6 +222,10 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *                     it with hiprtc; later queries of the shape run it
  *                     (0: the query compiles and waits, seconds on a cold
  *                     cache).  Both kernels give the same bits
+ *   warm           1  bqg_create runs one small query, so that a worker's    0 | 1
+ *                     first query does not pay the library's start-up (code
+ *                     object load, first launches, buffer sizing; read from
+ *                     BQGPU_OPTIONS at context creation only)
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);
@@ -229,7 +233,8 @@ int bqg_get_option(bqg_ctx* ctx, const char* name, int64_t* value);
 int bqg_reset_options(bqg_ctx* ctx);
 /* Wait for the background compiles of query-specialised kernels (option jit_async; ABI 9):
  * until none is queued or running, or timeout_ms (< 0: no limit).  *idle 1 when none is left
- * (0 on timeout); *compiled / *failed the background compiles finished so far in this process.
+ * (0 on timeout); *compiled / *failed the background jobs (a compile, or a load of a code object
+ * another process compiled into the disk cache) finished so far in this process.
  * Any out pointer may be NULL.  A benchmark calls it before its timed loop; a worker never
  * needs to. */
 int bqg_jit_wait(bqg_ctx* ctx, double timeout_ms, int32_t* idle, int64_t* compiled, int64_t* failed);
