@@ -533,6 +533,13 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
             del sc
     gen_s = time.perf_counter() - t_gen
     _stage('c5: RCCL communicator init (world %d)' % ws)
+    if os.environ.get('BQGPU_BENCH_ONE_GPU_RCCL') == '1':
+        # rehearsal of the multi-GPU run on a one-GPU box (with BQGPU_BENCH_DEVICE=0): RCCL
+        # refuses two ranks on one device of one host, so each rank claims a host of its own
+        # and the ranks talk over RCCL's socket transport (tools/dist_check.py does the same)
+        os.environ['NCCL_HOSTID'] = 'bqgpu-rank%d' % rank
+        os.environ.setdefault('NCCL_SOCKET_IFNAME', 'lo')
+        os.environ.setdefault('NCCL_IB_DISABLE', '1')
     with _stdout_to_stderr():  # librccl prints a banner on stdout at init
         uid = comm.broadcast_bytes(bdist.new_unique_id() if rank == 0 else None)
         rccl = bdist.RcclComm(dev, rank, ws, uid)

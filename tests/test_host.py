@@ -388,3 +388,13 @@ def test_ctable_tar_bytes_match_tarfile(nrows, monkeypatch):
                 tf.addfile(info, io.BytesIO(node))
         add('result_x1', tree)
     assert got == buf.getvalue()
+
+
+def test_option_names_match_the_header():
+    """bqueryd_amd._lib.OPTIONS (what the option tests walk) lists exactly the engine options
+    include/bqgpu.h documents."""
+    header = open(os.path.join(os.path.dirname(__file__), '..', 'include', 'bqgpu.h')).read()
+    block = header[header.index('Engine options (ABI 6)'):header.index('int bqg_set_option')]
+    names = re.findall(r'^ \*   (\w+)\s+-?\d', block, re.M)
+    assert len(names) >= 20, names
+    assert sorted(names) == sorted(_lib.OPTIONS), set(names) ^ set(_lib.OPTIONS)

@@ -36,10 +36,24 @@ def _check(merged, ref):
     return ok
 
 
+def one_gpu_rccl_env(rank):
+    """Every rank on GPU 0 over real RCCL (BQGPU_DIST_ONE_GPU=1): RCCL refuses two ranks on one
+    device of one host ("Duplicate GPU detected"), so each rank claims a host of its own
+    (NCCL_HOSTID) and the ranks talk over RCCL's socket transport on the loopback interface --
+    the merge's RCCL calls (grouped send / recv, all-gather) at world > 1 on a one-GPU box,
+    slowly.  Set before librccl initialises (the unique id below)."""
+    os.environ['NCCL_HOSTID'] = 'bqgpu-rank%d' % rank
+    os.environ.setdefault('NCCL_SOCKET_IFNAME', 'lo')
+    os.environ.setdefault('NCCL_IB_DISABLE', '1')
+    return 0
+
+
 def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist.init_process_group('gloo')
     rank, world = dist.get_rank(), dist.get_world_size()
+    if os.environ.get('BQGPU_DIST_ONE_GPU') == '1':
+        local = one_gpu_rccl_env(rank)
     uid = [bdist.new_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     dev = Device(local)
