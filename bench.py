@@ -549,10 +549,44 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
     colo.union(synth.query_columns(cfg))  # the rank's shard set, resident once (like the load)
     probe, _ = colo.groupby_tables(cfg['groupby'], cfg['aggs'])
     dtypes = {n: np.dtype(probe[0].dtypes[n]) for n in probe[0].names}
+    names = list(probe[0].names)
+    local_rows = sum(p_.nrows for p_ in probe)
     for p_ in probe:
         p_.close()
-    phase, timings = [], []
+    # the merged rows land in node-shared host memory (bqg_merge_shared_host): every rank copies
+    # its partition over its own link, as a one-process-per-GPU worker node would serve the
+    # reply -- no gather to rank 0 and no single large copy behind rank 0's link.  Sized from
+    # the largest rank's reduced table (ranks mostly share keys), grown if the merge has more.
+    _stage('c5: shared result block')
+    shm = {'cap': int(comm.max(local_rows) * 1.25) + 1024, 'block': None, 'n': 0}
+    shm_tag = comm.broadcast_bytes(('bqgpu-c5-%d-%d' % (os.getpid(), int(time.time()))).encode() if rank == 0 else None)
+
+    def open_block():
+        shm['n'] += 1
+        shm['block'] = bdist.SharedResult('%s-%d' % (shm_tag.decode(), shm['n']), shm['cap'], names, dtypes,
+                                          create=rank == 0)
+    if rank == 0:
+        open_block()
+    comm.barrier()
+    if rank != 0:
+        open_block()
+    phase, timings, merged_rows = [], [], []
     where = ['']
+
+    def merge(per, reduced):
+        while True:
+            try:
+                return bdist.merge_partials_shared(per, cfg['groupby'], cfg['aggs'], dtypes, rccl, shm['block'],
+                                                   reduced=reduced)
+            except ValueError as e:  # every rank alike: grow the block and merge again
+                comm.barrier()
+                shm['block'].close()
+                shm['cap'] = int(e.args[1])
+                if rank == 0:
+                    open_block()
+                comm.barrier()
+                if rank != 0:
+                    open_block()
 
     def step():
         _PROGRESS['stage'] = where[0] + ' shard pass'
@@ -561,11 +595,12 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
         timings.append(dev.last_timing())
         _PROGRESS['stage'] = where[0] + ' merge'
         t1 = time.perf_counter()
-        merged = bdist.merge_partials_device(per, cfg['groupby'], cfg['aggs'], dtypes, rccl, reduced=reduced)
+        n = merge(per, reduced)
         for p_ in per:
             p_.close()
         phase.append((t1 - t0, time.perf_counter() - t1))
-        return merged
+        merged_rows.append(n)
+        return n
 
     for i in range(warmup):
         where[0] = 'c5: warmup step %d/%d:' % (i + 1, warmup)
@@ -574,8 +609,8 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
             _stage('c5: waiting for background kernel compiles')
             dev.jit_wait(900)
     ok = None
-    if rank == 0 and out is not None:
-        ok = int(out['n'].sum()) == ws * rows  # every scanned row counted once, across the ranks
+    if rank == 0:  # every scanned row counted once, across the ranks (rank 0 reads the shared block)
+        ok = int(shm['block'].columns(out)['n'].sum()) == ws * rows
     # timed steps without device timing (with it, the merge waits for each phase's device work)
     dev.enable_timing(False)
     del phase[:], timings[:]
@@ -604,6 +639,8 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
     scan_ms = comm.max(float(np.mean([t['scan_ms'] for t in timings])))
     dev.enable_timing(False)
     _PROGRESS['device'] = None
+    comm.barrier()  # every rank done with the shared block before rank 0 unlinks it
+    shm['block'].close()
     rccl.close()
     colo.close()
     for t in tables:
@@ -614,8 +651,10 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
     alg = timings[-1]['bytes']
     return {
         'workload': ('C5: %d ranks x %d shards x %d rows = %d rows, groupby %s, aggs %s, one pass over each rank\'s '
-                     'shards + the aggregate=True merge across the ranks over RCCL (bqg_merge_host at world %d)'
+                     'shards + the aggregate=True merge across the ranks over RCCL (bqg_merge_shared_host at world '
+                     '%d: the merged rows into node-shared host memory, each rank\'s partition over its own link)'
                      % (ws, per_rank, shard_rows, ws * rows, cfg['groupby'], [a[1] for a in cfg['aggs']], ws)),
+        'merged_rows': merged_rows[-1] if merged_rows else None,
         'value': ws * rows * steps / elapsed,
         'unit': 'rows/s',
         'n_gpus': ws,

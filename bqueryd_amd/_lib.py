@@ -143,6 +143,7 @@ _PROTOS = {
     'bqg_merge': ([_P, _I32, _P, _I32, _I32, _P, _I32, ctypes.POINTER(_P)], ctypes.c_int),
     'bqg_merge_group': ([_I32, _P, _P, _P, _I32, _I32, _P, _I32, _P], ctypes.c_int),
     'bqg_merge_host': ([_P, _I32, _P, _I32, _I32, _P, _I32, ctypes.POINTER(_P)], ctypes.c_int),
+    'bqg_merge_shared_host': ([_P, _I32, _P, _I32, _I32, _P, _I32, _P, _I64, ctypes.POINTER(_I64)], ctypes.c_int),
     'bqg_merge_group_host': ([_I32, _P, _P, _P, _I32, _I32, _P, _I32, ctypes.POINTER(_P)], ctypes.c_int),
     'bqg_result_view_get': ([_P, ctypes.POINTER(ResultView)], ctypes.c_int),
     'bqg_hash_partition': ([_P, _P, _I32, _P, _I32, _I32, _P], ctypes.c_int),

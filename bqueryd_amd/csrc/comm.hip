@@ -165,6 +165,24 @@ struct CommState {
   // naming the collective a hung rank waits in): the phase entered last, -1 between merges
   std::atomic<int32_t> cur_phase{-1};
   std::atomic<int64_t> merges_started{0}, merges_done{0};
+  // the shared host result block of bqg_merge_shared_host, page-locked once (hipHostRegister)
+  // and kept registered while the caller keeps passing the same block
+  void* reg = nullptr;
+  size_t reg_bytes = 0;
+  void register_host(void* base, size_t bytes) {
+    if (reg == base && reg_bytes >= bytes) return;
+    if (reg) (void)hipHostUnregister(reg);
+    reg = nullptr;
+    reg_bytes = 0;
+    const hipError_t e = hipHostRegister(base, bytes, hipHostRegisterDefault);
+    if (e == hipErrorHostMemoryAlreadyRegistered) {
+      (void)hipGetLastError();  // the caller pinned it: use it as it is
+      return;
+    }
+    if (e != hipSuccess) comm_fail(BQG_E_OOM, std::string("hipHostRegister of the shared merge result: ") + hipGetErrorString(e));
+    reg = base;
+    reg_bytes = bytes;
+  }
   // in-process transport: an event on this rank's stream, and (rank 0) the copy descriptors
   // of a transfer step -- page-locked staging, its reuse guarded by desc_ev -- and their
   // device copy
@@ -199,6 +217,7 @@ void destroy_state(CommState* s) {
   s->ddesc.release();
   if (s->hcnt) (void)hipHostFree(s->hcnt);
   if (s->hdesc) (void)hipHostFree(s->hdesc);
+  if (s->reg) (void)hipHostUnregister(s->reg);
   if (s->ev) (void)hipEventDestroy(s->ev);
   if (s->desc_ev) (void)hipEventDestroy(s->desc_ev);
   delete s;
@@ -497,7 +516,19 @@ void xfer_p2p(std::vector<Local>& ranks, const std::vector<std::vector<P2P>>& se
 // where the merged table goes: a new device table on rank 0 (bqg_merge / bqg_merge_group), a
 // host result on rank 0 after the gather (bqg_merge_host), or a host result that every rank
 // fills with its own partition (bqg_merge_group_host driving every rank: no gather)
-enum class MergeOut { kDeviceRoot, kHostRoot, kHostDirect };
+// ... or (bqg_merge_shared_host, one process per GPU) host memory every rank's process maps:
+// each rank copies its partition into its slice over its own link (no gather to rank 0)
+enum class MergeOut { kDeviceRoot, kHostRoot, kHostDirect, kSharedHost };
+
+// the caller's shared block: column j at sum_{j' < j} align256(capacity << lg[j']) bytes,
+// rank r's rows after every lower rank's
+struct SharedOut {
+  unsigned char* base;
+  int64_t capacity;
+  int64_t* rows;
+};
+
+size_t shared_col_bytes(int64_t capacity, int lg) { return (((size_t)capacity << lg) + 255) & ~size_t(255); }
 
 // sum by key (MergeReduce, kernels.h) of the table `in` whose rows come from several sources
 // (row blocks [src_off[s], src_off[s + 1]), each unique by key) into `out` (capacity: every
@@ -551,7 +582,7 @@ void finish_reduce(Local& l, TableOwner& out) {
 }
 
 void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t>& dts, int reduced, MergeOut mode,
-                bqg_result** host_out) {
+                bqg_result** host_out, const SharedOut* sh) {
   const int ncols = (int)dts.size();
   if (n_keys < 1 || n_keys > ncols || n_keys > bqg::kMaxKeys) comm_fail(BQG_E_INVALID, "merge needs 1..4 key columns");
   if (ncols > bqg::kMergeMaxCols) comm_fail(BQG_E_UNSUPPORTED, "merge schema has too many columns");
@@ -636,6 +667,53 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     sync_all(ranks);
     *host_out = own.release();
   };
+  // the shared host result: every rank's row count (an all-gather), each rank's slice copied
+  // from its own GPU into the block every process maps, then an all-gather queued behind every
+  // rank's copies -- when it completes, every slice has landed (stream order on each rank)
+  auto to_shared = [&](std::vector<bqg_table*> src) {
+    enter(4);
+    double t0 = now_ms();
+    std::vector<int64_t> part_rows(W, 0);
+    if (W > 1) {
+      for (size_t i = 0; i < ranks.size(); ++i) {
+        HIPCK(hipSetDevice(bqg_internal_device(ranks[i].ctx)));
+        put_count((int64_t*)ranks[i].st->counts.p, src[i] ? nrows_of(ranks[i].ctx, src[i]) : 0, ranks[i].stream);
+      }
+      xfer_allgather_i64(ranks, 1);
+      Local& l0 = ranks[0];
+      HIPCK(hipSetDevice(bqg_internal_device(l0.ctx)));
+      HIPCK(hipMemcpyAsync(part_rows.data(), (int64_t*)l0.st->counts.p + W, sizeof(int64_t) * W, hipMemcpyDeviceToHost,
+                           l0.stream));
+      HIPCK(hipStreamSynchronize(l0.stream));
+    } else {
+      part_rows[0] = src[0] ? nrows_of(ranks[0].ctx, src[0]) : 0;
+    }
+    collective(4, t0);
+    int64_t total = 0;
+    for (int64_t r : part_rows) total += r;
+    *sh->rows = total;  // (every rank sees the same total, so every rank fails alike below)
+    if (total > sh->capacity)
+      comm_fail(BQG_E_INVALID, "shared merge result holds " + std::to_string(sh->capacity) + " rows, the merge has " +
+                                   std::to_string(total) + " (grow it to *rows and merge again)");
+    enter(5);
+    t0 = now_ms();
+    std::vector<size_t> coff(ncols + 1, 0);
+    for (int j = 0; j < ncols; ++j) coff[j + 1] = coff[j] + shared_col_bytes(sh->capacity, lg[j]);
+    for (size_t i = 0; i < ranks.size(); ++i) {
+      Local& l = ranks[i];
+      HIPCK(hipSetDevice(bqg_internal_device(l.ctx)));
+      l.st->register_host(sh->base, coff[ncols]);
+      int64_t off = 0;
+      for (int s2 = 0; s2 < l.st->rank; ++s2) off += part_rows[s2];
+      const int64_t n = part_rows[l.st->rank];
+      for (int j = 0; n && j < ncols; ++j)
+        HIPCK(hipMemcpyAsync(sh->base + coff[j] + ((size_t)off << lg[j]), col_ptr(l.ctx, src[i], j), (size_t)n << lg[j],
+                             hipMemcpyDeviceToHost, l.stream));
+    }
+    if (W > 1) xfer_allgather_i64(ranks, 1);
+    sync_all(ranks);
+    collective(5, t0);
+  };
   // 1. local reduce: the rank's tables summed by key (one hash reduce over their row-
   // concatenation, tables in order: the client's first-appearance order), unless the caller's
   // one table is already reduced
@@ -710,6 +788,11 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
     l.st->phase_ms[0] += now_ms() - t0;
   }
   // world 1 with a host result: the rank's reduced rows are the answer (no exchange)
+  if (W == 1 && mode == MergeOut::kSharedHost) {
+    to_shared({ranks[0].Lv});
+    for (Local& l : ranks) l.L.reset();
+    return;
+  }
   if (W == 1 && mode != MergeOut::kDeviceRoot) {
     enter(5);
     to_host({ranks[0].Lv});
@@ -787,6 +870,14 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       }
       l.st->phase_ms[3] += now_ms() - t0;
     }
+  }
+  if (mode == MergeOut::kSharedHost) {
+    // 5. every rank's partition straight into its slice of the shared host block
+    std::vector<bqg_table*> src;
+    for (Local& l : ranks) src.push_back(l.R.t);
+    to_shared(src);
+    for (Local& l : ranks) l.R.reset();
+    return;
   }
   if (mode == MergeOut::kHostDirect) {
     // 5. every rank's partition straight into its slice of the host result
@@ -886,10 +977,12 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
 
 int merge_entry(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,
                 int32_t n_keys, int32_t n_cols, const int32_t* dtypes, int32_t reduced, bqg_table** out,
-                MergeOut mode, bqg_result** host_out) {
+                MergeOut mode, bqg_result** host_out, const SharedOut* sh = nullptr) {
   bqg_ctx* c0 = n_local > 0 && ctxs ? ctxs[0] : nullptr;
   return comm_guard(c0, [&] {
-    if (n_local < 1 || !ctxs || !n_tables || !out || !dtypes || n_cols < 1 || (mode != MergeOut::kDeviceRoot && !host_out))
+    const bool host_mode = mode == MergeOut::kHostRoot || mode == MergeOut::kHostDirect;
+    if (n_local < 1 || !ctxs || !n_tables || !out || !dtypes || n_cols < 1 || (host_mode && !host_out) ||
+        (mode == MergeOut::kSharedHost && (!sh || !sh->base || !sh->rows || sh->capacity < 0)))
       comm_fail(BQG_E_INVALID, "bad merge arguments");
     if (host_out) *host_out = nullptr;
     std::vector<int32_t> dts(dtypes, dtypes + n_cols);
@@ -917,7 +1010,7 @@ int merge_entry(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, 
       }
     } progress{ranks};
     for (Local& l : ranks) l.st->merges_started.fetch_add(1, std::memory_order_relaxed);
-    merge_impl(ranks, n_keys, dts, reduced, mode, host_out);
+    merge_impl(ranks, n_keys, dts, reduced, mode, host_out, sh);
   });
 }
 
@@ -1054,6 +1147,14 @@ int bqg_merge_host(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int
                    const int32_t* dtypes, int32_t reduced, bqg_result** out) {
   bqg_table* unused = nullptr;
   return merge_entry(1, &ctx, &n_tables, tables, n_keys, n_cols, dtypes, reduced, &unused, MergeOut::kHostRoot, out);
+}
+
+int bqg_merge_shared_host(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int32_t n_keys, int32_t n_cols,
+                          const int32_t* dtypes, int32_t reduced, void* host, int64_t capacity_rows, int64_t* rows) {
+  bqg_table* unused = nullptr;
+  const SharedOut sh{(unsigned char*)host, capacity_rows, rows};
+  return merge_entry(1, &ctx, &n_tables, tables, n_keys, n_cols, dtypes, reduced, &unused, MergeOut::kSharedHost,
+                     nullptr, &sh);
 }
 
 int bqg_merge_group_host(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,

@@ -40,27 +40,6 @@ struct __align__(8) ScdSlot32 {
   uint32_t rc;    // rows (bits 0-15) | changes (bits 16-31)
 };
 
-// The two words of a slot's ScdSlot32 swap places with the slot's parity: word (s & 1) holds
-// `last`, the other `rc`.  The 64-row loop touches random slots' states with 32-bit accesses to
-// one field (the non-uniform step's `rc` update by each slot's first lane, `last` by its last
-// lane): with the fields at fixed offsets those addresses 8 s (+ 4) fall on every other LDS
-// bank only, so random slots met twice the bank conflicts of a 4-byte stride.  Swapped, either
-// field of random slots spreads over every bank.  (The per-slot lane-mask words of `tbl` get
-// the same treatment: half-wave h ORs into word h ^ (s & 1).)
-__device__ __forceinline__ uint32_t* scd_last_word(ScdSlot32* st, uint32_t s) {
-  return reinterpret_cast<uint32_t*>(st + s) + (s & 1u);
-}
-__device__ __forceinline__ uint32_t* scd_rc_word(ScdSlot32* st, uint32_t s) {
-  return reinterpret_cast<uint32_t*>(st + s) + ((s & 1u) ^ 1u);
-}
-__device__ __forceinline__ ScdSlot32 scd_get(const ScdSlot32* st, uint32_t s) {
-  const uint2 w = *reinterpret_cast<const uint2*>(st + s);
-  return (s & 1u) ? ScdSlot32{w.y, w.x} : ScdSlot32{w.x, w.y};
-}
-__device__ __forceinline__ void scd_put(ScdSlot32* st, uint32_t s, ScdSlot32 v) {
-  *reinterpret_cast<uint2*>(st + s) = (s & 1u) ? make_uint2(v.rc, v.last) : make_uint2(v.last, v.rc);
-}
-
 constexpr int kScdAhead = 4;  // 64-row steps loaded ahead of the one being folded
 
 __device__ __forceinline__ bool scd_equal(uint64_t a, uint64_t b, bool isf) {
@@ -212,7 +191,7 @@ __device__ __forceinline__ void scd_runs_loop(const ScanParams& p, const ScdLaun
       const uint32_t lastv = (uint32_t)__builtin_amdgcn_readlane(vb[3], 63);
       bool rs0 = d0;  // row 0 of the lane starts a value run of the slot
       if (lane == 0) {
-        const ScdSlot32 cur = scd_get(st32, s0);
+        const ScdSlot32 cur = st32[s0];
         const uint32_t rows = cur.rc & 0xFFFFu;
         uint32_t ch = (cur.rc >> 16) + add_ch;
         if (rows == 0) {
@@ -227,7 +206,7 @@ __device__ __forceinline__ void scd_runs_loop(const ScanParams& p, const ScdLaun
           ch += 1u;
           rs0 = true;
         }
-        scd_put(st32, s0, ScdSlot32{lastv, (rows + 256u) | (ch << 16)});
+        st32[s0] = ScdSlot32{lastv, (rows + 256u) | (ch << 16)};
       }
       if (do_cd) {
         const bool rs[4] = {rs0, d1, d2, d3};
@@ -324,7 +303,7 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         // depend on the order of the lanes); the slot's first lane clears it below
         // (32-bit ORs into the word's half of this lane's half-wave: the lanes of a hot slot
         // -- same-address atomics, serialised -- split over two addresses)
-        if (act) atomicOr(reinterpret_cast<unsigned int*>(&tbl[s]) + ((uint32_t)(lane >> 5) ^ (s & 1u)), 1u << (lane & 31));
+        if (act) atomicOr(reinterpret_cast<unsigned int*>(&tbl[s]) + (lane >> 5), 1u << (lane & 31));
         match = act ? tbl[s] : 0ull;
       }
       const uint64_t below = match & lanes_below;
@@ -357,7 +336,7 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
         if (!uni) tbl[s] = 0ull;  // after every lane's read of the mask (program order)
         const uint32_t add_rows = (uint32_t)__popcll(match), add_ch = (uint32_t)__popcll(dm & match);
         if (COMPACT) {
-          const ScdSlot32 cur = scd_get(st32, s);
+          const ScdSlot32 cur = st32[s];
           const uint32_t rows = cur.rc & 0xFFFFu;
           uint32_t ch = (cur.rc >> 16) + add_ch;
           if (rows == 0) {
@@ -373,8 +352,8 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
             run_start = true;
           }
           const uint32_t rc = (rows + add_rows) | (ch << 16);
-          if (uni) scd_put(st32, s, ScdSlot32{(uint32_t)lastv, rc});
-          else *scd_rc_word(st32, s) = rc;  // `last`: the slot's last lane, below
+          if (uni) st32[s] = ScdSlot32{(uint32_t)lastv, rc};
+          else st32[s].rc = rc;  // `last`: the slot's last lane, below
         } else {
           ScdSlot cur = st[s];
           uint32_t ch = cur.changes + add_ch;
@@ -395,7 +374,7 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       // compact: the slot's last lane in the step (the highest lane of its match mask) stores
       // its value as the slot's `last` -- after the first lane's read of the state above
       // (program order; the same address in both lanes' expressions)
-      if (COMPACT && !uni && act && (match >> lane) == 1ull) *scd_last_word(st32, s) = (uint32_t)vb;
+      if (COMPACT && !uni && act && (match >> lane) == 1ull) st32[s].last = (uint32_t)vb;
       // count_distinct of the same column: only the first row of a value run of its slot can
       // add a (slot, value) pair (every later row of the run repeats one already added), so
       // the pair check runs at run starts only (most rows of a sorted column skip it)
@@ -521,7 +500,7 @@ __device__ __forceinline__ void scd_fused_body(const ScanParams& p, const ScdLau
       if (COMPACT) {
         const ScdSlot32* s32 = reinterpret_cast<const ScdSlot32*>(vb);
         const uint32_t* f32 = reinterpret_cast<const uint32_t*>(s32 + S);
-        const ScdSlot32 c = scd_get(s32, (uint32_t)i);
+        const ScdSlot32 c = s32[i];
         const uint32_t rows = c.rc & 0xFFFFu;
         x.present = rows != 0;
         x.rows = rows;

@@ -156,6 +156,78 @@ def merge_partials_device(local_tables, groupby_cols, agg_list, dtypes, comm, re
     return _logical(_result_to_columns(dev, out, names)[0], dtypes)
 
 
+class SharedResult:
+    """A merged result in host memory shared by the node's rank processes
+    (``bqg_merge_shared_host``): rank 0 creates the block (POSIX shared memory), the other ranks
+    attach to it by name, and every rank's merge copies its partition into its slice over its
+    own link -- the result is complete in rank 0's memory when its merge returns, without a
+    gather to rank 0 or one large copy behind one link.  Layout (the library's): column j at
+    sum over j' < j of align256(capacity x itemsize(j')), rows in rank order."""
+
+    def __init__(self, name, capacity_rows, names, dtypes, create):
+        from multiprocessing import shared_memory
+        from .engine import device_dtype
+        self.name, self.names, self.create = name, list(names), bool(create)
+        self.dtypes = {n: np.dtype(dtypes[n]) for n in self.names}
+        self.capacity = int(capacity_rows)
+        self.offsets, off = [], 0
+        for n in self.names:
+            self.offsets.append(off)
+            off += (self.capacity * np.dtype(device_dtype(self.dtypes[n])).itemsize + 255) & ~255
+        self.nbytes = max(off, 1)
+        if create:
+            self.shm = shared_memory.SharedMemory(name=name, create=True, size=self.nbytes)
+        else:
+            self.shm = shared_memory.SharedMemory(name=name)
+            try:  # an attaching process must not unlink the creator's block at its exit
+                from multiprocessing import resource_tracker
+                resource_tracker.unregister(self.shm._name, 'shared_memory')
+            except Exception:
+                pass
+        self._bytes = np.frombuffer(self.shm.buf, np.uint8, self.nbytes)
+        self.ptr = self._bytes.ctypes.data
+
+    def columns(self, rows):
+        """The merged table: views of the block's first ``rows`` rows of every column."""
+        from .engine import device_dtype
+        out = OrderedDict()
+        for n, off in zip(self.names, self.offsets):
+            dt = np.dtype(device_dtype(self.dtypes[n]))
+            out[n] = self._bytes[off:off + rows * dt.itemsize].view(dt)
+        return _logical(out, self.dtypes)
+
+    def close(self):
+        self._bytes = None
+        try:
+            self.shm.close()
+        except BufferError:  # views still held by the caller: the mapping goes with the process
+            return
+        if self.create:
+            self.shm.unlink()
+
+
+def merge_partials_shared(local_tables, groupby_cols, agg_list, dtypes, comm, shared, reduced=False):
+    """``merge_partials_device`` for one process per GPU with the merged rows written straight
+    into ``shared`` (a ``SharedResult`` every rank maps; ``bqg_merge_shared_host``).  Returns
+    the merged row count on every rank (``shared.columns(rows)`` reads them on any rank).  A
+    block too small for the merge raises ValueError carrying the rows it needs (every rank alike)."""
+    from . import _lib as L
+    names, codes = _schema(groupby_cols, agg_list, dtypes)
+    if list(names) != shared.names:
+        raise ValueError('shared result columns %s, merge schema %s' % (shared.names, names))
+    tabs = [t for t in local_tables if t is not None]
+    arr = (ctypes.c_void_p * max(1, len(tabs)))(*[t.handle.value for t in tabs])
+    rows = ctypes.c_int64(0)
+    dev = comm.device
+    rc = L.lib().bqg_merge_shared_host(dev.handle, len(tabs), arr, len(groupby_cols), len(names), codes,
+                                       1 if reduced else 0, ctypes.c_void_p(shared.ptr), shared.capacity,
+                                       ctypes.byref(rows))
+    if rc == L.E_INVALID and rows.value > shared.capacity:
+        raise ValueError('shared merge result too small: %d rows needed' % rows.value, rows.value)
+    dev.check(rc)
+    return rows.value
+
+
 def merge_group_device(tables_per_rank, groupby_cols, agg_list, dtypes, group, reduced=False):
     """``merge_partials_device`` for every rank of a ``CommGroup`` from one host thread
     (``bqg_merge_group_host``): ``tables_per_rank[i]`` are rank i's device tables (on

@@ -51,7 +51,8 @@ extern "C" {
  *      when it read compact resident copies); bqg_table_device_bytes, bqg_table_build_compact,
  *      bqg_table_drop_compact (the compact copies' HBM, built and released explicitly);
  * 9 -- bqg_comm_progress (the merge phase a rank is in, readable while it runs); option
- *      jit_async and bqg_jit_wait (no query waits for a run-time compile). */
+ *      jit_async and bqg_jit_wait (no query waits for a run-time compile); option warm;
+ *      bqg_merge_shared_host (the merged rows straight into node-shared host memory). */
 #define BQG_ABI_VERSION 9
 
 /* error codes */
@@ -394,6 +395,18 @@ int bqg_factorize(bqg_ctx* ctx, bqg_table* t, int32_t col, int64_t* labels, void
  *                        communicator is driven by this call, each rank copies its reduced
  *                        partition straight into its slice of one pinned host result over
  *                        its own link (no gather to rank 0); rows come in rank order.
+ *   bqg_merge_shared_host (ABI 9) bqg_merge for one process per GPU, with the merged rows
+ *                        written into host memory that every rank's process maps (shared
+ *                        memory of the node): after the reduce each rank copies its partition
+ *                        into its slice over its own PCIe link -- no gather to rank 0 and no
+ *                        single 24 MB copy behind one link.  Layout of `host`: column j (schema
+ *                        order) at byte sum over j' < j of align256(capacity_rows x itemsize(j'));
+ *                        rank r's rows follow every lower rank's.  Every rank passes its own
+ *                        mapping of the same block (page-locked by the library on first use and
+ *                        kept registered while the same block is passed); *rows receives the
+ *                        merged rows on every rank; when they exceed capacity_rows every rank
+ *                        fails with BQG_E_INVALID (grow the block to *rows and merge again).
+ *                        When the call returns on any rank, every rank's slice has landed.
  * The receive-side reduce sums each key's partials in source-rank order (deterministic), and
  * a rank's rows come in first-appearance order of the rows it received. */
 #define BQG_UNIQUE_ID_BYTES 128
@@ -423,6 +436,8 @@ int bqg_merge_host(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int
                    const int32_t* dtypes, int32_t reduced, bqg_result** out);
 int bqg_merge_group_host(int32_t n_local, bqg_ctx* const* ctxs, const int32_t* n_tables, bqg_table* const* tables,
                          int32_t n_keys, int32_t n_cols, const int32_t* dtypes, int32_t reduced, bqg_result** out);
+int bqg_merge_shared_host(bqg_ctx* ctx, int32_t n_tables, bqg_table* const* tables, int32_t n_keys, int32_t n_cols,
+                          const int32_t* dtypes, int32_t reduced, void* host, int64_t capacity_rows, int64_t* rows);
 
 #ifdef __cplusplus
 }

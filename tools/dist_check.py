@@ -70,14 +70,37 @@ def main():
     merged = bdist.merge_partials_device(per, keys, aggs, dtypes, comm)
     colo = bdist.ColocatedShards(tables)
     merged_colo = colo.groupby_merged(keys, aggs, dtypes, comm)
+    # the same merge into node-shared host memory (bqg_merge_shared_host): rank 0 creates the
+    # block, every rank writes its partition into it; started too small, so the first call
+    # reports the rows it needs on every rank and the block grows
+    names = keys + [a[2] for a in aggs]
+    sh_name = ['bqgpu-dist-%d' % os.getpid() if rank == 0 else None]
+    dist.broadcast_object_list(sh_name, src=0)
+    cap = 1000
+    while True:
+        if rank == 0:
+            shared = bdist.SharedResult(sh_name[0] + '-%d' % cap, cap, names, dtypes, create=True)
+        dist.barrier()  # the other ranks attach after rank 0 created it
+        if rank != 0:
+            shared = bdist.SharedResult(sh_name[0] + '-%d' % cap, cap, names, dtypes, create=False)
+        try:
+            rows = bdist.merge_partials_shared(per, keys, aggs, dtypes, comm, shared)
+            break
+        except ValueError as e:
+            dist.barrier()  # every rank is done with the block before rank 0 unlinks it
+            shared.close()
+            cap = e.args[1]
     ok = True
     if rank == 0:
         from oracle import bquery_oracle as bo
         ref = bo.client_merge([bo.handle_work(s, keys, aggs, []) for s in shards], keys, aggs, aggregate=True)
-        ok = _check(merged, ref) and _check(merged_colo, ref)
-        print('dist_check world=%d groups=%d ok=%s' % (world, len(ref['n']), ok), flush=True)
+        merged_shared = {n: np.array(v) for n, v in shared.columns(rows).items()}
+        ok = _check(merged, ref) and _check(merged_colo, ref) and _check(merged_shared, ref) and cap > 1000
+        print('dist_check world=%d groups=%d shared_rows=%d ok=%s' % (world, len(ref['n']), rows, ok), flush=True)
     else:
         ok = merged is None and merged_colo is None
+    dist.barrier()
+    shared.close()
     for p in per:
         p.close()
     colo.close()
