@@ -2325,6 +2325,9 @@ static void warm_context(bqg_ctx* c) {
   }
   own.reset();
   HIPCHECK(hipStreamSynchronize(c->stream));
+  // the warm-up table's column blocks leave the context: no idle block of it may later stand in
+  // for an allocation that the column budget (option mem_cap_mb) would refuse
+  c->colpool.release();
   c->last = bqg_timing{};
 }
 
