@@ -803,6 +803,8 @@ def main(argv=None):
     ap.add_argument('--rows', type=int, default=None, help='override rows per shard')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-c5', action='store_true', help='leave out the c5 sub-record')
+    ap.add_argument('--no-cold-record', action='store_true',
+                    help='leave out the cold_start record (profiler runs: its generic-kernel steps share the trace)')
     ap.add_argument('--no-compact-record', action='store_true',
                     help='leave out the compact sub-record (profiler runs: its scans share the kernel name)')
     ap.add_argument('--compact', action='store_true',
@@ -878,7 +880,10 @@ def main(argv=None):
 
     # the first query on a fresh worker: an empty JIT cache (a new box), the query shape's
     # specialised kernel compiled in the background while this query runs the generic one
-    cold = _cold_first_query(dev, step)
+    cold = None if args.no_cold_record else _cold_first_query(dev, step)
+    if cold is None:
+        step()
+        dev.jit_wait(900)  # the timed steps run the specialised kernel
     for _ in range(args.warmup):
         out = step()
     cnt_col = [a[2] for a in cfg['aggs'] if a[1] == 'count']

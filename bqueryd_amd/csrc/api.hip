@@ -405,7 +405,10 @@ struct bqg_ctx {
   ColumnPool colpool;
   IngestPool ingest;  // cold-path staging: streams + pinned double buffers per decode thread
   int cu = 256;
-  size_t max_lds = 160 * 1024;  // LDS one gfx950 workgroup may take (the CU's 160 KiB; MI355X_MICROARCH.md)
+  // LDS one workgroup may take: the device's hipDeviceAttributeMaxSharedMemoryPerBlock, read at
+  // bqg_create (gfx950: 160 KiB, tools/micro/lds_attrs.hip on MI355X); the planner sizes
+  // workgroups per CU from it and check_launch refuses shapes past it
+  size_t max_lds = 160 * 1024;
   int64_t jit_min_rows() const { return opt[kOptJitMinRows]; }
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
@@ -819,7 +822,12 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
       if (!pl.p.sum_is_float[q] || pl.p.sum_conv[q] != 0) continue;
       const ColStats& cs = t->cols[pl.tcol[q]].stats;
       if (cs.empty || cs.has_nan || std::isinf(cs.fmin) || std::isinf(cs.fmax)) continue;
-      const double span = cs.fmax - cs.fmin, sq = span * span * 1.0000001;
+      // the centre is a rounded float mean: it may sit an ulp or two of the column's magnitude
+      // outside [min, max], so |x - centre| <= span + 4 ulp(magnitude); squared with a factor 2
+      // of headroom (timestamp-like columns, whose span is far below their magnitude,
+      // could reach 2^e at the old 1.0000001 margin and lose the limbs' top bits)
+      const double mag = std::max(std::fabs(cs.fmin), std::fabs(cs.fmax));
+      const double dev = (cs.fmax - cs.fmin) + 4.0 * std::ldexp(mag, -52), sq = dev * dev * 2.0;
       if (!std::isfinite(sq)) continue;
       pl.fx2_states |= 1 << i;
       pl.fx2_shift[i] = fx_shift_for(sq);
@@ -1340,7 +1348,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   // (the std pass's shared table with limbs: one workgroup per CU at most; past the LDS its
   // centred squares keep the float64 atomics)
   const bool fx1 = atomic_mode && pl.fx_states != 0,
-             fx2 = atomic_mode && pl.fx2_states != 0 && !(pl.mode == kShared && shared_lds(S, nsum2, true) > 160 * 1024);
+             fx2 = atomic_mode && pl.fx2_states != 0 && !(pl.mode == kShared && shared_lds(S, nsum2, true) > c->max_lds);
   const size_t o_fx = fx1 ? carve(S * 8 * kFxWords * (size_t)nsum) : 0,
                o_fx2 = fx2 ? carve(S * 8 * kFxWords * (size_t)nsum2) : 0,
                o_fxe = fx1 && pl.fx_slot_states ? carve(S * 4 * (size_t)nsum) : 0;
@@ -1393,8 +1401,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     const size_t lds = (size_t)S * kBlock * (8 + 8 * (size_t)nsum);
     // workgroups per CU: 3 when a row reads more than 4 bytes (C2 as stored, 16 B/row: 0.2441 ->
     // 0.2363 ms against 4, profiles/r5g_c2_launch_sweep.txt), 4 for the narrow compact rows
-    int per_cu = (int)std::min<size_t>(row_bytes > 4 ? 3 : kPrivatePerCu, (160 * 1024) / std::max<size_t>(lds, 1));
-    if (c->opt[kOptPrivatePerCu]) per_cu = std::min<int>((int)(160 * 1024 / std::max<size_t>(lds, 1)), (int)c->opt[kOptPrivatePerCu]);
+    int per_cu = (int)std::min<size_t>(row_bytes > 4 ? 3 : kPrivatePerCu, c->max_lds / std::max<size_t>(lds, 1));
+    if (c->opt[kOptPrivatePerCu]) per_cu = std::min<int>((int)(c->max_lds / std::max<size_t>(lds, 1)), (int)c->opt[kOptPrivatePerCu]);
     if (per_cu < 1) per_cu = 1;
     PrivateLaunch L{};
     L.blocks = scan_blocks(c, N, per_cu);
@@ -1502,7 +1510,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     if (c->timing) HIPCHECK(hipEventRecord(c->ev[1], st));
     if (pl.mode == kShared) {
       const size_t lds = shared_lds(S, nsum, fx1);
-      int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
+      int per_cu = (int)std::min<size_t>(8, c->max_lds / std::max<size_t>(lds, 1));
       check_launch(c, "shared scan", lds, scan_blocks(c, N, std::max(per_cu, 1)));
       launch_scan_shared(sp, sa, scan_blocks(c, N, std::max(per_cu, 1)), lds, st);
     } else if (pl.mode == kPartitioned) {
@@ -1595,8 +1603,8 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         // fewer header-scan prologues; workgroups per CU stay what the slot table allows
         {
           const size_t table = part_agg_lds(L.wbits, nsum, pk, L.fx);
-          const int per_cu_agg = std::max(1, (int)((160 * 1024) / part_agg_lds_launch(L.wbits, nsum, pk, kAggWin, L.fx)));
-          const size_t budget = (160 * 1024) / per_cu_agg - 1024;  // static LDS of the scans
+          const int per_cu_agg = std::max(1, (int)(c->max_lds / part_agg_lds_launch(L.wbits, nsum, pk, kAggWin, L.fx)));
+          const size_t budget = c->max_lds / per_cu_agg - 1024;  // static LDS of the scans
           L.win = kAggWin;
           while (L.win + 1024 <= kAggWinMax && table + 16 * (size_t)(L.win + 1024 + kAggK + 1) <= budget) L.win += 1024;
           if (c->opt[kOptPartWin]) {
@@ -1608,7 +1616,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         // aggregate workgroups per partition: one round of workgroups over the CUs (a 128 KiB
         // slot table allows one per CU)
         const size_t agg_lds = part_agg_lds_launch(L.wbits, nsum, pk, L.win, L.fx);
-        const int fit = std::max(1, (int)((160 * 1024) / agg_lds));
+        const int fit = std::max(1, (int)(c->max_lds / agg_lds));
         L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, (c->cu * fit + L.nparts / 2) / L.nparts));
         if (c->opt[kOptPartSplits]) L.splits = std::max(1, (int)std::min<int64_t>(L.ntiles, c->opt[kOptPartSplits]));
         if (pk) {
@@ -1755,7 +1763,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     sa2.fst = (uint32_t*)(b2 + ((S * 8 + 255) & ~size_t(255)));
     if (pl.mode == kPrivate) {
       const size_t lds = (size_t)S * kBlock * (8 + 8 * (size_t)nsum2);
-      int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
+      int per_cu = (int)std::min<size_t>(8, c->max_lds / std::max<size_t>(lds, 1));
       PrivateLaunch L{};
       L.blocks = scan_blocks(c, N, std::max(per_cu, 1));
       L.lds_bytes = lds;
@@ -1778,7 +1786,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       sa2.keys = sa.keys;
       if (pl.mode == kShared) {
         const size_t lds = shared_lds(S, nsum2, fx2);
-        int per_cu = (int)std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1));
+        int per_cu = (int)std::min<size_t>(8, c->max_lds / std::max<size_t>(lds, 1));
         check_launch(c, "shared scan (std pass)", lds, scan_blocks(c, N, std::max(per_cu, 1)));
         launch_scan_shared(q2, sa2, scan_blocks(c, N, std::max(per_cu, 1)), lds, st);
       } else {
@@ -1943,7 +1951,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
         const size_t blk_lds = (kBlock / 64) * d.wave_lds + (size_t)fused_cd.lds_bitmap_words * 4;
         if (blk_lds > kScdFusedMaxLds) d.cd.lds_bitmap_words = 0;  // no LDS pre-filter
         const size_t lds = (kBlock / 64) * d.wave_lds + (size_t)d.cd.lds_bitmap_words * 4;
-        const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
+        const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, c->max_lds / lds));
         waves = (uint64_t)c->cu * per_cu * (kBlock / 64);
       }
       const uint64_t needg = ((uint64_t)N + grain - 1) / grain;
@@ -2345,6 +2353,11 @@ int bqg_create(int device_ordinal, bqg_ctx** out) {
     HIPCHECK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     c->stream = c->own;
     c->cu = device_cu_count();
+    {
+      int lds = 0;
+      if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device_ordinal) == hipSuccess && lds > 0)
+        c->max_lds = (size_t)lds;
+    }
     for (int i = 0; i < 2; ++i) {
       HIPCHECK(hipHostMalloc(&c->stage[i], bqg_ctx::kStage, hipHostMallocDefault));
       HIPCHECK(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));

@@ -978,6 +978,46 @@ def test_fixed_point_sums_mixed_columns(mode, splits, oracle_c, engine_options):
     np.testing.assert_array_equal(runs[0]['a'], _fsum_by_group(k[sel], _fx_trunc(raw[sel], raw), runs[0]['k']))
 
 
+@pytest.mark.parametrize('mode', ['shared', 'global_dense'])
+def test_std_of_timestamp_like_columns(mode, oracle_c, engine_options):
+    """std's centred pass in fixed point over columns whose spread is far below their magnitude
+    (1e12 + k / 8; epoch seconds with sub-millisecond spread): the limb shift leaves headroom for
+    a centre an ulp outside [min, max].  Against the exact population std (the values
+    minus their base are exact doubles): the centre is the mean rounded to a double, which biases
+    the second moment by (mean - centre)^2 -- ~1e-8 of the variance here (DESIGN §4 states the
+    bound); bquery's row-order Welford (the oracle) drifts further at such magnitudes."""
+    rng = np.random.default_rng(57)
+    n = 400_000
+    if mode == 'global_dense':
+        engine_options(partition=0)
+    k = rng.integers(0, 300 if mode == 'shared' else 120_000, n).astype(np.int32)
+    v = 1e12 + rng.integers(0, 16, n) * 0.125
+    w = 1.7e9 + rng.normal(size=n) * 1e-3  # seconds-since-epoch-like, sub-millisecond spread
+    cols = OrderedDict(k=k, v=v, w=w)
+    aggs = [['v', 'std', 'vsd'], ['w', 'std', 'wsd'], ['v', 'mean', 'vm'], ['v', 'count', 'n']]
+    t = ShardTable(cols)
+    try:
+        got, _ = t.groupby(['k'], aggs)
+        info = t.dev.last_timing()
+    finally:
+        t.close()
+    assert info['mode'] == {'shared': 1, 'global_dense': 2}[mode], info
+    ref = oracle_c.groupby(cols, ['k'], aggs, None)
+    np.testing.assert_array_equal(got['k'], ref['k'])
+    np.testing.assert_array_equal(got['n'], ref['n'])
+    np.testing.assert_allclose(got['vm'], ref['vm'], rtol=1e-12, atol=0)
+    # std against the exact population std of the groups (the values shifted by their base are
+    # exact doubles, two passes)
+    for name, col, base in (('vsd', v, 1e12), ('wsd', w, 1.7e9)):
+        x = col - base
+        cnt = np.bincount(k, minlength=int(k.max()) + 1).astype(np.float64)
+        mean = np.bincount(k, weights=x) / np.maximum(cnt, 1)
+        var = np.bincount(k, weights=(x - mean[k]) ** 2) / np.maximum(cnt, 1)
+        # the rounded centre's bias: at most (ulp(magnitude) / 2)^2 on the variance
+        bias = 2.0 * (np.spacing(base) / 2.0) ** 2
+        np.testing.assert_allclose(got[name] ** 2, var[got['k']], rtol=1e-9, atol=bias, err_msg=name)
+
+
 @pytest.mark.parametrize('mode', ['shared', 'global_dense', 'hash', 'partitioned'])
 def test_fixed_point_sums_outlier_column(mode, oracle_c, engine_options):
     """A column of values near 1 with one 1e20 outlier: at the column-wide shift (from 1e20) the
