@@ -110,3 +110,58 @@ def test_decomposable_aggregations():
     assert not decomposable([['f', 'std', 'a']])
     assert not decomposable(['f'])  # aggregate=True needs 3-element specs (rpc.py:171)
     assert not decomposable([['f', 'sum']])
+
+
+def _shared_result_rank(rank, port, name, q):
+    import os
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    import numpy as np
+    import torch.distributed as dist
+    from bqueryd_amd import dist as bdist
+    dist.init_process_group('gloo', rank=rank, world_size=2)
+    dts = {'k': np.dtype(np.int32), 's': np.dtype(np.float64)}
+    try:
+        if rank == 0:
+            blk = bdist.SharedResult(name, 1000, ['k', 's'], dts, create=True)
+        dist.barrier()
+        if rank == 1:
+            blk = bdist.SharedResult(name, 1000, ['k', 's'], dts, create=False)
+            # the library's layout: column j at sum of align256(capacity x itemsize) before it
+            assert blk.offsets == [0, (1000 * 4 + 255) & ~255]
+            cols = blk.columns(5)
+            cols['k'][:] = np.arange(5, dtype=np.int32) + 10
+            cols['s'][:] = 0.5
+            del cols
+        dist.barrier()
+        if rank == 0:
+            got = blk.columns(5)
+            q.put((got['k'].tolist(), got['s'].tolist()))
+            del got
+        dist.barrier()
+        blk.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shared_result_block_between_ranks():
+    """dist.SharedResult (the host block bqg_merge_shared_host writes): rank 0 creates it, rank 1
+    attaches by name, the column layout is the library's, writes of one process are the other's
+    reads, and the creator unlinks it (no GPU: plain shared memory between two gloo ranks)."""
+    import multiprocessing as mp
+    import os
+    import socket
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    name = 'bqgpu-test-%d' % os.getpid()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_shared_result_rank, args=(r, port, name, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+    assert [p.exitcode for p in ps] == [0, 0]
+    assert q.get(timeout=10) == ([10, 11, 12, 13, 14], [0.5] * 5)
+    assert not os.path.exists('/dev/shm/' + name)

@@ -104,6 +104,42 @@ def test_rccl_merge_world_one():
     assert all(len(v) == 0 for v in empty.values())
 
 
+def test_shared_host_merge_world_one():
+    """bqg_merge_shared_host at world 1 (dist.SharedResult: a POSIX shared-memory block, as the
+    node's rank processes map it): the same rows as bqg_merge_host in the client's order; a
+    block too small reports the rows it needs and leaves the communicator usable; the block
+    is registered once and reused across merges; an empty merge writes no row."""
+    import os
+    from bqueryd_amd.engine import get_device
+    shards = _shards(4, 100_000, 25_000)
+    per = _device_results(shards)
+    dts = _dtypes()
+    names = list(dts)
+    comm = bdist.RcclComm(get_device())
+    small = big = None
+    try:
+        ref = bdist.merge_partials_device(per, KEYS, AGGS_SC, dts, comm)
+        small = bdist.SharedResult('bqgpu-test-small-%d' % os.getpid(), 100, names, dts, create=True)
+        with pytest.raises(ValueError) as ei:
+            bdist.merge_partials_shared(per, KEYS, AGGS_SC, dts, comm, small)
+        need = ei.value.args[1]
+        assert need == len(ref['n'])
+        big = bdist.SharedResult('bqgpu-test-big-%d' % os.getpid(), need + 7, names, dts, create=True)
+        for _ in range(2):  # the second merge reuses the registration
+            rows = bdist.merge_partials_shared(per, KEYS, AGGS_SC, dts, comm, big)
+            got = {n: np.array(v) for n, v in big.columns(rows).items()}
+            for n in names:
+                np.testing.assert_array_equal(got[n], ref[n], err_msg=n)
+        assert bdist.merge_partials_shared([], KEYS, AGGS_SC, dts, comm, big) == 0
+    finally:
+        comm.close()
+        for p in per:
+            p.close()
+        for b in (small, big):
+            if b is not None:
+                b.close()
+
+
 def test_rccl_comm_init_all_one_gpu():
     """bqg_comm_init_all (a process owning the node's GPUs) with the one GPU of this box."""
     from bqueryd_amd.engine import Device
