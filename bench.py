@@ -991,6 +991,12 @@ def main(argv=None):
                                             'itemsize x rows + the output table (G x columns x 8 B)',
             'bytes_read_per_launch': read_per_launch,
             'device_ms_per_query': device_avg,
+            # the same algorithmic bytes over the WHOLE query's device time (every kernel of the
+            # query, the fills, and the result's copy to host memory): what the kernels beside
+            # the scan cost -- for C2 the one-workgroup finish, for C3 the large-result emit
+            # (compaction, first-row bitmap, rank pass) and the 24 MB PCIe copy
+            'frac_whole_query_incl_result_copy': (bytes_per_launch / (device_avg * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                                  if device_avg == device_avg and device_avg > 0 else None),
         },
         'cpu_baseline': cpu,
         'cold_first_query_ms': cold['first_query_ms'] if cold else None,
