@@ -17,9 +17,10 @@ t0 = time.perf_counter()
 dev = Device(0)
 out['context_ms'] = 1e3 * (time.perf_counter() - t0)
 dev.set_option('compact', 0)
-cfg = synth.CONFIGS['c2']
-rows = int(sys.argv[1]) if len(sys.argv) > 1 else cfg['rows']
-cols = synth.taxi_shard(rows, config_id=2, columns=synth.query_columns(cfg))
+config = sys.argv[1] if len(sys.argv) > 1 else 'c2'
+cfg = synth.CONFIGS[config]
+rows = int(sys.argv[2]) if len(sys.argv) > 2 else cfg['rows']
+cols = synth.taxi_shard(rows, config_id=synth.CONFIG_ID[config], columns=synth.query_columns(cfg))
 t0 = time.perf_counter()
 table = ShardTable(cols, device=dev)
 dev.synchronize()
@@ -42,8 +43,9 @@ out['first'] = q(cfg['aggs'], cfg['where'])
 out['second'] = q(cfg['aggs'], cfg['where'])
 out['third'] = q(cfg['aggs'], cfg['where'])
 # another shape on the same table: what is per shape, not per process
-out['other_shape_first'] = q([['fare_amount', 'sum', 's']], [('passenger_count', '>', 3)])
-out['other_shape_second'] = q([['fare_amount', 'sum', 's']], [('passenger_count', '>', 3)])
+if config == 'c2':
+    out['other_shape_first'] = q([['fare_amount', 'sum', 's']], [('passenger_count', '>', 3)])
+    out['other_shape_second'] = q([['fare_amount', 'sum', 's']], [('passenger_count', '>', 3)])
 out['jit_wait'] = dev.jit_wait(600)
 out['after_compile'] = q(cfg['aggs'], cfg['where'])
 print(json.dumps(out))
