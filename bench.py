@@ -249,7 +249,7 @@ def _c5_local_ranks(args):
     for i in range(args.warmup):
         out = step()
         if i == 0:
-            devs[0].jit_wait(900)
+            devs[0].jit_wait(180)
     if int(out['n'].sum()) != n_shards * shard_rows:
         raise SystemExit('sanity check failed: %d merged rows' % int(out['n'].sum()))
     for d in devs:
@@ -607,7 +607,7 @@ def _c5_ranks(args, comm, dev, ws, rank, steps, warmup, shard_rows=None):
         out = step()
         if i == 0:
             _stage('c5: waiting for background kernel compiles')
-            dev.jit_wait(900)
+            dev.jit_wait(180)
     ok = None
     if rank == 0:  # every scanned row counted once, across the ranks (rank 0 reads the shared block)
         ok = int(shm['block'].columns(out)['n'].sum()) == ws * rows
@@ -717,7 +717,7 @@ def _cold_first_query(dev, step):
         first_ms = 1e3 * (time.perf_counter() - t0)
         first_spec = dev.last_timing()['specialized']
         t1 = time.perf_counter()
-        w = dev.jit_wait(900)
+        w = dev.jit_wait(180)
         wait_s = time.perf_counter() - t1
     finally:
         if old is None:
@@ -752,7 +752,7 @@ def _compact_record(dev, table, step, steps, warmup, full_ms, full_scan_ms):
         copy_bytes = table.device_bytes() - base_bytes
         if copy_bytes <= 0:
             return {'built': False, 'note': 'no column of this query has a narrower resident form'}
-        dev.jit_wait(900)  # the copies' query shape, compiled in the background: timed specialised
+        dev.jit_wait(180)  # the copies' query shape, compiled in the background: timed specialised
         for _ in range(warmup):
             step()
         dev.enable_timing(True, scan_only=True)
@@ -883,7 +883,7 @@ def main(argv=None):
     cold = None if args.no_cold_record else _cold_first_query(dev, step)
     if cold is None:
         step()
-        dev.jit_wait(900)  # the timed steps run the specialised kernel
+        dev.jit_wait(180)  # the timed steps run the specialised kernel
     for _ in range(args.warmup):
         out = step()
     cnt_col = [a[2] for a in cfg['aggs'] if a[1] == 'count']
