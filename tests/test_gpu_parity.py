@@ -1013,8 +1013,10 @@ def test_std_of_timestamp_like_columns(mode, oracle_c, engine_options):
         cnt = np.bincount(k, minlength=int(k.max()) + 1).astype(np.float64)
         mean = np.bincount(k, weights=x) / np.maximum(cnt, 1)
         var = np.bincount(k, weights=(x - mean[k]) ** 2) / np.maximum(cnt, 1)
-        # the rounded centre's bias: at most (ulp(magnitude) / 2)^2 on the variance
-        bias = 2.0 * (np.spacing(base) / 2.0) ** 2
+        # the rounded centre's bias on the variance: (mean - centre)^2, the centre within ~1.5
+        # ulp of the magnitude of the exact mean (the pass-1 sum is rounded to a float64 before
+        # the division, then the quotient)
+        bias = (2.0 * np.spacing(base)) ** 2
         np.testing.assert_allclose(got[name] ** 2, var[got['k']], rtol=1e-9, atol=bias, err_msg=name)
 
 
