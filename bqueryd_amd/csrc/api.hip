@@ -2295,27 +2295,30 @@ int bqg_reset_options(bqg_ctx* c) {
 // kernel's first launch resolves its symbol, and the private scan's partials / the pooled
 // pinned result blocks are allocated on first use.  One small C2-shaped query -- 3 columns, a
 // filter, sum / mean / count over 10 groups, 768 tiles so the partials reach their steady size
-// on a 256-CU device -- does all of it once; the table is freed before bqg_create returns.
+// on a 256-CU device -- does all of it once, and a C3- and a C4-shaped query launch the
+// partition / large-emit and distinct kernels once; the table is freed before bqg_create returns.
 static void warm_context(bqg_ctx* c) {
   const int64_t n = (int64_t)std::max(c->cu, 1) * 3 * 1024;
-  const int32_t dts[3] = {BQG_I32, BQG_F64, BQG_I8};
-  std::vector<int32_t> k((size_t)n);
+  const int32_t dts[4] = {BQG_I32, BQG_F64, BQG_I8, BQG_I32};
+  std::vector<int32_t> k((size_t)n), k2((size_t)n);
   std::vector<double> v((size_t)n);
   std::vector<int8_t> f((size_t)n);
   for (int64_t i = 0; i < n; ++i) {
     k[(size_t)i] = (int32_t)(i % 10);
     v[(size_t)i] = (double)(i % 97) * 0.25;
     f[(size_t)i] = (int8_t)(i % 5);
+    k2[(size_t)i] = (int32_t)(i % 100000);
   }
   bqg_table* t = nullptr;
   auto ok = [&](int rc) {
     if (rc != BQG_OK) fail(rc, "context warm-up query failed: %s", bqg_last_error(c));
   };
-  ok(bqg_table_create(c, n, 3, dts, &t));
+  ok(bqg_table_create(c, n, 4, dts, &t));
   std::unique_ptr<bqg_table, int (*)(bqg_table*)> own(t, bqg_table_destroy);
   ok(bqg_push_chunk(t, 0, k.data(), n, 0));
   ok(bqg_push_chunk(t, 1, v.data(), n, 0));
   ok(bqg_push_chunk(t, 2, f.data(), n, 0));
+  ok(bqg_push_chunk(t, 3, k2.data(), n, 0));
   ok(bqg_table_sync(t));
   const int64_t two = 2;
   const bqg_term term{2, BQG_T_GE, 1, &two, nullptr};
@@ -2330,6 +2333,21 @@ static void warm_context(bqg_ctx* c) {
     c->opt[kOptCompact] = saved;
     ok(rc);
     bqg_result_free(r);
+  }
+  // best effort (a failure here only leaves those kernels cold): the partitioned path with its
+  // large-result emit (C3's shape: two keys over 10^6 slots, 10^5 groups) and the fused
+  // distinct pass (C4's aggregations)
+  {
+    const int32_t keys2[2] = {3, 0};
+    const bqg_agg a3[2] = {{1, BQG_SUM}, {1, BQG_COUNT}};
+    const bqg_query q3{2, keys2, 0, nullptr, -1, 2, a3};
+    const bqg_agg a4[2] = {{2, BQG_COUNT_DISTINCT}, {2, BQG_SORTED_COUNT_DISTINCT}};
+    const bqg_query q4{1, &key, 0, nullptr, -1, 2, a4};
+    for (const bqg_query* qq : {&q3, &q4}) {
+      bqg_result* r = nullptr;
+      if (bqg_groupby(c, t, qq, &r) == BQG_OK) bqg_result_free(r);
+    }
+    c->err.clear();
   }
   own.reset();
   HIPCHECK(hipStreamSynchronize(c->stream));
