@@ -140,6 +140,48 @@ def test_shared_host_merge_world_one():
                 b.close()
 
 
+def test_comm_progress_counts_merges():
+    """bqg_comm_progress (what bench.py's watchdog reports for a rank whose collective does not
+    return): idle between merges, one more merge begun and ended per call, failures included;
+    readable from another thread while a merge runs."""
+    import threading
+    from bqueryd_amd.engine import get_device
+    dev = get_device()
+    shards = _shards(3, 80_000, 20_000)
+    per = _device_results(shards)
+    comm = bdist.RcclComm(dev)
+    seen = []
+    try:
+        p0 = bdist.merge_progress(dev)
+        assert p0['phase'] == 'idle' and p0['merges_started'] == p0['merges_done']
+        stop = threading.Event()
+
+        def poll():
+            while not stop.is_set():
+                seen.append(bdist.merge_progress(dev)['phase'])
+        th = threading.Thread(target=poll)
+        th.start()
+        try:
+            for _ in range(3):
+                bdist.merge_partials_device(per, KEYS, AGGS_SC, _dtypes(), comm)
+        finally:
+            stop.set()
+            th.join()
+        p1 = bdist.merge_progress(dev)
+        assert p1['phase'] == 'idle'
+        assert p1['merges_started'] == p0['merges_started'] + 3 and p1['merges_done'] == p0['merges_done'] + 3
+        with pytest.raises(Exception):  # a bad schema fails inside the merge: counted as ended
+            bdist.merge_partials_device(per, KEYS, AGGS_SC + [['fare_amount', 'sum', 'x']],
+                                        dict(_dtypes(), x=np.dtype(np.float64)), comm)
+        p2 = bdist.merge_progress(dev)
+        assert p2['phase'] == 'idle' and p2['merges_done'] - p2['merges_started'] == p1['merges_done'] - p1['merges_started']
+    finally:
+        comm.close()
+        for p in per:
+            p.close()
+    assert set(seen) <= set(bdist.MERGE_PHASES) | {'idle'}, set(seen)
+
+
 def test_rccl_comm_init_all_one_gpu():
     """bqg_comm_init_all (a process owning the node's GPUs) with the one GPU of this box."""
     from bqueryd_amd.engine import Device
