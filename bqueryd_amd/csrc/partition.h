@@ -64,6 +64,13 @@ __device__ __forceinline__ uint32_t block_excl_scan_1b(uint32_t v, uint32_t* wsu
 // scatter: workgroups of up to 1024 threads, each over a contiguous range of whole tiles
 constexpr int kPartBlock = 1024;
 
+// one 16-byte streaming store (the entries are read back by the aggregate only: no cache
+// residency to keep)
+__device__ __forceinline__ void st_nt16(void* dst, const void* src) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(*reinterpret_cast<const v4u*>(src), reinterpret_cast<v4u*>(dst));
+}
+
 // Tile-layout scatter.  A tile is T * 4 * K rows (TR).  The workgroup counting-sorts each of its
 // tiles by partition (slot >> wbits) in LDS and writes the sorted tile back LINEARLY to the
 // tile's own entry range [tile * TR, tile * TR + TR) with 16-byte stores of whole lines --
@@ -234,10 +241,10 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
     // linear copy-out: K 16-byte stores of meta and 2K per summed column, every thread
 #pragma unroll
     for (int k = 0; k < K; ++k)
-      *reinterpret_cast<uint4*>(L.meta + obase + 4 * (tid + k * T)) = *reinterpret_cast<const uint4*>(smeta + 4 * (tid + k * T));
+      st_nt16(L.meta + obase + 4 * (tid + k * T), smeta + 4 * (tid + k * T));
     if (with_rit)
       for (int i = tid; i < TR / 8; i += T)
-        *reinterpret_cast<uint4*>(L.rit + obase + 8 * i) = *reinterpret_cast<const uint4*>(srit + 8 * i);
+        st_nt16(L.rit + obase + 8 * i, srit + 8 * i);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (PACK || s >= nsum) break;
