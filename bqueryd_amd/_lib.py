@@ -33,7 +33,7 @@ ABI_VERSION = 9
 OPTIONS = ('jit', 'jit_min_rows', 'partition', 'part_wbits', 'part_k', 'part_threads', 'part_per_cu',
            'part_splits', 'part_narrow', 'fused_scd', 'scd_compact', 'scd_pack16', 'priv_ahead',
            'private_per_cu', 'small_emit', 'hash_slots', 'distinct_slots', 'part_pack', 'scd_runs', 'part_win', 'compact', 'part_first',
-           'fx_sums', 'mem_cap_mb', 'part_ring', 'jit_async', 'warm')
+           'fx_sums', 'mem_cap_mb', 'part_ring', 'jit_async', 'warm', 'slot_emit')
 
 
 class Term(ctypes.Structure):

@@ -346,7 +346,7 @@ struct ColumnPool {
 enum Opt {
   kOptJit, kOptJitMinRows, kOptPartition, kOptPartWbits, kOptPartK, kOptPartThreads, kOptPartPerCu,
   kOptPartSplits, kOptPartNarrow, kOptFusedScd, kOptScdCompact, kOptScdPack16, kOptPrivAhead,
-  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kOptMemCap, kOptPartRing, kOptJitAsync, kOptWarm, kNumOpts
+  kOptPrivatePerCu, kOptSmallEmit, kOptHashSlots, kOptDistinctSlots, kOptPartPack, kOptScdRuns, kOptPartWin, kOptCompact, kOptPartFirst, kOptFxSums, kOptMemCap, kOptPartRing, kOptJitAsync, kOptWarm, kOptSlotEmit, kNumOpts
 };
 struct OptDef {
   const char* name;
@@ -380,6 +380,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"part_ring", 0, 0, 2},                 // packed scatter (JIT): tiles of row loads in flight (0: 1)
     {"jit_async", 1, 0, 1},                 // a shape not compiled yet runs the generic kernel while hiprtc compiles it
     {"warm", 1, 0, 1},                      // bqg_create runs one small query (read at context creation only)
+    {"slot_emit", 1, 0, 2},                 // large slot spaces: emit without the compaction and its host round trip (2: via group records)
 };
 
 static int opt_index(const char* name) {
@@ -435,6 +436,8 @@ struct bqg_ctx {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // timing level 1: the first and last compact-copy build of the current query
   hipEvent_t ev_sh[2] = {nullptr, nullptr};
+  // the large-result emit: the group count has reached page-locked host memory
+  hipEvent_t ev_groups = nullptr;
   bool sh_timed = false;
   bqg_timing last{};
   double scan_ms_sum = 0;  // since timing was last enabled
@@ -821,13 +824,19 @@ void plan_query(bqg_ctx* c, bqg_table* t, const bqg_query* q, Plan& pl) {
       const int q = pl.std_cols[i];
       if (!pl.p.sum_is_float[q] || pl.p.sum_conv[q] != 0) continue;
       const ColStats& cs = t->cols[pl.tcol[q]].stats;
-      if (cs.empty || cs.has_nan || std::isinf(cs.fmin) || std::isinf(cs.fmax)) continue;
+      if (cs.empty) continue;
       // the centre is a rounded float mean: it may sit an ulp or two of the column's magnitude
       // outside [min, max], so |x - centre| <= span + 4 ulp(magnitude); squared with a factor 2
       // of headroom (timestamp-like columns, whose span is far below their magnitude,
-      // could reach 2^e at the old 1.0000001 margin and lose the limbs' top bits)
-      const double mag = std::max(std::fabs(cs.fmin), std::fabs(cs.fmax));
-      const double dev = (cs.fmax - cs.fmin) + 4.0 * std::ldexp(mag, -52), sq = dev * dev * 2.0;
+      // could reach 2^e at the old 1.0000001 margin and lose the limbs' top bits).  A column
+      // holding NaN or infinities: its finite values lie within +-fmaxabs; a group with a
+      // non-finite value has a non-finite centre, its squares land in the limbs' flags and its
+      // std is NaN anyway (the nonfinite pass) -- so these columns keep the limbs too (round 6:
+      // they took float64 atomics, whose sums depend on the arrival order)
+      const bool nonfinite = cs.has_nan || std::isinf(cs.fmin) || std::isinf(cs.fmax);
+      const double mag = nonfinite ? cs.fmaxabs : std::max(std::fabs(cs.fmin), std::fabs(cs.fmax));
+      const double span = nonfinite ? 2.0 * cs.fmaxabs : cs.fmax - cs.fmin;
+      const double dev = span + 4.0 * std::ldexp(mag, -52), sq = dev * dev * 2.0;
       if (!std::isfinite(sq)) continue;
       pl.fx2_states |= 1 << i;
       pl.fx2_shift[i] = fx_shift_for(sq);
@@ -2074,6 +2083,65 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     return;
   }
 
+  // ---- large slot spaces: no compaction, no host round trip before the emit (the group count
+  // is read from page-locked memory while the emit runs)
+  if (S > kSmallEmitSlots && c->opt[kOptSlotEmit]) {
+    const uint64_t nwords = ((uint64_t)N + 31) / 32;
+    const uint64_t nblocks = (nwords + 1023) / 1024;
+    // bitmap [nwords] u32 | hdr (256 B) | word pairs [nwords] u64 | block prefixes [nblocks] u32
+    const size_t bm_bytes = (nwords * 4 + 255) & ~size_t(255);
+    unsigned char* pb = (unsigned char*)c->prefix.ensure(bm_bytes + 256 + nwords * 8 + nblocks * 4 + 1024);
+    unsigned int* bitmap = (unsigned int*)pb;
+    unsigned long long* hdev = (unsigned long long*)(pb + bm_bytes);
+    unsigned long long* wpair = (unsigned long long*)(pb + bm_bytes + 256);
+    unsigned int* bprefix = (unsigned int*)(wpair + nwords);
+    unsigned long long* hh = (unsigned long long*)c->hhdr.ensure(64);
+    void* hh_dev = nullptr;
+    HIPCHECK(hipHostGetDevicePointer(&hh_dev, hh, 0));
+    // output columns at capacity S, laid out by the group count on the device (+ with
+    // slot_emit 2 the group records, S x ncols words)
+    size_t ocap = 0;
+    for (int j = 0; j < e.ncols; ++j) ocap += ((size_t)S * dtype_size(out_dt[j]) + 255) & ~size_t(255);
+    const bool aos = c->opt[kOptSlotEmit] == 2;
+    unsigned char* ob = (unsigned char*)c->outcols.ensure(ocap + 256 + (aos ? (size_t)S * e.ncols * 8 : 0));
+    launch_slot_emit(e, sa, S, nsum, N, bitmap, wpair, bprefix, hdev, (unsigned long long*)hh_dev, c->ev_groups, ob,
+                     aos ? (unsigned long long*)(ob + ocap + 256) : nullptr, st);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipEventSynchronize(c->ev_groups));
+    const uint64_t G = hh[0];
+    const unsigned long long total = hh[1];
+    const int filtered = pl.has_filter && (int64_t)total < N;
+    std::vector<size_t> offs;
+    size_t obytes = 0;
+    for (int j = 0; j < e.ncols; ++j) {
+      offs.push_back(obytes);
+      obytes += ((size_t)G * dtype_size(out_dt[j]) + 255) & ~size_t(255);
+    }
+    if (G == 0) {
+      HIPCHECK(hipStreamSynchronize(st));
+      finish_query(c, pl, 0, e.ncols);
+      *out = empty_result(out_dt, filtered);
+      return;
+    }
+    if (c->dev_target) {
+      if (c->timing == 1) HIPCHECK(hipEventRecord(c->ev[3], st));
+      std::vector<const void*> src;
+      for (int j = 0; j < e.ncols; ++j) src.push_back(ob + offs[j]);
+      table_from_device(c, out_dt, src, (int64_t)G);
+      finish_query(c, pl, (int64_t)G, e.ncols);
+      return;
+    }
+    BlockGuard blk;
+    blk.reset(c->pool, c->pool_get(obytes + 64));
+    HIPCHECK(hipMemcpyAsync(blk.b.p, ob, obytes, hipMemcpyDeviceToHost, st));
+    if (c->timing == 1) HIPCHECK(hipEventRecord(c->ev[3], st));
+    HIPCHECK(hipStreamSynchronize(st));
+    bqg_result* r = block_result(c, blk.release(), (int64_t)G, filtered, out_dt, offs);
+    finish_query(c, pl, (int64_t)G, e.ncols);
+    *out = r;
+    return;
+  }
+
   // ---- generic emit
   const uint64_t cblocks = (S + 4095) / 4096 + 1;
   unsigned char* lb = (unsigned char*)c->lists.ensure(S * 8 + (2 * cblocks + 4096) * 8 + 256);
@@ -2383,6 +2451,7 @@ int bqg_create(int device_ordinal, bqg_ctx** out) {
     // timing-only events: no system-scope fence (cache writeback) at each record
     for (int i = 0; i < 4; ++i) HIPCHECK(hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence));
     for (int i = 0; i < 2; ++i) HIPCHECK(hipEventCreateWithFlags(&c->ev_sh[i], hipEventDisableSystemFence));
+    HIPCHECK(hipEventCreateWithFlags(&c->ev_groups, hipEventDisableTiming));
     // last-workgroup-done counters of the finish kernels (each reset by its last workgroup)
     HIPCHECK(hipMemset(c->done.ensure(256), 0, 256));
     if (c->opt[kOptWarm]) warm_context(c);
@@ -2415,6 +2484,7 @@ int bqg_destroy(bqg_ctx* c) {
       if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     for (int i = 0; i < 2; ++i)
       if (c->ev_sh[i]) (void)hipEventDestroy(c->ev_sh[i]);
+    if (c->ev_groups) (void)hipEventDestroy(c->ev_groups);
     if (c->own) (void)hipStreamDestroy(c->own);
   });
   delete c;

@@ -535,15 +535,58 @@ __device__ __forceinline__ void store_elem(void* base, int dt, uint64_t idx, uin
   }
 }
 
+// a dense key's offset in its range from its slot code: 32-bit division when code, stride and
+// range fit (dense slot spaces stay below 2^27) -- a 64-bit division is a long software
+// sequence, and two keys' division and modulo were most of a 1 M-group emit's time
+__device__ __forceinline__ uint64_t key_offset(uint64_t code, const DevKey& k) {
+  if (((code | k.stride | k.range) >> 32) == 0) return (uint32_t)code / (uint32_t)k.stride % (uint32_t)k.range;
+  return (code / k.stride) % k.range;
+}
+
 struct SlotTotals {
   unsigned long long cnt;
   uint32_t fst;
   unsigned long long acc[kMaxSums];
   unsigned long long acc2[kMaxSums];  // centered second moments (std pass 2)
+  __device__ unsigned long long sum(int q) const { return acc[q]; }
+  __device__ unsigned long long m2(int q) const { return acc2[q]; }
 };
 
+// A slot's totals read where they lie (the emit kernels): a sum state is picked by the
+// column's runtime state index, and an array of all of them in registers would be indexed
+// dynamically -- which the compiler turns into an LDS array sized for 1024 threads (80 KB per
+// workgroup: one or two workgroups per CU, the 1 M-group emit latency-bound at ~1.5 waves per
+// SIMD; round 6)
+struct SlotRef {
+  unsigned long long cnt;
+  uint32_t fst;
+  const unsigned long long* acc;   // &sa.acc[s]: state q at acc[q * stride]
+  const unsigned long long* acc2;  // &sa.acc2[s] (std states) or nullptr
+  uint64_t stride;
+  __device__ unsigned long long sum(int q) const { return acc[(size_t)q * stride]; }
+  __device__ unsigned long long m2(int q) const { return acc2[(size_t)q * stride]; }
+};
+__device__ __forceinline__ SlotRef slot_ref(const SlotArrays& sa, uint64_t s, uint64_t nslots, unsigned long long cnt,
+                                            uint32_t fst) {
+  SlotRef t;
+  t.cnt = cnt;
+  t.fst = fst;
+  t.acc = sa.acc ? sa.acc + s : nullptr;
+  t.acc2 = sa.acc2 ? sa.acc2 + s : nullptr;
+  t.stride = nslots;
+  return t;
+}
+
+// OUT 0: column j at cols[j].out.  OUT 1: the output columns laid out by the group count G,
+// known on the device only (the large-result emit without a host round trip): column j at
+// cols[0].out + the 256-byte aligned sizes of columns 0..j-1 at G rows.  OUT 2: one record of
+// ncols 8-byte words per group at cols[0].out + rank * ncols * 8 (the words unnarrowed; a
+// record lands in one or two lines where four column stores would touch four random lines --
+// k_aos_columns then writes the columns in rank order)
+template <int OUT = 0, typename T>
 __device__ __forceinline__ void emit_slot(const EmitParams& e, uint64_t slot, uint64_t code, unsigned int rank,
-                                       const SlotTotals& t) {
+                                       const T& t, uint64_t G = 0) {
+  size_t goff = 0;
   for (int j = 0; j < e.ncols; ++j) {
     const EmitCol& c = e.cols[j];
     uint64_t bits = 0;
@@ -556,20 +599,20 @@ __device__ __forceinline__ void emit_slot(const EmitParams& e, uint64_t slot, ui
         bits = code;
         if (c.out_dtype == BQG_F32) bits = __float_as_uint((float)as_f64(code));
       } else {
-        const uint64_t off = (code / k.stride) % k.range;
+        const uint64_t off = key_offset(code, k);
         bits = (uint64_t)k.min + off;
       }
     } else {
       switch (c.op) {
         case BQG_SUM: {
-          unsigned long long a = t.acc[c.state];
+          unsigned long long a = t.sum(c.state);
           if (c.in_float && e.sum_dec[c.state] != 0.0) a = as_u64((double)(long long)a / e.sum_dec[c.state]);
           if (c.in_float) bits = (c.out_dtype == BQG_F32) ? (uint64_t)__float_as_uint((float)as_f64(a)) : a;
           else bits = a;  // wrap-around to the output width happens in store_elem
         } break;
         case BQG_COUNT: bits = t.cnt; break;
         case BQG_MEAN: {
-          const unsigned long long a = t.acc[c.state];
+          const unsigned long long a = t.sum(c.state);
           const double s = c.in_float ? (e.sum_dec[c.state] != 0.0 ? (double)(long long)a / e.sum_dec[c.state] : as_f64(a))
                                       : (c.in_dtype == BQG_U64 ? (double)(uint64_t)a : (double)(long long)a);
           bits = as_u64(s / (double)t.cnt);
@@ -588,7 +631,7 @@ __device__ __forceinline__ void emit_slot(const EmitParams& e, uint64_t slot, ui
           }
         } break;
         case BQG_STD: {
-          const double m2 = as_f64(t.acc2[c.state]);
+          const double m2 = as_f64(t.m2(c.state));
           bits = as_u64(t.cnt ? sqrt(m2 / (double)t.cnt) : __builtin_nan(""));
           // Welford: d * (x - mean) is inf * (inf - inf) at the first non-finite value
           if (e.nf_cnt[c.sum_state] && e.nf_cnt[c.sum_state][slot]) bits = as_u64(__builtin_nan(""));
@@ -607,7 +650,14 @@ __device__ __forceinline__ void emit_slot(const EmitParams& e, uint64_t slot, ui
         } break;
       }
     }
-    store_elem(c.out, c.out_dtype, rank, bits);
+    if (OUT == 2) {
+      static_cast<unsigned long long*>(e.cols[0].out)[(size_t)rank * e.ncols + j] = bits;
+    } else if (OUT == 1) {
+      store_elem(static_cast<unsigned char*>(e.cols[0].out) + goff, c.out_dtype, rank, bits);
+      goff += (((size_t)G << dtype_lg(c.out_dtype)) + 255) & ~size_t(255);
+    } else {
+      store_elem(c.out, c.out_dtype, rank, bits);
+    }
   }
 }
 

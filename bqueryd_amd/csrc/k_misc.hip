@@ -169,17 +169,9 @@ __global__ void k_rank(const uint32_t* list_fst, const uint32_t* list_slot, unsi
 
 __global__ void k_emit(EmitParams e, SlotArrays sa, const uint32_t* order, unsigned int n, int nsum,
                        uint64_t nslots) {
-  const int nsum2 = e.nsum2;
   for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t s = order[i];
-    SlotTotals t;
-    t.cnt = sa.cnt[s];
-    t.fst = sa.fst[s];
-#pragma unroll
-    for (int v = 0; v < kMaxSums; ++v) {
-      t.acc[v] = v < nsum ? sa.acc[(size_t)v * nslots + s] : 0ull;
-      t.acc2[v] = (sa.acc2 && v < nsum2) ? sa.acc2[(size_t)v * nslots + s] : 0ull;
-    }
+    const SlotRef t = slot_ref(sa, s, nslots, sa.cnt[s], sa.fst[s]);
     const uint64_t code = e.hash ? (uint64_t)sa.keys[s] : (uint64_t)s;
     emit_slot(e, s, code, i, t);
   }
@@ -192,23 +184,111 @@ __global__ void k_emit(EmitParams e, SlotArrays sa, const uint32_t* order, unsig
 __global__ void k_rank_emit(EmitParams e, SlotArrays sa, const uint32_t* list_fst, const uint32_t* list_slot,
                             unsigned int n, int nsum, uint64_t nslots, const unsigned int* bitmap,
                             const unsigned int* word_prefix, const unsigned int* block_prefix) {
-  const int nsum2 = e.nsum2;
   for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t f = list_fst[i];
     const uint32_t w = f >> 5;
     const unsigned int r = block_prefix[w >> 10] + word_prefix[w] +
                            (unsigned int)__popc(bitmap[w] & ((1u << (f & 31)) - 1u));
     const uint32_t s = list_slot[i];
-    SlotTotals t;
-    t.cnt = sa.cnt[s];
-    t.fst = f;
-#pragma unroll
-    for (int v = 0; v < kMaxSums; ++v) {
-      t.acc[v] = v < nsum ? sa.acc[(size_t)v * nslots + s] : 0ull;
-      t.acc2[v] = (sa.acc2 && v < nsum2) ? sa.acc2[(size_t)v * nslots + s] : 0ull;
-    }
+    const SlotRef t = slot_ref(sa, s, nslots, sa.cnt[s], f);
     const uint64_t code = e.hash ? (uint64_t)sa.keys[s] : (uint64_t)s;
     emit_slot(e, s, code, r, t);
+  }
+}
+
+// Large slot spaces without the compaction and its host round trip (round 6): the first-row
+// bitmap is set straight from the slot arrays (an occupied slot has cnt > 0), the rank scan
+// leaves the group count G on the device -- the emit lays the output columns out by it -- and
+// mirrors G and the passing rows into page-locked host memory, which the host reads after an
+// event while the emit runs; the copy of the G rows follows.
+__global__ __launch_bounds__(1024) void k_setbits_slots(SlotArrays sa, uint64_t nslots, unsigned int* bitmap,
+                                                        unsigned long long* rows_total) {
+  unsigned long long rows = 0;
+  for (uint64_t s = (uint64_t)blockIdx.x * 1024 + threadIdx.x; s < nslots; s += (uint64_t)gridDim.x * 1024) {
+    const unsigned long long n = sa.cnt[s];
+    if (n) {
+      const uint32_t f = sa.fst[s];
+      atomicOr(&bitmap[f >> 5], 1u << (f & 31));
+      rows += n;
+    }
+  }
+  __shared__ unsigned long long wr[16];
+  rows = wave_sum_u64(rows);
+  if ((threadIdx.x & 63) == 0) wr[threadIdx.x >> 6] = rows;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int q = 0; q < 16; ++q) t += wr[q];
+    if (t) atomicAdd(rows_total, t);
+  }
+}
+
+// exclusive scan of the bitmap's block totals in one workgroup (each thread a run of
+// consecutive blocks, one block-wide scan); hdr[0] = G, host[0] = G, host[1] = hdr[1]
+__global__ __launch_bounds__(1024) void k_block_scan_groups(unsigned int* block_sum, uint64_t nblocks,
+                                                            unsigned long long* hdr, unsigned long long* host) {
+  const uint64_t per = (nblocks + 1023) / 1024;
+  const uint64_t b0 = (uint64_t)threadIdx.x * per, b1 = min(b0 + per, nblocks);
+  unsigned int s = 0;
+  for (uint64_t i = b0; i < b1; ++i) s += block_sum[i];
+  unsigned int tot;
+  unsigned int e = block_excl_scan_1024(s, &tot);
+  for (uint64_t i = b0; i < b1; ++i) {
+    const unsigned int c = block_sum[i];
+    block_sum[i] = e;
+    e += c;
+  }
+  if (threadIdx.x == 0) {
+    hdr[0] = tot;
+    host[0] = tot;
+    host[1] = hdr[1];
+  }
+}
+
+// per bitmap word: its exclusive popcount prefix within its 1024-word block (high half) and
+// the word itself (low half) -- the emit's rank is then one 8-byte read per group
+__global__ __launch_bounds__(1024) void k_word_scan_pairs(const unsigned int* bitmap, uint64_t nwords,
+                                                          unsigned long long* word_pair, unsigned int* block_sum) {
+  const uint64_t w = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  const unsigned int b = w < nwords ? bitmap[w] : 0u;
+  unsigned int tot;
+  const unsigned int e = block_excl_scan_1024((unsigned int)__popc(b), &tot);
+  if (w < nwords) word_pair[w] = ((unsigned long long)e << 32) | b;
+  if (threadIdx.x == 0) block_sum[blockIdx.x] = tot;
+}
+
+template <int OUT>
+__global__ void k_rank_emit_slots(EmitParams e, SlotArrays sa, uint64_t nslots, int nsum,
+                                  const unsigned long long* word_pair, const unsigned int* block_prefix,
+                                  const unsigned long long* hdr) {
+  const uint64_t G = hdr[0];
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long n = sa.cnt[s];
+    if (!n) continue;
+    const uint32_t f = sa.fst[s];
+    const uint32_t w = f >> 5;
+    const unsigned long long pw = word_pair[w];
+    const unsigned int r = block_prefix[w >> 10] + (unsigned int)(pw >> 32) +
+                           (unsigned int)__popc((unsigned int)pw & ((1u << (f & 31)) - 1u));
+    const SlotRef t = slot_ref(sa, s, nslots, n, f);
+    const uint64_t code = e.hash ? (uint64_t)sa.keys[s] : s;
+    emit_slot<OUT>(e, s, code, r, t, G);
+  }
+}
+
+// the group records (emit_slot OUT 2) -> the output columns, in rank order: reads and writes
+// coalesced; column j at out + the 256-byte aligned sizes of columns 0..j-1 at G rows
+__global__ void k_aos_columns(EmitParams e, const unsigned long long* rec, unsigned char* out,
+                              const unsigned long long* hdr) {
+  const uint64_t G = hdr[0];
+  const int nc = e.ncols;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < G; r += (uint64_t)gridDim.x * blockDim.x) {
+    size_t off = 0;
+    for (int j = 0; j < nc; ++j) {
+      const int dt = e.cols[j].out_dtype;
+      store_elem(out + off, dt, r, rec[r * nc + j]);
+      off += (((size_t)G << dtype_lg(dt)) + 255) & ~size_t(255);
+    }
   }
 }
 
@@ -266,16 +346,8 @@ __global__ __launch_bounds__(1024) void k_emit_small(EmitParams e, SlotArrays sa
     hdr[0] = G;
     hdr[1] = total;
   }
-  const int nsum2 = e.nsum2;
   auto emit_one = [&](uint32_t s, unsigned int row) {
-    SlotTotals t;
-    t.cnt = sa.cnt[s];
-    t.fst = sa.fst[s];
-#pragma unroll
-    for (int q = 0; q < kMaxSums; ++q) {
-      t.acc[q] = q < nsum ? sa.acc[(size_t)q * nslots + s] : 0ull;
-      t.acc2[q] = (sa.acc2 && q < nsum2) ? sa.acc2[(size_t)q * nslots + s] : 0ull;
-    }
+    const SlotRef t = slot_ref(sa, s, nslots, sa.cnt[s], sa.fst[s]);
     const uint64_t code = e.hash ? (uint64_t)sa.keys[s] : (uint64_t)s;
     emit_slot(e, s, code, row, t);
   };
@@ -690,6 +762,32 @@ void launch_rank_emit_bitmap(const EmitParams& e, const SlotArrays& s, const uin
   hipLaunchKernelGGL(k_block_scan, dim3(1), dim3(1024), 0, st, block_prefix, nblocks);
   hipLaunchKernelGGL(k_rank_emit, dim3(g ? g : 1), dim3(256), 0, st, e, s, list_fst, list_slot, n, nsum, nslots,
                      bitmap, word_prefix, block_prefix);
+}
+void launch_slot_emit(const EmitParams& e, const SlotArrays& s, uint64_t nslots, int nsum, int64_t nrows,
+                      unsigned int* bitmap, unsigned long long* word_pair, unsigned int* block_prefix,
+                      unsigned long long* hdr, unsigned long long* host_hdr, hipEvent_t ev_groups,
+                      unsigned char* out, unsigned long long* rec, hipStream_t st) {
+  const uint64_t nwords = ((uint64_t)nrows + 31) / 32;
+  const uint64_t nblocks = (nwords + 1023) / 1024;
+  // hdr follows the bitmap: one fill zeroes both
+  (void)hipMemsetAsync(bitmap, 0, (size_t)((char*)hdr - (char*)bitmap) + 16, st);
+  const unsigned gs = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nslots + 1023) / 1024, 1024));
+  hipLaunchKernelGGL(k_setbits_slots, dim3(gs), dim3(1024), 0, st, s, nslots, bitmap, hdr + 1);
+  if (nwords)
+    hipLaunchKernelGGL(k_word_scan_pairs, dim3((unsigned)nblocks), dim3(1024), 0, st, bitmap, nwords, word_pair,
+                       block_prefix);
+  hipLaunchKernelGGL(k_block_scan_groups, dim3(1), dim3(1024), 0, st, block_prefix, nblocks, hdr, host_hdr);
+  (void)hipEventRecord(ev_groups, st);
+  const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nslots + 255) / 256, 4096));
+  EmitParams el = e;
+  if (rec) {
+    el.cols[0].out = rec;
+    hipLaunchKernelGGL(k_rank_emit_slots<2>, dim3(g), dim3(256), 0, st, el, s, nslots, nsum, word_pair, block_prefix, hdr);
+    hipLaunchKernelGGL(k_aos_columns, dim3(g), dim3(256), 0, st, e, rec, out, hdr);
+  } else {
+    el.cols[0].out = out;
+    hipLaunchKernelGGL(k_rank_emit_slots<1>, dim3(g), dim3(256), 0, st, el, s, nslots, nsum, word_pair, block_prefix, hdr);
+  }
 }
 void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order, unsigned int n, int nsum,
                  uint64_t nslots, hipStream_t st) {

@@ -27,7 +27,7 @@ __device__ __forceinline__ void emit_slot_private(const EmitParams& e, uint64_t 
     uint64_t bits;
     if (c.kind == 0) {
       const DevKey& k = e.keys[c.key];
-      bits = (uint64_t)k.min + (code / k.stride) % k.range;
+      bits = (uint64_t)k.min + key_offset(code, k);
     } else if (c.op == BQG_COUNT) {
       bits = t.cnt;
     } else {

@@ -1333,7 +1333,7 @@ def test_column_memory_budget(oracle_c):
 @pytest.mark.parametrize('opt,val', [('part_wbits', 6), ('part_wbits', 10), ('part_wbits', 13), ('scd_compact', 0),
                                      ('priv_ahead', 1), ('priv_ahead', 2), ('priv_ahead', 4),
                                      ('private_per_cu', 1), ('private_per_cu', 3), ('small_emit', 0),
-                                     ('part_ring', 1), ('part_ring', 2)])
+                                     ('part_ring', 1), ('part_ring', 2), ('slot_emit', 0)])
 def test_remaining_engine_options(opt, val, oracle_c, engine_options):
     """The engine options no other test sets, each at non-default values, on the query shape
     it steers (partition width and the scatter's ring: a partitioned C3-shaped query; the fused distinct pass's value
@@ -1343,7 +1343,7 @@ def test_remaining_engine_options(opt, val, oracle_c, engine_options):
     engine_options(**{opt: val, 'jit': 1, 'jit_min_rows': 0})
     rng = np.random.default_rng(sum(map(ord, opt)) * 16 + val)
     n = 400_003
-    if opt in ('part_wbits', 'part_ring'):  # (part_ring: packed entries, each block's spare tile)
+    if opt in ('part_wbits', 'part_ring', 'slot_emit'):  # (part_ring: packed entries, each block's spare tile)
         cols = OrderedDict(k=rng.integers(0, 90_000, n).astype(np.int32), g=rng.integers(1, 3, n).astype(np.int32),
                            v=np.round(rng.normal(size=n) * 64) / 64)
         keys, aggs, terms, mode = ['k', 'g'], [['v', 'sum', 's'], ['v', 'count', 'n']], [], 4
@@ -1365,3 +1365,75 @@ def test_remaining_engine_options(opt, val, oracle_c, engine_options):
     assert info['mode'] == mode, info
     ref = oracle_c.groupby(cols, keys, aggs, oracle_c.where_terms(cols, terms) if terms else None)
     assert_tables_equal(got, ref)
+
+
+def _same_bits(a, b):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    return a.dtype == b.dtype and a.shape == b.shape and (a.dtype.kind == 'O' and list(a) == list(b) or
+                                                          a.dtype.kind != 'O' and a.tobytes() == b.tobytes())
+
+
+@pytest.mark.parametrize('shape', ['partitioned', 'hash', 'wide_keys', 'nonfinite_std', 'distinct', 'filtered_empty',
+                                   'device_table'])
+def test_slot_emit_matches_compaction_emit(shape, oracle_c, engine_options):
+    """Round 6's large-result emit (option slot_emit: the first-row bitmap set straight from the
+    slot arrays, the group count left on the device for the emit's column layout and read by
+    the host while the emit runs -- no compaction pass, no host round trip before the emit)
+    against the compaction emit it replaces, bit for bit, on each slot mode with more than 8192
+    slots (slot_emit 2: the emit writes per-group records, a second pass the columns), and
+    against the C restatement.  (nonfinite_std: a std over a column holding NaN / infinities
+    keeps the fixed-point limbs, so its finite groups are the same bits run to run.)"""
+    rng = np.random.default_rng(sum(map(ord, shape)))
+    n = 300_007
+    terms = []
+    if shape == 'partitioned':
+        cols = OrderedDict(k=rng.integers(0, 90_000, n).astype(np.int32), g=rng.integers(1, 3, n).astype(np.int32),
+                           v=np.round(rng.normal(size=n) * 64) / 64)
+        keys, aggs = ['k', 'g'], [['v', 'sum', 's'], ['v', 'count', 'n']]
+    elif shape == 'hash':
+        pool = rng.integers(-2**40, 2**40, 40_000)
+        cols = OrderedDict(k=pool[rng.integers(0, pool.size, n)], v=rng.integers(-1000, 1000, n).astype(np.int64))
+        keys, aggs = ['k'], [['v', 'sum', 's'], ['v', 'mean', 'm']]
+    elif shape == 'wide_keys':
+        pool = rng.normal(size=30_000) * 1e6
+        cols = OrderedDict(f=pool[rng.integers(0, pool.size, n)], i=rng.integers(0, 3, n).astype(np.int64) << 40,
+                           v=rng.integers(0, 100, n).astype(np.int32))
+        keys, aggs = ['f', 'i'], [['v', 'sum', 's'], ['v', 'count', 'n']]
+    elif shape == 'nonfinite_std':
+        v = np.round(rng.normal(size=n) * 16) / 16
+        v[rng.integers(0, n, 300)] = np.nan
+        v[rng.integers(0, n, 300)] = np.inf
+        cols = OrderedDict(k=rng.integers(0, 20_000, n).astype(np.int32), v=v)
+        keys, aggs = ['k'], [['v', 'mean', 'm'], ['v', 'std', 'sd'], ['v', 'sum', 's']]
+    elif shape == 'distinct':
+        cols = OrderedDict(k=rng.integers(0, 20_000, n).astype(np.int32), d=rng.integers(0, 7, n).astype(np.int32))
+        keys, aggs = ['k'], [['d', 'count_distinct', 'cd'], ['d', 'sorted_count_distinct', 'scd']]
+    else:
+        cols = OrderedDict(k=rng.integers(0, 50_000, n).astype(np.int32), v=rng.integers(0, 100, n).astype(np.int64))
+        keys, aggs = ['k'], [['v', 'sum', 's'], ['v', 'count', 'n']]
+        if shape == 'filtered_empty':
+            terms = [('v', '>', 1000)]
+    t = ShardTable(cols)
+    try:
+        runs = []
+        for se in (1, 2, 0):
+            engine_options(slot_emit=se)
+            if shape == 'device_table':
+                r = t.groupby_table(keys, aggs)
+                try:
+                    runs.append((r.to_host(), False))
+                finally:
+                    r.close()
+            else:
+                runs.append(t.groupby(keys, aggs, where_terms=terms))
+    finally:
+        t.close()
+    (new, fnew), (rec, frec), (old, fold) = runs
+    assert fnew == fold and frec == fold and list(new) == list(old) and list(rec) == list(old)
+    for c in new:
+        assert _same_bits(new[c], old[c]) and _same_bits(rec[c], old[c]), c
+    if shape == 'filtered_empty':
+        assert fnew and all(len(x) == 0 for x in new.values())
+        return
+    ref = oracle_c.groupby(cols, keys, aggs, None)
+    assert_tables_equal(new, ref)

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""The last timed C2 steps of a rocprofv3 --kernel-trace --hip-trace run, as a timeline: every
-kernel (start / end) and every HIP API call between the step's first launch and the next step's
-first launch, in microseconds from the step start.  usage: step_timeline.py DIR"""
+"""The last timed steps of a rocprofv3 --kernel-trace --hip-trace [--memory-copy-trace] run, as a
+timeline: every kernel and copy (start / end) and every HIP API call between the step's first
+launch and the next step's first launch, in microseconds from the step start.
+usage: step_timeline.py DIR [ANCHOR]  (ANCHOR: a substring of the step's first kernel's name,
+default bq_jit_scan_private -- C2; bq_jit_part_scatter for C3)"""
 import csv
 import glob
 import os
@@ -12,9 +14,13 @@ kfile = glob.glob(os.path.join(d, '**', '*kernel_trace.csv'), recursive=True)[0]
 hfile = glob.glob(os.path.join(d, '**', '*hip_api_trace.csv'), recursive=True)[0]
 ks = [(int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'][:40]) for r in csv.DictReader(open(kfile))]
 hs = [(int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Function']) for r in csv.DictReader(open(hfile))]
+cfile = glob.glob(os.path.join(d, '**', '*memory_copy_trace.csv'), recursive=True)
+if cfile:
+    ks += [(int(r['Start_Timestamp']), int(r['End_Timestamp']), 'COPY ' + r.get('Direction', '')) for r in csv.DictReader(open(cfile[0]))]
 ks.sort()
 hs.sort()
-scans = [k for k in ks if 'bq_jit_scan_private' in k[2]]
+anchor = sys.argv[2] if len(sys.argv) > 2 else 'bq_jit_scan_private'
+scans = [k for k in ks if anchor in k[2]]
 print('scan launches', len(scans))
 for i in range(len(scans) - 4, len(scans) - 1):
     t0, t1 = scans[i][0], scans[i + 1][0]
