@@ -380,7 +380,7 @@ constexpr OptDef kOptDefs[kNumOpts] = {
     {"part_ring", 0, 0, 2},                 // packed scatter (JIT): tiles of row loads in flight (0: 1)
     {"jit_async", 1, 0, 1},                 // a shape not compiled yet runs the generic kernel while hiprtc compiles it
     {"warm", 1, 0, 1},                      // bqg_create runs one small query (read at context creation only)
-    {"slot_emit", 1, 0, 2},                 // large slot spaces: emit without the compaction and its host round trip (2: via group records)
+    {"slot_emit", 1, 0, 3},                 // large slot spaces: emit without the compaction and its host round trip (2: via group records, 3: first-row bitmap atomics)
 };
 
 static int opt_index(const char* name) {
@@ -423,6 +423,9 @@ struct bqg_ctx {
   DevBuf partials, counter, hdr, slots, terms, outcols, lists, bitmap, prefix, cdbuf, scdbuf, mask, misc, done;
   DevBuf strings;  // bqg_encode_bytes: the staged bytes and the dictionary's work arrays
   DevBuf nfbuf;    // the nonfinite pass's per-slot rows and counts
+  // the large-result emit's row map (one byte per row; a query's first rows hold its epoch)
+  DevBuf rowmap;
+  unsigned char rowmap_epoch = 0;
   HostBuf hhdr, hout;
   // pinned blocks for results (returned by bqg_result_free); shared with outstanding results
   // so a result may outlive its context
@@ -2104,8 +2107,23 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     for (int j = 0; j < e.ncols; ++j) ocap += ((size_t)S * dtype_size(out_dt[j]) + 255) & ~size_t(255);
     const bool aos = c->opt[kOptSlotEmit] == 2;
     unsigned char* ob = (unsigned char*)c->outcols.ensure(ocap + 256 + (aos ? (size_t)S * e.ncols * 8 : 0));
-    launch_slot_emit(e, sa, S, nsum, N, bitmap, wpair, bprefix, hdev, (unsigned long long*)hh_dev, c->ev_groups, ob,
-                     aos ? (unsigned long long*)(ob + ocap + 256) : nullptr, st);
+    // first rows marked in the row map (one byte per row, the query's epoch) up to 2^30 rows,
+    // else by bitmap atomics
+    unsigned char* row_map = nullptr;
+    unsigned char epoch = 0;
+    if ((uint64_t)N <= (1ull << 30) && c->opt[kOptSlotEmit] != 3) {
+      const size_t need = nwords * 32 + 256;
+      const void* before = c->rowmap.p;
+      const size_t cap_before = c->rowmap.cap;
+      row_map = (unsigned char*)c->rowmap.ensure(need);
+      if (row_map != before || c->rowmap.cap != cap_before || c->rowmap_epoch == 255) {
+        HIPCHECK(hipMemsetAsync(row_map, 0, c->rowmap.cap, st));
+        c->rowmap_epoch = 0;
+      }
+      epoch = ++c->rowmap_epoch;
+    }
+    launch_slot_emit(e, sa, S, N, bitmap, row_map, epoch, wpair, bprefix, hdev, (unsigned long long*)hh_dev,
+                     c->ev_groups, ob, aos ? (unsigned long long*)(ob + ocap + 256) : nullptr, st);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventSynchronize(c->ev_groups));
     const uint64_t G = hh[0];
@@ -2470,7 +2488,7 @@ int bqg_destroy(bqg_ctx* c) {
   int rc = guard(c, [&] {
     HIPCHECK(hipStreamSynchronize(c->stream));
     for (DevBuf* b : {&c->partials, &c->counter, &c->hdr, &c->slots, &c->terms, &c->outcols, &c->lists,
-                      &c->bitmap, &c->prefix, &c->cdbuf, &c->scdbuf, &c->mask, &c->misc, &c->done, &c->strings, &c->nfbuf})
+                      &c->bitmap, &c->prefix, &c->cdbuf, &c->scdbuf, &c->mask, &c->misc, &c->done, &c->strings, &c->nfbuf, &c->rowmap})
       b->release();
     c->hhdr.release();
     c->hout.release();

@@ -577,87 +577,80 @@ __device__ __forceinline__ SlotRef slot_ref(const SlotArrays& sa, uint64_t s, ui
   return t;
 }
 
-// OUT 0: column j at cols[j].out.  OUT 1: the output columns laid out by the group count G,
-// known on the device only (the large-result emit without a host round trip): column j at
-// cols[0].out + the 256-byte aligned sizes of columns 0..j-1 at G rows.  OUT 2: one record of
-// ncols 8-byte words per group at cols[0].out + rank * ncols * 8 (the words unnarrowed; a
-// record lands in one or two lines where four column stores would touch four random lines --
-// k_aos_columns then writes the columns in rank order)
-template <int OUT = 0, typename T>
+// one output column's value for one group (emit_slot's column loop body)
+template <typename T>
+__device__ __forceinline__ uint64_t column_bits(const EmitParams& e, const EmitCol& c, uint64_t slot, uint64_t code,
+                                               unsigned int rank, const T& t) {
+  uint64_t bits = 0;
+  if (c.kind == 0) {
+    const DevKey& k = e.keys[c.key];
+    if (e.hash == 2) {  // wide keys: the value at the slot's representative row
+      bits = key_at_row(e.key_cols[c.key], k.is_float, (uint32_t)code);
+      if (c.out_dtype == BQG_F32) bits = __float_as_uint((float)as_f64(bits));
+    } else if (k.is_float) {
+      bits = code;
+      if (c.out_dtype == BQG_F32) bits = __float_as_uint((float)as_f64(code));
+    } else {
+      const uint64_t off = key_offset(code, k);
+      bits = (uint64_t)k.min + off;
+    }
+  } else {
+    switch (c.op) {
+      case BQG_SUM: {
+        unsigned long long a = t.sum(c.state);
+        if (c.in_float && e.sum_dec[c.state] != 0.0) a = as_u64((double)(long long)a / e.sum_dec[c.state]);
+        if (c.in_float) bits = (c.out_dtype == BQG_F32) ? (uint64_t)__float_as_uint((float)as_f64(a)) : a;
+        else bits = a;  // wrap-around to the output width happens in store_elem
+      } break;
+      case BQG_COUNT: bits = t.cnt; break;
+      case BQG_MEAN: {
+        const unsigned long long a = t.sum(c.state);
+        const double s = c.in_float ? (e.sum_dec[c.state] != 0.0 ? (double)(long long)a / e.sum_dec[c.state] : as_f64(a))
+                                    : (c.in_dtype == BQG_U64 ? (double)(uint64_t)a : (double)(long long)a);
+        bits = as_u64(s / (double)t.cnt);
+        if (e.nf_cnt[c.sum_state]) {
+          // bquery's m += (x - m) / c: an infinity stays only as the group's last row and its
+          // one non-finite value (the next row makes inf - inf); NaN otherwise
+          const uint32_t k = e.nf_cnt[c.sum_state][slot];
+          if (k) {
+            double m = __builtin_nan("");
+            if (k == 1 && e.nf_row[c.sum_state][slot] == e.nf_last[slot]) {
+              const double x = as_f64(value_at_row(e.nf_col[c.sum_state], e.nf_row[c.sum_state][slot]));
+              if (__builtin_isinf(x)) m = x;
+            }
+            bits = as_u64(m);
+          }
+        }
+      } break;
+      case BQG_STD: {
+        const double m2 = as_f64(t.m2(c.state));
+        bits = as_u64(t.cnt ? sqrt(m2 / (double)t.cnt) : __builtin_nan(""));
+        // Welford: d * (x - mean) is inf * (inf - inf) at the first non-finite value
+        if (e.nf_cnt[c.sum_state] && e.nf_cnt[c.sum_state][slot]) bits = as_u64(__builtin_nan(""));
+      } break;
+      case BQG_COUNT_DISTINCT: bits = e.cd[c.state][slot]; break;
+      case BQG_SORTED_COUNT_DISTINCT: {
+        // bquery rule: the first processed row initialises slot 0 (counts 1 only when that
+        // row has label 0, i.e. row 0 passes); every other group's first value is compared
+        // with the zero-initialised last value.
+        unsigned long long ch = e.scd_changes[c.state][slot];
+        const unsigned long long fv = e.scd_first[c.state][slot];
+        const bool first_differs = c.in_float ? !(as_f64(fv) == 0.0) : (fv != 0ull);
+        if (rank == 0) ch += (t.fst == 0u) ? 1ull : 0ull;
+        else ch += first_differs ? 1ull : 0ull;
+        bits = ch;
+      } break;
+    }
+  }
+  return bits;
+}
+
+template <typename T>
 __device__ __forceinline__ void emit_slot(const EmitParams& e, uint64_t slot, uint64_t code, unsigned int rank,
-                                       const T& t, uint64_t G = 0) {
-  size_t goff = 0;
+                                       const T& t) {
   for (int j = 0; j < e.ncols; ++j) {
     const EmitCol& c = e.cols[j];
-    uint64_t bits = 0;
-    if (c.kind == 0) {
-      const DevKey& k = e.keys[c.key];
-      if (e.hash == 2) {  // wide keys: the value at the slot's representative row
-        bits = key_at_row(e.key_cols[c.key], k.is_float, (uint32_t)code);
-        if (c.out_dtype == BQG_F32) bits = __float_as_uint((float)as_f64(bits));
-      } else if (k.is_float) {
-        bits = code;
-        if (c.out_dtype == BQG_F32) bits = __float_as_uint((float)as_f64(code));
-      } else {
-        const uint64_t off = key_offset(code, k);
-        bits = (uint64_t)k.min + off;
-      }
-    } else {
-      switch (c.op) {
-        case BQG_SUM: {
-          unsigned long long a = t.sum(c.state);
-          if (c.in_float && e.sum_dec[c.state] != 0.0) a = as_u64((double)(long long)a / e.sum_dec[c.state]);
-          if (c.in_float) bits = (c.out_dtype == BQG_F32) ? (uint64_t)__float_as_uint((float)as_f64(a)) : a;
-          else bits = a;  // wrap-around to the output width happens in store_elem
-        } break;
-        case BQG_COUNT: bits = t.cnt; break;
-        case BQG_MEAN: {
-          const unsigned long long a = t.sum(c.state);
-          const double s = c.in_float ? (e.sum_dec[c.state] != 0.0 ? (double)(long long)a / e.sum_dec[c.state] : as_f64(a))
-                                      : (c.in_dtype == BQG_U64 ? (double)(uint64_t)a : (double)(long long)a);
-          bits = as_u64(s / (double)t.cnt);
-          if (e.nf_cnt[c.sum_state]) {
-            // bquery's m += (x - m) / c: an infinity stays only as the group's last row and its
-            // one non-finite value (the next row makes inf - inf); NaN otherwise
-            const uint32_t k = e.nf_cnt[c.sum_state][slot];
-            if (k) {
-              double m = __builtin_nan("");
-              if (k == 1 && e.nf_row[c.sum_state][slot] == e.nf_last[slot]) {
-                const double x = as_f64(value_at_row(e.nf_col[c.sum_state], e.nf_row[c.sum_state][slot]));
-                if (__builtin_isinf(x)) m = x;
-              }
-              bits = as_u64(m);
-            }
-          }
-        } break;
-        case BQG_STD: {
-          const double m2 = as_f64(t.m2(c.state));
-          bits = as_u64(t.cnt ? sqrt(m2 / (double)t.cnt) : __builtin_nan(""));
-          // Welford: d * (x - mean) is inf * (inf - inf) at the first non-finite value
-          if (e.nf_cnt[c.sum_state] && e.nf_cnt[c.sum_state][slot]) bits = as_u64(__builtin_nan(""));
-        } break;
-        case BQG_COUNT_DISTINCT: bits = e.cd[c.state][slot]; break;
-        case BQG_SORTED_COUNT_DISTINCT: {
-          // bquery rule: the first processed row initialises slot 0 (counts 1 only when that
-          // row has label 0, i.e. row 0 passes); every other group's first value is compared
-          // with the zero-initialised last value.
-          unsigned long long ch = e.scd_changes[c.state][slot];
-          const unsigned long long fv = e.scd_first[c.state][slot];
-          const bool first_differs = c.in_float ? !(as_f64(fv) == 0.0) : (fv != 0ull);
-          if (rank == 0) ch += (t.fst == 0u) ? 1ull : 0ull;
-          else ch += first_differs ? 1ull : 0ull;
-          bits = ch;
-        } break;
-      }
-    }
-    if (OUT == 2) {
-      static_cast<unsigned long long*>(e.cols[0].out)[(size_t)rank * e.ncols + j] = bits;
-    } else if (OUT == 1) {
-      store_elem(static_cast<unsigned char*>(e.cols[0].out) + goff, c.out_dtype, rank, bits);
-      goff += (((size_t)G << dtype_lg(c.out_dtype)) + 255) & ~size_t(255);
-    } else {
-      store_elem(c.out, c.out_dtype, rank, bits);
-    }
+    store_elem(c.out, c.out_dtype, rank, column_bits(e, c, slot, code, rank, t));
   }
 }
 

@@ -223,6 +223,59 @@ __global__ __launch_bounds__(1024) void k_setbits_slots(SlotArrays sa, uint64_t 
   }
 }
 
+// The same marks without atomics (round 6): one byte per row, set to the query's epoch (1..255)
+// with a plain store -- distinct groups have distinct first rows, so no two stores meet -- and
+// read back as "byte == epoch"; the map is cleared only when the epoch wraps.  1 M random bit
+// atomics took 43 us at C3 (the atomic unit's rate), the byte stores and the 100 MB read-back
+// a fraction of that, and no bitmap fill.
+__global__ __launch_bounds__(1024) void k_mark_rows(SlotArrays sa, uint64_t nslots, unsigned char* map,
+                                                    unsigned char epoch, unsigned long long* rows_total) {
+  unsigned long long rows = 0;
+  for (uint64_t s = (uint64_t)blockIdx.x * 1024 + threadIdx.x; s < nslots; s += (uint64_t)gridDim.x * 1024) {
+    const unsigned long long n = sa.cnt[s];
+    if (n) {
+      map[sa.fst[s]] = epoch;
+      rows += n;
+    }
+  }
+  __shared__ unsigned long long wr[16];
+  rows = wave_sum_u64(rows);
+  if ((threadIdx.x & 63) == 0) wr[threadIdx.x >> 6] = rows;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int q = 0; q < 16; ++q) t += wr[q];
+    if (t) atomicAdd(rows_total, t);
+  }
+}
+
+// 4 bytes -> 4 flag bits (byte == epoch), exact (no borrow between bytes)
+__device__ __forceinline__ unsigned int epoch_bits4(unsigned int d, unsigned int ep4) {
+  const unsigned int t = d ^ ep4;
+  const unsigned int nz = ((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t;  // high bit: byte != epoch
+  const unsigned int hi = ~nz & 0x80808080u;
+  return ((hi >> 7) & 1u) | ((hi >> 14) & 2u) | ((hi >> 21) & 4u) | ((hi >> 28) & 8u);
+}
+
+// the row map's 32-row words (32 bytes per thread, two 16-byte loads) as bitmap words:
+// per word its exclusive popcount prefix in its 1024-word block and the word (k_word_scan_pairs)
+__global__ __launch_bounds__(1024) void k_map_scan_pairs(const unsigned char* map, uint64_t nwords, unsigned char epoch,
+                                                         unsigned long long* word_pair, unsigned int* block_sum) {
+  const uint64_t w = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  unsigned int b = 0;
+  if (w < nwords) {
+    const uint4 lo = load_stream16(map + w * 32), hi = load_stream16(map + w * 32 + 16);
+    const unsigned int ep4 = 0x01010101u * epoch;
+    b = epoch_bits4(lo.x, ep4) | epoch_bits4(lo.y, ep4) << 4 | epoch_bits4(lo.z, ep4) << 8 |
+        epoch_bits4(lo.w, ep4) << 12 | epoch_bits4(hi.x, ep4) << 16 | epoch_bits4(hi.y, ep4) << 20 |
+        epoch_bits4(hi.z, ep4) << 24 | epoch_bits4(hi.w, ep4) << 28;
+  }
+  unsigned int tot;
+  const unsigned int e = block_excl_scan_1024((unsigned int)__popc(b), &tot);
+  if (w < nwords) word_pair[w] = ((unsigned long long)e << 32) | b;
+  if (threadIdx.x == 0) block_sum[blockIdx.x] = tot;
+}
+
 // exclusive scan of the bitmap's block totals in one workgroup (each thread a run of
 // consecutive blocks, one block-wide scan); hdr[0] = G, host[0] = G, host[1] = hdr[1]
 __global__ __launch_bounds__(1024) void k_block_scan_groups(unsigned int* block_sum, uint64_t nblocks,
@@ -257,22 +310,60 @@ __global__ __launch_bounds__(1024) void k_word_scan_pairs(const unsigned int* bi
   if (threadIdx.x == 0) block_sum[blockIdx.x] = tot;
 }
 
-template <int OUT>
-__global__ void k_rank_emit_slots(EmitParams e, SlotArrays sa, uint64_t nslots, int nsum,
-                                  const unsigned long long* word_pair, const unsigned int* block_prefix,
-                                  const unsigned long long* hdr) {
+// The emit with the columns outermost: K slots per thread (slot = block base + k * 256 + tid,
+// coalesced per k), their counts, first rows, rank words and keys loaded together, then per
+// output column -- its descriptor read once for the K slots, the K values computed (their
+// loads issued together), then stored.  (Per slot, each column's descriptor fields are a chain
+// of dependent scalar loads: the one-slot emit spent ~2/3 of its wave cycles waiting and took
+// 54-56 us at C3.)
+// The stores at random ranks are ~3/4 of the pass (C3: 52.6 us; 13.8 without them, 20.9 with
+// them in slot order) and are bound by their number, not their lines: REC (option slot_emit 2)
+// writes each group's values into its record (ncols 8-byte words at rec + rank * ncols, one
+// line or two) and k_aos_columns the columns in rank order -- 59 + 12.9 us, slower.
+template <int K, bool REC>
+__global__ __launch_bounds__(256) void k_rank_emit_cols(EmitParams e, SlotArrays sa, uint64_t nslots,
+                                                        const unsigned long long* word_pair,
+                                                        const unsigned int* block_prefix, const unsigned long long* hdr,
+                                                        unsigned char* out) {
   const uint64_t G = hdr[0];
-  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (uint64_t)gridDim.x * blockDim.x) {
-    const unsigned long long n = sa.cnt[s];
-    if (!n) continue;
-    const uint32_t f = sa.fst[s];
-    const uint32_t w = f >> 5;
-    const unsigned long long pw = word_pair[w];
-    const unsigned int r = block_prefix[w >> 10] + (unsigned int)(pw >> 32) +
-                           (unsigned int)__popc((unsigned int)pw & ((1u << (f & 31)) - 1u));
-    const SlotRef t = slot_ref(sa, s, nslots, n, f);
-    const uint64_t code = e.hash ? (uint64_t)sa.keys[s] : s;
-    emit_slot<OUT>(e, s, code, r, t, G);
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 * K; base < nslots; base += (uint64_t)gridDim.x * 256 * K) {
+    uint64_t s[K], code[K];
+    unsigned long long n[K];
+    uint32_t f[K];
+    unsigned int r[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      s[k] = base + (uint64_t)k * 256 + threadIdx.x;
+      n[k] = s[k] < nslots ? sa.cnt[s[k]] : 0ull;
+      f[k] = s[k] < nslots ? sa.fst[s[k]] : 0u;
+      code[k] = (e.hash && n[k]) ? (uint64_t)sa.keys[s[k]] : s[k];
+    }
+    unsigned long long pw[K];
+    unsigned int bp[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t w = f[k] >> 5;
+      pw[k] = n[k] ? word_pair[w] : 0ull;
+      bp[k] = n[k] ? block_prefix[w >> 10] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      r[k] = bp[k] + (unsigned int)(pw[k] >> 32) + (unsigned int)__popc((unsigned int)pw[k] & ((1u << (f[k] & 31)) - 1u));
+    size_t goff = 0;
+    for (int j = 0; j < e.ncols; ++j) {
+      const EmitCol c = e.cols[j];
+      uint64_t bits[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        bits[k] = n[k] ? column_bits(e, c, s[k], code[k], r[k], slot_ref(sa, s[k], nslots, n[k], f[k])) : 0ull;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (!n[k]) continue;
+        if (REC) reinterpret_cast<unsigned long long*>(out)[(size_t)r[k] * e.ncols + j] = bits[k];
+        else store_elem(out + goff, c.out_dtype, r[k], bits[k]);
+      }
+      goff += (((size_t)G << dtype_lg(c.out_dtype)) + 255) & ~size_t(255);
+    }
   }
 }
 
@@ -763,30 +854,39 @@ void launch_rank_emit_bitmap(const EmitParams& e, const SlotArrays& s, const uin
   hipLaunchKernelGGL(k_rank_emit, dim3(g ? g : 1), dim3(256), 0, st, e, s, list_fst, list_slot, n, nsum, nslots,
                      bitmap, word_prefix, block_prefix);
 }
-void launch_slot_emit(const EmitParams& e, const SlotArrays& s, uint64_t nslots, int nsum, int64_t nrows,
-                      unsigned int* bitmap, unsigned long long* word_pair, unsigned int* block_prefix,
-                      unsigned long long* hdr, unsigned long long* host_hdr, hipEvent_t ev_groups,
-                      unsigned char* out, unsigned long long* rec, hipStream_t st) {
+void launch_slot_emit(const EmitParams& e, const SlotArrays& s, uint64_t nslots, int64_t nrows,
+                      unsigned int* bitmap, unsigned char* row_map, unsigned char epoch,
+                      unsigned long long* word_pair, unsigned int* block_prefix, unsigned long long* hdr,
+                      unsigned long long* host_hdr, hipEvent_t ev_groups, unsigned char* out,
+                      unsigned long long* rec, hipStream_t st) {
   const uint64_t nwords = ((uint64_t)nrows + 31) / 32;
   const uint64_t nblocks = (nwords + 1023) / 1024;
-  // hdr follows the bitmap: one fill zeroes both
-  (void)hipMemsetAsync(bitmap, 0, (size_t)((char*)hdr - (char*)bitmap) + 16, st);
   const unsigned gs = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nslots + 1023) / 1024, 1024));
-  hipLaunchKernelGGL(k_setbits_slots, dim3(gs), dim3(1024), 0, st, s, nslots, bitmap, hdr + 1);
-  if (nwords)
-    hipLaunchKernelGGL(k_word_scan_pairs, dim3((unsigned)nblocks), dim3(1024), 0, st, bitmap, nwords, word_pair,
-                       block_prefix);
+  if (row_map) {
+    (void)hipMemsetAsync(hdr, 0, 16, st);
+    hipLaunchKernelGGL(k_mark_rows, dim3(gs), dim3(1024), 0, st, s, nslots, row_map, epoch, hdr + 1);
+    if (nwords)
+      hipLaunchKernelGGL(k_map_scan_pairs, dim3((unsigned)nblocks), dim3(1024), 0, st, row_map, nwords, epoch,
+                         word_pair, block_prefix);
+  } else {
+    // hdr follows the bitmap: one fill zeroes both
+    (void)hipMemsetAsync(bitmap, 0, (size_t)((char*)hdr - (char*)bitmap) + 16, st);
+    hipLaunchKernelGGL(k_setbits_slots, dim3(gs), dim3(1024), 0, st, s, nslots, bitmap, hdr + 1);
+    if (nwords)
+      hipLaunchKernelGGL(k_word_scan_pairs, dim3((unsigned)nblocks), dim3(1024), 0, st, bitmap, nwords, word_pair,
+                         block_prefix);
+  }
   hipLaunchKernelGGL(k_block_scan_groups, dim3(1), dim3(1024), 0, st, block_prefix, nblocks, hdr, host_hdr);
   (void)hipEventRecord(ev_groups, st);
-  const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nslots + 255) / 256, 4096));
-  EmitParams el = e;
+  const unsigned gk = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nslots + 1023) / 1024, 4096));
   if (rec) {
-    el.cols[0].out = rec;
-    hipLaunchKernelGGL(k_rank_emit_slots<2>, dim3(g), dim3(256), 0, st, el, s, nslots, nsum, word_pair, block_prefix, hdr);
-    hipLaunchKernelGGL(k_aos_columns, dim3(g), dim3(256), 0, st, e, rec, out, hdr);
+    hipLaunchKernelGGL((k_rank_emit_cols<4, true>), dim3(gk), dim3(256), 0, st, e, s, nslots, word_pair, block_prefix,
+                       hdr, (unsigned char*)rec);
+    const unsigned ga = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nslots + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_aos_columns, dim3(ga), dim3(256), 0, st, e, rec, out, hdr);
   } else {
-    el.cols[0].out = out;
-    hipLaunchKernelGGL(k_rank_emit_slots<1>, dim3(g), dim3(256), 0, st, el, s, nslots, nsum, word_pair, block_prefix, hdr);
+    hipLaunchKernelGGL((k_rank_emit_cols<4, false>), dim3(gk), dim3(256), 0, st, e, s, nslots, word_pair, block_prefix,
+                       hdr, out);
   }
 }
 void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order, unsigned int n, int nsum,

@@ -227,14 +227,16 @@ int bqg_last_timing(bqg_ctx* ctx, bqg_timing* out);
  *                     first query does not pay the library's start-up (code
  *                     object load, first launches, buffer sizing; read from
  *                     BQGPU_OPTIONS at context creation only)
- *   slot_emit      1  slot spaces above 8192: the first-appearance ranks     0 | 1 | 2
- *                     come from a first-row bitmap set straight from the
- *                     slot arrays and the group count stays on the device
- *                     for the emit (no compaction pass, no host round trip
- *                     before the emit); 2: the same, the emit writing one
- *                     record per group and a second pass the columns in
- *                     rank order; 0: compaction, count read back, then the
- *                     emit.  All give the same result
+ *   slot_emit      1  slot spaces above 8192: the first-appearance ranks     0 .. 3
+ *                     come from the groups' first rows marked straight from
+ *                     the slot arrays (a byte per row holding the query's
+ *                     epoch, up to 2^30 rows; bitmap atomics beyond) and the
+ *                     group count stays on the device for the emit (no
+ *                     compaction pass, no host round trip before the emit);
+ *                     2: the same, the emit writing one record per group and
+ *                     a second pass the columns in rank order; 3: bitmap
+ *                     atomics at every size; 0: compaction, count read back,
+ *                     then the emit.  All give the same result
  * An unknown name or out-of-range value fails with BQG_E_INVALID.  bqg_reset_options restores
  * the defaults (then the environment's values). */
 int bqg_set_option(bqg_ctx* ctx, const char* name, int64_t value);

@@ -16,4 +16,4 @@ for r in csv.DictReader(open(f)):
         print('%-10s %-50s %8.1f us' % (sys.argv[2], r['Name'][:50], float(r['AverageNs']) / 1e3))
 PY
 }
-run base BQGPU_OPTIONS=slot_emit=1 && run aos BQGPU_OPTIONS=slot_emit=2 && run old BQGPU_OPTIONS=slot_emit=0
+run base BQGPU_OPTIONS=slot_emit=1 && run p1_nolookup BQG_EMIT_PROBE=1 && run p2_nostore BQG_EMIT_PROBE=2 && run p3_nobits BQG_EMIT_PROBE=3 && run k8 BQG_EMIT_PROBE=8 && run k1 BQG_EMIT_PROBE=9
