@@ -1502,7 +1502,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     if (pl.mode != kPartitioned && c->opt[kOptPartNarrow] != 0) set_sum_codes(t, pl, &e);
     // the other float sums as fixed-point limbs (the same bits on every run)
     if (pl.mode != kPartitioned) set_sum_fx(pl);
-    HIPCHECK(hipMemsetAsync(sa.hash_fill, 0, 8, st));
+    if (pl.p.hash) HIPCHECK(hipMemsetAsync(sa.hash_fill, 0, 8, st));  // (+ overflow flag)
     // fixed-point states with per-slot shifts: each slot's largest exponent first (one pass over
     // the same rows; the hash modes insert their keys here already)
     auto fx_emax_pass = [&]() {
@@ -2093,11 +2093,13 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     const uint64_t nblocks = (nwords + 1023) / 1024;
     // bitmap [nwords] u32 | hdr (256 B) | word pairs [nwords] u64 | block prefixes [nblocks] u32
     const size_t bm_bytes = (nwords * 4 + 255) & ~size_t(255);
-    unsigned char* pb = (unsigned char*)c->prefix.ensure(bm_bytes + 256 + nwords * 8 + nblocks * 4 + 1024);
+    unsigned char* pb = (unsigned char*)c->prefix.ensure(bm_bytes + 256 + nwords * 8 + nblocks * 4 + 1024 + 8192);
     unsigned int* bitmap = (unsigned int*)pb;
     unsigned long long* hdev = (unsigned long long*)(pb + bm_bytes);
     unsigned long long* wpair = (unsigned long long*)(pb + bm_bytes + 256);
     unsigned int* bprefix = (unsigned int*)(wpair + nwords);
+    // the marking pass's per-workgroup passing rows (up to 1024 workgroups)
+    unsigned long long* rows_part = (unsigned long long*)(pb + ((bm_bytes + 256 + nwords * 8 + nblocks * 4 + 255) & ~size_t(255)));
     unsigned long long* hh = (unsigned long long*)c->hhdr.ensure(64);
     void* hh_dev = nullptr;
     HIPCHECK(hipHostGetDevicePointer(&hh_dev, hh, 0));
@@ -2122,7 +2124,7 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
       }
       epoch = ++c->rowmap_epoch;
     }
-    launch_slot_emit(e, sa, S, N, bitmap, row_map, epoch, wpair, bprefix, hdev, (unsigned long long*)hh_dev,
+    launch_slot_emit(e, sa, S, N, bitmap, row_map, epoch, wpair, bprefix, rows_part, hdev, (unsigned long long*)hh_dev,
                      c->ev_groups, ob, aos ? (unsigned long long*)(ob + ocap + 256) : nullptr, st);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventSynchronize(c->ev_groups));

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(1024) void k_setbits_slots(SlotArrays sa, uint64_t 
 // atomics took 43 us at C3 (the atomic unit's rate), the byte stores and the 100 MB read-back
 // a fraction of that, and no bitmap fill.
 __global__ __launch_bounds__(1024) void k_mark_rows(SlotArrays sa, uint64_t nslots, unsigned char* map,
-                                                    unsigned char epoch, unsigned long long* rows_total) {
+                                                    unsigned char epoch, unsigned long long* rows_part) {
   unsigned long long rows = 0;
   for (uint64_t s = (uint64_t)blockIdx.x * 1024 + threadIdx.x; s < nslots; s += (uint64_t)gridDim.x * 1024) {
     const unsigned long long n = sa.cnt[s];
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(1024) void k_mark_rows(SlotArrays sa, uint64_t nslo
   if (threadIdx.x == 0) {
     unsigned long long t = 0;
     for (int q = 0; q < 16; ++q) t += wr[q];
-    if (t) atomicAdd(rows_total, t);
+    rows_part[blockIdx.x] = t;  // every workgroup: no zeroing, no atomics
   }
 }
 
@@ -279,7 +279,13 @@ __global__ __launch_bounds__(1024) void k_map_scan_pairs(const unsigned char* ma
 // exclusive scan of the bitmap's block totals in one workgroup (each thread a run of
 // consecutive blocks, one block-wide scan); hdr[0] = G, host[0] = G, host[1] = hdr[1]
 __global__ __launch_bounds__(1024) void k_block_scan_groups(unsigned int* block_sum, uint64_t nblocks,
+                                                            const unsigned long long* rows_part, int nrp,
                                                             unsigned long long* hdr, unsigned long long* host) {
+  // passing rows: the marking workgroups' counts (rows_part), or hdr[1] from the bitmap pass
+  __shared__ unsigned long long rsum[16];
+  unsigned long long rp = rows_part && (int)threadIdx.x < nrp ? rows_part[threadIdx.x] : 0ull;
+  rp = wave_sum_u64(rp);
+  if ((threadIdx.x & 63) == 0) rsum[threadIdx.x >> 6] = rp;
   const uint64_t per = (nblocks + 1023) / 1024;
   const uint64_t b0 = (uint64_t)threadIdx.x * per, b1 = min(b0 + per, nblocks);
   unsigned int s = 0;
@@ -292,9 +298,13 @@ __global__ __launch_bounds__(1024) void k_block_scan_groups(unsigned int* block_
     e += c;
   }
   if (threadIdx.x == 0) {
+    unsigned long long rows = 0;
+    for (int q = 0; q < 16; ++q) rows += rsum[q];
+    if (rows_part) hdr[1] = rows;
+    else rows = hdr[1];
     hdr[0] = tot;
     host[0] = tot;
-    host[1] = hdr[1];
+    host[1] = rows;
   }
 }
 
@@ -856,15 +866,15 @@ void launch_rank_emit_bitmap(const EmitParams& e, const SlotArrays& s, const uin
 }
 void launch_slot_emit(const EmitParams& e, const SlotArrays& s, uint64_t nslots, int64_t nrows,
                       unsigned int* bitmap, unsigned char* row_map, unsigned char epoch,
-                      unsigned long long* word_pair, unsigned int* block_prefix, unsigned long long* hdr,
+                      unsigned long long* word_pair, unsigned int* block_prefix,
+                      unsigned long long* rows_part, unsigned long long* hdr,
                       unsigned long long* host_hdr, hipEvent_t ev_groups, unsigned char* out,
                       unsigned long long* rec, hipStream_t st) {
   const uint64_t nwords = ((uint64_t)nrows + 31) / 32;
   const uint64_t nblocks = (nwords + 1023) / 1024;
   const unsigned gs = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nslots + 1023) / 1024, 1024));
   if (row_map) {
-    (void)hipMemsetAsync(hdr, 0, 16, st);
-    hipLaunchKernelGGL(k_mark_rows, dim3(gs), dim3(1024), 0, st, s, nslots, row_map, epoch, hdr + 1);
+    hipLaunchKernelGGL(k_mark_rows, dim3(gs), dim3(1024), 0, st, s, nslots, row_map, epoch, rows_part);
     if (nwords)
       hipLaunchKernelGGL(k_map_scan_pairs, dim3((unsigned)nblocks), dim3(1024), 0, st, row_map, nwords, epoch,
                          word_pair, block_prefix);
@@ -876,7 +886,8 @@ void launch_slot_emit(const EmitParams& e, const SlotArrays& s, uint64_t nslots,
       hipLaunchKernelGGL(k_word_scan_pairs, dim3((unsigned)nblocks), dim3(1024), 0, st, bitmap, nwords, word_pair,
                          block_prefix);
   }
-  hipLaunchKernelGGL(k_block_scan_groups, dim3(1), dim3(1024), 0, st, block_prefix, nblocks, hdr, host_hdr);
+  hipLaunchKernelGGL(k_block_scan_groups, dim3(1), dim3(1024), 0, st, block_prefix, nblocks,
+                     (const unsigned long long*)(row_map ? rows_part : nullptr), (int)gs, hdr, host_hdr);
   (void)hipEventRecord(ev_groups, st);
   const unsigned gk = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nslots + 1023) / 1024, 4096));
   if (rec) {

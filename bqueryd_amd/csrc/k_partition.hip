@@ -588,7 +588,7 @@ void launch_partitioned(const ScanParams& p, const SlotArrays& s, const PartLaun
   const unsigned grid = (unsigned)(((L.nparts + 7) / 8) * 8 * L.splits);
   const unsigned cgrid = (unsigned)std::min<uint64_t>((p.nslots + 255) / 256, 4096);
   if (L.pack) {
-    (void)hipMemsetAsync(L.tile_mark, 0, (size_t)L.ntiles * 4 + 256, st);  // marks + the list's count
+    // (the tile marks and the list's length are zeroed by the scatter)
 #define BQG_AGGP(NS) hipLaunchKernelGGL((k_part_aggregate<2, 2, NS, true, true>), dim3(grid), dim3(1024), agg_lds, st, p, L, s)
     if (p.nsum == 0) BQG_AGGP(0); else BQG_AGGP(1);
 #undef BQG_AGGP

@@ -179,8 +179,9 @@ void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order
                  unsigned int n, int nsum, uint64_t nslots, hipStream_t st);
 // large slot spaces, no compaction and no host round trip before the emit: the groups' first
 // rows marked -- in row_map (one byte per row, = epoch; cleared by the caller when the epoch
-// wraps) or, with row_map null, in the bitmap by atomics (hdr then sits after the bitmap and is
-// zeroed with it) -- their rank scan with the group count in hdr[0] (passing rows in hdr[1];
+// wraps; the marking workgroups' passing rows in rows_part [1024], summed by the rank scan) or,
+// with row_map null, in the bitmap by atomics (hdr then sits after the bitmap and is zeroed
+// with it) -- their rank scan with the group count in hdr[0] (passing rows in hdr[1];
 // both mirrored to host_hdr, page-locked, device-mapped, readable once ev_groups has
 // completed), then the emit over the slots with the output columns at `out` laid out by that
 // count (column j after the 256-byte aligned sizes of columns 0..j-1); with `rec` (capacity
@@ -188,7 +189,8 @@ void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order
 // the columns from them in rank order (without, it stores the columns at the ranks)
 void launch_slot_emit(const EmitParams& e, const SlotArrays& s, uint64_t nslots, int64_t nrows,
                       unsigned int* bitmap, unsigned char* row_map, unsigned char epoch,
-                      unsigned long long* word_pair, unsigned int* block_prefix, unsigned long long* hdr,
+                      unsigned long long* word_pair, unsigned int* block_prefix,
+                      unsigned long long* rows_part, unsigned long long* hdr,
                       unsigned long long* host_hdr, hipEvent_t ev_groups, unsigned char* out,
                       unsigned long long* rec, hipStream_t st);
 // slot spaces up to kSmallEmitSlots: compaction + ordering + emit in one workgroup (output

@@ -137,6 +137,12 @@ __device__ __forceinline__ void part_scatter_body(const ScanParams& p, const Par
   lds_barrier();
   const int64_t begin = (int64_t)blockIdx.x * L.rows_per_block;
   const int64_t end = (p.nrows < begin + L.rows_per_block ? p.nrows : begin + L.rows_per_block);
+  if (PACK) {
+    // the aggregate's first-tile marks of this block's tiles and (block 0) the marked list's
+    // length, zeroed here rather than by a fill between the two kernels (round 6)
+    for (int64_t t = begin / TR + tid; t < (end + TR - 1) / TR; t += T) L.tile_mark[t] = 0u;
+    if (blockIdx.x == 0 && tid == 0) *L.nmarked = 0u;
+  }
   if (begin >= end) return;
   const uint64_t lowmask = (1ull << L.wbits) - 1ull;
   const int per = (P + T - 1) / T;  // partitions per thread in the tile scan

@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 tail -2 $OUT/pytest_slot.txt
 timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_merge.py -m gpu > $OUT/pytest_parity.txt 2>&1 || { tail -30 $OUT/pytest_parity.txt; exit 1; }
 tail -2 $OUT/pytest_parity.txt
-for se in 1 2 3 0; do
+for se in 1 0; do
 BQGPU_OPTIONS="slot_emit=$se" timeout -k 10 300 python bench.py --config c3 --steps 20 --warmup 3 --no-cpu-baseline --no-compact-record --no-cold-record > $OUT/c3_se$se.json 2> $OUT/c3_se$se.err || exit $?
 python3 -c "import json;d=json.load(open('$OUT/c3_se$se.json'));r=d['roofline'];c=d.get('c5') or {};print('slot_emit=$se C3 ms', round(d['ms_per_step'],4), 'device', round(r['device_ms_per_query'],4), 'kernels', round(r['kernel_avg_ms'],4), 'frac', round(r['frac'],4), 'C5 ms', c.get('ms_per_step'))"
 done
