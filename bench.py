@@ -922,6 +922,7 @@ def main(argv=None):
         step_t()
     dev.synchronize()
     device_avg = float(np.mean([t['total_ms'] for t in timings])) if timings else float('nan')
+    copy_avg = float(np.mean([t['copy_ms'] for t in timings])) if timings else float('nan')
     achieved = bytes_per_launch / (scan_avg * 1e-3) / 1e9 if scan_avg > 0 else 0.0
 
     # the generic (precompiled) kernel's steady step: what a cold shape's first query is held to
@@ -997,6 +998,13 @@ def main(argv=None):
             # (compaction, first-row bitmap, rank pass) and the 24 MB PCIe copy
             'frac_whole_query_incl_result_copy': (bytes_per_launch / (device_avg * 1e-3) / 1e9 / HBM_PEAK_GBS
                                                   if device_avg == device_avg and device_avg > 0 else None),
+            # ... and over every kernel of the query (its device time less the result's copy to
+            # host memory, which runs at the PCIe rate): what the kernels beside the counted ones
+            # cost (for C3 the large-result emit: first-row marks, rank scan, emit)
+            'result_copy_ms': copy_avg if copy_avg == copy_avg else None,
+            'device_ms_per_query_excl_result_copy': (device_avg - copy_avg if copy_avg == copy_avg else None),
+            'frac_all_kernels': (bytes_per_launch / ((device_avg - copy_avg) * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                 if copy_avg == copy_avg and device_avg - copy_avg > 0 else None),
         },
         'cpu_baseline': cpu,
         'cold_first_query_ms': cold['first_query_ms'] if cold else None,

@@ -29,7 +29,7 @@ T_FALSE, T_TRUE, T_EQ, T_NE, T_IN, T_NIN, T_GT, T_GE, T_LT, T_LE = -1, 0, 1, 2, 
 
 E_INVALID, E_UNSUPPORTED, E_HIP, E_OOM, E_STATE = -1, -2, -3, -4, -5
 UNIQUE_ID_BYTES = 128
-ABI_VERSION = 9
+ABI_VERSION = 10
 OPTIONS = ('jit', 'jit_min_rows', 'partition', 'part_wbits', 'part_k', 'part_threads', 'part_per_cu',
            'part_splits', 'part_narrow', 'fused_scd', 'scd_compact', 'scd_pack16', 'priv_ahead',
            'private_per_cu', 'small_emit', 'hash_slots', 'distinct_slots', 'part_pack', 'scd_runs', 'part_win', 'compact', 'part_first',
@@ -64,7 +64,8 @@ class Timing(ctypes.Structure):
                 ('bytes', ctypes.c_int64), ('mode', ctypes.c_int32), ('specialized', ctypes.c_int32),
                 ('narrow', ctypes.c_int32), ('regrows', ctypes.c_int32),
                 ('bytes_read', ctypes.c_int64), ('compact_ms', ctypes.c_double),
-                ('scan_ms_sum', ctypes.c_double), ('timed_queries', ctypes.c_int64)]
+                ('scan_ms_sum', ctypes.c_double), ('timed_queries', ctypes.c_int64),
+                ('copy_ms', ctypes.c_double)]
 
 
 # enum bqg_decode

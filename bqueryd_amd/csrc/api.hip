@@ -439,6 +439,9 @@ struct bqg_ctx {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // timing level 1: the first and last compact-copy build of the current query
   hipEvent_t ev_sh[2] = {nullptr, nullptr};
+  // timing level 1: the start of the result's copy to host memory (large results)
+  hipEvent_t ev_copy = nullptr;
+  bool copy_timed = false;
   // the large-result emit: the group count has reached page-locked host memory
   hipEvent_t ev_groups = nullptr;
   bool sh_timed = false;
@@ -1284,6 +1287,7 @@ void finish_query(bqg_ctx* c, const Plan& pl, int64_t G, int ncols) {
   c->last.bytes = pl.alg_bytes + out;
   c->last.bytes_read = pl.read_bytes + out;
   c->last.compact_ms = NAN;
+  c->last.copy_ms = NAN;
   if (!c->timing) return;
   float ms = 0;
   HIPCHECK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
@@ -1299,12 +1303,18 @@ void finish_query(bqg_ctx* c, const Plan& pl, int64_t G, int ncols) {
       HIPCHECK(hipEventElapsedTime(&ms, c->ev_sh[0], c->ev_sh[1]));
       c->last.compact_ms = ms;
     }
+    c->last.copy_ms = 0.0;
+    if (c->copy_timed) {
+      HIPCHECK(hipEventElapsedTime(&ms, c->ev_copy, c->ev[3]));
+      c->last.copy_ms = ms;
+    }
   }
 }
 
 // Runs the passes of one groupby; returns the device output columns through `res`.
 void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out) {
   c->sh_timed = false;
+  c->copy_timed = false;
   Plan pl;
   plan_query(c, t, q, pl);
   EmitParams e;
@@ -2153,6 +2163,10 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
     }
     BlockGuard blk;
     blk.reset(c->pool, c->pool_get(obytes + 64));
+    if (c->timing == 1) {
+      HIPCHECK(hipEventRecord(c->ev_copy, st));
+      c->copy_timed = true;
+    }
     HIPCHECK(hipMemcpyAsync(blk.b.p, ob, obytes, hipMemcpyDeviceToHost, st));
     if (c->timing == 1) HIPCHECK(hipEventRecord(c->ev[3], st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -2222,6 +2236,10 @@ void run_groupby(bqg_ctx* c, bqg_table* t, const bqg_query* q, bqg_result** out)
   }
   BlockGuard blk;
   blk.reset(c->pool, c->pool_get(obytes + 64));
+  if (c->timing == 1) {
+    HIPCHECK(hipEventRecord(c->ev_copy, st));
+    c->copy_timed = true;
+  }
   HIPCHECK(hipMemcpyAsync(blk.b.p, ob, obytes, hipMemcpyDeviceToHost, st));
   if (c->timing == 1) HIPCHECK(hipEventRecord(c->ev[3], st));
   HIPCHECK(hipStreamSynchronize(st));
@@ -2472,6 +2490,7 @@ int bqg_create(int device_ordinal, bqg_ctx** out) {
     for (int i = 0; i < 4; ++i) HIPCHECK(hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence));
     for (int i = 0; i < 2; ++i) HIPCHECK(hipEventCreateWithFlags(&c->ev_sh[i], hipEventDisableSystemFence));
     HIPCHECK(hipEventCreateWithFlags(&c->ev_groups, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&c->ev_copy, hipEventDisableSystemFence));
     // last-workgroup-done counters of the finish kernels (each reset by its last workgroup)
     HIPCHECK(hipMemset(c->done.ensure(256), 0, 256));
     if (c->opt[kOptWarm]) warm_context(c);
@@ -2505,6 +2524,7 @@ int bqg_destroy(bqg_ctx* c) {
     for (int i = 0; i < 2; ++i)
       if (c->ev_sh[i]) (void)hipEventDestroy(c->ev_sh[i]);
     if (c->ev_groups) (void)hipEventDestroy(c->ev_groups);
+    if (c->ev_copy) (void)hipEventDestroy(c->ev_copy);
     if (c->own) (void)hipStreamDestroy(c->own);
   });
   delete c;

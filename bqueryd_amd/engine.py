@@ -57,7 +57,7 @@ class Device:
         self.check(self._lib.bqg_last_timing(self.handle, ctypes.byref(t)))
         return {'scan_ms': t.scan_ms, 'scan_launches': t.scan_launches, 'total_ms': t.total_ms,
                 'rows': t.rows, 'bytes': t.bytes, 'bytes_read': t.bytes_read, 'compact_ms': t.compact_ms,
-                'scan_ms_sum': t.scan_ms_sum, 'timed_queries': t.timed_queries,
+                'scan_ms_sum': t.scan_ms_sum, 'timed_queries': t.timed_queries, 'copy_ms': t.copy_ms,
                 'mode': t.mode, 'specialized': bool(t.specialized),
                 'narrow': bool(t.narrow), 'pack16': t.narrow == 2, 'regrows': t.regrows}
 

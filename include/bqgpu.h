@@ -52,8 +52,10 @@ extern "C" {
  *      bqg_table_drop_compact (the compact copies' HBM, built and released explicitly);
  * 9 -- bqg_comm_progress (the merge phase a rank is in, readable while it runs); option
  *      jit_async and bqg_jit_wait (no query waits for a run-time compile); option warm;
- *      bqg_merge_shared_host (the merged rows straight into node-shared host memory). */
-#define BQG_ABI_VERSION 9
+ *      bqg_merge_shared_host (the merged rows straight into node-shared host memory);
+ * 10 -- bqg_timing.copy_ms (the result's copy to host memory inside total_ms); option
+ *      slot_emit (the large-result emit without compaction or host round trip). */
+#define BQG_ABI_VERSION 10
 
 /* error codes */
 #define BQG_OK 0
@@ -146,6 +148,9 @@ typedef struct {
                             (0 when none was built; timing level 1 only, else NaN) (ABI 8) */
   double scan_ms_sum;    /* scan_ms summed over every query since timing was (re-)enabled, and */
   int64_t timed_queries; /* how many (ABI 8): a benchmark loop reads them once at its end */
+  double copy_ms;        /* the part of total_ms spent copying the result to host memory (large
+                            results; 0 when the emit wrote it there directly; timing level 1
+                            only, else NaN) (ABI 10) */
 } bqg_timing;
 
 /* ---------------- lifecycle ---------------- */

@@ -253,7 +253,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(declared) == set(_lib._PROTOS), set(declared) ^ set(_lib._PROTOS)
-    assert lib.bqg_abi_version() == _lib.ABI_VERSION == 9
+    assert lib.bqg_abi_version() == _lib.ABI_VERSION == 10
 
 
 def test_library_fails_loudly_without_gpu():
