@@ -900,6 +900,17 @@ void launch_slot_emit(const EmitParams& e, const SlotArrays& s, uint64_t nslots,
                        hdr, out);
   }
 }
+__global__ void k_zero_ranges(ZeroRanges z) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (int r = 0; r < z.n; ++r)
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < z.words[r]; i += stride) z.p[r][i] = 0u;
+}
+void launch_zero_ranges(const ZeroRanges& z, hipStream_t st) {
+  uint64_t most = 1;
+  for (int r = 0; r < z.n; ++r) most = std::max<uint64_t>(most, z.words[r]);
+  const unsigned g = (unsigned)std::min<uint64_t>((most + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_zero_ranges, dim3(g), dim3(256), 0, st, z);
+}
 void launch_emit(const EmitParams& e, const SlotArrays& s, const uint32_t* order, unsigned int n, int nsum,
                  uint64_t nslots, hipStream_t st) {
   const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 4096);

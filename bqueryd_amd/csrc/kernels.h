@@ -196,6 +196,14 @@ void launch_slot_emit(const EmitParams& e, const SlotArrays& s, uint64_t nslots,
 // slot spaces up to kSmallEmitSlots: compaction + ordering + emit in one workgroup (output
 // columns of capacity nslots); hdr[0] = groups, hdr[1] = passing rows
 constexpr uint32_t kSmallEmitSlots = 8192;
+// up to kZeroRanges word ranges zeroed by one kernel launch
+constexpr int kZeroRanges = 4;
+struct ZeroRanges {
+  int n;
+  unsigned int* p[kZeroRanges];
+  uint64_t words[kZeroRanges];
+};
+void launch_zero_ranges(const ZeroRanges& z, hipStream_t st);
 void launch_emit_small(const EmitParams& e, const SlotArrays& s, uint32_t nslots, int nsum,
                        unsigned long long* hdr, hipStream_t st);
 
