@@ -1257,9 +1257,37 @@ void table_from_device(bqg_ctx* c, const std::vector<int>& dts, const std::vecto
         for (Column& col : t->cols) t->ctx->colpool.put(col.dev, col.bytes);
     }
   } undo{t.get()};
-  for (Column& col : t->cols) alloc_column(c, col, n, false);
-  for (size_t j = 0; j < dts.size(); ++j)
-    if (n > 0) HIPCHECK(hipMemcpyAsync(t->cols[j].dev, src[j], (size_t)n * dtype_size(dts[j]), hipMemcpyDeviceToDevice, c->stream));
+  // one kernel copies the rows and zeroes every column's tail (a fill and a copy per column
+  // cost ~10 us each: ~40 us of C5's shard pass); per-column calls when a pointer or size is
+  // not 16-byte aligned
+  for (Column& col : t->cols) {
+    size_t cap = 0;
+    col.dev = (unsigned char*)col_alloc(c, column_bytes(n, col.dtype), &cap);
+    if (!col.dev) fail(BQG_E_OOM, "device allocation of a column (%zu bytes) failed", column_bytes(n, col.dtype));
+    col.bytes = cap;
+  }
+  bool one = dts.size() <= (size_t)kMaxCopyCols;
+  for (size_t j = 0; j < dts.size() && one; ++j)
+    one = ((uintptr_t)src[j] & 15) == 0 && ((uintptr_t)t->cols[j].dev & 15) == 0 && (t->cols[j].bytes & 15) == 0;
+  if (one) {
+    ColumnCopies cc{};
+    cc.n = (int)dts.size();
+    for (size_t j = 0; j < dts.size(); ++j) {
+      cc.dst[j] = t->cols[j].dev;
+      cc.src[j] = (const unsigned char*)src[j];
+      cc.used[j] = (uint64_t)n * dtype_size(dts[j]);
+      cc.cap[j] = t->cols[j].bytes;
+    }
+    launch_column_copies(cc, c->stream);
+    HIPCHECK(hipGetLastError());
+  } else {
+    for (size_t j = 0; j < dts.size(); ++j) {
+      Column& col = t->cols[j];
+      const size_t used = (size_t)n * dtype_size(dts[j]);
+      HIPCHECK(hipMemsetAsync(col.dev + used, 0, col.bytes - used, c->stream));
+      if (n > 0) HIPCHECK(hipMemcpyAsync(col.dev, src[j], used, hipMemcpyDeviceToDevice, c->stream));
+    }
+  }
   HIPCHECK(hipStreamSynchronize(c->stream));
   undo.t = nullptr;
   c->tables.push_back(t.get());

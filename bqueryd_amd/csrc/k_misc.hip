@@ -900,6 +900,34 @@ void launch_slot_emit(const EmitParams& e, const SlotArrays& s, uint64_t nslots,
                        hdr, out);
   }
 }
+__global__ void k_column_copies(ColumnCopies cc) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (int j = 0; j < cc.n; ++j) {
+    const uint64_t used = cc.used[j], units = cc.cap[j] / 16;
+    uint4* d = reinterpret_cast<uint4*>(cc.dst[j]);
+    const uint4* src = reinterpret_cast<const uint4*>(cc.src[j]);
+    for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride) {
+      const uint64_t b = u * 16;
+      if (b + 16 <= used) {
+        d[u] = src[u];
+      } else if (b >= used) {
+        d[u] = make_uint4(0u, 0u, 0u, 0u);
+      } else {  // the unit holding the last rows: their bytes, then zeros (no read past them)
+        unsigned char tmp[16];
+        for (int k = 0; k < 16; ++k) tmp[k] = b + k < used ? cc.src[j][b + k] : (unsigned char)0;
+        uint4 v;
+        __builtin_memcpy(&v, tmp, 16);
+        d[u] = v;
+      }
+    }
+  }
+}
+void launch_column_copies(const ColumnCopies& cc, hipStream_t st) {
+  uint64_t units = 0;
+  for (int j = 0; j < cc.n; ++j) units = std::max<uint64_t>(units, cc.cap[j] / 16);
+  const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((units + 255) / 256, 2048));
+  hipLaunchKernelGGL(k_column_copies, dim3(g), dim3(256), 0, st, cc);
+}
 __global__ void k_zero_ranges(ZeroRanges z) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (int r = 0; r < z.n; ++r)

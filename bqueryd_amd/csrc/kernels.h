@@ -196,6 +196,18 @@ void launch_slot_emit(const EmitParams& e, const SlotArrays& s, uint64_t nslots,
 // slot spaces up to kSmallEmitSlots: compaction + ordering + emit in one workgroup (output
 // columns of capacity nslots); hdr[0] = groups, hdr[1] = passing rows
 constexpr uint32_t kSmallEmitSlots = 8192;
+// a result's columns copied into a new device table's columns, each column's tail past its
+// rows zeroed, in one kernel launch (table_from_device: a fill and a copy per column cost ~10 us
+// each)
+constexpr int kMaxCopyCols = kMaxKeys + kMaxAggs;
+struct ColumnCopies {
+  int n;
+  unsigned char* dst[kMaxCopyCols];      // 16-byte aligned, cap bytes
+  const unsigned char* src[kMaxCopyCols];  // 16-byte aligned, used bytes
+  uint64_t used[kMaxCopyCols];
+  uint64_t cap[kMaxCopyCols];            // a multiple of 16
+};
+void launch_column_copies(const ColumnCopies& cc, hipStream_t st);
 // up to kZeroRanges word ranges zeroed by one kernel launch
 constexpr int kZeroRanges = 4;
 struct ZeroRanges {
