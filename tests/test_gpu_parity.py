@@ -1440,3 +1440,34 @@ def test_slot_emit_matches_compaction_emit(shape, oracle_c, engine_options):
         return
     ref = oracle_c.groupby(cols, keys, aggs, None)
     assert_tables_equal(new, ref)
+
+
+def test_slot_emit_row_map_epochs(oracle_c, engine_options):
+    """The row map of the large-result emit holds one byte per row, the query's epoch (1..255),
+    and is cleared only when the epoch wraps or the map grows: 300 large-result queries on one
+    context -- past a wrap -- alternating two tables whose first rows differ, then a larger
+    table (the map grows) and the first again, each against the C restatement."""
+    rng = np.random.default_rng(255)
+
+    def shard(n, k):
+        return OrderedDict(k=rng.integers(0, k, n).astype(np.int32), v=rng.integers(0, 100, n).astype(np.int64))
+
+    a_cols, b_cols, big_cols = shard(40_000, 20_000), shard(30_000, 15_000), shard(120_000, 30_000)
+    aggs = [['v', 'sum', 's'], ['v', 'count', 'n']]
+    refs = {}
+    tables = {}
+    try:
+        for name, cols in (('a', a_cols), ('b', b_cols), ('big', big_cols)):
+            tables[name] = ShardTable(cols)
+            refs[name] = oracle_c.groupby(cols, ['k'], aggs, None)
+        for q in range(300):
+            name = 'a' if q % 2 == 0 else 'b'
+            got, _ = tables[name].groupby(['k'], aggs)
+            if q % 37 == 0 or q >= 250:
+                assert_tables_equal(got, refs[name])
+        for name in ('big', 'a', 'big'):
+            got, _ = tables[name].groupby(['k'], aggs)
+            assert_tables_equal(got, refs[name])
+    finally:
+        for t in tables.values():
+            t.close()
