@@ -363,6 +363,46 @@ struct CopyDesc {
   unsigned long long bytes;
 };
 
+// A rank's slice of every column into the node-shared host result (bqg_merge_shared_host),
+// one launch instead of one DMA copy per column (each copy past the first costs ~8-10 us,
+// profiles/r6aq_d2h_chunks_micro.txt): 16-byte stores at 16-byte aligned host addresses (PCIe
+// writes of whole units, ~50 GB/s, profiles/r6s_host_write_micro.txt); the unit at each end of
+// a slice is written byte by byte, since the neighbouring rank's rows share it.
+struct SliceCopies {
+  int n;
+  const unsigned char* src[bqg::kMergeMaxCols];
+  unsigned char* dst[bqg::kMergeMaxCols];  // device mapping of the host block
+  unsigned long long bytes[bqg::kMergeMaxCols];
+};
+
+__global__ __launch_bounds__(256) void k_slices_to_host(SliceCopies s) {
+  const int j = blockIdx.y;
+  const unsigned char* src = s.src[j];
+  const uintptr_t d0 = (uintptr_t)s.dst[j], d1 = d0 + s.bytes[j];
+  const uintptr_t a0 = d0 & ~(uintptr_t)15, a1 = (d1 + 15) & ~(uintptr_t)15;
+  const bool agree4 = (((uintptr_t)src - d0) & 3) == 0;
+  for (uintptr_t a = a0 + ((uintptr_t)blockIdx.x * 256 + threadIdx.x) * 16; a < a1; a += (uintptr_t)gridDim.x * 256 * 16) {
+    if (a >= d0 && a + 16 <= d1) {
+      const unsigned char* p = src + (a - d0);
+      uint4 v;
+      if (((uintptr_t)p & 15) == 0) {
+        v = *reinterpret_cast<const uint4*>(p);
+      } else if (agree4) {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+        v = make_uint4(q[0], q[1], q[2], q[3]);
+      } else {
+        unsigned char t[16];
+        for (int k = 0; k < 16; ++k) t[k] = p[k];
+        __builtin_memcpy(&v, t, 16);
+      }
+      *reinterpret_cast<uint4*>(a) = v;
+    } else {
+      for (int k = 0; k < 16; ++k)
+        if (a + k >= d0 && a + k < d1) *reinterpret_cast<unsigned char*>(a + k) = src[a + k - d0];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_batch_copy(const CopyDesc* d) {
   const CopyDesc c = d[blockIdx.y];
   const unsigned long long stride = (unsigned long long)gridDim.x * 256;
@@ -706,9 +746,26 @@ void merge_impl(std::vector<Local>& ranks, int n_keys, const std::vector<int32_t
       int64_t off = 0;
       for (int s2 = 0; s2 < l.st->rank; ++s2) off += part_rows[s2];
       const int64_t n = part_rows[l.st->rank];
-      for (int j = 0; n && j < ncols; ++j)
-        HIPCK(hipMemcpyAsync(sh->base + coff[j] + ((size_t)off << lg[j]), col_ptr(l.ctx, src[i], j), (size_t)n << lg[j],
-                             hipMemcpyDeviceToHost, l.stream));
+      void* hdev = nullptr;
+      if (n && ncols <= bqg::kMergeMaxCols && hipHostGetDevicePointer(&hdev, sh->base, 0) == hipSuccess && hdev) {
+        SliceCopies sc{};
+        sc.n = ncols;
+        unsigned long long most = 0;
+        for (int j = 0; j < ncols; ++j) {
+          sc.src[j] = (const unsigned char*)col_ptr(l.ctx, src[i], j);
+          sc.dst[j] = (unsigned char*)hdev + coff[j] + ((size_t)off << lg[j]);
+          sc.bytes[j] = (unsigned long long)n << lg[j];
+          most = std::max(most, sc.bytes[j]);
+        }
+        const unsigned gx = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>((most / 16 + 2 + 255) / 256, 1024));
+        hipLaunchKernelGGL(k_slices_to_host, dim3(gx, (unsigned)ncols), dim3(256), 0, l.stream, sc);
+        HIPCK(hipGetLastError());
+      } else {
+        (void)hipGetLastError();
+        for (int j = 0; n && j < ncols; ++j)
+          HIPCK(hipMemcpyAsync(sh->base + coff[j] + ((size_t)off << lg[j]), col_ptr(l.ctx, src[i], j), (size_t)n << lg[j],
+                               hipMemcpyDeviceToHost, l.stream));
+      }
     }
     if (W > 1) xfer_allgather_i64(ranks, 1);
     sync_all(ranks);
