@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 tail -2 $OUT/pytest_slot.txt
 true
 true
-for se in 1; do break
+for se in 1; do
 BQGPU_OPTIONS="slot_emit=$se" timeout -k 10 300 python bench.py --config c3 --steps 20 --warmup 3 --no-cpu-baseline --no-compact-record --no-cold-record > $OUT/c3_se$se.json 2> $OUT/c3_se$se.err || exit $?
 python3 -c "import json;d=json.load(open('$OUT/c3_se$se.json'));r=d['roofline'];c=d.get('c5') or {};print('slot_emit=$se C3 ms', round(d['ms_per_step'],4), 'device', round(r['device_ms_per_query'],4), 'kernels', round(r['kernel_avg_ms'],4), 'frac', round(r['frac'],4), 'C5 ms', c.get('ms_per_step'))"
 done
