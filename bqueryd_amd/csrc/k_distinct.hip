@@ -409,10 +409,10 @@ void launch_scd(const ScanParams& p, const SlotArrays& s, const ScdLaunch& d, hi
   if (want > (uint64_t)dc.waves) want = (uint64_t)dc.waves;
   if (want < 1) want = 1;
   int per = (int)(((uint64_t)dc.waves + want - 1) / want);
-  // few slots: runs of up to 32 chunks, ~64 runs per slot -- stage 2 then folds one run per
-  // lane (C4's 1792 chunks x 265 slots: 29.7 + 13.7 us against 20.5 + 34.0 us at 4 chunks a
-  // run, profiles/r5s_c4_combine.txt)
-  if (per < 32 && dc.waves > 64 * per) per = std::min(32, (int)((dc.waves + 63) / 64));
+  // few slots: runs of up to 16 chunks, >= 64 runs per slot -- stage 2 then folds one or two
+  // runs per lane (C4's 1792 chunks x 265 slots: 19.2 + 15.8 us at 16 chunks a run, 30.3 + 13.3
+  // at 28, 15.4 + 21.8 at 8, profiles/r6bc_c4_combine_sweep.txt; 20.5 + 34.0 at 4, r5s_)
+  if (per < 16 && dc.waves > 64 * per) per = std::min(16, (int)((dc.waves + 63) / 64));
   const int runs = (int)(((uint64_t)dc.waves + per - 1) / per);
   const uint64_t items = S * (uint64_t)runs;
   hipLaunchKernelGGL(k_scd_combine_runs, dim3((unsigned)((items + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, dc, S,
